@@ -1,0 +1,85 @@
+// Shared helpers for the sparknet_amd HIP kernels (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in this directory:
+//  * activations are NHWC bf16 on device (channels innermost), params are fp32
+//    masters with bf16 compute shadows;
+//  * every entry point is `extern "C"` and takes an explicit hipStream_t so the
+//    Python side (ctypes) can launch on torch's current stream and the whole
+//    training step can be captured into a hipGraph;
+//  * wave size is 64, blocks are multiples of 64 threads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef uint16_t bf16_t;  // raw storage type of a bf16 element
+
+#define SN_DEV __device__ __forceinline__
+
+SN_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// Round-to-nearest-even f32 -> bf16 (hipcc lowers the __bf16 cast to v_cvt_pk_bf16_f32,
+// which keeps NaNs NaN — see MI355X_MICROARCH "Correctness boundaries").
+SN_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+SN_DEV void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+SN_DEV uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+SN_DEV uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack2(f[0], f[1]);
+  r.y = pack2(f[2], f[3]);
+  r.z = pack2(f[4], f[5]);
+  r.w = pack2(f[6], f[7]);
+  return r;
+}
+
+SN_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+SN_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Philox4x32-10 counter-based RNG: dropout masks are regenerated in backward
+// from (seed, offset, element index) instead of being stored.
+SN_DEV uint4 philox4x32(uint2 key, uint4 ctr) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += W0;
+    key.y += W1;
+  }
+  return ctr;
+}
+
+#define SN_CHECK_LAUNCH() (hipGetLastError() == hipSuccess ? 0 : 1)
+
+static inline int sn_blocks(long long n, int per_block, int cap = 65535 * 8) {
+  long long b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (int)b;
+}

@@ -1,0 +1,388 @@
+// MFMA GEMM for gfx950 — the single matrix engine behind Convolution (fwd / dgrad /
+// wgrad, implicit-GEMM over NHWC activations), InnerProduct and Deconvolution.
+//
+// Replaces the reference's per-image im2col + cublasSgemm loop
+// (caffe/src/caffe/layers/conv_layer.cu:14-21, base_conv_layer.cpp:312-376,
+//  inner_product_layer.cu:22-54, math_functions.cu:14-28) with ONE launch per layer
+// over the whole batch.
+//
+//   C_g[m][n] (op)= sum_k A_g(m, k) * B_g(n, k)          g = group, split-K over k
+//
+// Operands are bf16, accumulation is fp32 on v_mfma_f32_16x16x32_bf16.  Each operand
+// is a "virtual row-major matrix" that is either
+//   KC : [rows = M (or N)] x [cols = K]   (reduction dim contiguous)  -> ds_read_b128
+//   MC : [rows = K] x [cols = M (or N)]   (reduction dim strided)     -> ds_read_b64_tr_b16
+// so NT / NN / TN products all stage their tiles straight from global memory without a
+// transpose pass: the transposition happens in the LDS read (CDNA4 tr_b16).
+// A virtual matrix is either DENSE (ptr + row*ld + col) or IM2COL: the implicit
+// [N*P*Q pixels] x [R*S*Cg] patch matrix of an NHWC tensor, gathered on the fly with
+// zero-fill for padding — no column buffer in HBM.
+//
+// Tile 128x128x64, 256 threads (2x2 waves, 64x64 per wave = 4x4 MFMA tiles), LDS
+// double buffered (64 KiB) with XOR swizzles that make both the b128 row reads and the
+// tr_b16 transposed reads bank-conflict free, register-staged global->LDS copies
+// issued one tile ahead (load early / write late), XCD-aware bijective block remap.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
+constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile, either orientation
+
+enum { OP_DENSE = 0, OP_IM2COL = 1 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2 };
+
+}  // namespace
+
+extern "C" {
+
+struct SnConvGeom {
+  int N, H, W, C;  // input tensor (NHWC); C = channel stride of a pixel
+  int P, Q;        // output spatial
+  int R, S;        // kernel
+  int sh, sw, ph, pw, dh, dw;
+  int Cg;          // channels per group (multiple of 8)
+};
+
+struct SnOperand {
+  const bf16_t* ptr;
+  long long ld;       // row stride (elements) for DENSE
+  long long gstride;  // per-group offset: elements (DENSE) / channels (IM2COL)
+  SnConvGeom g;
+};
+
+struct SnGemmArgs {
+  int M, N, K;
+  int groups, splits, kchunk;  // kchunk: reduction length per split (multiple of 64)
+  int a_mc, a_mode, b_mc, b_mode, epi;
+  SnOperand A, B;
+  void* C;
+  long long ldc, c_gstride, c_split_stride;
+  const float* bias;  // per output column n (offset by g*N), EPI_BF16 only
+  int relu;
+};
+
+}  // extern "C"
+
+namespace {
+
+SN_DEV int swz_mc(int k) { return (((k & 3) | (((k >> 3) & 1) << 2)) << 5); }
+SN_DEV int kc_off(int row, int kc) { return row * 128 + ((kc ^ ((row >> 1) & 7)) << 4); }
+SN_DEV int mc_off(int k, int mc) { return k * 256 + ((mc << 4) ^ swz_mc(k)); }
+
+// Per-thread staging state of one operand.  KC tiles: the thread owns 4 chunks on rows
+// (tid>>3)+32i, chunk column tid&7 (fixed).  MC tiles: rows (tid>>4)+16i, chunk column
+// tid&15 (fixed).
+template <int MC, int MODE>
+struct Stager {
+  const bf16_t* base;
+  long long ld;
+  SnConvGeom g;
+  int coff;         // IM2COL group channel offset
+  int fixed;        // KC: kc ; MC: mc
+  int row0;         // first row of this thread (tile-relative)
+  // KC+IM2COL: per-row pixel decode (rows are fixed across k)
+  int pn[4], ph[4], pw[4];
+  bool pv[4];
+  // MC+IM2COL: column decode (cols are fixed across k)
+  int ctap_r, ctap_s, cc;
+  bool cv;
+  uint4 reg[4];
+
+  SN_DEV void init(const SnOperand& op, int grp, int tid, int tile_row0, int rows_lim,
+                   int tile_col0, int cols_lim) {
+    ld = op.ld;
+    g = op.g;
+    if (MODE == OP_DENSE) {
+      base = op.ptr + (long long)grp * op.gstride;
+      coff = 0;
+    } else {
+      base = op.ptr;
+      coff = (int)(grp * op.gstride);
+    }
+    if (!MC) {
+      fixed = tid & 7;
+      row0 = tid >> 3;
+      if (MODE == OP_IM2COL) {
+        const int PQ = g.P * g.Q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int pix = tile_row0 + row0 + 32 * i;
+          pv[i] = pix < rows_lim;
+          int n = pix / PQ, pq = pix - n * PQ;
+          int p = pq / g.Q, q = pq - p * g.Q;
+          pn[i] = n * g.H;
+          ph[i] = p * g.sh - g.ph;
+          pw[i] = q * g.sw - g.pw;
+        }
+      }
+    } else {
+      fixed = tid & 15;
+      row0 = tid >> 4;
+      if (MODE == OP_IM2COL) {
+        int col = tile_col0 + fixed * 8;
+        cv = col < cols_lim;
+        int tap = col / g.Cg;
+        cc = col - tap * g.Cg;
+        ctap_r = tap / g.S;
+        ctap_s = tap - ctap_r * g.S;
+      }
+    }
+  }
+
+  SN_DEV uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+  // Issue the global loads of the tile whose first reduction index is k_tile.
+  // KC: rows are M/N indices (tile_row0 + ...), cols k.  MC: rows k, cols M/N.
+  SN_DEV void load(int k_tile, int k_lim, int tile_rc0, int rc_lim) {
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    if (!MC) {
+      const int k = k_tile + fixed * 8;
+      const bool kv = k < k_lim;
+      if (MODE == OP_DENSE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int row = tile_rc0 + row0 + 32 * i;
+          reg[i] = (kv && row < rc_lim) ? ld16(base + (long long)row * ld + k) : z;
+        }
+      } else {
+        int tap = k / g.Cg, c = k - tap * g.Cg;
+        int r = tap / g.S, s = tap - r * g.S;
+        int dh = r * g.dh, dw = s * g.dw;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int h = ph[i] + dh, w = pw[i] + dw;
+          bool v = kv && pv[i] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          long long off = ((long long)(pn[i] + h) * g.W + w) * g.C + coff + c;
+          reg[i] = v ? ld16(base + off) : z;
+        }
+      }
+    } else {
+      const int col = tile_rc0 + fixed * 8;
+      if (MODE == OP_DENSE) {
+        const bool cvd = col < rc_lim;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int k = k_tile + row0 + 16 * i;
+          reg[i] = (cvd && k < k_lim) ? ld16(base + (long long)k * ld + col) : z;
+        }
+      } else {
+        const int PQ = g.P * g.Q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int pix = k_tile + row0 + 16 * i;
+          int n = pix / PQ, pq = pix - n * PQ;
+          int p = pq / g.Q, q = pq - p * g.Q;
+          int h = p * g.sh - g.ph + ctap_r * g.dh;
+          int w = q * g.sw - g.pw + ctap_s * g.dw;
+          bool v = cv && pix < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          long long off = ((long long)(n * g.H + h) * g.W + w) * g.C + coff + cc;
+          reg[i] = v ? ld16(base + off) : z;
+        }
+      }
+    }
+  }
+
+  SN_DEV void store(char* lds) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int off = MC ? mc_off(row0 + 16 * i, fixed) : kc_off(row0 + 32 * i, fixed);
+      *reinterpret_cast<uint4*>(lds + off) = reg[i];
+    }
+  }
+};
+
+// Fragment of a 16-row subtile (rows x0..x0+15 of the operand's M/N axis) for k-step s
+// (32 reduction elements), laid out as the 16x16x32 MFMA operand: lane l holds
+// X[x0 + (l&15)][32s + 8(l>>4) + j], j = 0..7.
+template <int MC>
+SN_DEV bf16x8_t read_frag(const char* lds, int x0, int s, int lane) {
+  if (!MC) {
+    int row = x0 + (lane & 15);
+    int kc = s * 4 + (lane >> 4);
+    uint4 v = *reinterpret_cast<const uint4*>(lds + kc_off(row, kc));
+    return __builtin_bit_cast(bf16x8_t, v);
+  } else {
+    int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    int col_b = (x0 + 4 * p) * 2;
+    int k0 = s * 32 + gq * 8 + q;
+    int k1 = k0 + 4;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const char* a0 = lds + k0 * 256 + (col_b ^ swz_mc(k0));
+    const char* a1 = lds + k1 * 256 + (col_b ^ swz_mc(k1));
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, r);
+  }
+}
+
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI>
+__global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_m = (args.M + BM - 1) / BM;
+
+  // XCD-aware bijective remap: blocks that share an XCD (same bid % 8) get a
+  // contiguous range of tile ids, so tiles sharing an operand panel share an L2.
+  int bid = blockIdx.x;
+  const int nwg = gridDim.x;
+  if (nwg >= 16) {
+    int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  }
+  const int tm = bid % tiles_m, tn = bid / tiles_m;
+  const int m_blk = tm * BM, n_blk = tn * BN;
+  const int split = blockIdx.y, grp = blockIdx.z;
+  const int k0 = split * args.kchunk;
+  const int k1 = min(args.K, k0 + args.kchunk);
+
+
+  Stager<AMC, AMODE> sa;
+  Stager<BMC, BMODE> sb;
+  sa.init(args.A, grp, tid, m_blk, args.M, m_blk, args.M);
+  sb.init(args.B, grp, tid, n_blk, args.N, n_blk, args.N);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wm0 = (wave & 1) * 64, wn0 = (wave >> 1) * 64;
+  const int nk = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
+
+  if (nk > 0) {
+    sa.load(k0, k1, m_blk, args.M);
+    sb.load(k0, k1, n_blk, args.N);
+    sa.store(smem);
+    sb.store(smem + TILE_BYTES);
+    __syncthreads();
+  }
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(k0 + (kt + 1) * BK, k1, m_blk, args.M);
+      sb.load(k0 + (kt + 1) * BK, k1, n_blk, args.N);
+    }
+    const char* la = smem + cur * (2 * TILE_BYTES);
+    const char* lb = la + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fb[i] = read_frag<BMC>(lb, wn0 + 16 * i, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag<AMC>(la, wm0 + 16 * i, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      sa.store(smem + (cur ^ 1) * (2 * TILE_BYTES));
+      sb.store(smem + (cur ^ 1) * (2 * TILE_BYTES) + TILE_BYTES);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // Epilogue.  acc[i][j] holds D[n][m] with m = lane&15 (+16j), n = 4(lane>>4)+r (+16i):
+  // each lane owns 4 consecutive output columns of one output row.
+  const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m_blk + wm0 + 16 * j + mrow_l;
+    if (m >= args.M) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n_blk + wn0 + 16 * i + ncol_l;
+      if (n >= args.N) continue;
+      const bool full = (n + 3 < args.N) && ((args.ldc & 3) == 0);
+      f32x4 v = acc[i][j];
+      if (EPI == EPI_BF16) {
+        bf16_t* C = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride + (long long)m * args.ldc;
+        float o[4] = {v[0], v[1], v[2], v[3]};
+        if (args.bias) {
+          const float* bz = args.bias + (long long)grp * args.N;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] += (n + r < args.N) ? bz[n + r] : 0.f;
+        }
+        if (args.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
+        }
+        if (full) {
+          uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          *reinterpret_cast<uint2*>(C + n) = pk;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < args.N) C[n + r] = f2bf(o[r]);
+        }
+      } else {
+        float* C = reinterpret_cast<float*>(args.C) + split * args.c_split_stride +
+                   grp * args.c_gstride + (long long)m * args.ldc;
+        if (full) {
+          float4* p = reinterpret_cast<float4*>(C + n);
+          if (EPI == EPI_F32_ACC) {
+            float4 o = *p;
+            *p = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+          } else {
+            *p = make_float4(v[0], v[1], v[2], v[3]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < args.N) {
+              if (EPI == EPI_F32_ACC)
+                C[n + r] += v[r];
+              else
+                C[n + r] = v[r];
+            }
+        }
+      }
+    }
+  }
+}
+
+template <int AMC, int AMODE, int BMC, int BMODE>
+int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
+  switch (a.epi) {
+    case EPI_BF16:
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16>), grid, dim3(NTHR), 0, st, a);
+      break;
+    case EPI_F32:
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32>), grid, dim3(NTHR), 0, st, a);
+      break;
+    case EPI_F32_ACC:
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC>), grid, dim3(NTHR), 0, st, a);
+      break;
+    default:
+      return 2;
+  }
+  return SN_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
+  const SnGemmArgs& a = *args;
+  if (a.M <= 0 || a.N <= 0) return 0;
+  if (a.kchunk <= 0 || (a.kchunk % BK) != 0) return 3;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, a.splits, a.groups);
+  // Supported operand combinations (see module docstring).
+  const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  switch (key) {
+    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE>(a, grid, stream);    // NT dense
+    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE>(a, grid, stream);   // conv fwd/dgrad
+    case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE>(a, grid, stream);    // NN dense
+    case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE>(a, grid, stream);    // TN dense
+    case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL>(a, grid, stream);   // conv wgrad
+    case 0b1000: return launch_epi<1, OP_DENSE, 0, OP_DENSE>(a, grid, stream);    // TT-ish
+    default: return 4;
+  }
+}

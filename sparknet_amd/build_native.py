@@ -1,0 +1,106 @@
+"""In-tree builder for the native parts of sparknet_amd.
+
+Two shared libraries are produced inside the package (so they travel with the repo
+snapshot to a GPU box and are what the Python processes load):
+
+* ``sparknet_amd/lib/libsn_kernels.so`` — every ``csrc/kernels/*.hip`` file compiled by
+  hipcc for gfx950 (MFMA GEMM / implicit-GEMM conv, pooling, LRN, dropout, softmax-loss,
+  fused solver updates, data augmentation ...).  C ABI, launched through ctypes on
+  torch's current HIP stream.
+* ``sparknet_amd/lib/libsn_runtime.so`` — host C++ runtime (``csrc/runtime/*.cpp``):
+  prototxt-independent pieces of the engine that the reference keeps native
+  (data prefetch ring / worker threads, BlobProto packing, timers).
+
+The builder is incremental (mtime based) and compiles translation units in parallel.
+``python -m sparknet_amd.build_native`` or ``__graft_entry__.build()`` drive it.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+LIBDIR = Path(__file__).resolve().parent / "lib"
+OBJDIR = ROOT / "build" / "obj"
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = os.environ.get("SN_OFFLOAD_ARCH", "gfx950")
+
+HIP_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-ffp-contract=fast",
+    "-munsafe-fp-atomics",
+    f"-I{CSRC / 'kernels'}",
+]
+CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", f"-I{CSRC / 'runtime'}"]
+
+KERNEL_LIB = LIBDIR / "libsn_kernels.so"
+RUNTIME_LIB = LIBDIR / "libsn_runtime.so"
+
+
+def _deps(src: Path) -> list[Path]:
+    hdrs = list((CSRC / "kernels").glob("*.h")) + list((CSRC / "runtime").glob("*.h"))
+    return [src] + hdrs
+
+
+def _stale(obj: Path, deps: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def _compile(src: Path, hip: bool) -> Path:
+    obj = OBJDIR / (src.stem + (".hip.o" if hip else ".cpp.o"))
+    if _stale(obj, _deps(src)):
+        obj.parent.mkdir(parents=True, exist_ok=True)
+        if hip:
+            cmd = [HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)]
+        else:
+            cmd = ["g++", *CXX_FLAGS, "-c", str(src), "-o", str(obj)]
+        _run(cmd)
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> dict:
+    """Compile and link both libraries; returns {name: path}."""
+    if force and OBJDIR.exists():
+        for f in OBJDIR.glob("*.o"):
+            f.unlink()
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    hip_srcs = sorted((CSRC / "kernels").glob("*.hip"))
+    cpp_srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        hip_objs = list(ex.map(lambda s: _compile(s, True), hip_srcs))
+        cpp_objs = list(ex.map(lambda s: _compile(s, False), cpp_srcs))
+    out = {}
+    if hip_objs:
+        if force or _stale(KERNEL_LIB, hip_objs):
+            _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, hip_objs),
+                  "-o", str(KERNEL_LIB)])
+        out["kernels"] = str(KERNEL_LIB)
+    if cpp_objs:
+        if force or _stale(RUNTIME_LIB, cpp_objs):
+            _run(["g++", "-shared", "-fPIC", "-pthread", *map(str, cpp_objs), "-o", str(RUNTIME_LIB)])
+        out["runtime"] = str(RUNTIME_LIB)
+    if verbose:
+        print(out)
+    return out
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,120 @@
+"""ctypes bindings of the native kernel library (``libsn_kernels.so``).
+
+torch is imported first so that its HIP runtime (SONAME ``libamdhip64.so.7``) is the one
+our library binds to — there is exactly one HIP runtime per process and our kernels
+launch on torch's current stream (graph-capturable).
+
+On a machine with a GPU the library MUST load: ``kernels()`` raises instead of silently
+falling back to PyTorch ops.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_LIBDIR = Path(__file__).resolve().parent.parent / "lib"
+_kern = None
+_rt = None
+
+
+class SnConvGeom(C.Structure):
+    _fields_ = [(n, C.c_int) for n in
+                ("N", "H", "W", "C", "P", "Q", "R", "S", "sh", "sw", "ph", "pw", "dh", "dw", "Cg")]
+
+
+class SnOperand(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("ld", C.c_longlong), ("gstride", C.c_longlong),
+                ("g", SnConvGeom)]
+
+
+class SnGemmArgs(C.Structure):
+    _fields_ = [("M", C.c_int), ("N", C.c_int), ("K", C.c_int),
+                ("groups", C.c_int), ("splits", C.c_int), ("kchunk", C.c_int),
+                ("a_mc", C.c_int), ("a_mode", C.c_int), ("b_mc", C.c_int), ("b_mode", C.c_int),
+                ("epi", C.c_int),
+                ("A", SnOperand), ("B", SnOperand),
+                ("C", C.c_void_p), ("ldc", C.c_longlong), ("c_gstride", C.c_longlong),
+                ("c_split_stride", C.c_longlong),
+                ("bias", C.c_void_p), ("relu", C.c_int)]
+
+
+def lib_path(name: str = "libsn_kernels.so") -> Path:
+    return _LIBDIR / name
+
+
+def available() -> bool:
+    return lib_path().exists()
+
+
+def kernels():
+    """Load (once) and return the kernel library.  Builds it if missing."""
+    global _kern
+    if _kern is None:
+        p = lib_path()
+        if not p.exists():
+            from .. import build_native
+            build_native.build()
+        _kern = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+        _kern.sn_gemm.argtypes = [C.POINTER(SnGemmArgs), C.c_void_p]
+        _kern.sn_gemm.restype = C.c_int
+    return _kern
+
+
+def runtime():
+    global _rt
+    if _rt is None:
+        p = lib_path("libsn_runtime.so")
+        if not p.exists():
+            from .. import build_native
+            build_native.build()
+        _rt = C.CDLL(str(p))
+    return _rt
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"sparknet_amd kernel '{what}' failed with code {rc}")
+
+
+def call(name: str, *args):
+    """Call ``sn_<name>(..., stream)`` with ctypes-converted args on the current stream."""
+    fn = getattr(kernels(), "sn_" + name)
+    conv = []
+    for a in args:
+        if isinstance(a, torch.Tensor):
+            conv.append(C.c_void_p(a.data_ptr()))
+        elif a is None:
+            conv.append(C.c_void_p(0))
+        elif isinstance(a, bool):
+            conv.append(C.c_int(int(a)))
+        elif isinstance(a, int):
+            conv.append(C.c_longlong(a))
+        elif isinstance(a, float):
+            conv.append(C.c_float(a))
+        else:
+            conv.append(a)
+    conv.append(C.c_void_p(stream_ptr()))
+    fn.restype = C.c_int
+    check(fn(*conv), name)
+
+
+def loaded_libraries() -> list[str]:
+    """Which sparknet native libraries are mapped into this process (for diagnostics)."""
+    out = []
+    try:
+        with open(f"/proc/{os.getpid()}/maps") as f:
+            for line in f:
+                if "libsn_" in line or "libamdhip64" in line:
+                    path = line.split()[-1]
+                    if path not in out:
+                        out.append(path)
+    except OSError:
+        pass
+    return out
