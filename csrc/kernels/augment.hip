@@ -1,0 +1,72 @@
+// Device-side data transform: uint8 planar (N, C, Hs, Ws) minibatch -> bf16 NHWC
+// (N, crop, crop, C) with random crop, mirror, mean subtraction and scale in ONE pass.
+//
+// Reference: DataTransformer::Transform (caffe/src/caffe/data_transformer.cpp:17-130) on
+// the host per image, and SparkNet's ImageNetApp crop/mean closures executed inside the
+// JNA data callback (src/main/scala/apps/ImageNetApp.scala:160-176, whose mean
+// subtraction is a no-op — SURVEY §7.5; here it is applied correctly).
+// Crop offsets / mirror flags come from Philox(seed, counter) per image so the kernel can
+// be replayed inside a graph without host involvement; TEST phase uses centre crops.
+#include "common.h"
+
+__global__ void augment_kernel(const uint8_t* __restrict__ src, bf16_t* __restrict__ dst, int N, int C, int Hs, int Ws,
+                               int crop_h, int crop_w, const float* __restrict__ mean, int mean_mode, float scale,
+                               const long long* __restrict__ rng, int train, int mirror, int* __restrict__ offs_out) {
+  const long long total = (long long)N * crop_h * crop_w;
+  const unsigned long long seed = rng ? (unsigned long long)rng[0] : 0ull;
+  const unsigned long long counter = rng ? (unsigned long long)rng[1] : 0ull;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int w = (int)(i % crop_w);
+    const int h = (int)((i / crop_w) % crop_h);
+    const int n = (int)(i / ((long long)crop_w * crop_h));
+    int ho, wo, mir;
+    if (train) {
+      uint4 u = philox4x32(make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)),
+                           make_uint4((uint32_t)n, 0xA5A50000u, (uint32_t)counter, (uint32_t)(counter >> 32)));
+      ho = (int)(u.x % (uint32_t)(Hs - crop_h + 1));
+      wo = (int)(u.y % (uint32_t)(Ws - crop_w + 1));
+      mir = mirror ? (int)(u.z & 1u) : 0;
+    } else {
+      ho = (Hs - crop_h) / 2;
+      wo = (Ws - crop_w) / 2;
+      mir = 0;
+    }
+    if (offs_out && h == 0 && w == 0) {
+      offs_out[3 * n] = ho;
+      offs_out[3 * n + 1] = wo;
+      offs_out[3 * n + 2] = mir;
+    }
+    const int sh = h + ho;
+    const int sw = (mir ? (crop_w - 1 - w) : w) + wo;
+    bf16_t* o = dst + i * C;
+    for (int c = 0; c < C; ++c) {
+      const long long si = (((long long)n * C + c) * Hs + sh) * Ws + sw;
+      float v = (float)src[si];
+      if (mean_mode == 1) v -= mean[c];
+      else if (mean_mode == 2) v -= mean[((long long)c * Hs + sh) * Ws + sw];
+      o[c] = f2bf(v * scale);
+    }
+  }
+}
+
+extern "C" int sn_augment(const uint8_t* src, bf16_t* dst, long long N, long long C, long long Hs, long long Ws,
+                          long long crop_h, long long crop_w, const float* mean, long long mean_mode, float scale,
+                          const long long* rng, long long train, long long mirror, int* offs_out, hipStream_t st) {
+  if (crop_h > Hs || crop_w > Ws) return 9;
+  long long total = N * crop_h * crop_w;
+  hipLaunchKernelGGL(augment_kernel, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, src, dst, (int)N, (int)C,
+                     (int)Hs, (int)Ws, (int)crop_h, (int)crop_w, mean, (int)mean_mode, scale, rng, (int)train,
+                     (int)mirror, offs_out);
+  return SN_CHECK_LAUNCH();
+}
+
+// labels: uint8/int32 -> float (JavaData label blob is [B, 1] float, ProtoLoader.scala:53)
+__global__ void labels_kernel(const int* __restrict__ src, float* __restrict__ dst, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (float)src[i];
+}
+
+extern "C" int sn_labels_to_float(const int* src, float* dst, long long n, hipStream_t st) {
+  hipLaunchKernelGGL(labels_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, dst, (int)n);
+  return SN_CHECK_LAUNCH();
+}

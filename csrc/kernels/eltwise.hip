@@ -1,0 +1,241 @@
+// Elementwise / data-movement kernels on bf16 tensors (16-B vectorised, grid-stride).
+//
+//  * ReLU fwd/bwd (caffe/src/caffe/layers/relu_layer.cu:9-41) — standalone form; the
+//    common conv/IP + in-place ReLU pair is fused into the GEMM epilogue instead.
+//  * Dropout fwd/bwd (dropout_layer.cu:10-45 + curandGenerate): the keep mask is
+//    Philox4x32-10(seed, counter | element, layer stream) regenerated in backward,
+//    so nothing is stored (reference: a uint32 per element).
+//  * fp32 -> bf16 cast of the flat parameter buffer (compute shadow refresh).
+//  * Philox counter advance (device side, so captured graphs get fresh masks per replay).
+//  * Sum of bf16 tensors (Split backward / gradient accumulation).
+//  * im2col (explicit, for convs whose per-group channel count is not a multiple of 8 —
+//    i.e. the 3-channel input layer), col2im (stride>1 dgrad), weight flip-transpose
+//    (turns dgrad into a forward implicit-GEMM conv).
+#include "common.h"
+
+// ---------------- ReLU ----------------
+__global__ void relu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8, float slope) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = f[k] > 0.f ? f[k] : f[k] * slope;
+    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+}
+
+__global__ void relu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, bf16_t* __restrict__ dx,
+                         long long n8, float slope) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    float g[8], v[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
+    unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = v[k] > 0.f ? g[k] : g[k] * slope;
+    reinterpret_cast<uint4*>(dx)[i] = pack8(g);
+  }
+}
+
+extern "C" int sn_relu_fwd(const bf16_t* x, bf16_t* y, long long n, float slope, hipStream_t st) {
+  if (n % 8) return 7;
+  hipLaunchKernelGGL(relu_fwd, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, x, y, n / 8, slope);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_relu_bwd(const bf16_t* dy, const bf16_t* x, bf16_t* dx, long long n, float slope, hipStream_t st) {
+  if (n % 8) return 7;
+  hipLaunchKernelGGL(relu_bwd, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, dy, x, dx, n / 8, slope);
+  return SN_CHECK_LAUNCH();
+}
+
+// ---------------- Dropout ----------------
+// keep(i) = philox(key=seed, ctr=(i_lo, i_hi | stream<<16, counter_lo, counter_hi)).x > thr
+__global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8,
+                               const long long* __restrict__ rng, int stream, uint32_t thr, float scale) {
+  const unsigned long long seed = (unsigned long long)rng[0];
+  const unsigned long long counter = (unsigned long long)rng[1];
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      unsigned long long e = (unsigned long long)(i * 8 + k);
+      uint4 ctr = make_uint4((uint32_t)e, (uint32_t)(e >> 32) | ((uint32_t)(stream & 0xffff) << 16),
+                             (uint32_t)counter, (uint32_t)(counter >> 32));
+      uint32_t u = philox4x32(key, ctr).x;
+      f[k] = (u > thr) ? f[k] * scale : 0.f;
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+}
+
+extern "C" int sn_dropout(const bf16_t* x, bf16_t* y, long long n, const long long* rng, long long stream,
+                          float ratio, hipStream_t st) {
+  if (n % 8) return 7;
+  uint32_t thr = (uint32_t)((double)4294967295u * (double)ratio);
+  float scale = 1.f / (1.f - ratio);
+  hipLaunchKernelGGL(dropout_kernel, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, x, y, n / 8, rng,
+                     (int)stream, thr, scale);
+  return SN_CHECK_LAUNCH();
+}
+
+__global__ void advance_rng_kernel(long long* rng) {
+  if (threadIdx.x == 0) rng[1] += 1;
+}
+
+extern "C" int sn_advance_rng(long long* rng, hipStream_t st) {
+  hipLaunchKernelGGL(advance_rng_kernel, dim3(1), dim3(64), 0, st, rng);
+  return SN_CHECK_LAUNCH();
+}
+
+// ---------------- casts / sums ----------------
+__global__ void cast_f32_bf16(const float* __restrict__ src, bf16_t* __restrict__ dst, long long n) {
+  long long n4 = n / 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 v = reinterpret_cast<const float4*>(src)[i];
+    reinterpret_cast<uint2*>(dst)[i] = make_uint2(pack2(v.x, v.y), pack2(v.z, v.w));
+  }
+  for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = f2bf(src[i]);
+}
+
+extern "C" int sn_cast_f32_bf16(const float* src, bf16_t* dst, long long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_f32_bf16, dim3(sn_blocks(n / 4 + 1, 256, 16384)), dim3(256), 0, st, src, dst, n);
+  return SN_CHECK_LAUNCH();
+}
+
+// out = sum_k in_k (k < 8), bf16
+struct Ptrs8 { const bf16_t* p[8]; };
+__global__ void sum_bf16(Ptrs8 in, int k, bf16_t* __restrict__ out, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      float f[8];
+      unpack8(reinterpret_cast<const uint4*>(in.p[j])[i], f);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] += f[t];
+    }
+    reinterpret_cast<uint4*>(out)[i] = pack8(acc);
+  }
+}
+
+extern "C" int sn_sum_bf16(const bf16_t* const* ptrs, long long k, bf16_t* out, long long n, hipStream_t st) {
+  if (n % 8 || k > 8 || k < 1) return 7;
+  Ptrs8 in;
+  for (int j = 0; j < 8; ++j) in.p[j] = j < k ? ptrs[j] : nullptr;
+  hipLaunchKernelGGL(sum_bf16, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, in, (int)k, out, n / 8);
+  return SN_CHECK_LAUNCH();
+}
+
+// ---------------- im2col / col2im / weight flip ----------------
+struct ConvG {
+  int N, H, W, C, P, Q, R, S, sh, sw, ph, pw, dh, dw, Cg, Kpad, coff;
+};
+
+// col[m][k] (row = pixel (n,p,q), k = (r, s, c) with c fastest, zero-padded to Kpad)
+__global__ void im2col_nhwc(const bf16_t* __restrict__ x, bf16_t* __restrict__ col, ConvG g) {
+  const int kc = g.Kpad / 8;
+  const long long total = (long long)g.N * g.P * g.Q * kc;
+  const int K = g.R * g.S * g.Cg;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int k0 = (int)(i % kc) * 8;
+    const long long m = i / kc;
+    const int q = (int)(m % g.Q), p = (int)((m / g.Q) % g.P), n = (int)(m / ((long long)g.Q * g.P));
+    float f[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      int k = k0 + t;
+      float v = 0.f;
+      if (k < K) {
+        int c = k % g.Cg, tap = k / g.Cg;
+        int s = tap % g.S, r = tap / g.S;
+        int h = p * g.sh - g.ph + r * g.dh, w = q * g.sw - g.pw + s * g.dw;
+        if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
+          v = bf2f(x[(((long long)n * g.H + h) * g.W + w) * g.C + g.coff + c]);
+      }
+      f[t] = v;
+    }
+    reinterpret_cast<uint4*>(col)[i] = pack8(f);
+  }
+}
+
+// dx[n,h,w,coff+c] = sum over (p,q,r,s) mapping to (h,w) of dcol[(n,p,q)][(r,s,c)]  (gather)
+__global__ void col2im_nhwc(const bf16_t* __restrict__ dcol, bf16_t* __restrict__ dx, ConvG g) {
+  const long long total = (long long)g.N * g.H * g.W * g.Cg;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.Cg);
+    const long long pix = i / g.Cg;
+    const int w = (int)(pix % g.W), h = (int)((pix / g.W) % g.H), n = (int)(pix / ((long long)g.W * g.H));
+    float acc = 0.f;
+    for (int r = 0; r < g.R; ++r) {
+      int hh = h + g.ph - r * g.dh;
+      if (hh < 0 || hh % g.sh) continue;
+      int p = hh / g.sh;
+      if (p >= g.P) continue;
+      for (int s = 0; s < g.S; ++s) {
+        int ww = w + g.pw - s * g.dw;
+        if (ww < 0 || ww % g.sw) continue;
+        int q = ww / g.sw;
+        if (q >= g.Q) continue;
+        acc += bf2f(dcol[(((long long)n * g.P + p) * g.Q + q) * g.Kpad + (r * g.S + s) * g.Cg + c]);
+      }
+    }
+    dx[pix * g.C + g.coff + c] = f2bf(acc);
+  }
+}
+
+static ConvG mkconv(long long N, long long H, long long W, long long C, long long P, long long Q, long long R,
+                    long long S, long long sh, long long sw, long long ph, long long pw, long long dh, long long dw,
+                    long long Cg, long long Kpad, long long coff) {
+  ConvG g;
+  g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C; g.P = (int)P; g.Q = (int)Q; g.R = (int)R; g.S = (int)S;
+  g.sh = (int)sh; g.sw = (int)sw; g.ph = (int)ph; g.pw = (int)pw; g.dh = (int)dh; g.dw = (int)dw;
+  g.Cg = (int)Cg; g.Kpad = (int)Kpad; g.coff = (int)coff;
+  return g;
+}
+
+extern "C" int sn_im2col(const bf16_t* x, bf16_t* col, long long N, long long H, long long W, long long C, long long P,
+                         long long Q, long long R, long long S, long long sh, long long sw, long long ph, long long pw,
+                         long long dh, long long dw, long long Cg, long long Kpad, long long coff, hipStream_t st) {
+  if (Kpad % 8) return 7;
+  ConvG g = mkconv(N, H, W, C, P, Q, R, S, sh, sw, ph, pw, dh, dw, Cg, Kpad, coff);
+  long long total = N * P * Q * (Kpad / 8);
+  hipLaunchKernelGGL(im2col_nhwc, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, x, col, g);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_col2im(const bf16_t* dcol, bf16_t* dx, long long N, long long H, long long W, long long C,
+                         long long P, long long Q, long long R, long long S, long long sh, long long sw, long long ph,
+                         long long pw, long long dh, long long dw, long long Cg, long long Kpad, long long coff,
+                         hipStream_t st) {
+  ConvG g = mkconv(N, H, W, C, P, Q, R, S, sh, sw, ph, pw, dh, dw, Cg, Kpad, coff);
+  long long total = N * H * W * Cg;
+  hipLaunchKernelGGL(col2im_nhwc, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, dcol, dx, g);
+  return SN_CHECK_LAUNCH();
+}
+
+// w [G][Kg][R][S][Cg]  ->  wt [G][Cg][R][S][Kg] with (r, s) flipped: the dgrad of a
+// stride-1 conv is a forward conv of dy with these weights and pad' = R-1-pad.
+__global__ void flip_weights(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt, int G, int Kg, int R, int S,
+                             int Cg) {
+  const long long total = (long long)G * Kg * R * S * Cg;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % Cg);
+    long long t = i / Cg;
+    int s = (int)(t % S); t /= S;
+    int r = (int)(t % R); t /= R;
+    int k = (int)(t % Kg);
+    int g = (int)(t / Kg);
+    long long o = ((((long long)g * Cg + c) * R + (R - 1 - r)) * S + (S - 1 - s)) * Kg + k;
+    wt[o] = w[i];
+  }
+}
+
+extern "C" int sn_flip_weights(const bf16_t* w, bf16_t* wt, long long G, long long Kg, long long R, long long S,
+                               long long Cg, hipStream_t st) {
+  long long total = G * Kg * R * S * Cg;
+  hipLaunchKernelGGL(flip_weights, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, w, wt, (int)G, (int)Kg,
+                     (int)R, (int)S, (int)Cg);
+  return SN_CHECK_LAUNCH();
+}

@@ -1,0 +1,204 @@
+// Max / average pooling on NHWC bf16 tensors (Caffe ceil-mode geometry).
+//
+// Reference: MaxPoolForward / AvePoolForward / MaxPoolBackward / AvePoolBackward
+// (caffe/src/caffe/layers/pooling_layer.cu:11-80, 217-296): one thread per NCHW output
+// element with a float/int mask.  Here one thread owns 8 consecutive channels of one
+// output pixel (16-B loads/stores), the argmax mask is a uint8 window offset (4x less
+// traffic than Caffe's int mask) and the backward pass is a gather (no atomics).
+#include "common.h"
+
+struct PoolGeom {
+  int N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw;
+};
+
+template <bool VEC>
+__global__ void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                            PoolGeom g) {
+  const int cv = VEC ? g.C / 8 : g.C;
+  const long long total = (long long)g.N * g.P * g.Q * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * (VEC ? 8 : 1);
+    long long pix = i / cv;
+    const int q = (int)(pix % g.Q);
+    const int p = (int)((pix / g.Q) % g.P);
+    const int n = (int)(pix / ((long long)g.Q * g.P));
+    const int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
+    const int he = min(hs + g.kh, g.H), we = min(ws + g.kw, g.W);
+    const int h0 = max(hs, 0), w0 = max(ws, 0);
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+    for (int h = h0; h < he; ++h)
+      for (int w = w0; w < we; ++w) {
+        const bf16_t* src = x + (((long long)n * g.H + h) * g.W + w) * g.C + c0;
+        const int widx = (h - hs) * g.kw + (w - ws);
+        if (VEC) {
+          float f[8];
+          unpack8(*reinterpret_cast<const uint4*>(src), f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (f[k] > best[k]) { best[k] = f[k]; arg[k] = widx; }
+        } else {
+          float f = bf2f(src[0]);
+          if (f > best[0]) { best[0] = f; arg[0] = widx; }
+        }
+      }
+    const long long o = pix * g.C + c0;
+    if (VEC) {
+      *reinterpret_cast<uint4*>(y + o) = pack8(best);
+      if (mask) {
+        uint2 m;
+        m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+        m.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+        *reinterpret_cast<uint2*>(mask + o) = m;
+      }
+    } else {
+      y[o] = f2bf(best[0]);
+      if (mask) mask[o] = (uint8_t)arg[0];
+    }
+  }
+}
+
+template <bool VEC>
+__global__ void avepool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g) {
+  const int cv = VEC ? g.C / 8 : g.C;
+  const long long total = (long long)g.N * g.P * g.Q * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * (VEC ? 8 : 1);
+    long long pix = i / cv;
+    const int q = (int)(pix % g.Q);
+    const int p = (int)((pix / g.Q) % g.P);
+    const int n = (int)(pix / ((long long)g.Q * g.P));
+    int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
+    int he = min(hs + g.kh, g.H + g.ph), we = min(ws + g.kw, g.W + g.pw);
+    const float inv = 1.f / (float)((he - hs) * (we - ws));
+    hs = max(hs, 0); ws = max(ws, 0); he = min(he, g.H); we = min(we, g.W);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int h = hs; h < he; ++h)
+      for (int w = ws; w < we; ++w) {
+        const bf16_t* src = x + (((long long)n * g.H + h) * g.W + w) * g.C + c0;
+        if (VEC) {
+          float f[8];
+          unpack8(*reinterpret_cast<const uint4*>(src), f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += f[k];
+        } else {
+          acc[0] += bf2f(src[0]);
+        }
+      }
+    const long long o = pix * g.C + c0;
+    if (VEC) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] *= inv;
+      *reinterpret_cast<uint4*>(y + o) = pack8(acc);
+    } else {
+      y[o] = f2bf(acc[0] * inv);
+    }
+  }
+}
+
+// Backward: one thread per 8 channels of one INPUT pixel; gathers every output window
+// that contains the pixel.
+template <bool VEC, bool MAX>
+__global__ void pool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
+                         PoolGeom g) {
+  const int cv = VEC ? g.C / 8 : g.C;
+  const long long total = (long long)g.N * g.H * g.W * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * (VEC ? 8 : 1);
+    long long pix = i / cv;
+    const int w = (int)(pix % g.W);
+    const int h = (int)((pix / g.W) % g.H);
+    const int n = (int)(pix / ((long long)g.W * g.H));
+    const int hp = h + g.ph, wp = w + g.pw;
+    const int p0 = hp < g.kh ? 0 : (hp - g.kh) / g.sh + 1;
+    const int p1 = min(hp / g.sh + 1, g.P);
+    const int q0 = wp < g.kw ? 0 : (wp - g.kw) / g.sw + 1;
+    const int q1 = min(wp / g.sw + 1, g.Q);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int p = p0; p < p1; ++p)
+      for (int q = q0; q < q1; ++q) {
+        const long long o = (((long long)n * g.P + p) * g.Q + q) * g.C + c0;
+        const int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
+        float scale = 1.f;
+        if (!MAX) {
+          int he = min(hs + g.kh, g.H + g.ph), we = min(ws + g.kw, g.W + g.pw);
+          scale = 1.f / (float)((he - hs) * (we - ws));
+        }
+        const int widx = (h - hs) * g.kw + (w - ws);
+        if (VEC) {
+          float f[8];
+          unpack8(*reinterpret_cast<const uint4*>(dy + o), f);
+          if (MAX) {
+            uint2 m = *reinterpret_cast<const uint2*>(mask + o);
+            const uint32_t mw[2] = {m.x, m.y};
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if ((int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == widx) acc[k] += f[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += f[k] * scale;
+          }
+        } else {
+          float f = bf2f(dy[o]);
+          if (MAX) {
+            if ((int)mask[o] == widx) acc[0] += f;
+          } else {
+            acc[0] += f * scale;
+          }
+        }
+      }
+    const long long o = pix * g.C + c0;
+    if (VEC)
+      *reinterpret_cast<uint4*>(dx + o) = pack8(acc);
+    else
+      dx[o] = f2bf(acc[0]);
+  }
+}
+
+static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long long P, long long Q, long long kh,
+                       long long kw, long long sh, long long sw, long long ph, long long pw) {
+  PoolGeom g;
+  g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C; g.P = (int)P; g.Q = (int)Q;
+  g.kh = (int)kh; g.kw = (int)kw; g.sh = (int)sh; g.sw = (int)sw; g.ph = (int)ph; g.pw = (int)pw;
+  return g;
+}
+
+extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long N, long long H, long long W,
+                           long long C, long long P, long long Q, long long kh, long long kw, long long sh,
+                           long long sw, long long ph, long long pw, long long method, hipStream_t st) {
+  PoolGeom g = mkgeom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  if (method == 0 && kh * kw > 255) return 6;
+  const bool vec = (C % 8) == 0;
+  long long total = N * P * Q * (vec ? C / 8 : C);
+  dim3 grid(sn_blocks(total, 256, 16384));
+  if (method == 0) {
+    if (vec) hipLaunchKernelGGL(maxpool_fwd<true>, grid, dim3(256), 0, st, x, y, mask, g);
+    else hipLaunchKernelGGL(maxpool_fwd<false>, grid, dim3(256), 0, st, x, y, mask, g);
+  } else {
+    if (vec) hipLaunchKernelGGL(avepool_fwd<true>, grid, dim3(256), 0, st, x, y, g);
+    else hipLaunchKernelGGL(avepool_fwd<false>, grid, dim3(256), 0, st, x, y, g);
+  }
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, long long N, long long H, long long W,
+                           long long C, long long P, long long Q, long long kh, long long kw, long long sh,
+                           long long sw, long long ph, long long pw, long long method, hipStream_t st) {
+  PoolGeom g = mkgeom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const bool vec = (C % 8) == 0;
+  long long total = N * H * W * (vec ? C / 8 : C);
+  dim3 grid(sn_blocks(total, 256, 16384));
+  if (method == 0) {
+    if (vec) hipLaunchKernelGGL((pool_bwd<true, true>), grid, dim3(256), 0, st, dy, mask, dx, g);
+    else hipLaunchKernelGGL((pool_bwd<false, true>), grid, dim3(256), 0, st, dy, mask, dx, g);
+  } else {
+    if (vec) hipLaunchKernelGGL((pool_bwd<true, false>), grid, dim3(256), 0, st, dy, mask, dx, g);
+    else hipLaunchKernelGGL((pool_bwd<false, false>), grid, dim3(256), 0, st, dy, mask, dx, g);
+  }
+  return SN_CHECK_LAUNCH();
+}

@@ -1,0 +1,349 @@
+"""Solvers: SGD (+ Nesterov, AdaGrad, RMSProp, AdaDelta, Adam) with Caffe semantics.
+
+References: ``Solver`` (caffe/src/caffe/solver.cpp — Init :44-190, Step :193-282,
+Test :338-411, TestAndStoreResult :413-444 (SparkNet-added), Snapshot :447-499,
+Restore :510-519), ``SGDSolver`` (caffe/src/caffe/solvers/sgd_solver.cpp — GetLearningRate
+:27-63, ClipGradients :81-99, ApplyUpdate :102-116, Normalize :119-142, Regularize
+:145-204, ComputeUpdateValue :207-239, snapshot/restore :242-343) and the other solvers
+in caffe/src/caffe/solvers/*.cpp.  The reference SparkNet shim always constructed an
+SGDSolver (libccaffe/ccaffe.cpp:131); here the ``type`` field is honoured.
+
+MI355X-first: the whole update — global-norm clip, 1/iter_size, L1/L2 decay with
+per-param decay_mult, per-param lr_mult, momentum / adaptive history, the master write
+and the bf16 shadow write — is ONE fused HIP kernel over the flat parameter buffer
+(``csrc/kernels/solver.hip``).  Hyper-parameters live in a small device tensor so the
+update can be replayed inside a captured hipGraph.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import time
+from typing import Callable
+
+import torch
+
+from .. import proto
+from .net import Net, blob_proto_to_tensor
+
+log = logging.getLogger("sparknet_amd.solver")
+
+SOLVER_KINDS = {"SGD": 0, "Nesterov": 1, "AdaGrad": 2, "RMSProp": 3, "AdaDelta": 4, "Adam": 5}
+_LEGACY_TYPES = {0: "SGD", 1: "Nesterov", 2: "AdaGrad", 3: "RMSProp", 4: "AdaDelta", 5: "Adam"}
+N_HISTORY = {"SGD": 1, "Nesterov": 1, "AdaGrad": 1, "RMSProp": 1, "AdaDelta": 2, "Adam": 2}
+
+# hyper tensor layout (device, fp32)
+H_LR, H_MOM, H_WD, H_CLIP, H_NORM, H_DELTA, H_MOM2, H_RMS, H_CORR, H_T = range(10)
+N_HYPER = 16
+
+
+class Solver:
+    def __init__(self, param, *, device="cpu", dtype=None, seed: int | None = None,
+                 train_net: Net | None = None, build_test_nets: bool = True):
+        if isinstance(param, str):
+            param = proto.read_solver(param)
+        self.param = proto.copy(param)
+        p = self.param
+        self.type = p.type if p.HasField("type") else (
+            _LEGACY_TYPES[int(p.solver_type)] if p.HasField("solver_type") else "SGD")
+        if self.type not in SOLVER_KINDS:
+            raise ValueError(f"Unknown solver type {self.type!r}")
+        self.device = torch.device(device)
+        if seed is None:
+            seed = int(p.random_seed) if p.random_seed >= 0 else 1701
+        self.seed = seed
+        self.iter = 0
+        self.current_step = 0
+        self.callbacks: list = []
+        self.action_request: Callable[[], str] | None = None
+        self.losses: list[torch.Tensor] = []
+        self.smoothed_loss = 0.0
+        self.net = train_net if train_net is not None else self._init_train_net(dtype)
+        self.test_nets: list[Net] = []
+        if build_test_nets:
+            self._init_test_nets(dtype)
+        self.history: list[torch.Tensor] = []
+        self._init_state()
+
+    # -- construction (Solver::InitTrainNet / InitTestNets) ------------------------------
+    def _net_param_source(self):
+        p = self.param
+        n = int(p.HasField("train_net_param")) + int(p.HasField("train_net")) + \
+            int(p.HasField("net_param")) + int(p.HasField("net"))
+        if n != 1:
+            raise ValueError("SolverParameter must specify exactly one of train_net_param, train_net, "
+                             "net_param, net")
+        if p.HasField("train_net_param"):
+            return proto.copy(p.train_net_param)
+        if p.HasField("train_net"):
+            return proto.read_net(p.train_net)
+        if p.HasField("net_param"):
+            return proto.copy(p.net_param)
+        return proto.read_net(p.net)
+
+    def _init_train_net(self, dtype) -> Net:
+        netp = self._net_param_source()
+        state = proto.NetState(phase=proto.TRAIN)
+        state.MergeFrom(netp.state)
+        state.MergeFrom(self.param.train_state)
+        netp.state.CopyFrom(state)
+        return Net(netp, device=self.device, dtype=dtype, seed=self.seed)
+
+    def _init_test_nets(self, dtype) -> None:
+        p = self.param
+        sources = []
+        for tp in p.test_net_param:
+            sources.append(proto.copy(tp))
+        for tf in p.test_net:
+            sources.append(proto.read_net(tf))
+        remaining = len(p.test_iter) - len(sources)
+        if remaining > 0:
+            if p.HasField("net_param"):
+                sources += [proto.copy(p.net_param)] * remaining
+            elif p.HasField("net"):
+                base = proto.read_net(p.net)
+                sources += [base] * remaining
+        if len(p.test_state) and len(p.test_state) != len(sources):
+            raise ValueError("test_state must be unspecified or specified once per test net")
+        for i, netp in enumerate(sources):
+            netp = proto.copy(netp)
+            state = proto.NetState(phase=proto.TEST)
+            state.MergeFrom(netp.state)
+            if len(p.test_state):
+                state.MergeFrom(p.test_state[i])
+            netp.state.CopyFrom(state)
+            tn = Net(netp, device=self.device, dtype=self.net.dtype, seed=self.seed, allocate=True)
+            tn.share_trained_layers_with(self.net)
+            self.test_nets.append(tn)
+
+    def _init_state(self) -> None:
+        n = self.net.num_param_elems
+        self.history = [torch.zeros(max(n, 1), dtype=torch.float32, device=self.device)
+                        for _ in range(N_HISTORY[self.type])]
+        self.hyper = torch.zeros(N_HYPER, dtype=torch.float32, device=self.device)
+        self._hyper_host = torch.zeros(N_HYPER, dtype=torch.float32,
+                                       pin_memory=self.device.type == "cuda")
+        self._build_tables()
+
+    def _build_tables(self) -> None:
+        """Chunk table for the fused update kernel: (start, count, lr_mult, decay_mult)."""
+        from .. import ops
+        segs = self.net.param_segments()
+        self.segments = segs
+        self._tables = ops.solver_tables(segs, self.net.num_param_elems, self.device)
+
+    # -- learning rate (SGDSolver::GetLearningRate) ------------------------------------
+    def get_learning_rate(self) -> float:
+        p = self.param
+        pol = p.lr_policy
+        it = self.iter
+        if pol == "fixed":
+            return p.base_lr
+        if pol == "step":
+            self.current_step = it // p.stepsize
+            return p.base_lr * math.pow(p.gamma, self.current_step)
+        if pol == "exp":
+            return p.base_lr * math.pow(p.gamma, it)
+        if pol == "inv":
+            return p.base_lr * math.pow(1.0 + p.gamma * it, -p.power)
+        if pol == "multistep":
+            if self.current_step < len(p.stepvalue) and it >= p.stepvalue[self.current_step]:
+                self.current_step += 1
+            return p.base_lr * math.pow(p.gamma, self.current_step)
+        if pol == "poly":
+            return p.base_lr * math.pow(1.0 - float(it) / float(p.max_iter), p.power)
+        if pol == "sigmoid":
+            return p.base_lr * (1.0 / (1.0 + math.exp(-p.gamma * (float(it) - float(p.stepsize)))))
+        raise ValueError(f"Unknown learning rate policy: {pol!r}")
+
+    def hyper_values(self, rate: float) -> list[float]:
+        p = self.param
+        h = [0.0] * N_HYPER
+        h[H_LR] = rate
+        h[H_MOM] = p.momentum
+        h[H_WD] = p.weight_decay
+        h[H_CLIP] = p.clip_gradients
+        h[H_NORM] = 1.0 / max(1, p.iter_size)
+        h[H_DELTA] = p.delta
+        h[H_MOM2] = p.momentum2
+        h[H_RMS] = p.rms_decay
+        t = self.iter + 1
+        if self.type == "Adam":
+            h[H_CORR] = math.sqrt(1.0 - math.pow(p.momentum2, t)) / (1.0 - math.pow(p.momentum, t))
+        h[H_T] = float(t)
+        return h
+
+    def stage_hyper(self, rate: float | None = None) -> float:
+        """Write this iteration's hyper-parameters into the device tensor (async H2D)."""
+        rate = self.get_learning_rate() if rate is None else rate
+        self._hyper_host.copy_(torch.tensor(self.hyper_values(rate)))
+        self.hyper.copy_(self._hyper_host, non_blocking=True)
+        return rate
+
+    # -- update (ApplyUpdate) -------------------------------------------------------------
+    def apply_update(self) -> float:
+        rate = self.stage_hyper()
+        if self.param.display and self.iter % self.param.display == 0:
+            log.info("Iteration %d, lr = %g", self.iter, rate)
+        self.update_params()
+        return rate
+
+    def update_params(self) -> None:
+        from .. import ops
+        l1 = self.param.regularization_type == "L1"
+        if self.param.regularization_type not in ("L1", "L2"):
+            raise ValueError(f"Unknown regularization type: {self.param.regularization_type}")
+        net = self.net
+        ops.solver_update(SOLVER_KINDS[self.type], net.flat_data, net.flat_diff, self.history,
+                          net.flat_compute if net.flat_compute is not net.flat_data else None,
+                          self._tables, self.hyper, l1, self.param.clip_gradients > 0)
+
+    # -- main loop (Solver::Step) -----------------------------------------------------------
+    def iteration(self):
+        """One training iteration minus bookkeeping: returns the device loss."""
+        net = self.net
+        net.clear_param_diffs()
+        for cb in self.callbacks:
+            getattr(cb, "on_start", lambda: None)()
+        loss = None
+        for _ in range(max(1, self.param.iter_size)):
+            l = net.forward_backward()
+            loss = l if loss is None else loss + l
+            from .. import ops
+            ops.advance_rng(net.ctx.rng_state)
+        if self.param.iter_size > 1:
+            loss = loss / self.param.iter_size
+        for cb in self.callbacks:
+            getattr(cb, "on_gradients_ready", lambda: None)()
+        self.apply_update()
+        return loss
+
+    def step(self, iters: int) -> None:
+        start_iter = self.iter
+        stop_iter = self.iter + iters
+        avg = max(1, self.param.average_loss)
+        while self.iter < stop_iter:
+            loss = self.iteration()
+            self.losses.append(loss.detach())
+            if len(self.losses) > avg:
+                self.losses.pop(0)
+            display = self.param.display and self.iter % self.param.display == 0
+            self.iter += 1
+            if display:
+                self.smoothed_loss = float(torch.stack(self.losses).mean())
+                log.info("Iteration %d, loss = %g", self.iter - 1, self.smoothed_loss)
+            if self.param.snapshot and self.iter % self.param.snapshot == 0:
+                self.snapshot()
+            req = self.action_request() if self.action_request else "none"
+            if req == "snapshot":
+                self.snapshot()
+            elif req == "stop":
+                break
+        del start_iter
+
+    def solve(self, resume_file: str | None = None) -> None:
+        """Solver::Solve: run to max_iter with periodic testing."""
+        if resume_file:
+            self.restore(resume_file)
+        p = self.param
+        while self.iter < p.max_iter:
+            if p.test_interval and self.iter % p.test_interval == 0 and (self.iter > 0 or p.test_initialization):
+                self.test_all()
+            n = p.max_iter - self.iter
+            if p.test_interval:
+                n = min(n, p.test_interval - self.iter % p.test_interval)
+            self.step(n)
+        if p.snapshot_after_train and (not p.snapshot or self.iter % p.snapshot != 0):
+            self.snapshot()
+        if p.display and self.iter % p.display == 0:
+            self.test_all()
+
+    # -- testing ------------------------------------------------------------------------------
+    def test(self, test_net_id: int = 0, iters: int | None = None) -> list[float]:
+        """Solver::Test — mean of every output blob over ``test_iter`` batches."""
+        scores = self.test_and_store_result(test_net_id, iters)
+        n = iters if iters is not None else self.param.test_iter[test_net_id]
+        res = [s / max(n, 1) for s in scores]
+        tn = self.test_nets[test_net_id]
+        names = [b.name for b in tn.output_blobs]
+        for name, v in zip(names, res):
+            log.info("    Test net output #%s: %s = %g", test_net_id, name, v)
+        return res
+
+    def test_and_store_result(self, test_net_id: int = 0, iters: int | None = None) -> list[float]:
+        """SparkNet's Solver::TestAndStoreResult (solver.cpp:413-444): per-output SUM over
+        ``iters`` forward passes of the test net (weights shared with the train net)."""
+        tn = self.test_nets[test_net_id]
+        n = iters if iters is not None else self.param.test_iter[test_net_id]
+        acc = None
+        for _ in range(n):
+            tn.forward()
+            vals = torch.stack([b.data.float().sum() for b in tn.output_blobs])
+            acc = vals if acc is None else acc + vals
+        return [] if acc is None else acc.cpu().tolist()
+
+    def test_all(self) -> list[list[float]]:
+        return [self.test(i) for i in range(len(self.test_nets))]
+
+    # -- snapshot / restore -----------------------------------------------------------------
+    def _prefix(self) -> str:
+        return self.param.snapshot_prefix or "snapshot"
+
+    def snapshot(self, prefix: str | None = None) -> tuple[str, str]:
+        prefix = prefix or self._prefix()
+        model = f"{prefix}_iter_{self.iter}.caffemodel"
+        state = f"{prefix}_iter_{self.iter}.solverstate"
+        d = os.path.dirname(model)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        from ..utils.checkpoint import save_caffemodel
+        save_caffemodel(self.net, model, write_diff=self.param.snapshot_diff)
+        proto.write_binary(state, self.solver_state(model))
+        log.info("Snapshotting to %s / %s", model, state)
+        return model, state
+
+    def solver_state(self, learned_net: str = ""):
+        st = proto.SolverState(iter=self.iter, learned_net=learned_net, current_step=self.current_step)
+        for h in self.history:
+            for prm in self.net.learnable_params:
+                seg = h[prm.offset:prm.offset + prm.count].view(prm.shape)
+                bp = st.history.add()
+                bp.shape.dim.extend(prm.caffe_shape)
+                bp.data.extend(prm.to_caffe(seg).cpu().reshape(-1).tolist())
+        return st
+
+    def restore(self, state_file: str) -> None:
+        st = proto.read_binary(state_file, proto.SolverState)
+        self.iter = st.iter
+        self.current_step = st.current_step
+        if st.learned_net:
+            self.net.copy_trained_layers_from(st.learned_net)
+        params = self.net.learnable_params
+        if len(st.history) != len(params) * len(self.history):
+            raise ValueError("Incorrect length of history blobs.")
+        k = 0
+        for h in self.history:
+            for prm in params:
+                t = blob_proto_to_tensor(st.history[k])
+                h[prm.offset:prm.offset + prm.count].view(prm.shape).copy_(
+                    prm.from_caffe(t).to(h.device))
+                k += 1
+        log.info("Restored solver state from %s (iter %d)", state_file, self.iter)
+
+    # -- SparkNet-facing helpers --------------------------------------------------------------
+    def add_callback(self, cb) -> None:
+        self.callbacks.append(cb)
+
+
+def create_solver(param, **kw) -> Solver:
+    """SolverRegistry::CreateSolver (solver_factory.hpp): one class, kind from ``type``."""
+    return Solver(param, **kw)
+
+
+def timed(fn):
+    def wrap(*a, **k):
+        t = time.perf_counter()
+        r = fn(*a, **k)
+        return r, time.perf_counter() - t
+    return wrap

@@ -1,0 +1,230 @@
+"""Neuron (elementwise) layers: ReLU, Dropout, Sigmoid, TanH, AbsVal, BNLL, Exp, Log,
+Power, Threshold, PReLU.
+
+References: caffe/src/caffe/layers/{relu,dropout,sigmoid,tanh,absval,bnll,exp,log,power,
+threshold,prelu}_layer.{cpp,cu}.  ReLU and Dropout are on the hot path and run HIP
+kernels (ReLU forward is usually fused into the producing conv/IP epilogue by the net);
+Dropout regenerates its Philox mask in backward instead of storing it.  The remaining
+neurons are expressed as tensor math (used by the sigmoid cifar variants and tests).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from ..core.layer import Layer, register
+
+
+class NeuronLayer(Layer):
+    exact_bottoms = 1
+    exact_tops = 1
+
+    def reshape(self, bottoms, tops):
+        tops[0].reshape(bottoms[0].shape, self.dtype)
+
+
+@register("ReLU")
+class ReLULayer(NeuronLayer):
+    fused = False  # forward folded into the producer's GEMM epilogue
+
+    def layer_setup(self, bottoms, tops):
+        self.slope = float(self.lp.relu_param.negative_slope)
+
+    def forward(self, bottoms, tops):
+        if self.fused:
+            return
+        tops[0].data = ops.relu_forward(bottoms[0].data, self.slope)
+
+    def backward(self, tops, propagate_down, bottoms):
+        if propagate_down[0]:
+            # in-place: bottom data was overwritten by top data; sign(y) == sign(x) for slope >= 0
+            ref = bottoms[0].data
+            bottoms[0].diff = ops.relu_backward(tops[0].diff, ref, self.slope)
+
+
+@register("Dropout")
+class DropoutLayer(NeuronLayer):
+    def layer_setup(self, bottoms, tops):
+        self.ratio = float(self.lp.dropout_param.dropout_ratio)
+        if not 0.0 <= self.ratio < 1.0:
+            raise ValueError("dropout_ratio must be in [0, 1)")
+        self.stream = self.ctx.next_stream_id()
+
+    def forward(self, bottoms, tops):
+        if self.phase == 0 and self.ratio > 0:  # TRAIN
+            tops[0].data = ops.dropout_forward(bottoms[0].data, self.ratio, self.ctx.rng_state, self.stream)
+        elif tops[0] is not bottoms[0]:
+            tops[0].data = bottoms[0].data
+
+    def backward(self, tops, propagate_down, bottoms):
+        if not propagate_down[0]:
+            return
+        if self.phase == 0 and self.ratio > 0:
+            bottoms[0].diff = ops.dropout_backward(tops[0].diff, self.ratio, self.ctx.rng_state, self.stream)
+        elif tops[0] is not bottoms[0]:
+            bottoms[0].diff = tops[0].diff
+
+
+class _Elementwise(NeuronLayer):
+    """y = f(x), dx = dy * f'(x, y), computed in fp32 and stored in the compute dtype."""
+
+    def f(self, x):
+        raise NotImplementedError
+
+    def df(self, x, y):
+        raise NotImplementedError
+
+    def forward(self, bottoms, tops):
+        x = bottoms[0].data
+        self._x = x.float() if tops[0] is bottoms[0] else None
+        tops[0].data = self.f(x.float()).to(x.dtype)
+
+    def backward(self, tops, propagate_down, bottoms):
+        if not propagate_down[0]:
+            return
+        x = self._x if self._x is not None else bottoms[0].data.float()
+        y = tops[0].data.float()
+        bottoms[0].diff = (tops[0].diff.float() * self.df(x, y)).to(tops[0].diff.dtype)
+
+
+@register("Sigmoid")
+class SigmoidLayer(_Elementwise):
+    def f(self, x):
+        return torch.sigmoid(x)
+
+    def df(self, x, y):
+        return y * (1 - y)
+
+
+@register("TanH")
+class TanHLayer(_Elementwise):
+    def f(self, x):
+        return torch.tanh(x)
+
+    def df(self, x, y):
+        return 1 - y * y
+
+
+@register("AbsVal")
+class AbsValLayer(_Elementwise):
+    def f(self, x):
+        return x.abs()
+
+    def df(self, x, y):
+        return torch.sign(x)
+
+
+@register("BNLL")
+class BNLLLayer(_Elementwise):
+    def f(self, x):
+        return torch.where(x > 0, x + torch.log1p(torch.exp(-x)), torch.log1p(torch.exp(x)))
+
+    def df(self, x, y):
+        e = torch.exp(torch.clamp(x, max=50.0))
+        return e / (e + 1)
+
+
+@register("Exp")
+class ExpLayer(_Elementwise):
+    def layer_setup(self, bottoms, tops):
+        p = self.lp.exp_param
+        base, self.scale, self.shift = float(p.base), float(p.scale), float(p.shift)
+        self.log_base = 1.0 if base == -1 else math.log(base)
+        if base != -1 and base <= 0:
+            raise ValueError("base must be strictly positive")
+
+    def f(self, x):
+        return torch.exp((self.shift + self.scale * x) * self.log_base)
+
+    def df(self, x, y):
+        return y * self.log_base * self.scale
+
+
+@register("Log")
+class LogLayer(_Elementwise):
+    def layer_setup(self, bottoms, tops):
+        p = self.lp.log_param
+        base, self.scale, self.shift = float(p.base), float(p.scale), float(p.shift)
+        self.inv_log_base = 1.0 if base == -1 else 1.0 / math.log(base)
+
+    def f(self, x):
+        return torch.log(self.shift + self.scale * x) * self.inv_log_base
+
+    def df(self, x, y):
+        return self.scale * self.inv_log_base / (self.shift + self.scale * x)
+
+
+@register("Power")
+class PowerLayer(_Elementwise):
+    def layer_setup(self, bottoms, tops):
+        p = self.lp.power_param
+        self.power, self.scale, self.shift = float(p.power), float(p.scale), float(p.shift)
+
+    def f(self, x):
+        return torch.pow(self.shift + self.scale * x, self.power)
+
+    def df(self, x, y):
+        if self.power == 0 or self.scale == 0:
+            return torch.zeros_like(x)
+        return self.power * self.scale * torch.pow(self.shift + self.scale * x, self.power - 1)
+
+
+@register("Threshold")
+class ThresholdLayer(NeuronLayer):
+    def layer_setup(self, bottoms, tops):
+        self.t = float(self.lp.threshold_param.threshold)
+
+    def forward(self, bottoms, tops):
+        tops[0].data = (bottoms[0].data.float() > self.t).to(self.dtype)
+
+    def backward(self, tops, propagate_down, bottoms):
+        if propagate_down[0]:
+            raise NotImplementedError("Threshold layer has no backward")
+
+
+@register("PReLU")
+class PReLULayer(NeuronLayer):
+    def layer_setup(self, bottoms, tops):
+        p = self.lp.prelu_param
+        C = bottoms[0].shape[1] if len(bottoms[0].shape) > 1 else 1
+        self.shared = p.channel_shared
+        filler = p.filler if p.HasField("filler") else None
+        if filler is None:
+            from .. import proto
+            filler = proto.FillerParameter(type="constant", value=0.25)
+        self.slope = self.add_param((1,) if self.shared else (C,), filler=filler)
+
+    def _a(self, x):
+        a = self.slope.data.float()
+        return a.reshape(-1) if (self.shared or x.dim() != 4) else a  # NHWC: channel is last
+
+    def _bcast(self, a, x):
+        if self.shared:
+            return a.reshape([1] * x.dim())
+        if x.dim() == 4:
+            return a.reshape(1, 1, 1, -1)
+        return a.reshape([1, -1] + [1] * (x.dim() - 2))
+
+    def forward(self, bottoms, tops):
+        x = bottoms[0].data.float()
+        self._x = x
+        a = self._bcast(self.slope.data.float(), x)
+        tops[0].data = torch.where(x > 0, x, x * a).to(self.dtype)
+
+    def backward(self, tops, propagate_down, bottoms):
+        x = self._x
+        dy = tops[0].diff.float()
+        a = self._bcast(self.slope.data.float(), x)
+        if self.param_grads_needed(0):
+            g = dy * x * (x <= 0)
+            if self.shared:
+                self.slope.diff += g.sum().reshape(1)
+            elif x.dim() == 4:
+                self.slope.diff += g.sum(dim=(0, 1, 2))
+            else:
+                dims = [d for d in range(x.dim()) if d != 1]
+                self.slope.diff += g.sum(dim=dims)
+        if propagate_down[0]:
+            bottoms[0].diff = (dy * torch.where(x > 0, torch.ones_like(x), a)).to(self.dtype)

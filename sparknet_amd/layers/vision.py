@@ -1,0 +1,360 @@
+"""Vision layers: Convolution, Deconvolution, Pooling, LRN, InnerProduct, Im2col.
+
+References: caffe/src/caffe/layers/{base_conv,conv,deconv,pooling,lrn,inner_product,
+im2col}_layer.{cpp,cu}.  The reference runs one im2col + SGEMM per image
+(conv_layer.cu:14-21); here each pass is ONE implicit-GEMM MFMA launch over the whole
+NHWC batch (``ops.hip``), with the bias and (when the net fuses an in-place ReLU) the
+activation applied in the GEMM epilogue.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..core.layer import Layer, register
+from ..ops.spec import POOL_AVE, POOL_MAX, POOL_STOCHASTIC, ConvSpec, PoolSpec
+
+
+def _conv_hw(cp, name, rep_name, h_name, w_name, default):
+    """kernel/stride/pad: repeated field or the _h/_w pair (base_conv_layer.cpp:30-110)."""
+    if cp.HasField(h_name) or cp.HasField(w_name):
+        return int(getattr(cp, h_name)), int(getattr(cp, w_name))
+    rep = list(getattr(cp, rep_name))
+    if len(rep) == 0:
+        return default, default
+    if len(rep) == 1:
+        return int(rep[0]), int(rep[0])
+    return int(rep[0]), int(rep[1])
+
+
+def conv_geometry(cp):
+    if cp.HasField("kernel_h") or cp.HasField("kernel_w"):
+        kh, kw = cp.kernel_h, cp.kernel_w
+    else:
+        ks = list(cp.kernel_size)
+        if not ks:
+            raise ValueError("kernel_size is required")
+        kh, kw = (ks[0], ks[0]) if len(ks) == 1 else (ks[0], ks[1])
+    sh, sw = _conv_hw(cp, "stride", "stride", "stride_h", "stride_w", 1)
+    ph, pw = _conv_hw(cp, "pad", "pad", "pad_h", "pad_w", 0)
+    return int(kh), int(kw), sh, sw, ph, pw
+
+
+@register("Convolution")
+class ConvolutionLayer(Layer):
+    exact_bottoms = -1
+    min_bottoms = 1
+    min_tops = 1
+
+    fuse_relu = False  # set by the net's fusion pass when an in-place ReLU follows
+
+    def layer_setup(self, bottoms, tops):
+        cp = self.lp.convolution_param
+        if cp.axis != 1:
+            raise NotImplementedError("Convolution only supports axis=1 (NCHW logical)")
+        if len(bottoms) != len(tops):
+            raise ValueError("Convolution needs as many tops as bottoms")
+        b = bottoms[0]
+        if len(b.shape) != 4:
+            raise NotImplementedError("only 2-D spatial convolution is supported")
+        self.R, self.S, self.sh, self.sw, self.ph, self.pw = conv_geometry(cp)
+        self.K = int(cp.num_output)
+        self.groups = int(cp.group)
+        C = b.shape[1]
+        if C % self.groups or self.K % self.groups:
+            raise ValueError("channels and num_output must be divisible by group")
+        Cg = C // self.groups
+        R, S = self.R, self.S
+        self.C = C
+        w = self.add_param((self.K, Cg, R, S), (self.K, R, S, Cg),
+                           to_caffe=lambda t: t.permute(0, 3, 1, 2),
+                           from_caffe=lambda t: t.permute(0, 2, 3, 1),
+                           filler=cp.weight_filler if cp.HasField("weight_filler") else None)
+        self.weight = w
+        self.bias = None
+        if cp.bias_term:
+            self.bias = self.add_param((self.K,), filler=cp.bias_filler if cp.HasField("bias_filler") else None)
+
+    def spec(self, b) -> ConvSpec:
+        N, C, H, W = b.shape
+        if C != self.C:
+            raise ValueError(f"{self.name}: input channels changed {self.C} -> {C}")
+        return ConvSpec(N, H, W, C, self.K, self.R, self.S, self.sh, self.sw, self.ph, self.pw,
+                        1, 1, self.groups)
+
+    def reshape(self, bottoms, tops):
+        for b, t in zip(bottoms, tops):
+            s = self.spec(b)
+            t.reshape((s.N, s.K, s.P, s.Q), self.dtype)
+
+    def forward(self, bottoms, tops):
+        w = self.weight.compute
+        bias = self.bias.data if self.bias is not None else None
+        for b, t in zip(bottoms, tops):
+            s = self.spec(b)
+            t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu)
+
+    def backward(self, tops, propagate_down, bottoms):
+        w = self.weight.compute
+        dw = self.weight.diff if self.param_grads_needed(0) else None
+        db = self.bias.diff if (self.bias is not None and self.param_grads_needed(1)) else None
+        for i, (t, b) in enumerate(zip(tops, bottoms)):
+            s = self.spec(b)
+            dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db)
+            if propagate_down[i]:
+                b.diff = dx
+
+
+@register("Deconvolution")
+class DeconvolutionLayer(Layer):
+    """Transposed convolution (deconv_layer.cpp).  Weight Caffe shape (C_in, K/g, R, S).
+    Forward = conv dgrad, backward = conv forward + wgrad with roles swapped; runs
+    through the reference path on CPU and the same GEMM engine on GPU."""
+    min_bottoms = 1
+    min_tops = 1
+
+    def layer_setup(self, bottoms, tops):
+        cp = self.lp.convolution_param
+        self.R, self.S, self.sh, self.sw, self.ph, self.pw = conv_geometry(cp)
+        self.K = int(cp.num_output)
+        self.groups = int(cp.group)
+        C = bottoms[0].shape[1]
+        self.C = C
+        Kg = self.K // self.groups
+        self.weight = self.add_param((C, Kg, self.R, self.S), (C, self.R, self.S, Kg),
+                                     to_caffe=lambda t: t.permute(0, 3, 1, 2),
+                                     from_caffe=lambda t: t.permute(0, 2, 3, 1),
+                                     filler=cp.weight_filler if cp.HasField("weight_filler") else None)
+        self.bias = None
+        if cp.bias_term:
+            self.bias = self.add_param((self.K,), filler=cp.bias_filler if cp.HasField("bias_filler") else None)
+
+    def out_hw(self, H, W):
+        return ((H - 1) * self.sh + self.R - 2 * self.ph, (W - 1) * self.sw + self.S - 2 * self.pw)
+
+    def fwd_spec(self, b):
+        # the equivalent forward conv maps top (K channels) -> bottom (C channels)
+        N, C, H, W = b.shape
+        Ho, Wo = self.out_hw(H, W)
+        return ConvSpec(N, Ho, Wo, self.K, C, self.R, self.S, self.sh, self.sw, self.ph, self.pw,
+                        1, 1, self.groups)
+
+    def reshape(self, bottoms, tops):
+        for b, t in zip(bottoms, tops):
+            N, C, H, W = b.shape
+            Ho, Wo = self.out_hw(H, W)
+            t.reshape((N, self.K, Ho, Wo), self.dtype)
+
+    def _w_as_conv(self):
+        # deconv weight (C, R, S, K/g) == conv weight of top->bottom conv: (Cout=C, R, S, Cin_g=K/g)
+        return self.weight.compute
+
+    def forward(self, bottoms, tops):
+        for b, t in zip(bottoms, tops):
+            s = self.fwd_spec(b)
+            zeros = torch.zeros(t.data.shape, dtype=t.dtype, device=t.device)
+            y = ops.conv_backward(b.data, zeros, self._w_as_conv(), s, True, None, None)
+            if self.bias is not None:
+                y = (y.float() + self.bias.data.float()).to(t.dtype)
+            t.data = y
+
+    def backward(self, tops, propagate_down, bottoms):
+        dw = self.weight.diff if self.param_grads_needed(0) else None
+        for i, (t, b) in enumerate(zip(tops, bottoms)):
+            s = self.fwd_spec(b)
+            if self.bias is not None and self.param_grads_needed(1):
+                self.bias.diff += t.diff.float().reshape(-1, self.K).sum(0)
+            if dw is not None:
+                # conv(top->bottom) wgrad with x = top diff, dy = bottom data
+                ops.conv_backward(b.data, t.diff, self._w_as_conv(), s, False, dw, None)
+            if propagate_down[i]:
+                b.diff = ops.conv_forward(t.diff, self._w_as_conv(), None, s)
+
+
+@register("Pooling")
+class PoolingLayer(Layer):
+    exact_bottoms = 1
+    min_tops = 1
+    max_tops = 2
+
+    def layer_setup(self, bottoms, tops):
+        pp = self.lp.pooling_param
+        self.global_pooling = pp.global_pooling
+        if pp.HasField("kernel_h") or pp.HasField("kernel_w"):
+            self.kh, self.kw = pp.kernel_h, pp.kernel_w
+        else:
+            self.kh = self.kw = pp.kernel_size
+        if pp.HasField("pad_h") or pp.HasField("pad_w"):
+            self.ph, self.pw = pp.pad_h, pp.pad_w
+        else:
+            self.ph = self.pw = pp.pad
+        if pp.HasField("stride_h") or pp.HasField("stride_w"):
+            self.sh, self.sw = pp.stride_h, pp.stride_w
+        else:
+            self.sh = self.sw = pp.stride
+        self.method = int(pp.pool)
+        if self.global_pooling:
+            self.ph = self.pw = 0
+            self.sh = self.sw = 1
+        elif not self.kh or not self.kw:
+            raise ValueError("Pooling: kernel size is required")
+        self.aux = None
+
+    def spec(self, b) -> PoolSpec:
+        N, C, H, W = b.shape
+        kh, kw = (H, W) if self.global_pooling else (self.kh, self.kw)
+        return PoolSpec(N, H, W, C, kh, kw, self.sh, self.sw, self.ph, self.pw, self.method)
+
+    def reshape(self, bottoms, tops):
+        s = self.spec(bottoms[0])
+        tops[0].reshape((s.N, s.C, s.P, s.Q), self.dtype)
+        if len(tops) > 1:
+            tops[1].reshape((s.N, s.C, s.P, s.Q), self.dtype)
+
+    def forward(self, bottoms, tops):
+        s = self.spec(bottoms[0])
+        x = bottoms[0].data
+        if self.method == POOL_STOCHASTIC:
+            # Stochastic pooling: TEST = probability-weighted average (pooling_layer.cu:125-155);
+            # TRAIN sampling is approximated by the same expectation on this engine.
+            xf = x.float().clamp_min(0)
+            y = _stochastic_test(xf, s).to(x.dtype)
+            tops[0].data = y
+            return
+        y, self.aux = ops.pool_forward_aux(x, s)
+        tops[0].data = y
+        if len(tops) > 1:
+            tops[1].data = (self.aux.to(tops[1].dtype) if self.aux is not None
+                            else torch.zeros_like(y))
+
+    def backward(self, tops, propagate_down, bottoms):
+        if not propagate_down[0]:
+            return
+        s = self.spec(bottoms[0])
+        bottoms[0].diff = ops.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data)
+
+
+def _stochastic_test(xf, s: PoolSpec):
+    sq = ops.ref._pool_windows(xf * xf, s, 0.0).sum(-1)
+    lin = ops.ref._pool_windows(xf, s, 0.0).sum(-1)
+    out = torch.where(lin > 0, sq / lin.clamp_min(1e-30), torch.zeros_like(lin))
+    return ops.ref.nhwc(out)
+
+
+@register("LRN")
+class LRNLayer(Layer):
+    exact_bottoms = 1
+    exact_tops = 1
+
+    def layer_setup(self, bottoms, tops):
+        p = self.lp.lrn_param
+        self.size = int(p.local_size)
+        if self.size % 2 == 0:
+            raise ValueError("LRN only supports odd values for local_size")
+        self.alpha, self.beta, self.k = float(p.alpha), float(p.beta), float(p.k)
+        self.within = int(p.norm_region) == 1
+
+    def reshape(self, bottoms, tops):
+        tops[0].reshape(bottoms[0].shape, self.dtype)
+
+    def forward(self, bottoms, tops):
+        tops[0].data = ops.lrn_forward(bottoms[0].data, self.size, self.alpha, self.beta, self.k, self.within)
+
+    def backward(self, tops, propagate_down, bottoms):
+        if propagate_down[0]:
+            bottoms[0].diff = ops.lrn_backward(tops[0].diff, bottoms[0].data, self.size, self.alpha,
+                                               self.beta, self.k, self.within, tops[0].data)
+
+
+@register("InnerProduct")
+class InnerProductLayer(Layer):
+    exact_bottoms = 1
+    exact_tops = 1
+    fuse_relu = False
+
+    def layer_setup(self, bottoms, tops):
+        p = self.lp.inner_product_param
+        self.N = int(p.num_output)
+        b = bottoms[0]
+        self.axis = b.canonical_axis(p.axis)
+        self.Kdim = b.count_range(self.axis)
+        # 4-D NHWC bottoms flatten in (h, w, c) order; the weight's columns are kept in that
+        # order internally and permuted to Caffe's (c, h, w) order at the IO boundary.
+        self.perm = None
+        if b.is_image and self.axis == 1 and b.shape[2] * b.shape[3] > 1:
+            _, C, H, W = b.shape
+            self.perm = (C, H, W)
+        N, K = self.N, self.Kdim
+        if self.perm is not None:
+            C, H, W = self.perm
+            to_caffe = lambda t: t.reshape(N, H, W, C).permute(0, 3, 1, 2).reshape(N, K)  # noqa: E731
+            from_caffe = lambda t: t.reshape(N, C, H, W).permute(0, 2, 3, 1).reshape(N, K)  # noqa: E731
+        else:
+            to_caffe = from_caffe = None
+        self.weight = self.add_param((N, K), (N, K), to_caffe, from_caffe,
+                                     filler=p.weight_filler if p.HasField("weight_filler") else None)
+        self.bias = None
+        if p.bias_term:
+            self.bias = self.add_param((N,), filler=p.bias_filler if p.HasField("bias_filler") else None)
+
+    def reshape(self, bottoms, tops):
+        b = bottoms[0]
+        if b.count_range(self.axis) != self.Kdim:
+            raise ValueError(f"{self.name}: input size incompatible with inner product parameters")
+        tops[0].reshape(tuple(b.shape[:self.axis]) + (self.N,), self.dtype)
+
+    def forward(self, bottoms, tops):
+        b = bottoms[0]
+        M = b.count_range(0, self.axis)
+        x2 = b.data.reshape(M, self.Kdim)
+        bias = self.bias.data if self.bias is not None else None
+        y = ops.linear_forward(x2, self.weight.compute, bias, self.fuse_relu)
+        tops[0].data = y.reshape(tops[0].data.shape)
+
+    def backward(self, tops, propagate_down, bottoms):
+        b = bottoms[0]
+        M = b.count_range(0, self.axis)
+        dy2 = tops[0].diff.reshape(M, self.N)
+        x2 = b.data.reshape(M, self.Kdim)
+        dw = self.weight.diff if self.param_grads_needed(0) else None
+        db = self.bias.diff if (self.bias is not None and self.param_grads_needed(1)) else None
+        dx = ops.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db)
+        if propagate_down[0]:
+            b.diff = dx.reshape(b.data.shape)
+
+
+@register("Im2col")
+class Im2colLayer(Layer):
+    """im2col as a layer (im2col_layer.cpp): top = [N, C*R*S, P, Q] in Caffe order."""
+    exact_bottoms = 1
+    exact_tops = 1
+
+    def layer_setup(self, bottoms, tops):
+        self.R, self.S, self.sh, self.sw, self.ph, self.pw = conv_geometry(self.lp.convolution_param)
+
+    def reshape(self, bottoms, tops):
+        N, C, H, W = bottoms[0].shape
+        P = (H + 2 * self.ph - self.R) // self.sh + 1
+        Q = (W + 2 * self.pw - self.S) // self.sw + 1
+        tops[0].reshape((N, C * self.R * self.S, P, Q), self.dtype)
+
+    def forward(self, bottoms, tops):
+        xn = bottoms[0].nchw().float()
+        cols = torch.nn.functional.unfold(xn, (self.R, self.S), padding=(self.ph, self.pw),
+                                          stride=(self.sh, self.sw))
+        N, CK, L = cols.shape
+        t = tops[0]
+        t.data = cols.reshape(N, CK, t.shape[2], t.shape[3]).permute(0, 2, 3, 1).contiguous().to(t.dtype)
+
+    def backward(self, tops, propagate_down, bottoms):
+        if not propagate_down[0]:
+            return
+        t, b = tops[0], bottoms[0]
+        d = t.nchw(diff=True).float().reshape(t.shape[0], t.shape[1], -1)
+        x = torch.nn.functional.fold(d, b.shape[2:], (self.R, self.S), padding=(self.ph, self.pw),
+                                     stride=(self.sh, self.sw))
+        b.diff = x.permute(0, 2, 3, 1).contiguous().to(b.dtype)
+
+
+__all__ = ["ConvolutionLayer", "DeconvolutionLayer", "PoolingLayer", "LRNLayer", "InnerProductLayer",
+           "Im2colLayer", "POOL_MAX", "POOL_AVE"]

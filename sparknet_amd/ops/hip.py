@@ -1,0 +1,370 @@
+"""HIP implementations of the op API (MI355X / gfx950).
+
+Every function here launches hand-written kernels from ``libsn_kernels.so`` on torch's
+current stream (so a whole iteration can be captured into a hipGraph).  PyTorch is only
+used for allocation and for trivial glue on uncommon shapes (zero-padding operands whose
+channel counts are not multiples of 8).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from .gemm import (EPI_BF16, EPI_F32, EPI_F32_ACC, ConvGeom, Dense, Im2col, colsum, gemm,
+                   linear_dgrad, linear_fwd, linear_wgrad)
+from .spec import POOL_MAX, ConvSpec, PoolSpec
+
+call = _lib.call
+BF16 = torch.bfloat16
+
+
+def _c(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _round8(n: int) -> int:
+    return -(-n // 8) * 8
+
+
+# --------------------------------------------------------------------------------------
+# Convolution
+# --------------------------------------------------------------------------------------
+
+def _implicit_ok(s: ConvSpec) -> bool:
+    return s.Cg % 8 == 0 and s.C % 8 == 0
+
+
+def _weight_kpad(w: torch.Tensor, s: ConvSpec) -> tuple[torch.Tensor, int]:
+    """Weights as [K, Kpad] bf16 with K-dim (r, s, c) zero-padded to a multiple of 8."""
+    kred = s.R * s.S * s.Cg
+    kpad = _round8(kred)
+    w2 = w.reshape(s.K, kred)
+    if kpad == kred:
+        return _c(w2), kpad
+    out = torch.zeros((s.K, kpad), dtype=BF16, device=w.device)
+    out[:, :kred].copy_(w2)
+    return out, kpad
+
+
+def _im2col(x: torch.Tensor, s: ConvSpec, g: int, kpad: int) -> torch.Tensor:
+    M = s.N * s.P * s.Q
+    col = torch.empty((M, kpad), dtype=BF16, device=x.device)
+    call("im2col", x, col, s.N, s.H, s.W, s.C, s.P, s.Q, s.R, s.S, s.sh, s.sw, s.ph, s.pw, s.dh, s.dw,
+         s.Cg, kpad, g * s.Cg)
+    return col
+
+
+def _geom(s: ConvSpec) -> ConvGeom:
+    return ConvGeom(s.N, s.H, s.W, s.C, s.P, s.Q, s.R, s.S, s.sh, s.sw, s.ph, s.pw, s.dh, s.dw, s.Cg)
+
+
+def conv_forward(x, w, b, s: ConvSpec, relu=False):
+    x = _c(x)
+    assert x.dtype == BF16 and w.dtype == BF16, (x.dtype, w.dtype)
+    M = s.N * s.P * s.Q
+    y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device)
+    if _implicit_ok(s):
+        kred = s.R * s.S * s.Cg
+        A = Im2col(x, _geom(s), kcontig=True, gstride=s.Cg)
+        B = Dense(_c(w.reshape(s.K, kred)), kred, True, gstride=s.Kg * kred)
+        gemm(M, s.Kg, kred, A, B, y, s.K, epi=EPI_BF16, groups=s.groups, c_gstride=s.Kg, bias=b, relu=relu)
+        return y
+    wp, kpad = _weight_kpad(w, s)
+    y2 = y.view(M, s.K)
+    for g in range(s.groups):
+        col = _im2col(x, s, g, kpad)
+        wg = wp[g * s.Kg:(g + 1) * s.Kg]
+        bg = b[g * s.Kg:(g + 1) * s.Kg] if b is not None else None
+        gemm(M, s.Kg, kpad, Dense(col, kpad, True), Dense(_c(wg), kpad, True), y2[:, g * s.Kg:], s.K,
+             epi=EPI_BF16, bias=bg, relu=relu)
+    return y
+
+
+def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
+    out = torch.zeros((t2.shape[0], n), dtype=t2.dtype, device=t2.device)
+    out[:, :t2.shape[1]].copy_(t2)
+    return out
+
+
+def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None):
+    dy = _c(dy)
+    x = _c(x)
+    M = s.N * s.P * s.Q
+    dy2 = dy.view(M, s.K)
+    if db is not None:
+        colsum(dy2, db, accumulate=True)
+    kred = s.R * s.S * s.Cg
+    if dw is not None:
+        if _implicit_ok(s) and s.Kg % 8 == 0:
+            A = Dense(dy2, s.K, kcontig=False, gstride=s.Kg)
+            B = Im2col(x, _geom(s), kcontig=False, gstride=s.Cg)
+            gemm(s.Kg, kred, M, A, B, dw, kred, epi=EPI_F32_ACC, groups=s.groups, c_gstride=s.Kg * kred)
+        else:
+            kpad = _round8(kred)
+            kgp = _round8(s.Kg)
+            dw2 = dw.view(s.K, kred)
+            for g in range(s.groups):
+                col = _im2col(x, s, g, kpad)
+                dyg = dy2[:, g * s.Kg:(g + 1) * s.Kg]
+                dyg = _c(dyg) if kgp == s.Kg else _pad_cols(dyg, kgp)
+                tmp = torch.zeros((kgp, kpad), dtype=torch.float32, device=x.device)
+                gemm(kgp, kpad, M, Dense(dyg, dyg.stride(0), False), Dense(col, kpad, False), tmp, kpad,
+                     epi=EPI_F32)
+                dw2[g * s.Kg:(g + 1) * s.Kg].add_(tmp[:s.Kg, :kred])
+    if not need_dx:
+        return None
+    dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
+    if s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0:
+        # dgrad == forward conv of dy with flipped / transposed weights, pad' = R-1-pad
+        wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
+        call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
+        g2 = ConvGeom(s.N, s.P, s.Q, s.K, s.H, s.W, s.R, s.S, 1, 1, s.R - 1 - s.ph, s.S - 1 - s.pw, 1, 1, s.Kg)
+        kr2 = s.R * s.S * s.Kg
+        A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
+        B = Dense(wt.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
+        gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg)
+        return dx
+    # generic: dcol = dy_g @ W_g, then col2im (gather, no atomics)
+    wp, kpad = _weight_kpad(w, s)
+    kgp = _round8(s.Kg)
+    for g in range(s.groups):
+        dyg = dy2[:, g * s.Kg:(g + 1) * s.Kg]
+        dyg = _c(dyg) if kgp == s.Kg else _pad_cols(dyg, kgp)
+        wg = wp[g * s.Kg:(g + 1) * s.Kg]
+        if kgp != s.Kg:
+            wg = torch.cat([wg, torch.zeros((kgp - s.Kg, kpad), dtype=BF16, device=x.device)])
+        dcol = torch.empty((M, kpad), dtype=BF16, device=x.device)
+        gemm(M, kpad, kgp, Dense(dyg, dyg.stride(0), True), Dense(_c(wg), kpad, False), dcol, kpad, epi=EPI_BF16)
+        call("col2im", dcol, dx, s.N, s.H, s.W, s.C, s.P, s.Q, s.R, s.S, s.sh, s.sw, s.ph, s.pw, s.dh, s.dw,
+             s.Cg, kpad, g * s.Cg)
+    return dx
+
+
+# --------------------------------------------------------------------------------------
+# InnerProduct
+# --------------------------------------------------------------------------------------
+
+def linear_forward(x2, w, b, relu=False):
+    return linear_fwd(_c(x2), _c(w), b, relu)
+
+
+def linear_backward(dy2, x2, w, need_dx, dw=None, db=None):
+    dy2 = _c(dy2)
+    if db is not None:
+        colsum(dy2, db, accumulate=True)
+    if dw is not None:
+        linear_wgrad(dy2, _c(x2), dw, accumulate=True)
+    return linear_dgrad(dy2, _c(w)) if need_dx else None
+
+
+# --------------------------------------------------------------------------------------
+# Pooling / LRN
+# --------------------------------------------------------------------------------------
+
+def _pool_args(s: PoolSpec):
+    return (s.N, s.H, s.W, s.C, s.P, s.Q, s.kh, s.kw, s.sh, s.sw, s.ph, s.pw, s.method)
+
+
+def pool_forward_mask(x, s: PoolSpec):
+    x = _c(x)
+    y = torch.empty((s.N, s.P, s.Q, s.C), dtype=BF16, device=x.device)
+    mask = torch.empty((s.N, s.P, s.Q, s.C), dtype=torch.uint8, device=x.device) if s.method == POOL_MAX else None
+    call("pool_fwd", x, y, mask, *_pool_args(s))
+    return y, mask
+
+
+def pool_forward(x, s: PoolSpec):
+    return pool_forward_mask(x, s)[0]
+
+
+def pool_backward(dy, x, s: PoolSpec, mask=None, y=None):
+    dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=dy.device)
+    if s.method == POOL_MAX and mask is None:
+        _, mask = pool_forward_mask(x, s)
+    call("pool_bwd", _c(dy), mask, dx, *_pool_args(s))
+    return dx
+
+
+def lrn_forward(x, size, alpha, beta, k, within=False):
+    x = _c(x)
+    N, H, W, Cc = x.shape
+    y = torch.empty_like(x)
+    if within:
+        call("lrn_within_fwd", x, y, None, N, H, W, Cc, size, float(alpha), float(beta))
+    else:
+        call("lrn_across_fwd", x, y, N, H, W, Cc, size, float(alpha), float(beta), float(k))
+    return y
+
+
+def lrn_backward(dy, x, size, alpha, beta, k, within=False, y=None):
+    x, dy = _c(x), _c(dy)
+    N, H, W, Cc = x.shape
+    dx = torch.empty_like(x)
+    if within:
+        sbuf = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        u = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        call("lrn_within_bwd", x, dy, sbuf, u, dx, N, H, W, Cc, size, float(alpha), float(beta))
+    else:
+        call("lrn_across_bwd", x, dy, dx, N, H, W, Cc, size, float(alpha), float(beta), float(k))
+    return dx
+
+
+# --------------------------------------------------------------------------------------
+# Elementwise
+# --------------------------------------------------------------------------------------
+
+def relu_forward(x, slope=0.0):
+    x = _c(x)
+    if x.numel() % 8:
+        xf = x.float()
+        return torch.where(xf > 0, xf, xf * slope).to(x.dtype)
+    y = torch.empty_like(x)
+    call("relu_fwd", x, y, x.numel(), float(slope))
+    return y
+
+
+def relu_backward(dy, x, slope=0.0):
+    dy, x = _c(dy), _c(x)
+    if x.numel() % 8:
+        xf = x.float()
+        return (dy.float() * torch.where(xf > 0, 1.0, slope)).to(dy.dtype)
+    dx = torch.empty_like(dy)
+    call("relu_bwd", dy, x, dx, x.numel(), float(slope))
+    return dx
+
+
+def _dropout(x, ratio, rng_state, stream):
+    x = _c(x)
+    if x.numel() % 8:
+        raise NotImplementedError("dropout on GPU needs element count % 8 == 0")
+    y = torch.empty_like(x)
+    call("dropout", x, y, x.numel(), rng_state, int(stream), float(ratio))
+    return y
+
+
+def dropout_forward(x, ratio, rng_state, stream):
+    return _dropout(x, ratio, rng_state, stream)
+
+
+def dropout_backward(dy, ratio, rng_state, stream):
+    return _dropout(dy, ratio, rng_state, stream)
+
+
+def cast_f32_to_bf16(src, dst):
+    call("cast_f32_bf16", src, dst, src.numel())
+
+
+def advance_rng(rng_state):
+    call("advance_rng", rng_state)
+
+
+def sum_bf16(tensors, out=None):
+    out = torch.empty_like(tensors[0]) if out is None else out
+    n = out.numel()
+    for i in range(0, len(tensors), 8):
+        chunk = [_c(t) for t in tensors[i:i + 8]]
+        if i:
+            chunk = [out] + chunk[:7]
+        arr = (C.c_void_p * 8)(*[t.data_ptr() for t in chunk] + [0] * (8 - len(chunk)))
+        _lib.check(_lib.kernels().sn_sum_bf16(arr, C.c_longlong(len(chunk)), C.c_void_p(out.data_ptr()),
+                                              C.c_longlong(n), C.c_void_p(_lib.stream_ptr())), "sum_bf16")
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# Softmax / loss / accuracy
+# --------------------------------------------------------------------------------------
+
+def softmax_loss_forward(x2, labels, ignore_label=None, normalize=True, outer_num=None):
+    x2 = _c(x2)
+    M, Cn = x2.shape
+    dev = x2.device
+    prob = torch.empty((M, Cn), dtype=torch.float32, device=dev)
+    rows = torch.empty((2, M), dtype=torch.float32, device=dev)
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    lab = _c(labels.reshape(-1).float())
+    call("softmax_xent_fwd", x2, lab, prob, rows[0], rows[1], out[0:1], out[1:2], M, Cn,
+         int(ignore_label is not None), int(ignore_label or 0), int(normalize),
+         int(outer_num if outer_num is not None else M))
+    return out[0], prob, out[1:2]
+
+
+def softmax_loss_backward(prob, labels, loss_weight, norm, ignore_label=None, dtype=BF16):
+    M, Cn = prob.shape
+    dx = torch.empty((M, Cn), dtype=BF16, device=prob.device)
+    lw = loss_weight.reshape(-1).float()
+    call("softmax_xent_bwd", prob, _c(labels.reshape(-1).float()), lw, norm, dx, M, Cn,
+         int(ignore_label is not None), int(ignore_label or 0))
+    return dx if dtype == BF16 else dx.to(dtype)
+
+
+def softmax_forward(x2):
+    x2 = _c(x2)
+    y = torch.empty_like(x2)
+    call("softmax_fwd", x2, y, x2.shape[0], x2.shape[1])
+    return y
+
+
+def softmax_backward(dy2, y2):
+    dx = torch.empty_like(y2)
+    call("softmax_bwd", _c(dy2), _c(y2), dx, y2.shape[0], y2.shape[1])
+    return dx
+
+
+def accuracy(x2, labels, top_k=1, ignore_label=None):
+    x2 = _c(x2)
+    M, Cn = x2.shape
+    rows = torch.empty((2, M), dtype=torch.float32, device=x2.device)
+    out = torch.empty(2, dtype=torch.float32, device=x2.device)
+    call("accuracy", x2, _c(labels.reshape(-1).float()), rows[0], rows[1], out[0:1], out[1:2], M, Cn,
+         int(top_k), int(ignore_label is not None), int(ignore_label or 0))
+    return out[0]
+
+
+# --------------------------------------------------------------------------------------
+# Solver
+# --------------------------------------------------------------------------------------
+
+CHUNK = 8192
+
+
+def solver_tables(segments, total: int, device) -> dict:
+    pos, mult = [], []
+    for off, cnt, lm, dm in segments:
+        padded = -(-cnt // 64) * 64
+        for s in range(0, padded, CHUNK):
+            pos.append((off + s, min(CHUNK, padded - s)))
+            mult.append((lm, dm))
+    nparts = max(1, min(1024, -(-total // (256 * 16))))
+    return {
+        "pos": torch.tensor(pos or [(0, 0)], dtype=torch.int64, device=device),
+        "mult": torch.tensor(mult or [(0.0, 0.0)], dtype=torch.float32, device=device),
+        "n": len(pos),
+        "part": torch.empty(nparts, dtype=torch.float32, device=device),
+        "total": total,
+    }
+
+
+def solver_update(kind, data, diff, history, compute, tables, hyper, l1, clip):
+    h0 = history[0]
+    h1 = history[1] if len(history) > 1 else history[0]
+    call("solver_update", int(kind), data, diff, h0, h1, compute, tables["pos"], tables["mult"], tables["n"],
+         hyper, int(l1), int(clip), tables["part"], tables["part"].numel(), tables["total"])
+
+
+def scale_shadow(flat, shadow, scale: float):
+    call("scale_shadow", flat, shadow, flat.numel(), float(scale))
+
+
+# --------------------------------------------------------------------------------------
+# Data augmentation
+# --------------------------------------------------------------------------------------
+
+def augment(src_u8, dst, crop, mean=None, mean_mode=0, scale=1.0, rng_state=None, train=True, mirror=False,
+            offs_out=None):
+    N, Cc, Hs, Ws = src_u8.shape
+    call("augment", _c(src_u8), dst, N, Cc, Hs, Ws, crop, crop, mean, int(mean_mode), float(scale), rng_state,
+         int(train), int(mirror), offs_out)
+    return dst

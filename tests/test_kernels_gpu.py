@@ -1,0 +1,192 @@
+"""HIP kernels vs the PyTorch fp32 reference (ops.ref) on identical bf16 inputs.
+
+Mirrors the reference's per-layer GPU-vs-CPU tests (caffe/src/caffe/test/test_*_layer.cpp
+run over {CPU, GPU} with the CPU as oracle).
+"""
+import pytest
+import torch
+
+from sparknet_amd.ops import ref
+from sparknet_amd.ops.spec import POOL_AVE, POOL_MAX, ConvSpec, PoolSpec
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(*shape, scale=1.0, dev="cuda"):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def close(a, b, tol=2e-2, what=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err / scale < tol, f"{what}: rel err {err / scale:.3e} (abs {err:.3e}, scale {scale:.3e})"
+
+
+CONV_CASES = [
+    # N, H, W, C, K, R, S, stride, pad, groups
+    (2, 13, 13, 16, 32, 3, 3, 1, 1, 1),
+    (2, 27, 27, 48, 64, 5, 5, 1, 2, 2),      # AlexNet conv2-like (grouped)
+    (2, 35, 35, 3, 16, 11, 11, 4, 0, 1),     # conv1-like (explicit im2col path)
+    (2, 16, 16, 32, 24, 1, 1, 1, 0, 1),      # 1x1
+    (2, 15, 15, 16, 16, 3, 3, 2, 1, 1),      # stride 2 dgrad fallback
+    (2, 12, 12, 20, 50, 5, 5, 1, 0, 1),      # LeNet conv2 (odd channels)
+    (3, 9, 9, 64, 40, 3, 3, 1, 1, 2),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv(gpu, case):
+    from sparknet_amd.ops import hip
+    N, H, W, Cc, K, R, S, st, pd, g = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    x = rnd(N, H, W, Cc)
+    w = rnd(K, R, S, Cc // g, scale=0.2)
+    b = torch.randn(K, device="cuda")
+    y = hip.conv_forward(x, w, b, s, relu=True)
+    close(y, ref.conv_forward(x, w, b, s, relu=True), what="fwd")
+    dy = rnd(N, s.P, s.Q, K)
+    dw = torch.zeros(K, R, S, Cc // g, device="cuda")
+    db = torch.zeros(K, device="cuda")
+    dx = hip.conv_backward(dy, x, w, s, True, dw, db)
+    dw_r = torch.zeros_like(dw)
+    db_r = torch.zeros_like(db)
+    dx_r = ref.conv_backward(dy, x, w, s, True, dw_r, db_r)
+    close(dx, dx_r, what="dgrad")
+    close(dw, dw_r, what="wgrad")
+    close(db, db_r, 1e-3, what="bias")
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 9216, 4096), (64, 800, 500), (100, 64, 10)])
+def test_linear(gpu, M, K, N):
+    from sparknet_amd.ops import hip
+    x, w = rnd(M, K), rnd(N, K, scale=0.05)
+    b = torch.randn(N, device="cuda")
+    close(hip.linear_forward(x, w, b, True), ref.linear_forward(x, w, b, True))
+    dy = rnd(M, N)
+    dw, db = torch.zeros(N, K, device="cuda"), torch.zeros(N, device="cuda")
+    dwr, dbr = torch.zeros_like(dw), torch.zeros_like(db)
+    dx = hip.linear_backward(dy, x, w, True, dw, db)
+    dxr = ref.linear_backward(dy, x, w, True, dwr, dbr)
+    close(dx, dxr)
+    close(dw, dwr)
+    close(db, dbr, 1e-3)
+
+
+@pytest.mark.parametrize("method", [POOL_MAX, POOL_AVE])
+@pytest.mark.parametrize("geo", [(2, 55, 55, 96, 3, 2, 0), (2, 32, 32, 32, 3, 2, 0), (2, 8, 8, 24, 3, 2, 1),
+                                 (2, 7, 7, 16, 7, 1, 0), (2, 6, 6, 3, 2, 2, 0)])
+def test_pool(gpu, method, geo):
+    from sparknet_amd.ops import hip
+    N, H, W, Cc, k, st, pd = geo
+    s = PoolSpec(N, H, W, Cc, k, k, st, st, pd, pd, method)
+    x = rnd(N, H, W, Cc)
+    y, mask = hip.pool_forward_mask(x, s)
+    close(y, ref.pool_forward(x, s), 1e-2)
+    dy = rnd(N, s.P, s.Q, Cc)
+    close(hip.pool_backward(dy, x, s, mask), ref.pool_backward(dy, x, s), 1e-2)
+
+
+@pytest.mark.parametrize("within", [False, True])
+@pytest.mark.parametrize("geo", [(2, 13, 13, 96, 5), (2, 8, 8, 256, 5), (2, 6, 6, 20, 3), (2, 5, 5, 16, 9)])
+def test_lrn(gpu, within, geo):
+    from sparknet_amd.ops import hip
+    N, H, W, Cc, size = geo
+    x = rnd(N, H, W, Cc, scale=3.0)
+    a, bta, k = (5e-5, 0.75, 1.0) if within else (1e-2, 0.75, 2.0)
+    y = hip.lrn_forward(x, size, a, bta, k, within)
+    close(y, ref.lrn_forward(x, size, a, bta, k, within))
+    dy = rnd(N, H, W, Cc)
+    close(hip.lrn_backward(dy, x, size, a, bta, k, within), ref.lrn_backward(dy, x, size, a, bta, k, within))
+
+
+def test_relu_dropout(gpu):
+    from sparknet_amd.ops import hip
+    x = rnd(4, 4096)
+    close(hip.relu_forward(x, 0.1), ref.relu_forward(x, 0.1), 1e-2)
+    dy = rnd(4, 4096)
+    close(hip.relu_backward(dy, x, 0.1), ref.relu_backward(dy, x, 0.1), 1e-2)
+    rng = torch.tensor([1234567, 42], dtype=torch.int64, device="cuda")
+    y = hip.dropout_forward(x, 0.5, rng, 3)
+    yr = ref.dropout_forward(x.cpu(), 0.5, 1234567, 42, 3)
+    close(y, yr, 1e-2)
+    keep = (y != 0).float().mean().item()
+    assert 0.45 < keep < 0.55
+
+
+def test_softmax_loss_and_accuracy(gpu):
+    from sparknet_amd.ops import hip
+    x = rnd(256, 1000, scale=2.0)
+    lab = torch.randint(0, 1000, (256,), device="cuda").float()
+    loss, prob, norm = hip.softmax_loss_forward(x, lab, None, True, 256)
+    lr, pr, nr = ref.softmax_loss_forward(x.cpu(), lab.cpu(), None, True, 256)
+    assert abs(loss.item() - lr.item()) < 1e-3 * abs(lr.item())
+    close(prob, pr, 1e-3)
+    lw = torch.tensor([1.0], device="cuda")
+    g = hip.softmax_loss_backward(prob, lab, lw, norm)
+    gr = ref.softmax_loss_backward(pr, lab.cpu(), 1.0, nr)
+    close(g, gr, 1e-2)
+    # ignore label path
+    lab2 = lab.clone()
+    lab2[:10] = 7
+    loss2, _, norm2 = hip.softmax_loss_forward(x, lab2, 7, True, 256)
+    lr2, _, nr2 = ref.softmax_loss_forward(x.cpu(), lab2.cpu(), 7, True, 256)
+    assert abs(loss2.item() - lr2.item()) < 1e-3 * abs(lr2.item())
+    assert norm2.item() == nr2.item()
+    for k in (1, 5):
+        a = hip.accuracy(x, lab, k).item()
+        ar = ref.accuracy(x.cpu(), lab.cpu(), k).item()
+        assert abs(a - ar) < 1e-6
+    close(hip.softmax_forward(x), ref.softmax_forward(x), 1e-2)
+    y = hip.softmax_forward(x)
+    dy = rnd(256, 1000)
+    close(hip.softmax_backward(dy, y), ref.softmax_backward(dy, y), 2e-2)
+
+
+@pytest.mark.parametrize("kind", range(6))
+@pytest.mark.parametrize("l1,clip", [(False, False), (True, True)])
+def test_solver_update(gpu, kind, l1, clip):
+    from sparknet_amd.ops import hip
+    from sparknet_amd.core.solver import N_HYPER
+    total = 64 * 41
+    segs = [(0, 1000, 1.0, 1.0), (1024, 600, 2.0, 0.0), (1664, 900, 0.5, 3.0)]
+    w = torch.randn(total, device="cuda")
+    g = torch.randn(total, device="cuda")
+    hist = [torch.rand(total, device="cuda") for _ in range(2)]
+    hyper = torch.zeros(N_HYPER, device="cuda")
+    hyper[:9] = torch.tensor([0.01, 0.9, 5e-4, 5.0 if clip else -1, 0.5, 1e-8, 0.999, 0.98, 0.7])
+    tabs = hip.solver_tables(segs, total, "cuda")
+    wr, gr, hr = w.cpu().clone(), g.cpu().clone(), [h.cpu().clone() for h in hist]
+    lr = torch.zeros(total)
+    dc = torch.zeros(total)
+    for off, cnt, lm, dm in segs:
+        padded = -(-cnt // 64) * 64
+        lr[off:off + padded] = lm
+        dc[off:off + padded] = dm
+    shadow = torch.empty(total, dtype=torch.bfloat16, device="cuda")
+    hip.solver_update(kind, w, g, hist, shadow, tabs, hyper, l1, clip)
+    ref.solver_update_ref(kind, wr, gr, hr, lr, dc, hyper.cpu().tolist(), l1, clip)
+    close(w, wr, 1e-5)
+    close(hist[0], hr[0], 1e-4)
+    close(shadow, wr, 1e-2)
+
+
+def test_cast_and_augment(gpu):
+    from sparknet_amd.ops import hip
+    src = torch.randn(1003, device="cuda")
+    dst = torch.empty(1003, dtype=torch.bfloat16, device="cuda")
+    hip.cast_f32_to_bf16(src, dst)
+    assert torch.equal(dst, src.to(torch.bfloat16))
+    img = torch.randint(0, 256, (4, 3, 40, 44), dtype=torch.uint8, device="cuda")
+    mean = torch.tensor([100.0, 110.0, 120.0], device="cuda")
+    out = torch.empty((4, 32, 32, 3), dtype=torch.bfloat16, device="cuda")
+    offs = torch.zeros((4, 3), dtype=torch.int32, device="cuda")
+    rng = torch.tensor([7, 3], dtype=torch.int64, device="cuda")
+    hip.augment(img, out, 32, mean, 1, 0.5, rng, True, True, offs)
+    for n in range(4):
+        ho, wo, mir = offs[n].tolist()
+        crop = img[n, :, ho:ho + 32, wo:wo + 32].float()
+        if mir:
+            crop = crop.flip(-1)
+        expect = ((crop - mean.view(3, 1, 1)) * 0.5).permute(1, 2, 0)
+        close(out[n], expect, 1e-2)
