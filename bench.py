@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Headline benchmark: AlexNet/CaffeNet (bvlc_reference_caffenet, 227x227) training
+images/sec on N MI355X GPUs — SparkNet's ImageNetApp algorithm: per-GPU batch 256,
+tau = 50 local SGD steps per round, then an RCCL all-reduce weight average.
+
+Every timed step is a full training iteration: H2D of a uint8 256x3x256x256 synthetic
+batch on a side stream, on-device random crop 227 + mirror + mean subtraction, forward,
+backward, fused SGD/momentum/weight-decay update (bf16 compute, fp32 masters), and every
+tau-th step the cross-GPU weight average.  Random-init weights, synthetic data.
+
+Single GPU:  python bench.py --steps 50 --warmup 10
+N GPUs:      python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+                 --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_IMG_S = 193.2  # CaffeNet training, Caffe no-cuDNN, K40
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--model", default="caffenet", choices=["caffenet", "alexnet", "googlenet", "vgg16",
+                                                            "cifar10_quick", "cifar10_full"])
+    p.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the model's train batch)")
+    p.add_argument("--tau", type=int, default=50)
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--profile-steps", type=int, default=0)
+    return p.parse_args()
+
+
+DEFAULTS = {  # model: (batch, channels, src hw, crop, classes, mean)
+    "caffenet": (256, 3, 256, 227, 1000, [104.0, 117.0, 123.0]),
+    "alexnet": (256, 3, 256, 227, 1000, [104.0, 117.0, 123.0]),
+    "googlenet": (32, 3, 256, 224, 1000, [104.0, 117.0, 123.0]),
+    "vgg16": (64, 3, 256, 224, 1000, [104.0, 117.0, 123.0]),
+    "cifar10_quick": (100, 3, 32, 32, 10, [125.0, 123.0, 114.0]),
+    "cifar10_full": (100, 3, 32, 32, 10, [125.0, 123.0, 114.0]),
+}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    import torch
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from sparknet_amd import models
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.data.prefetch import DeviceFeeder, SyntheticSource
+    from sparknet_amd.engine import LocalSGDTrainer, fuse_relu
+    from sparknet_amd.ops import _lib
+    from sparknet_amd.parallel import Comm
+
+    _lib.kernels()
+    comm = Comm(device=dev) if world > 1 else None
+    B, C, HW, crop, classes, mean = DEFAULTS[args.model]
+    B = args.batch or B
+    kw = dict(train_batch=B, test_batch=max(1, min(B, 50)))
+    if args.model in ("caffenet", "alexnet", "googlenet", "vgg16"):
+        kw["crop"] = crop
+    solver_param = models.solver_for(args.model, **kw)
+    solver = Solver(solver_param, device=dev, seed=1701 + rank, build_test_nets=False)
+    net = solver.net
+    fuse_relu(net)
+    src = SyntheticSource(B, C, HW, HW, classes=classes, pool=3, seed=rank)
+    feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
+                          mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev)
+    trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph)
+    trainer.broadcast_initial()
+
+    # warmup (includes hipGraph capture and one averaging collective to set up RCCL)
+    for _ in range(max(1, args.warmup)):
+        trainer.local_step()
+    if comm is not None:
+        trainer.average()
+    torch.cuda.synchronize(dev)
+    if comm is not None:
+        comm.barrier()
+    torch.cuda.synchronize(dev)
+
+    t0 = time.perf_counter()
+    loss = None
+    for k in range(args.steps):
+        loss = trainer.local_step()
+        if (k + 1) % args.tau == 0:
+            trainer.average()
+    if comm is not None:
+        comm.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if comm is not None:
+        elapsed = comm.max_over_ranks(elapsed)
+    final_loss = float(loss) if loss is not None else float("nan")
+
+    ms = 1000.0 * elapsed / args.steps
+    img_s = world * B * args.steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": "images/sec AlexNet training (227x227) at 1/2/4/8 MI355X; scaling efficiency",
+            "value": round(img_s, 1),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(img_s / BASELINE_IMG_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic (uint8 256x256 -> on-device random crop/mirror/mean), random-init weights",
+            "config": {
+                "model": f"{args.model} (bvlc_reference_caffenet / AlexNet)" if args.model == "caffenet"
+                else args.model,
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
+                "hipgraph": not args.no_graph,
+                "final_loss": round(final_loss, 4),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,1 @@
+"""Data pipeline: loaders, samplers, host batch sources and the device feeder."""

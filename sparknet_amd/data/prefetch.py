@@ -1,0 +1,147 @@
+"""Device input pipeline: pinned host uint8 minibatches -> side-stream H2D -> on-device
+augment kernel -> the net's JavaData blobs.
+
+Replaces SparkNet's JNA data callback (caffe/src/caffe/layers/java_data_layer.cpp:37-44,
+src/main/scala/libs/Net.scala:194-233), which ran synchronously inside Forward and was
+followed by an implicit synchronous H2D copy (caffe/src/caffe/syncedmem.cpp:61-69), and
+Caffe's prefetch thread (base_data_layer.cpp:70-96).  Here:
+
+* a host ring of pinned uint8 batches (raw planar CHW bytes, 4x smaller than float),
+* ``hipMemcpyAsync`` of batch k+1 on a dedicated copy stream while step k computes,
+* an event hand-off, then ONE augment launch (crop / mirror / mean / scale / NCHW->NHWC
+  / uint8->bf16) on the compute stream writing straight into the data blob.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import _lib
+
+
+class HostBatchSource:
+    """Iterator protocol: ``next_batch() -> (uint8 [N,C,H,W] tensor, int32 [N] labels)``."""
+
+    def next_batch(self):
+        raise NotImplementedError
+
+
+class SyntheticSource(HostBatchSource):
+    """Synthetic uint8 images / labels of a fixed shape (the benchmark data): a small
+    pool of random batches generated once and cycled, so the timed loop still moves a
+    full minibatch over PCIe every step."""
+
+    def __init__(self, batch, channels, height, width, classes=1000, pool=4, seed=0, pin=True):
+        g = torch.Generator().manual_seed(seed)
+        self.batches = []
+        for _ in range(pool):
+            x = torch.randint(0, 256, (batch, channels, height, width), dtype=torch.uint8, generator=g)
+            y = torch.randint(0, classes, (batch,), dtype=torch.int32, generator=g)
+            if pin and torch.cuda.is_available():
+                x, y = x.pin_memory(), y.pin_memory()
+            self.batches.append((x, y))
+        self.i = 0
+
+    def next_batch(self):
+        b = self.batches[self.i % len(self.batches)]
+        self.i += 1
+        return b
+
+
+class TensorSource(HostBatchSource):
+    """Cycle over an in-memory uint8 dataset (e.g. CIFAR-10 from CifarLoader)."""
+
+    def __init__(self, images: torch.Tensor, labels: torch.Tensor, batch: int, sampler=None, pin=True):
+        self.images, self.labels, self.batch = images, labels.int(), batch
+        self.sampler = sampler
+        self.pos = 0
+        n = images.shape[0]
+        self.nbatches = n // batch
+        self.pin = pin and torch.cuda.is_available()
+
+    def next_batch(self):
+        if self.sampler is not None:
+            idx = self.sampler.next_index()
+        else:
+            idx = self.pos % self.nbatches
+            self.pos += 1
+        sl = slice(idx * self.batch, (idx + 1) * self.batch)
+        x, y = self.images[sl].contiguous(), self.labels[sl].contiguous()
+        if self.pin:
+            x, y = x.pin_memory(), y.pin_memory()
+        return x, y
+
+
+class DeviceFeeder:
+    """Double-buffered H2D + augment into a net's data/label blobs."""
+
+    def __init__(self, source: HostBatchSource, data_blob, label_blob, *, crop: int | None = None,
+                 mean=None, scale: float = 1.0, mirror: bool = False, train: bool = True,
+                 rng_state: torch.Tensor | None = None, device="cuda", slots: int = 2):
+        self.source = source
+        self.data_blob, self.label_blob = data_blob, label_blob
+        self.device = torch.device(device)
+        x0, y0 = source.batches[0] if isinstance(source, SyntheticSource) else source.next_batch()
+        self.shape = tuple(x0.shape)
+        N, C, H, W = self.shape
+        self.crop = crop or H
+        self.scale, self.mirror, self.train = scale, mirror, train
+        self.mean_mode, self.mean = 0, None
+        if mean is not None:
+            m = torch.as_tensor(mean, dtype=torch.float32).to(self.device)
+            self.mean_mode = 1 if m.numel() == C else 2
+            self.mean = m.contiguous()
+        self.rng_state = rng_state if rng_state is not None else torch.tensor([1, 0], dtype=torch.int64,
+                                                                              device=self.device)
+        self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.slots = [(torch.empty(self.shape, dtype=torch.uint8, device=self.device),
+                       torch.empty((N,), dtype=torch.int32, device=self.device)) for _ in range(slots)]
+        self.events = [None] * slots
+        self.k = 0
+        self._pending = None
+        if not isinstance(source, SyntheticSource):
+            self._first = (x0, y0)
+        else:
+            self._first = None
+
+    def prefetch(self) -> None:
+        """Issue the H2D copy of the next host batch into the next slot (copy stream)."""
+        if self._first is not None:
+            x, y = self._first
+            self._first = None
+        else:
+            x, y = self.source.next_batch()
+        slot = self.k % len(self.slots)
+        dx, dy = self.slots[slot]
+        if self.copy_stream is not None:
+            # the slot is reused only after the compute stream consumed it
+            self.copy_stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.copy_stream):
+                dx.copy_(x, non_blocking=True)
+                dy.copy_(y, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.copy_stream)
+            self.events[slot] = ev
+        else:
+            dx.copy_(x)
+            dy.copy_(y)
+        self._pending = slot
+        self.k += 1
+
+    def stage(self) -> None:
+        """Compute stream: wait for the slot, augment into the data blob, labels -> float."""
+        if self._pending is None:
+            self.prefetch()
+        slot = self._pending
+        self._pending = None
+        if self.events[slot] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.events[slot])
+        src, lab = self.slots[slot]
+        from ..ops import hip
+        hip.augment(src, self.data_blob.data, self.crop, self.mean, self.mean_mode, self.scale, self.rng_state,
+                    self.train, self.mirror)
+        _lib.call("labels_to_float", lab, self.label_blob.data, lab.numel())
+
+    def __call__(self, layer=None, tops=None) -> None:
+        """JavaData-layer source hook (eager mode): stage + prefetch the next batch."""
+        self.stage()
+        self.prefetch()

@@ -1,0 +1,156 @@
+"""Execution engine: graph-captured solver iterations and SparkNet's round structure.
+
+* :class:`GraphStep` captures ONE full training iteration (gradient memset, forward,
+  backward, Philox advance, fused solver update) into a hipGraph via
+  ``torch.cuda.CUDAGraph`` and replays it; per-iteration hyper-parameters (learning
+  rate, Adam correction) are staged into a device tensor with one async H2D copy before
+  each replay.  This removes the Python/launch overhead of ~100 kernels per iteration
+  (the reference instead paid a host sync for every loss scalar).
+* :class:`LocalSGDTrainer` runs SparkNet's algorithm (src/main/scala/apps/CifarApp.scala:
+  95-136, ImageNetApp.scala:106-189) on one process per GPU: every rank runs tau local
+  solver steps on its own data shard, then the flat fp32 weights are averaged with an
+  RCCL all-reduce (:mod:`sparknet_amd.parallel.comm`) — the Spark driver's
+  broadcast / collect / reduce / divide loop collapsed into one collective.
+"""
+from __future__ import annotations
+
+import logging
+import time
+
+import torch
+
+from . import ops
+from .core.solver import Solver
+
+log = logging.getLogger("sparknet_amd.engine")
+
+
+def fuse_relu(net) -> int:
+    """Fold in-place ReLU (slope 0) into the producing Convolution / InnerProduct
+    epilogue.  Returns the number of fused pairs.  The ReLU layer keeps its backward."""
+    n = 0
+    for li in range(1, len(net.layers)):
+        relu = net.layers[li]
+        prod = net.layers[li - 1]
+        if relu.type_name != "ReLU" or getattr(relu, "slope", 1.0) != 0.0:
+            continue
+        if net.bottom_ids[li] != net.top_ids[li]:
+            continue
+        if prod.type_name not in ("Convolution", "InnerProduct") or len(net.top_ids[li - 1]) != 1:
+            continue
+        if net.top_ids[li - 1][0] != net.bottom_ids[li][0]:
+            continue
+        prod.fuse_relu = True
+        relu.fused = True
+        n += 1
+    return n
+
+
+class GraphStep:
+    """One captured solver iteration (iter_size = 1)."""
+
+    def __init__(self, solver: Solver, warmup: int = 2, pre=None):
+        self.solver = solver
+        self.pre = pre  # callable run (eagerly) before each replay, e.g. feeder.stage
+        self.graph = None
+        self.loss = None
+        self.warmup = warmup
+
+    def _body(self):
+        s = self.solver
+        net = s.net
+        net.clear_param_diffs()
+        loss = net.forward_backward()
+        ops.advance_rng(net.ctx.rng_state)
+        s.update_params()
+        return loss
+
+    def capture(self) -> None:
+        s = self.solver
+        dev = s.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                if self.pre:
+                    self.pre()
+                s.stage_hyper()
+                self._body()
+                s.iter += 1
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        if self.pre:
+            self.pre()
+        s.stage_hyper()
+        with torch.cuda.graph(self.graph):
+            self.loss = self._body()
+        # the capture did not execute: replay it once as a real iteration
+        self.graph.replay()
+        s.iter += 1
+
+    def step(self):
+        s = self.solver
+        if self.graph is None:
+            self.capture()
+            return self.loss
+        if self.pre:
+            self.pre()
+        s.stage_hyper()
+        self.graph.replay()
+        s.iter += 1
+        return self.loss
+
+
+class LocalSGDTrainer:
+    """tau local steps + weight averaging per round (SparkNet's model averaging)."""
+
+    def __init__(self, solver: Solver, comm=None, tau: int = 50, feeder=None, use_graph: bool = True,
+                 log_every: int = 0):
+        self.solver = solver
+        self.comm = comm
+        self.tau = tau
+        self.feeder = feeder
+        self.round = 0
+        self.use_graph = use_graph and solver.device.type == "cuda"
+        self.step_fn = GraphStep(solver, pre=self._pre) if self.use_graph else None
+        self.log_every = log_every
+        self.times = {"compute": 0.0, "allreduce": 0.0}
+
+    def _pre(self):
+        if self.feeder is not None:
+            self.feeder.stage()
+            self.feeder.prefetch()
+
+    def broadcast_initial(self) -> None:
+        """All ranks start from rank 0's initial weights (CifarApp.scala:92)."""
+        if self.comm is not None and self.comm.world_size > 1:
+            self.comm.broadcast_params(self.solver.net)
+
+    def local_step(self):
+        if self.use_graph:
+            return self.step_fn.step()
+        self._pre()
+        loss = self.solver.iteration()
+        self.solver.iter += 1
+        return loss
+
+    def average(self) -> None:
+        if self.comm is not None and self.comm.world_size > 1:
+            self.comm.average_params(self.solver.net)
+
+    def run_round(self):
+        loss = None
+        for _ in range(self.tau):
+            loss = self.local_step()
+        self.average()
+        self.round += 1
+        return loss
+
+    def train(self, rounds: int, on_round=None):
+        for r in range(rounds):
+            t = time.perf_counter()
+            loss = self.run_round()
+            if on_round:
+                on_round(r, loss, time.perf_counter() - t)
+        return self.round

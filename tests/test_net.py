@@ -1,0 +1,185 @@
+"""Net construction semantics (caffe/src/caffe/test/test_net.cpp, test_split_layer.cpp)
+and whole-net numerics against an independent fp64 NCHW PyTorch oracle."""
+import pytest
+import torch
+
+from sparknet_amd import dsl, models, proto
+from sparknet_amd.core.net import Net, filter_net, insert_splits
+
+import torch_oracle
+
+
+def _dummy(name, shapes, fillers=None):
+    lp = proto.LayerParameter(name=name, type="DummyData")
+    for i, s in enumerate(shapes):
+        lp.top.append(name if i == 0 else f"{name}{i}")
+        lp.dummy_data_param.shape.add().dim.extend(s)
+    for f in fillers or []:
+        lp.dummy_data_param.data_filler.add().CopyFrom(f)
+    return lp
+
+
+def test_filter_net_phase_level_stage():
+    n = proto.parse_prototxt("""
+      name: "f"
+      layer { name: "a" type: "Silence" bottom: "x" include { phase: TRAIN } }
+      layer { name: "b" type: "Silence" bottom: "x" include { phase: TEST } }
+      layer { name: "c" type: "Silence" bottom: "x" include { min_level: 2 } }
+      layer { name: "d" type: "Silence" bottom: "x" include { stage: "s1" } }
+      layer { name: "e" type: "Silence" bottom: "x" exclude { not_stage: "s1" } }
+    """)
+    n.state.phase = proto.TRAIN
+    assert [l.name for l in filter_net(n).layer] == ["a"]
+    n.state.level = 3
+    n.state.stage.append("s1")
+    assert [l.name for l in filter_net(n).layer] == ["a", "c", "d", "e"]
+
+
+def test_insert_splits_names_and_loss_weight():
+    n = proto.parse_prototxt("""
+      name: "s"
+      layer { name: "data" type: "DummyData" top: "data" top: "label"
+              dummy_data_param { shape { dim: 2 dim: 3 } shape { dim: 2 } } }
+      layer { name: "ip" type: "InnerProduct" bottom: "data" top: "ip" inner_product_param { num_output: 4 } }
+      layer { name: "acc" type: "Accuracy" bottom: "ip" bottom: "label" top: "acc" }
+      layer { name: "loss" type: "SoftmaxWithLoss" bottom: "ip" bottom: "label" top: "loss" }
+    """)
+    s = insert_splits(n)
+    names = [l.name for l in s.layer]
+    assert "ip_ip_0_split" in names and "label_data_1_split" in names
+    split = s.layer[names.index("ip_ip_0_split")]
+    assert list(split.top) == ["ip_ip_0_split_0", "ip_ip_0_split_1"]
+    assert s.layer[names.index("acc")].bottom[0] == "ip_ip_0_split_0"
+    assert s.layer[names.index("loss")].bottom[0] == "ip_ip_0_split_1"
+
+
+def test_need_backward_pruning_and_outputs():
+    net = Net(models.lenet(train_batch=2, test_batch=2), phase=proto.TEST)
+    nb = dict(zip(net.layer_names, net.layer_need_backward))
+    assert nb["conv1"] and nb["ip2"]
+    assert not nb["accuracy"]
+    assert not any(net.bottom_need_backward[net.layer_names.index("conv1")])  # data needs no grad
+    assert sorted(b.name for b in net.output_blobs) == ["accuracy", "loss"]
+
+
+def test_param_sharing_by_name():
+    n = proto.parse_prototxt("""
+      name: "share"
+      layer { name: "data" type: "DummyData" top: "data" dummy_data_param { shape { dim: 2 dim: 5 }
+              data_filler { type: "gaussian" } } }
+      layer { name: "ip1" type: "InnerProduct" bottom: "data" top: "ip1" param { name: "w" } param { name: "b" }
+              inner_product_param { num_output: 5 weight_filler { type: "gaussian" } } }
+      layer { name: "ip2" type: "InnerProduct" bottom: "ip1" top: "ip2" param { name: "w" } param { name: "b" }
+              inner_product_param { num_output: 5 weight_filler { type: "gaussian" } } }
+      layer { name: "loss" type: "EuclideanLoss" bottom: "ip2" bottom: "data" top: "loss" }
+    """)
+    net = Net(n, phase=proto.TRAIN)
+    assert len(net.learnable_params) == 2
+    w1, w2 = net.layer_by_name("ip1").params[0], net.layer_by_name("ip2").params[0]
+    assert w1.data.data_ptr() == w2.data.data_ptr() and w1.diff.data_ptr() == w2.diff.data_ptr()
+    net.clear_param_diffs()
+    net.forward_backward()
+    # gradient of the shared weight == sum of both uses (check vs oracle)
+    wts = {"ip1": [p.to_caffe() for p in net.layer_by_name("ip1").params],
+           "ip2": [p.to_caffe() for p in net.layer_by_name("ip2").params]}
+    wts["ip2"] = wts["ip1"]
+    x = net.blob_by_name("data").data.clone()
+    # oracle with true sharing: the same leaf used twice
+    lw = [t.double().clone().requires_grad_(True) for t in wts["ip1"]]
+    h = x.double() @ lw[0].t() + lw[1]
+    h = h @ lw[0].t() + lw[1]
+    loss = ((h - x.double()) ** 2).sum() / 2 / 2
+    loss.backward()
+    assert torch.allclose(w1.diff.double(), lw[0].grad, rtol=1e-4, atol=1e-5)
+
+
+def _oracle_compare(netparam, batch_inputs, tol=2e-4, wscale=0.1):
+    net = Net(netparam, phase=proto.TRAIN)
+    g = torch.Generator().manual_seed(3)
+    for p in net.learnable_params:  # non-trivial weights for every param
+        p.set_caffe(torch.randn(p.caffe_shape, generator=g) * wscale)
+    for name, t in batch_inputs.items():
+        net.blob_by_name(name).set_nchw(t)
+    net.clear_param_diffs()
+    loss = net.forward_backward()
+    weights = {l.name: [p.to_caffe() for p in l.params] for l in net.layers if l.params}
+    tot, outs, leaves = torch_oracle.run(netparam, proto.TRAIN, weights, batch_inputs)
+    tot.backward()
+    assert abs(float(loss) - float(tot)) < tol * max(1.0, abs(float(tot))), (float(loss), float(tot))
+    for lname, ws in leaves.items():
+        mine = net.layer_by_name(lname).params
+        for p, w in zip(mine, ws):
+            d = p.to_caffe(p.diff).double()
+            err = (d - w.grad).abs().max().item()
+            scale = w.grad.abs().max().item() + 1e-12
+            assert err / scale < 1e-3, (lname, err, scale)
+
+
+def test_cifar10_quick_matches_oracle():
+    n = models.cifar10_quick(train_batch=3, test_batch=3)
+    g = torch.Generator().manual_seed(0)
+    _oracle_compare(n, {"data": torch.randn(3, 3, 32, 32, generator=g),
+                        "label": torch.tensor([[1.0], [7.0], [3.0]])})
+
+
+def test_cifar10_full_matches_oracle():
+    n = models.cifar10_full(train_batch=2, test_batch=2)
+    g = torch.Generator().manual_seed(1)
+    # moderate logits: Caffe clamps p_label at FLT_MIN (loss <= 87.34), the oracle does not
+    _oracle_compare(n, {"data": torch.randn(2, 3, 32, 32, generator=g) * 0.3,
+                        "label": torch.tensor([[4.0], [9.0]])})
+
+
+def test_caffenet_small_matches_oracle():
+    """Grouped convs, cross-channel LRN, IP on a 4-D (NHWC) bottom with HWC->CHW weight
+    permutation, dropout in TEST-like identity (ratio 0 here)."""
+    n = models.caffenet(train_batch=2, test_batch=2, crop=99, classes=7)
+    for l in n.layer:
+        if l.type == "Dropout":
+            l.dropout_param.dropout_ratio = 0.0
+        if l.type == "InnerProduct" and l.name in ("fc6", "fc7"):
+            l.inner_product_param.num_output = 16
+    g = torch.Generator().manual_seed(2)
+    _oracle_compare(n, {"data": torch.randn(2, 3, 99, 99, generator=g),
+                        "label": torch.tensor([[1.0], [5.0]])})
+
+
+def test_googlenet_small_matches_oracle():
+    n = models.googlenet(train_batch=1, test_batch=1, crop=64, classes=5, aux=False)
+    for l in n.layer:
+        if l.type == "Dropout":
+            l.dropout_param.dropout_ratio = 0.0
+        if l.name == "pool5/7x7_s1":
+            l.pooling_param.ClearField("kernel_h")
+            l.pooling_param.ClearField("kernel_w")
+            l.pooling_param.ClearField("stride_h")
+            l.pooling_param.ClearField("stride_w")
+            l.pooling_param.global_pooling = True
+    g = torch.Generator().manual_seed(4)
+    _oracle_compare(n, {"data": torch.randn(1, 3, 64, 64, generator=g), "label": torch.tensor([[3.0]])},
+                    wscale=0.03)
+
+
+def test_forward_reshape_and_blob_views():
+    net = Net(models.cifar10_quick(train_batch=2, test_batch=2), phase=proto.TRAIN)
+    b = net.blob_by_name("conv1")
+    assert b.shape == (2, 32, 32, 32) and tuple(b.data.shape) == (2, 32, 32, 32)
+    assert tuple(net.blob_by_name("pool1").nchw().shape) == (2, 32, 16, 16)
+
+
+def test_loss_weight_scales_gradient():
+    base = models.cifar10_quick(train_batch=2, test_batch=2)
+    inputs = {"data": torch.randn(2, 3, 32, 32), "label": torch.tensor([[1.0], [2.0]])}
+    grads = []
+    for lw in (1.0, 2.5):
+        n = proto.copy(base)
+        for l in n.layer:
+            if l.type == "SoftmaxWithLoss":
+                l.loss_weight.append(lw)
+        net = Net(n, phase=proto.TRAIN, seed=5)
+        for k, v in inputs.items():
+            net.blob_by_name(k).set_nchw(v)
+        net.clear_param_diffs()
+        net.forward_backward()
+        grads.append(net.flat_diff.clone())
+    assert torch.allclose(grads[1], 2.5 * grads[0], rtol=1e-4, atol=1e-9)
