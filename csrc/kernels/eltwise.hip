@@ -239,3 +239,82 @@ extern "C" int sn_flip_weights(const bf16_t* w, bf16_t* wt, long long G, long lo
                      (int)R, (int)S, (int)Cg);
   return SN_CHECK_LAUNCH();
 }
+
+// ---------------- space-to-depth folding of strided low-channel convolutions -------------
+// A stride-f conv with R x S taps on C channels (e.g. AlexNet conv1: f=4, 11x11x3) equals a
+// stride-1 conv with ceil(R/f) x ceil(S/f) taps on f*f*Cp channels of the space-to-depth
+// input, Cp >= C chosen so f*f*Cp % 8 == 0.  That turns the reference's per-image im2col
+// + SGEMM (the single most expensive layer of the net) into the implicit-GEMM fast path.
+//   x2[n][i][j][(dy*f + dx)*Cp + c] = x[n][i*f + dy - ph][j*f + dx - pw][c]   (0 outside)
+__global__ void s2d_input(const bf16_t* __restrict__ x, bf16_t* __restrict__ x2, int N, int H, int W, int C,
+                          int Hs, int Ws, int f, int Cp, int ph, int pw) {
+  const long long total = (long long)N * Hs * Ws;
+  const int C2 = f * f * Cp;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(i % Ws), r = (int)((i / Ws) % Hs), n = (int)(i / ((long long)Ws * Hs));
+    bf16_t* o = x2 + i * C2;
+    for (int dy = 0; dy < f; ++dy) {
+      const int h = r * f + dy - ph;
+      for (int dx = 0; dx < f; ++dx) {
+        const int w = j * f + dx - pw;
+        const bool v = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        const bf16_t* s = x + (((long long)n * H + h) * W + w) * C;
+        for (int c = 0; c < Cp; ++c) o[(dy * f + dx) * Cp + c] = (v && c < C) ? s[c] : (bf16_t)0;
+      }
+    }
+  }
+}
+
+// W [K][R][S][C] (bf16) -> W2 [K][Rf][Sf][f*f*Cp] (bf16, zero padded)
+__global__ void s2d_weight(const bf16_t* __restrict__ w, bf16_t* __restrict__ w2, int K, int R, int S, int C,
+                           int f, int Cp, int Rf, int Sf) {
+  const int C2 = f * f * Cp;
+  const long long total = (long long)K * Rf * Sf * C2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int cc = (int)(i % C2);
+    long long t = i / C2;
+    const int sf = (int)(t % Sf); t /= Sf;
+    const int rf = (int)(t % Rf);
+    const int k = (int)(t / Rf);
+    const int c = cc % Cp, d = cc / Cp, dx = d % f, dy = d / f;
+    const int r = rf * f + dy, s = sf * f + dx;
+    w2[i] = (r < R && s < S && c < C) ? w[(((long long)k * R + r) * S + s) * C + c] : (bf16_t)0;
+  }
+}
+
+// dW [K][R][S][C] (f32) += fold(dW2 [K][Rf][Sf][f*f*Cp] (f32))
+__global__ void s2d_weight_grad(const float* __restrict__ dw2, float* __restrict__ dw, int K, int R, int S, int C,
+                                int f, int Cp, int Rf, int Sf) {
+  const long long total = (long long)K * R * S * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    long long t = i / C;
+    const int s = (int)(t % S); t /= S;
+    const int r = (int)(t % R);
+    const int k = (int)(t / R);
+    const int rf = r / f, dy = r % f, sf = s / f, dx = s % f;
+    dw[i] += dw2[(((long long)k * Rf + rf) * Sf + sf) * (f * f * Cp) + (dy * f + dx) * Cp + c];
+  }
+}
+
+extern "C" int sn_s2d_input(const bf16_t* x, bf16_t* x2, long long N, long long H, long long W, long long C,
+                            long long Hs, long long Ws, long long f, long long Cp, long long ph, long long pw,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(s2d_input, dim3(sn_blocks(N * Hs * Ws, 256, 16384)), dim3(256), 0, st, x, x2, (int)N, (int)H,
+                     (int)W, (int)C, (int)Hs, (int)Ws, (int)f, (int)Cp, (int)ph, (int)pw);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_s2d_weight(const bf16_t* w, bf16_t* w2, long long K, long long R, long long S, long long C,
+                             long long f, long long Cp, long long Rf, long long Sf, hipStream_t st) {
+  hipLaunchKernelGGL(s2d_weight, dim3(sn_blocks(K * Rf * Sf * f * f * Cp, 256, 16384)), dim3(256), 0, st, w, w2,
+                     (int)K, (int)R, (int)S, (int)C, (int)f, (int)Cp, (int)Rf, (int)Sf);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_s2d_weight_grad(const float* dw2, float* dw, long long K, long long R, long long S, long long C,
+                                  long long f, long long Cp, long long Rf, long long Sf, hipStream_t st) {
+  hipLaunchKernelGGL(s2d_weight_grad, dim3(sn_blocks(K * R * S * C, 256, 16384)), dim3(256), 0, st, dw2, dw, (int)K,
+                     (int)R, (int)S, (int)C, (int)f, (int)Cp, (int)Rf, (int)Sf);
+  return SN_CHECK_LAUNCH();
+}

@@ -104,12 +104,21 @@ __global__ void colsum_pass1(const bf16_t* __restrict__ x, long long rows, int c
   }
 }
 
+// Pass 2: one 256-thread block per group of 64 columns; the 4 waves split the partial
+// rows, lanes own columns (coalesced), fixed-order combine in LDS (deterministic).
 __global__ void colsum_pass2(const float* __restrict__ part, int nparts, int cols, float* out, int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(long long)p * cols + c];
-  out[c] = (accumulate ? out[c] : 0.f) + s;
+  if (c < cols)
+    for (int p = w; p < nparts; p += 4) s += part[(long long)p * cols + c];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[c] = (accumulate ? out[c] : 0.f) + t;
+  }
 }
 
 // part must hold nparts*cols floats; returns via out[cols] (+= if accumulate).
@@ -122,7 +131,7 @@ extern "C" int sn_colsum_bf16(const bf16_t* x, long long rows, long long cols, l
   long long rpb = (rows + nparts - 1) / nparts;
   hipLaunchKernelGGL(colsum_pass1, dim3((unsigned)nparts), dim3(threads), threads * 8 * sizeof(float), st, x,
                      rows, (int)cols, ld, rpb, part);
-  hipLaunchKernelGGL(colsum_pass2, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, st, part, (int)nparts,
+  hipLaunchKernelGGL(colsum_pass2, dim3((unsigned)((cols + 63) / 64)), dim3(256), 0, st, part, (int)nparts,
                      (int)cols, out, (int)accumulate);
   return SN_CHECK_LAUNCH();
 }

@@ -83,7 +83,8 @@ def choose_splits(M: int, N: int, K: int, groups: int = 1) -> tuple[int, int]:
     tiles = -(-M // BM) * -(-N // BN) * groups
     splits = 1
     if tiles < TARGET_BLOCKS and K > 4 * BK:
-        splits = min(-(-TARGET_BLOCKS // tiles), max(1, K // (4 * BK)), 32)
+        ws_cap = max(1, (256 << 20) // max(1, 4 * M * N * groups))  # fp32 partial slabs <= 256 MB
+        splits = max(1, min(-(-TARGET_BLOCKS // tiles), K // (4 * BK), 256, ws_cap))
     kchunk = -(-K // splits)
     kchunk = -(-kchunk // BK) * BK
     splits = -(-K // kchunk)

@@ -60,9 +60,38 @@ def _geom(s: ConvSpec) -> ConvGeom:
     return ConvGeom(s.N, s.H, s.W, s.C, s.P, s.Q, s.R, s.S, s.sh, s.sw, s.ph, s.pw, s.dh, s.dw, s.Cg)
 
 
+def _s2d_plan(s: ConvSpec):
+    """Space-to-depth fold for strided, low-channel, ungrouped convs (input layers):
+    returns (f, Cp, Rf, Sf, folded ConvSpec) or None."""
+    if _implicit_ok(s) or s.groups != 1 or s.sh != s.sw or s.sh < 2 or s.dh != 1 or s.dw != 1:
+        return None
+    f = s.sh
+    cp = s.C
+    while (f * f * cp) % 8:
+        cp += 1
+    rf, sf = -(-s.R // f), -(-s.S // f)
+    hs, ws = s.P + rf - 1, s.Q + sf - 1
+    s2 = ConvSpec(s.N, hs, ws, f * f * cp, s.K, rf, sf, 1, 1, 0, 0, 1, 1, 1)
+    assert s2.P == s.P and s2.Q == s.Q
+    return f, cp, rf, sf, s2
+
+
+def _s2d_input(x, s: ConvSpec, plan):
+    f, cp, rf, sf, s2 = plan
+    x2 = torch.empty((s.N, s2.H, s2.W, s2.C), dtype=BF16, device=x.device)
+    call("s2d_input", x, x2, s.N, s.H, s.W, s.C, s2.H, s2.W, f, cp, s.ph, s.pw)
+    return x2
+
+
 def conv_forward(x, w, b, s: ConvSpec, relu=False):
     x = _c(x)
     assert x.dtype == BF16 and w.dtype == BF16, (x.dtype, w.dtype)
+    plan = _s2d_plan(s)
+    if plan is not None:
+        f, cp, rf, sf, s2 = plan
+        w2 = torch.empty((s.K, rf, sf, s2.C), dtype=BF16, device=x.device)
+        call("s2d_weight", _c(w), w2, s.K, s.R, s.S, s.C, f, cp, rf, sf)
+        return conv_forward(_s2d_input(x, s, plan), w2, b, s2, relu)
     M = s.N * s.P * s.Q
     y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device)
     if _implicit_ok(s):
@@ -96,6 +125,16 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None):
     if db is not None:
         colsum(dy2, db, accumulate=True)
     kred = s.R * s.S * s.Cg
+    plan = _s2d_plan(s) if s.Kg % 8 == 0 else None
+    if dw is not None and plan is not None:
+        f, cp, rf, sf, s2 = plan
+        x2 = _s2d_input(x, s, plan)
+        k2 = rf * sf * s2.C
+        dw2 = torch.empty((s.K, k2), dtype=torch.float32, device=x.device)
+        gemm(s.K, k2, M, Dense(dy2, s.K, kcontig=False), Im2col(x2, _geom(s2), kcontig=False), dw2, k2,
+             epi=EPI_F32)
+        call("s2d_weight_grad", dw2, dw, s.K, s.R, s.S, s.C, f, cp, rf, sf)
+        dw = None
     if dw is not None:
         if _implicit_ok(s) and s.Kg % 8 == 0:
             A = Dense(dy2, s.K, kcontig=False, gstride=s.Kg)

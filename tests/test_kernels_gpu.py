@@ -27,7 +27,9 @@ CONV_CASES = [
     # N, H, W, C, K, R, S, stride, pad, groups
     (2, 13, 13, 16, 32, 3, 3, 1, 1, 1),
     (2, 27, 27, 48, 64, 5, 5, 1, 2, 2),      # AlexNet conv2-like (grouped)
-    (2, 35, 35, 3, 16, 11, 11, 4, 0, 1),     # conv1-like (explicit im2col path)
+    (2, 35, 35, 3, 16, 11, 11, 4, 0, 1),     # conv1-like (space-to-depth folded path)
+    (2, 30, 30, 3, 16, 7, 7, 2, 3, 1),       # GoogLeNet conv1-like (s2d with channel pad 3->4)
+    (2, 28, 28, 1, 20, 5, 5, 1, 0, 1),       # LeNet conv1 (explicit im2col path)
     (2, 16, 16, 32, 24, 1, 1, 1, 0, 1),      # 1x1
     (2, 15, 15, 16, 16, 3, 3, 2, 1, 1),      # stride 2 dgrad fallback
     (2, 12, 12, 20, 50, 5, 5, 1, 0, 1),      # LeNet conv2 (odd channels)

@@ -182,4 +182,5 @@ def test_loss_weight_scales_gradient():
         net.clear_param_diffs()
         net.forward_backward()
         grads.append(net.flat_diff.clone())
-    assert torch.allclose(grads[1], 2.5 * grads[0], rtol=1e-4, atol=1e-9)
+    scale = grads[0].abs().max()
+    assert torch.allclose(grads[1], 2.5 * grads[0], rtol=1e-3, atol=1e-5 * float(scale))
