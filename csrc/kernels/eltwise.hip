@@ -248,20 +248,30 @@ extern "C" int sn_flip_weights(const bf16_t* w, bf16_t* wt, long long G, long lo
 //   x2[n][i][j][(dy*f + dx)*Cp + c] = x[n][i*f + dy - ph][j*f + dx - pw][c]   (0 outside)
 __global__ void s2d_input(const bf16_t* __restrict__ x, bf16_t* __restrict__ x2, int N, int H, int W, int C,
                           int Hs, int Ws, int f, int Cp, int ph, int pw) {
-  const long long total = (long long)N * Hs * Ws;
+  // one thread per 16-B output chunk (8 folded channels): coalesced stores, the scattered
+  // 2-B gathers hit L1/L2 (neighbouring chunks read the same input rows).
   const int C2 = f * f * Cp;
+  const int cv = C2 / 8;
+  const long long total = (long long)N * Hs * Ws * cv;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(i % Ws), r = (int)((i / Ws) % Hs), n = (int)(i / ((long long)Ws * Hs));
-    bf16_t* o = x2 + i * C2;
-    for (int dy = 0; dy < f; ++dy) {
-      const int h = r * f + dy - ph;
-      for (int dx = 0; dx < f; ++dx) {
-        const int w = j * f + dx - pw;
-        const bool v = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-        const bf16_t* s = x + (((long long)n * H + h) * W + w) * C;
-        for (int c = 0; c < Cp; ++c) o[(dy * f + dx) * Cp + c] = (v && c < C) ? s[c] : (bf16_t)0;
+    const int e0 = (int)(i % cv) * 8;
+    const long long pix = i / cv;
+    const int j = (int)(pix % Ws), r = (int)((pix / Ws) % Hs), n = (int)(pix / ((long long)Ws * Hs));
+    uint32_t w32[4];
+#pragma unroll
+    for (int t = 0; t < 8; t += 2) {
+      bf16_t v2[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = e0 + t + u;
+        const int d = e / Cp, c = e - d * Cp;
+        const int h = r * f + d / f - ph, w = j * f + d % f - pw;
+        const bool v = c < C && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        v2[u] = v ? x[(((long long)n * H + h) * W + w) * C + c] : (bf16_t)0;
       }
+      w32[t / 2] = (uint32_t)v2[0] | ((uint32_t)v2[1] << 16);
     }
+    reinterpret_cast<uint4*>(x2)[i] = make_uint4(w32[0], w32[1], w32[2], w32[3]);
   }
 }
 
@@ -300,7 +310,9 @@ __global__ void s2d_weight_grad(const float* __restrict__ dw2, float* __restrict
 extern "C" int sn_s2d_input(const bf16_t* x, bf16_t* x2, long long N, long long H, long long W, long long C,
                             long long Hs, long long Ws, long long f, long long Cp, long long ph, long long pw,
                             hipStream_t st) {
-  hipLaunchKernelGGL(s2d_input, dim3(sn_blocks(N * Hs * Ws, 256, 16384)), dim3(256), 0, st, x, x2, (int)N, (int)H,
+  if ((f * f * Cp) % 8) return 7;
+  hipLaunchKernelGGL(s2d_input, dim3(sn_blocks(N * Hs * Ws * (f * f * Cp / 8), 256, 16384)), dim3(256), 0, st, x, x2,
+                     (int)N, (int)H,
                      (int)W, (int)C, (int)Hs, (int)Ws, (int)f, (int)Cp, (int)ph, (int)pw);
   return SN_CHECK_LAUNCH();
 }

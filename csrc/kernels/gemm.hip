@@ -18,16 +18,17 @@
 // [N*P*Q pixels] x [R*S*Cg] patch matrix of an NHWC tensor, gathered on the fly with
 // zero-fill for padding — no column buffer in HBM.
 //
-// Tile 128x128x64, 256 threads (2x2 waves, 64x64 per wave = 4x4 MFMA tiles), LDS
-// double buffered (64 KiB) with XOR swizzles that make both the b128 row reads and the
-// tr_b16 transposed reads bank-conflict free, register-staged global->LDS copies
-// issued one tile ahead (load early / write late), XCD-aware bijective block remap.
+// Block tile BM x BN x 64 with 256 threads = 4 waves, each wave owning a 64x64 output
+// sub-tile (4x4 MFMA tiles): (BM, BN) = (128, 128) or (256, 64) for skinny N (e.g.
+// 48-channel grouped dgrad).  LDS double buffered with XOR swizzles that make both the
+// b128 row reads and the tr_b16 transposed reads bank-conflict free, register-staged
+// global->LDS copies issued one tile ahead (load early / write late), XCD-aware
+// bijective block remap.
 #include "common.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
-constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile, either orientation
+constexpr int BK = 64, NTHR = 256;
 
 enum { OP_DENSE = 0, OP_IM2COL = 1 };
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2 };
@@ -60,37 +61,48 @@ struct SnGemmArgs {
   long long ldc, c_gstride, c_split_stride;
   const float* bias;  // per output column n (offset by g*N), EPI_BF16 only
   int relu;
+  int tile;           // 0: 128x128, 1: 256x64
 };
 
 }  // extern "C"
 
 namespace {
 
-SN_DEV int swz_mc(int k) { return (((k & 3) | (((k >> 3) & 1) << 2)) << 5); }
+// KC tile: [TILE rows][64 k] bf16, 128-B rows, 16-B chunk index XOR (row>>1)&7.
 SN_DEV int kc_off(int row, int kc) { return row * 128 + ((kc ^ ((row >> 1) & 7)) << 4); }
-SN_DEV int mc_off(int k, int mc) { return k * 256 + ((mc << 4) ^ swz_mc(k)); }
 
-// Per-thread staging state of one operand.  KC tiles: the thread owns 4 chunks on rows
-// (tid>>3)+32i, chunk column tid&7 (fixed).  MC tiles: rows (tid>>4)+16i, chunk column
-// tid&15 (fixed).
-template <int MC, int MODE>
+// MC tile: [64 k rows][TILE cols] bf16 (TILE*2-byte rows).  32-B granules XOR-swizzled
+// so the 8 rows a half-wave tr-reads land in 8 distinct granules of the 256-B bank row.
+template <int TILE>
+SN_DEV int swz_mc(int k) {
+  if (TILE >= 128) return (((k & 3) | (((k >> 3) & 1) << 2)) << 5);
+  return ((((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 5);  // 128-B rows: 2 rows per bank row
+}
+template <int TILE>
+SN_DEV int mc_off(int k, int mc) { return k * (TILE * 2) + ((mc << 4) ^ swz_mc<TILE>(k)); }
+
+// Per-thread staging state of one operand tile (TILE = rows of the M/N axis).
+//   KC: chunks on rows (tid>>3) + 32i, chunk column tid&7 (fixed), TILE/32 chunks.
+//   MC: CPR = TILE/8 chunks per k-row; rows tid/CPR + (256/CPR) i, column tid%CPR.
+template <int MC, int MODE, int TILE>
 struct Stager {
+  static constexpr int NCH = TILE / 32;
+  static constexpr int CPR = TILE / 8;
+  static constexpr int RPP = MC ? (NTHR / CPR) : 32;  // rows per pass
   const bf16_t* base;
   long long ld;
   SnConvGeom g;
-  int coff;         // IM2COL group channel offset
-  int fixed;        // KC: kc ; MC: mc
-  int row0;         // first row of this thread (tile-relative)
-  // KC+IM2COL: per-row pixel decode (rows are fixed across k)
-  int pn[4], ph[4], pw[4];
-  bool pv[4];
-  // MC+IM2COL: column decode (cols are fixed across k)
-  int ctap_r, ctap_s, cc;
+  int coff;   // IM2COL group channel offset
+  int fixed;  // KC: kc ; MC: mc
+  int row0;   // first row of this thread (tile-relative)
+  int pn[NCH], ph[NCH], pw[NCH];  // KC+IM2COL: per-row pixel decode (rows fixed across k)
+  bool pv[NCH];
+  int ctap_r, ctap_s, cc;  // MC+IM2COL: column decode (cols fixed across k)
   bool cv;
-  uint4 reg[4];
+  uint4 reg[NCH];
 
-  SN_DEV void init(const SnOperand& op, int grp, int tid, int tile_row0, int rows_lim,
-                   int tile_col0, int cols_lim) {
+  SN_DEV void init(const SnOperand& op, int grp, int tid, int tile_row0, int rows_lim, int tile_col0,
+                   int cols_lim) {
     ld = op.ld;
     g = op.g;
     if (MODE == OP_DENSE) {
@@ -106,7 +118,7 @@ struct Stager {
       if (MODE == OP_IM2COL) {
         const int PQ = g.P * g.Q;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NCH; ++i) {
           int pix = tile_row0 + row0 + 32 * i;
           pv[i] = pix < rows_lim;
           int n = pix / PQ, pq = pix - n * PQ;
@@ -117,8 +129,8 @@ struct Stager {
         }
       }
     } else {
-      fixed = tid & 15;
-      row0 = tid >> 4;
+      fixed = tid % CPR;
+      row0 = tid / CPR;
       if (MODE == OP_IM2COL) {
         int col = tile_col0 + fixed * 8;
         cv = col < cols_lim;
@@ -133,7 +145,6 @@ struct Stager {
   SN_DEV uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
   // Issue the global loads of the tile whose first reduction index is k_tile.
-  // KC: rows are M/N indices (tile_row0 + ...), cols k.  MC: rows k, cols M/N.
   SN_DEV void load(int k_tile, int k_lim, int tile_rc0, int rc_lim) {
     const uint4 z = make_uint4(0, 0, 0, 0);
     if (!MC) {
@@ -141,7 +152,7 @@ struct Stager {
       const bool kv = k < k_lim;
       if (MODE == OP_DENSE) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NCH; ++i) {
           int row = tile_rc0 + row0 + 32 * i;
           reg[i] = (kv && row < rc_lim) ? ld16(base + (long long)row * ld + k) : z;
         }
@@ -150,7 +161,7 @@ struct Stager {
         int r = tap / g.S, s = tap - r * g.S;
         int dh = r * g.dh, dw = s * g.dw;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NCH; ++i) {
           int h = ph[i] + dh, w = pw[i] + dw;
           bool v = kv && pv[i] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
           long long off = ((long long)(pn[i] + h) * g.W + w) * g.C + coff + c;
@@ -162,15 +173,15 @@ struct Stager {
       if (MODE == OP_DENSE) {
         const bool cvd = col < rc_lim;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          int k = k_tile + row0 + 16 * i;
+        for (int i = 0; i < NCH; ++i) {
+          int k = k_tile + row0 + RPP * i;
           reg[i] = (cvd && k < k_lim) ? ld16(base + (long long)k * ld + col) : z;
         }
       } else {
         const int PQ = g.P * g.Q;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          int pix = k_tile + row0 + 16 * i;
+        for (int i = 0; i < NCH; ++i) {
+          int pix = k_tile + row0 + RPP * i;
           int n = pix / PQ, pq = pix - n * PQ;
           int p = pq / g.Q, q = pq - p * g.Q;
           int h = p * g.sh - g.ph + ctap_r * g.dh;
@@ -185,8 +196,8 @@ struct Stager {
 
   SN_DEV void store(char* lds) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int off = MC ? mc_off(row0 + 16 * i, fixed) : kc_off(row0 + 32 * i, fixed);
+    for (int i = 0; i < NCH; ++i) {
+      int off = MC ? mc_off<TILE>(row0 + RPP * i, fixed) : kc_off(row0 + 32 * i, fixed);
       *reinterpret_cast<uint4*>(lds + off) = reg[i];
     }
   }
@@ -195,7 +206,7 @@ struct Stager {
 // Fragment of a 16-row subtile (rows x0..x0+15 of the operand's M/N axis) for k-step s
 // (32 reduction elements), laid out as the 16x16x32 MFMA operand: lane l holds
 // X[x0 + (l&15)][32s + 8(l>>4) + j], j = 0..7.
-template <int MC>
+template <int MC, int TILE>
 SN_DEV bf16x8_t read_frag(const char* lds, int x0, int s, int lane) {
   if (!MC) {
     int row = x0 + (lane & 15);
@@ -203,13 +214,15 @@ SN_DEV bf16x8_t read_frag(const char* lds, int x0, int s, int lane) {
     uint4 v = *reinterpret_cast<const uint4*>(lds + kc_off(row, kc));
     return __builtin_bit_cast(bf16x8_t, v);
   } else {
+    // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q, cols 4p..4p+3
+    // of a 4x16 block; lane i receives column i of the 4 rows.  Two reads = 8 k values.
     int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
     int col_b = (x0 + 4 * p) * 2;
     int k0 = s * 32 + gq * 8 + q;
     int k1 = k0 + 4;
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-    const char* a0 = lds + k0 * 256 + (col_b ^ swz_mc(k0));
-    const char* a1 = lds + k1 * 256 + (col_b ^ swz_mc(k1));
+    const char* a0 = lds + k0 * (TILE * 2) + (col_b ^ swz_mc<TILE>(k0));
+    const char* a1 = lds + k1 * (TILE * 2) + (col_b ^ swz_mc<TILE>(k1));
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
     s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -217,9 +230,12 @@ SN_DEV bf16x8_t read_frag(const char* lds, int x0, int s, int lane) {
   }
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int EPI>
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN>
 __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int WN = BN / 64, WM = 4 / WN;  // waves along N / M (64x64 per wave)
+  static_assert(WM * 64 == BM, "tile/wave layout mismatch");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (args.M + BM - 1) / BM;
 
@@ -237,9 +253,8 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
   const int k0 = split * args.kchunk;
   const int k1 = min(args.K, k0 + args.kchunk);
 
-
-  Stager<AMC, AMODE> sa;
-  Stager<BMC, BMODE> sb;
+  Stager<AMC, AMODE, BM> sa;
+  Stager<BMC, BMODE, BN> sb;
   sa.init(args.A, grp, tid, m_blk, args.M, m_blk, args.M);
   sb.init(args.B, grp, tid, n_blk, args.N, n_blk, args.N);
 
@@ -249,14 +264,14 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int wm0 = (wave & 1) * 64, wn0 = (wave >> 1) * 64;
+  const int wm0 = (wave % WM) * 64, wn0 = (wave / WM) * 64;
   const int nk = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
 
   if (nk > 0) {
     sa.load(k0, k1, m_blk, args.M);
     sb.load(k0, k1, n_blk, args.N);
     sa.store(smem);
-    sb.store(smem + TILE_BYTES);
+    sb.store(smem + A_BYTES);
     __syncthreads();
   }
   int cur = 0;
@@ -266,15 +281,15 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
       sa.load(k0 + (kt + 1) * BK, k1, m_blk, args.M);
       sb.load(k0 + (kt + 1) * BK, k1, n_blk, args.N);
     }
-    const char* la = smem + cur * (2 * TILE_BYTES);
-    const char* lb = la + TILE_BYTES;
+    const char* la = smem + cur * STAGE;
+    const char* lb = la + A_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8_t fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fb[i] = read_frag<BMC>(lb, wn0 + 16 * i, s, lane);
+      for (int i = 0; i < 4; ++i) fb[i] = read_frag<BMC, BN>(lb, wn0 + 16 * i, s, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag<AMC>(la, wm0 + 16 * i, s, lane);
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -282,8 +297,9 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
     }
     if (more) {
-      sa.store(smem + (cur ^ 1) * (2 * TILE_BYTES));
-      sb.store(smem + (cur ^ 1) * (2 * TILE_BYTES) + TILE_BYTES);
+      char* nxt = smem + (cur ^ 1) * STAGE;
+      sa.store(nxt);
+      sb.store(nxt + A_BYTES);
     }
     __syncthreads();
     cur ^= 1;
@@ -323,8 +339,8 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
             if (n + r < args.N) C[n + r] = f2bf(o[r]);
         }
       } else {
-        float* C = reinterpret_cast<float*>(args.C) + split * args.c_split_stride +
-                   grp * args.c_gstride + (long long)m * args.ldc;
+        float* C = reinterpret_cast<float*>(args.C) + split * args.c_split_stride + grp * args.c_gstride +
+                   (long long)m * args.ldc;
         if (full) {
           float4* p = reinterpret_cast<float4*>(C + n);
           if (EPI == EPI_F32_ACC) {
@@ -348,22 +364,38 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
   }
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE>
+template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN>
 int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16>), grid, dim3(NTHR), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN>), grid, dim3(NTHR), 0, st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32>), grid, dim3(NTHR), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN>), grid, dim3(NTHR), 0, st, a);
       break;
     case EPI_F32_ACC:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC>), grid, dim3(NTHR), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN>), grid, dim3(NTHR), 0, st, a);
       break;
     default:
       return 2;
   }
   return SN_CHECK_LAUNCH();
+}
+
+template <int BM, int BN>
+int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, a.splits, a.groups);
+  const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  switch (key) {
+    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, BM, BN>(a, grid, stream);    // NT dense
+    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, BM, BN>(a, grid, stream);   // conv fwd/dgrad
+    case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE, BM, BN>(a, grid, stream);    // NN dense
+    case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE, BM, BN>(a, grid, stream);    // TN dense
+    case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL, BM, BN>(a, grid, stream);   // conv wgrad
+    case 0b1000: return launch_epi<1, OP_DENSE, 0, OP_DENSE, BM, BN>(a, grid, stream);
+    default: return 4;
+  }
 }
 
 }  // namespace
@@ -372,17 +404,6 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   const SnGemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
   if (a.kchunk <= 0 || (a.kchunk % BK) != 0) return 3;
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles, a.splits, a.groups);
-  // Supported operand combinations (see module docstring).
-  const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
-  switch (key) {
-    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE>(a, grid, stream);    // NT dense
-    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE>(a, grid, stream);   // conv fwd/dgrad
-    case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE>(a, grid, stream);    // NN dense
-    case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE>(a, grid, stream);    // TN dense
-    case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL>(a, grid, stream);   // conv wgrad
-    case 0b1000: return launch_epi<1, OP_DENSE, 0, OP_DENSE>(a, grid, stream);    // TT-ish
-    default: return 4;
-  }
+  if (a.tile == 1) return launch_tile<256, 64>(a, stream);
+  return launch_tile<128, 128>(a, stream);
 }

@@ -106,17 +106,26 @@ __global__ void colsum_pass1(const bf16_t* __restrict__ x, long long rows, int c
 
 // Pass 2: one 256-thread block per group of 64 columns; the 4 waves split the partial
 // rows, lanes own columns (coalesced), fixed-order combine in LDS (deterministic).
-__global__ void colsum_pass2(const float* __restrict__ part, int nparts, int cols, float* out, int accumulate) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+__global__ void __launch_bounds__(1024) colsum_pass2(const float* __restrict__ part, int nparts, int cols, float* out,
+                                                     int accumulate) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;  // 16 waves split the partial rows
   const int c = blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (c < cols)
-    for (int p = w; p < nparts; p += 4) s += part[(long long)p * cols + c];
-  red[w][lane] = s;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < cols) {
+    int p = w;
+    for (; p + 16 < nparts; p += 32) {
+      s0 += part[(long long)p * cols + c];
+      s1 += part[(long long)(p + 16) * cols + c];
+    }
+    if (p < nparts) s0 += part[(long long)p * cols + c];
+  }
+  red[w][lane] = s0 + s1;
   __syncthreads();
   if (w == 0 && c < cols) {
-    float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][lane];
     out[c] = (accumulate ? out[c] : 0.f) + t;
   }
 }
@@ -131,7 +140,7 @@ extern "C" int sn_colsum_bf16(const bf16_t* x, long long rows, long long cols, l
   long long rpb = (rows + nparts - 1) / nparts;
   hipLaunchKernelGGL(colsum_pass1, dim3((unsigned)nparts), dim3(threads), threads * 8 * sizeof(float), st, x,
                      rows, (int)cols, ld, rpb, part);
-  hipLaunchKernelGGL(colsum_pass2, dim3((unsigned)((cols + 63) / 64)), dim3(256), 0, st, part, (int)nparts,
+  hipLaunchKernelGGL(colsum_pass2, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st, part, (int)nparts,
                      (int)cols, out, (int)accumulate);
   return SN_CHECK_LAUNCH();
 }

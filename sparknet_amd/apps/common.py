@@ -1,0 +1,75 @@
+"""Shared plumbing of the training entry points (one process per GPU).
+
+Launch: ``python -m sparknet_amd.apps.<app> ...`` on one GPU, or
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 -m
+sparknet_amd.apps.<app> ...`` for N GPUs (replaces ``spark-submit --class apps.X jar N``,
+README.md:26).  Ranks map 1:1 to GPUs.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+
+import torch
+
+
+def base_parser(desc: str, **defaults) -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description=desc)
+    p.add_argument("--data", default=None, help="dataset directory (omit for --synthetic)")
+    p.add_argument("--synthetic", action="store_true", help="synthetic data of the dataset's shape")
+    p.add_argument("--model", default=defaults.get("model"))
+    p.add_argument("--tau", type=int, default=defaults.get("tau", 10), help="local SGD steps per round")
+    p.add_argument("--rounds", type=int, default=defaults.get("rounds", 100))
+    p.add_argument("--test-every", type=int, default=defaults.get("test_every", 10))
+    p.add_argument("--batch", type=int, default=defaults.get("batch", 100))
+    p.add_argument("--test-batch", type=int, default=defaults.get("test_batch", 100))
+    p.add_argument("--weights", default=None, help=".caffemodel to initialise from")
+    p.add_argument("--resume", default=None, help="checkpoint prefix to resume from")
+    p.add_argument("--snapshot-every", type=int, default=0, help="checkpoint every k rounds (0 = off)")
+    p.add_argument("--snapshot-prefix", default="sparknet")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--cpu", action="store_true", help="run the fp32 reference path on the CPU")
+    p.add_argument("--sync-sgd", action="store_true", help="all-reduce gradients every step (tau=1 semantics)")
+    p.add_argument("--log-dir", default=None)
+    p.add_argument("--fail-at-round", type=int, default=-1, help="fault injection: rank 0 exits at round r")
+    return p
+
+
+def setup(args):
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.cpu or not torch.cuda.is_available():
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        from ..ops import _lib
+        _lib.kernels()
+    from ..parallel import Comm
+    comm = Comm(device=dev if dev.type == "cuda" else None) if world > 1 else None
+    return rank, world, dev, comm
+
+
+class StopFlag:
+    """SIGINT -> stop, SIGHUP -> snapshot at the next round boundary
+    (caffe/src/caffe/util/signal_handler.cpp:14-115 semantics)."""
+
+    def __init__(self):
+        self.request = "none"
+        try:
+            signal.signal(signal.SIGINT, self._stop)
+            signal.signal(signal.SIGHUP, self._snap)
+        except ValueError:  # not in the main thread
+            pass
+
+    def _stop(self, *a):
+        self.request = "stop"
+
+    def _snap(self, *a):
+        self.request = "snapshot"
+
+    def take(self) -> str:
+        r, self.request = self.request, "none"
+        return r

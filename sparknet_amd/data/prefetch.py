@@ -71,6 +71,35 @@ class TensorSource(HostBatchSource):
         return x, y
 
 
+class WindowedSource(HostBatchSource):
+    """SparkNet's per-round sampling: each round (``tau`` draws) uses a fresh random
+    contiguous window of tau minibatches of this rank's shard (MinibatchSampler.scala:18-19)."""
+
+    def __init__(self, images: torch.Tensor, labels: torch.Tensor, batch: int, tau: int, seed: int = 0,
+                 pin: bool = True):
+        from .sampler import MinibatchSampler
+        self._Sampler = MinibatchSampler
+        self.images, self.labels, self.batch, self.tau = images, labels.int(), batch, tau
+        self.nbatches = images.shape[0] // batch
+        if self.nbatches < 1:
+            raise ValueError("shard smaller than one minibatch")
+        self.seed = seed
+        self.round = 0
+        self.sampler = None
+        self.pin = pin and torch.cuda.is_available()
+
+    def next_batch(self):
+        if self.sampler is None or self.sampler.image_pos >= self.sampler.n:
+            self.sampler = self._Sampler(self.nbatches, min(self.tau, self.nbatches), seed=self.seed * 7919 + self.round)
+            self.round += 1
+        idx = self.sampler.next_index()
+        sl = slice(idx * self.batch, (idx + 1) * self.batch)
+        x, y = self.images[sl].contiguous(), self.labels[sl].contiguous()
+        if self.pin:
+            x, y = x.pin_memory(), y.pin_memory()
+        return x, y
+
+
 class DeviceFeeder:
     """Double-buffered H2D + augment into a net's data/label blobs."""
 
@@ -136,10 +165,36 @@ class DeviceFeeder:
         if self.events[slot] is not None:
             torch.cuda.current_stream(self.device).wait_event(self.events[slot])
         src, lab = self.slots[slot]
+        if self.device.type != "cuda":
+            self._stage_cpu(src, lab)
+            return
         from ..ops import hip
         hip.augment(src, self.data_blob.data, self.crop, self.mean, self.mean_mode, self.scale, self.rng_state,
                     self.train, self.mirror)
         _lib.call("labels_to_float", lab, self.label_blob.data, lab.numel())
+
+    def _stage_cpu(self, src, lab) -> None:
+        """Reference (CPU) version of the augment kernel semantics."""
+        x = src.float()
+        N, C, H, W = x.shape
+        if self.mean_mode == 1:
+            x = x - self.mean.view(1, -1, 1, 1)
+        elif self.mean_mode == 2:
+            x = x - self.mean.view(1, C, H, W)
+        c = self.crop
+        out = torch.empty((N, C, c, c))
+        g = torch.Generator().manual_seed(int(self.rng_state[0]) * 1000003 + self.k)
+        for n in range(N):
+            if self.train:
+                ho = int(torch.randint(0, H - c + 1, (1,), generator=g))
+                wo = int(torch.randint(0, W - c + 1, (1,), generator=g))
+                mir = self.mirror and bool(torch.randint(0, 2, (1,), generator=g))
+            else:
+                ho, wo, mir = (H - c) // 2, (W - c) // 2, False
+            crop = x[n, :, ho:ho + c, wo:wo + c]
+            out[n] = crop.flip(-1) if mir else crop
+        self.data_blob.set_nchw(out * self.scale)
+        self.label_blob.data.copy_(lab.float().reshape(self.label_blob.data.shape))
 
     def __call__(self, layer=None, tops=None) -> None:
         """JavaData-layer source hook (eager mode): stage + prefetch the next batch."""

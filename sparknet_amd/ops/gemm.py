@@ -79,8 +79,17 @@ def _operand(op) -> tuple[_lib.SnOperand, int, int]:
     return s, 0 if op.kcontig else 1, OP_IM2COL
 
 
-def choose_splits(M: int, N: int, K: int, groups: int = 1) -> tuple[int, int]:
-    tiles = -(-M // BM) * -(-N // BN) * groups
+TILES = {0: (128, 128), 1: (256, 64)}
+
+
+def choose_tile(M: int, N: int) -> int:
+    """256x64 for skinny N (<= 64 per group, e.g. 48-channel grouped dgrad), else 128x128."""
+    return 1 if N <= 64 and M >= 256 else 0
+
+
+def choose_splits(M: int, N: int, K: int, groups: int = 1, tile: int = 0) -> tuple[int, int]:
+    bm, bn = TILES[tile]
+    tiles = -(-M // bm) * -(-N // bn) * groups
     splits = 1
     if tiles < TARGET_BLOCKS and K > 4 * BK:
         ws_cap = max(1, (256 << 20) // max(1, 4 * M * N * groups))  # fp32 partial slabs <= 256 MB
@@ -100,8 +109,9 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         return
     sa, a_mc, a_mode = _operand(A)
     sb, b_mc, b_mode = _operand(B)
+    tile = choose_tile(M, N)
     if splits is None:
-        splits, kchunk = choose_splits(M, N, K, groups)
+        splits, kchunk = choose_splits(M, N, K, groups, tile)
     else:
         kchunk = -(-(-(-K // splits)) // BK) * BK
         splits = max(1, -(-K // kchunk))
@@ -110,12 +120,12 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
     if splits == 1:
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, BK), a_mc, a_mode, b_mc, b_mode, epi,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
-                               bias.data_ptr() if bias is not None else 0, int(relu))
+                               bias.data_ptr() if bias is not None else 0, int(relu), tile)
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         return
     ws = torch.empty((groups, splits, M, N), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
-                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0)
+                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0, tile)
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
     _lib.call("splitk_reduce", ws, splits, M * N, M, N, N, out, ldc, mode, bias, int(relu),
@@ -195,6 +205,6 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate
 def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = True) -> None:
     """out[N] (+)= sum over rows of a bf16 [M, N] matrix (bias gradient)."""
     M, N = x.shape
-    nparts = max(1, min(1024, M // 64))
+    nparts = max(1, min(256, M // 256))
     part = torch.empty((nparts, N), dtype=torch.float32, device=x.device)
     _lib.call("colsum_bf16", x, M, N, x.stride(0), part, nparts, out, int(accumulate))

@@ -35,7 +35,7 @@ def test_identity_asymmetric(gpu):
     assert torch.equal(y.float(), w.float().t())
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 4096, 9216), (64, 10, 500), (128, 200, 136)])
+@pytest.mark.parametrize("M,N,K", [(256, 4096, 9216), (64, 10, 500), (128, 200, 136), (300, 200, 40)])
 def test_linear_dgrad(gpu, M, N, K):
     from sparknet_amd.ops import gemm
     dy, w = _bf(M, N, device=gpu), _bf(N, K, device=gpu)
@@ -43,7 +43,7 @@ def test_linear_dgrad(gpu, M, N, K):
     _close(dx, dy.float() @ w.float())
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 4096, 9216), (64, 10, 500), (300, 24, 136)])
+@pytest.mark.parametrize("M,N,K", [(256, 4096, 9216), (64, 10, 500), (300, 24, 136), (100, 300, 48), (512, 320, 56)])
 def test_linear_wgrad(gpu, M, N, K):
     from sparknet_amd.ops import gemm
     dy, x = _bf(M, N, device=gpu), _bf(M, K, device=gpu)
