@@ -47,6 +47,16 @@ SN_DEV uint4 pack8(const float* f) {
   return r;
 }
 
+// Fast division by a runtime-invariant divisor for 0 <= n < 2^24 (pixel / tap indices):
+// fp32 reciprocal estimate + one correction step replaces the ~40-instruction integer
+// division sequence in the implicit-GEMM address generators.
+SN_DEV int fdiv(int n, int d, float inv) {
+  int q = __float2int_rz((float)n * inv);
+  int r = n - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
 SN_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

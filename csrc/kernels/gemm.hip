@@ -99,6 +99,7 @@ struct Stager {
   bool pv[NCH];
   int ctap_r, ctap_s, cc;  // MC+IM2COL: column decode (cols fixed across k)
   bool cv;
+  float invPQ, invQ, invCg, invS;
   uint4 reg[NCH];
 
   SN_DEV void init(const SnOperand& op, int grp, int tid, int tile_row0, int rows_lim, int tile_col0,
@@ -117,12 +118,16 @@ struct Stager {
       row0 = tid >> 3;
       if (MODE == OP_IM2COL) {
         const int PQ = g.P * g.Q;
+        invPQ = 1.f / (float)PQ;
+        invQ = 1.f / (float)g.Q;
+        invCg = 1.f / (float)g.Cg;
+        invS = 1.f / (float)g.S;
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
           int pix = tile_row0 + row0 + 32 * i;
           pv[i] = pix < rows_lim;
-          int n = pix / PQ, pq = pix - n * PQ;
-          int p = pq / g.Q, q = pq - p * g.Q;
+          int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
+          int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
           pn[i] = n * g.H;
           ph[i] = p * g.sh - g.ph;
           pw[i] = q * g.sw - g.pw;
@@ -132,6 +137,8 @@ struct Stager {
       fixed = tid % CPR;
       row0 = tid / CPR;
       if (MODE == OP_IM2COL) {
+        invPQ = 1.f / (float)(g.P * g.Q);
+        invQ = 1.f / (float)g.Q;
         int col = tile_col0 + fixed * 8;
         cv = col < cols_lim;
         int tap = col / g.Cg;
@@ -157,8 +164,8 @@ struct Stager {
           reg[i] = (kv && row < rc_lim) ? ld16(base + (long long)row * ld + k) : z;
         }
       } else {
-        int tap = k / g.Cg, c = k - tap * g.Cg;
-        int r = tap / g.S, s = tap - r * g.S;
+        int tap = fdiv(k, g.Cg, invCg), c = k - tap * g.Cg;
+        int r = fdiv(tap, g.S, invS), s = tap - r * g.S;
         int dh = r * g.dh, dw = s * g.dw;
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
@@ -182,8 +189,8 @@ struct Stager {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
           int pix = k_tile + row0 + RPP * i;
-          int n = pix / PQ, pq = pix - n * PQ;
-          int p = pq / g.Q, q = pq - p * g.Q;
+          int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
+          int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
           int h = p * g.sh - g.ph + ctap_r * g.dh;
           int w = q * g.sw - g.pw + ctap_s * g.dw;
           bool v = cv && pix < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;

@@ -75,6 +75,8 @@ def _operand(op) -> tuple[_lib.SnOperand, int, int]:
     assert op.x.dtype == torch.bfloat16 and op.x.is_contiguous()
     g = op.geom
     assert g.Cg % 8 == 0 and g.C % 8 == 0, "implicit conv needs channels % 8 == 0"
+    # the kernel's fp32-reciprocal index division is exact below 2^24
+    assert g.N * g.P * g.Q < (1 << 24) and g.N * g.H * g.W < (1 << 24), "conv too large for one launch"
     s = _lib.SnOperand(op.x.data_ptr(), 0, op.gstride, g.c_struct())
     return s, 0 if op.kcontig else 1, OP_IM2COL
 
@@ -205,6 +207,6 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate
 def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = True) -> None:
     """out[N] (+)= sum over rows of a bf16 [M, N] matrix (bias gradient)."""
     M, N = x.shape
-    nparts = max(1, min(256, M // 256))
+    nparts = max(1, min(1024, M // 64))
     part = torch.empty((nparts, N), dtype=torch.float32, device=x.device)
     _lib.call("colsum_bf16", x, M, N, x.stride(0), part, nparts, out, int(accumulate))
