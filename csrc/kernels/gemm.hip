@@ -26,6 +26,8 @@
 // bijective block remap.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int BK = 64, NTHR = 256;
@@ -100,7 +102,7 @@ struct Stager {
   int ctap_r, ctap_s, cc;  // MC+IM2COL: column decode (cols fixed across k)
   bool cv;
   float invPQ, invQ, invCg, invS;
-  uint4 reg[NCH];
+  uint4 reg[2][NCH];  // two staging sets: tile k+1 waits in one while tile k+2 loads into the other
 
   SN_DEV void init(const SnOperand& op, int grp, int tid, int tile_row0, int rows_lim, int tile_col0,
                    int cols_lim) {
@@ -152,6 +154,7 @@ struct Stager {
   SN_DEV uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
   // Issue the global loads of the tile whose first reduction index is k_tile.
+  template <int SET>
   SN_DEV void load(int k_tile, int k_lim, int tile_rc0, int rc_lim) {
     const uint4 z = make_uint4(0, 0, 0, 0);
     if (!MC) {
@@ -161,7 +164,7 @@ struct Stager {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
           int row = tile_rc0 + row0 + 32 * i;
-          reg[i] = (kv && row < rc_lim) ? ld16(base + (long long)row * ld + k) : z;
+          reg[SET][i] = (kv && row < rc_lim) ? ld16(base + (long long)row * ld + k) : z;
         }
       } else {
         int tap = fdiv(k, g.Cg, invCg), c = k - tap * g.Cg;
@@ -172,7 +175,7 @@ struct Stager {
           int h = ph[i] + dh, w = pw[i] + dw;
           bool v = kv && pv[i] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
           long long off = ((long long)(pn[i] + h) * g.W + w) * g.C + coff + c;
-          reg[i] = v ? ld16(base + off) : z;
+          reg[SET][i] = v ? ld16(base + off) : z;
         }
       }
     } else {
@@ -182,7 +185,7 @@ struct Stager {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
           int k = k_tile + row0 + RPP * i;
-          reg[i] = (cvd && k < k_lim) ? ld16(base + (long long)k * ld + col) : z;
+          reg[SET][i] = (cvd && k < k_lim) ? ld16(base + (long long)k * ld + col) : z;
         }
       } else {
         const int PQ = g.P * g.Q;
@@ -195,17 +198,18 @@ struct Stager {
           int w = q * g.sw - g.pw + ctap_s * g.dw;
           bool v = cv && pix < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
           long long off = ((long long)(n * g.H + h) * g.W + w) * g.C + coff + cc;
-          reg[i] = v ? ld16(base + off) : z;
+          reg[SET][i] = v ? ld16(base + off) : z;
         }
       }
     }
   }
 
+  template <int SET>
   SN_DEV void store(char* lds) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       int off = MC ? mc_off<TILE>(row0 + RPP * i, fixed) : kc_off(row0 + 32 * i, fixed);
-      *reinterpret_cast<uint4*>(lds + off) = reg[i];
+      *reinterpret_cast<uint4*>(lds + off) = reg[SET][i];
     }
   }
 };
@@ -274,21 +278,7 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
   const int wm0 = (wave % WM) * 64, wn0 = (wave / WM) * 64;
   const int nk = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
 
-  if (nk > 0) {
-    sa.load(k0, k1, m_blk, args.M);
-    sb.load(k0, k1, n_blk, args.N);
-    sa.store(smem);
-    sb.store(smem + A_BYTES);
-    __syncthreads();
-  }
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      sa.load(k0 + (kt + 1) * BK, k1, m_blk, args.M);
-      sb.load(k0 + (kt + 1) * BK, k1, n_blk, args.N);
-    }
-    const char* la = smem + cur * STAGE;
+  auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -303,13 +293,38 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      char* nxt = smem + (cur ^ 1) * STAGE;
-      sa.store(nxt);
-      sb.store(nxt + A_BYTES);
+  };
+  // Two-deep software pipeline over two LDS stages and two register staging sets:
+  // while stage S is consumed, tile kt+1 (already in registers set 1-S) is written to
+  // stage 1-S and tile kt+2 is in flight into register set S — every global load gets
+  // two MFMA phases to land.
+  auto step = [&](auto S_, int kt) {
+    constexpr int S = decltype(S_)::value;
+    if (kt + 2 < nk) {
+      sa.template load<S>(k0 + (kt + 2) * BK, k1, m_blk, args.M);
+      sb.template load<S>(k0 + (kt + 2) * BK, k1, n_blk, args.N);
+    }
+    compute(smem + S * STAGE);
+    if (kt + 1 < nk) {
+      sa.template store<1 - S>(smem + (1 - S) * STAGE);
+      sb.template store<1 - S>(smem + (1 - S) * STAGE + A_BYTES);
     }
     __syncthreads();
-    cur ^= 1;
+  };
+  if (nk > 0) {
+    sa.template load<0>(k0, k1, m_blk, args.M);
+    sb.template load<0>(k0, k1, n_blk, args.N);
+    if (nk > 1) {
+      sa.template load<1>(k0 + BK, k1, m_blk, args.M);
+      sb.template load<1>(k0 + BK, k1, n_blk, args.N);
+    }
+    sa.template store<0>(smem);
+    sb.template store<0>(smem + A_BYTES);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
   }
 
   // Epilogue.  acc[i][j] holds D[n][m] with m = lane&15 (+16j), n = 4(lane>>4)+r (+16i):
