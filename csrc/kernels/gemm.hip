@@ -83,29 +83,39 @@ SN_DEV int swz_mc(int k) {
 template <int TILE>
 SN_DEV int mc_off(int k, int mc) { return k * (TILE * 2) + ((mc << 4) ^ swz_mc<TILE>(k)); }
 
-// Per-thread staging state of one operand tile (TILE = rows of the M/N axis).
-//   KC: chunks on rows (tid>>3) + 32i, chunk column tid&7 (fixed), TILE/32 chunks.
-//   MC: CPR = TILE/8 chunks per k-row; rows tid/CPR + (256/CPR) i, column tid%CPR.
+// Zero source for LDS-DMA lanes that fall outside the matrix (padding, ragged edges).
+__device__ __attribute__((aligned(16))) uint4 g_zero16[1];
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// Global->LDS staging of one operand tile with global_load_lds_dwordx4 (LDS-DMA, no VGPR
+// round trip and no ds_write pass).  One wave-instruction writes 1 KB of LDS linearly
+// (lane l -> byte 16 l), so the XOR swizzle of the LDS image is applied on the SOURCE
+// side: lane l of instruction j of wave w fills LDS row r = (w*NI + j)*RPI + l/CPL at
+// physical 16-B slot l%CPL, and therefore fetches the LOGICAL chunk that the swizzle
+// maps to that slot.  Lanes outside the matrix read a zero page.
+//   KC: [TILE rows][64 k], 8 chunks per row, 8 rows per instruction.
+//   MC: [64 k rows][TILE cols], TILE/8 chunks per row.
 template <int MC, int MODE, int TILE>
-struct Stager {
-  static constexpr int NCH = TILE / 32;
-  static constexpr int CPR = TILE / 8;
-  static constexpr int RPP = MC ? (NTHR / CPR) : 32;  // rows per pass
+struct GStager {
+  static constexpr int NI = TILE / 32;            // wave-instructions per wave per tile
+  static constexpr int CPL = MC ? TILE / 8 : 8;   // 16-B chunks per LDS row
+  static constexpr int RPI = 64 / CPL;            // LDS rows per wave-instruction
+  static_assert(NI % 2 == 0, "KC chunk pattern repeats with period 2 in j");
   const bf16_t* base;
   long long ld;
   SnConvGeom g;
-  int coff;   // IM2COL group channel offset
-  int fixed;  // KC: kc ; MC: mc
-  int row0;   // first row of this thread (tile-relative)
-  int pn[NCH], ph[NCH], pw[NCH];  // KC+IM2COL: per-row pixel decode (rows fixed across k)
-  bool pv[NCH];
-  int ctap_r, ctap_s, cc;  // MC+IM2COL: column decode (cols fixed across k)
-  bool cv;
+  int coff;
+  int rr[NI];  // tile-relative LDS row of this lane in instruction j
+  int ch[NI];  // logical 16-B chunk this lane fetches in instruction j
+  int pn[NI], ph[NI], pw[NI];  // KC+IM2COL: pixel decode (rows fixed across k)
+  bool pv[NI];
+  int cr[NI], cs[NI], cc[NI];  // MC+IM2COL: column decode (cols fixed across k)
+  bool cv[NI];
   float invPQ, invQ, invCg, invS;
-  uint4 reg[2][NCH];  // two staging sets: tile k+1 waits in one while tile k+2 loads into the other
 
-  SN_DEV void init(const SnOperand& op, int grp, int tid, int tile_row0, int rows_lim, int tile_col0,
-                   int cols_lim) {
+  SN_DEV void init(const SnOperand& op, int grp, int wave, int lane, int tile_row0, int rows_lim,
+                   int tile_col0, int cols_lim) {
     ld = op.ld;
     g = op.g;
     if (MODE == OP_DENSE) {
@@ -115,101 +125,92 @@ struct Stager {
       base = op.ptr;
       coff = (int)(grp * op.gstride);
     }
-    if (!MC) {
-      fixed = tid & 7;
-      row0 = tid >> 3;
-      if (MODE == OP_IM2COL) {
-        const int PQ = g.P * g.Q;
-        invPQ = 1.f / (float)PQ;
-        invQ = 1.f / (float)g.Q;
-        invCg = 1.f / (float)g.Cg;
-        invS = 1.f / (float)g.S;
+    invPQ = 1.f / (float)(g.P * g.Q);
+    invQ = 1.f / (float)g.Q;
+    invCg = 1.f / (float)g.Cg;
+    invS = 1.f / (float)g.S;
 #pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          int pix = tile_row0 + row0 + 32 * i;
-          pv[i] = pix < rows_lim;
-          int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
-          int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
-          pn[i] = n * g.H;
-          ph[i] = p * g.sh - g.ph;
-          pw[i] = q * g.sw - g.pw;
-        }
+    for (int j = 0; j < NI; ++j) {
+      const int row = (wave * NI + j) * RPI + lane / CPL, pos = lane % CPL;
+      rr[j] = row;
+      ch[j] = MC ? (pos ^ (swz_mc<TILE>(row) >> 4)) : (pos ^ ((row >> 1) & 7));
+      if (MODE == OP_IM2COL && !MC) {
+        const int PQ = g.P * g.Q;
+        int pix = tile_row0 + row;
+        pv[j] = pix < rows_lim;
+        int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
+        int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
+        pn[j] = n * g.H;
+        ph[j] = p * g.sh - g.ph;
+        pw[j] = q * g.sw - g.pw;
       }
-    } else {
-      fixed = tid % CPR;
-      row0 = tid / CPR;
-      if (MODE == OP_IM2COL) {
-        invPQ = 1.f / (float)(g.P * g.Q);
-        invQ = 1.f / (float)g.Q;
-        int col = tile_col0 + fixed * 8;
-        cv = col < cols_lim;
+      if (MODE == OP_IM2COL && MC) {
+        int col = tile_col0 + ch[j] * 8;
+        cv[j] = col < cols_lim;
         int tap = col / g.Cg;
-        cc = col - tap * g.Cg;
-        ctap_r = tap / g.S;
-        ctap_s = tap - ctap_r * g.S;
+        cc[j] = col - tap * g.Cg;
+        cr[j] = tap / g.S;
+        cs[j] = tap - cr[j] * g.S;
       }
     }
   }
 
-  SN_DEV uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+  SN_DEV void dma(const bf16_t* src, bool valid, char* lds) {
+    const void* s = valid ? (const void*)src : (const void*)g_zero16;
+    __builtin_amdgcn_global_load_lds(s, (lds_void*)lds, 16, 0, 0);
+  }
 
-  // Issue the global loads of the tile whose first reduction index is k_tile.
-  template <int SET>
-  SN_DEV void load(int k_tile, int k_lim, int tile_rc0, int rc_lim) {
-    const uint4 z = make_uint4(0, 0, 0, 0);
+  // Issue the LDS-DMA of the tile whose first reduction index is k_tile into `lds`.
+  SN_DEV void issue(char* lds, int wave, int k_tile, int k_lim, int tile_rc0, int rc_lim) {
+    char* dst = lds + wave * NI * 1024;
     if (!MC) {
-      const int k = k_tile + fixed * 8;
-      const bool kv = k < k_lim;
       if (MODE == OP_DENSE) {
 #pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          int row = tile_rc0 + row0 + 32 * i;
-          reg[SET][i] = (kv && row < rc_lim) ? ld16(base + (long long)row * ld + k) : z;
+        for (int j = 0; j < NI; ++j) {
+          int row = tile_rc0 + rr[j], k = k_tile + ch[j] * 8;
+          dma(base + (long long)row * ld + k, row < rc_lim && k < k_lim, dst + j * 1024);
         }
       } else {
-        int tap = fdiv(k, g.Cg, invCg), c = k - tap * g.Cg;
-        int r = fdiv(tap, g.S, invS), s = tap - r * g.S;
-        int dh = r * g.dh, dw = s * g.dw;
+        int kk[2], cch[2], dh[2], dw[2];
 #pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          int h = ph[i] + dh, w = pw[i] + dw;
-          bool v = kv && pv[i] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          long long off = ((long long)(pn[i] + h) * g.W + w) * g.C + coff + c;
-          reg[SET][i] = v ? ld16(base + off) : z;
+        for (int e = 0; e < 2; ++e) {
+          kk[e] = k_tile + ch[e] * 8;
+          int tap = fdiv(kk[e], g.Cg, invCg);
+          cch[e] = kk[e] - tap * g.Cg;
+          int r = fdiv(tap, g.S, invS), s = tap - r * g.S;
+          dh[e] = r * g.dh;
+          dw[e] = s * g.dw;
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int e = j & 1;
+          int h = ph[j] + dh[e], w = pw[j] + dw[e];
+          bool v = kk[e] < k_lim && pv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          long long off = ((long long)(pn[j] + h) * g.W + w) * g.C + coff + cch[e];
+          dma(base + off, v, dst + j * 1024);
         }
       }
     } else {
-      const int col = tile_rc0 + fixed * 8;
       if (MODE == OP_DENSE) {
-        const bool cvd = col < rc_lim;
 #pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          int k = k_tile + row0 + RPP * i;
-          reg[SET][i] = (cvd && k < k_lim) ? ld16(base + (long long)k * ld + col) : z;
+        for (int j = 0; j < NI; ++j) {
+          int k = k_tile + rr[j], col = tile_rc0 + ch[j] * 8;
+          dma(base + (long long)k * ld + col, k < k_lim && col < rc_lim, dst + j * 1024);
         }
       } else {
         const int PQ = g.P * g.Q;
 #pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          int pix = k_tile + row0 + RPP * i;
+        for (int j = 0; j < NI; ++j) {
+          int pix = k_tile + rr[j];
           int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
           int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
-          int h = p * g.sh - g.ph + ctap_r * g.dh;
-          int w = q * g.sw - g.pw + ctap_s * g.dw;
-          bool v = cv && pix < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          long long off = ((long long)(n * g.H + h) * g.W + w) * g.C + coff + cc;
-          reg[SET][i] = v ? ld16(base + off) : z;
+          int h = p * g.sh - g.ph + cr[j] * g.dh;
+          int w = q * g.sw - g.pw + cs[j] * g.dw;
+          bool v = cv[j] && pix < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          long long off = ((long long)(n * g.H + h) * g.W + w) * g.C + coff + cc[j];
+          dma(base + off, v, dst + j * 1024);
         }
       }
-    }
-  }
-
-  template <int SET>
-  SN_DEV void store(char* lds) {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      int off = MC ? mc_off<TILE>(row0 + RPP * i, fixed) : kc_off(row0 + 32 * i, fixed);
-      *reinterpret_cast<uint4*>(lds + off) = reg[SET][i];
     }
   }
 };
@@ -246,7 +247,11 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int WN = BN / 64, WM = 4 / WN;  // waves along N / M (64x64 per wave)
   static_assert(WM * 64 == BM, "tile/wave layout mismatch");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // Two distinct LDS objects (one per stage): the compiler's alias scopes then prove that
+  // the ds_reads of one stage do not depend on the DMA in flight into the other, so it
+  // does not drain vmcnt before every k-step's first ds_read.
+  __shared__ __attribute__((aligned(16))) char smem0[STAGE];
+  __shared__ __attribute__((aligned(16))) char smem1[STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (args.M + BM - 1) / BM;
 
@@ -264,10 +269,11 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
   const int k0 = split * args.kchunk;
   const int k1 = min(args.K, k0 + args.kchunk);
 
-  Stager<AMC, AMODE, BM> sa;
-  Stager<BMC, BMODE, BN> sb;
-  sa.init(args.A, grp, tid, m_blk, args.M, m_blk, args.M);
-  sb.init(args.B, grp, tid, n_blk, args.N, n_blk, args.N);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  GStager<AMC, AMODE, BM> sa;
+  GStager<BMC, BMODE, BN> sb;
+  sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M);
+  sb.init(args.B, grp, wv, lane, n_blk, args.N, n_blk, args.N);
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -294,37 +300,23 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
     }
   };
-  // Two-deep software pipeline over two LDS stages and two register staging sets:
-  // while stage S is consumed, tile kt+1 (already in registers set 1-S) is written to
-  // stage 1-S and tile kt+2 is in flight into register set S — every global load gets
-  // two MFMA phases to land.
-  auto step = [&](auto S_, int kt) {
-    constexpr int S = decltype(S_)::value;
-    if (kt + 2 < nk) {
-      sa.template load<S>(k0 + (kt + 2) * BK, k1, m_blk, args.M);
-      sb.template load<S>(k0 + (kt + 2) * BK, k1, n_blk, args.N);
-    }
-    compute(smem + S * STAGE);
-    if (kt + 1 < nk) {
-      sa.template store<1 - S>(smem + (1 - S) * STAGE);
-      sb.template store<1 - S>(smem + (1 - S) * STAGE + A_BYTES);
-    }
-    __syncthreads();
+  auto issue = [&](char* st, int kt) {
+    sa.issue(st, wv, k0 + kt * BK, k1, m_blk, args.M);
+    sb.issue(st + A_BYTES, wv, k0 + kt * BK, k1, n_blk, args.N);
   };
-  if (nk > 0) {
-    sa.template load<0>(k0, k1, m_blk, args.M);
-    sb.template load<0>(k0, k1, n_blk, args.N);
-    if (nk > 1) {
-      sa.template load<1>(k0 + BK, k1, m_blk, args.M);
-      sb.template load<1>(k0 + BK, k1, n_blk, args.N);
-    }
-    sa.template store<0>(smem);
-    sb.template store<0>(smem + A_BYTES);
+  // One barrier per K-step: retire this wave's DMA of tile kt, barrier (all waves' DMAs
+  // landed AND all reads of the other stage from step kt-1 are done), then start the DMA
+  // of tile kt+1 into the other stage and run the MFMAs of tile kt under it.
+  auto step = [&](char* cur, char* nxt, int kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-  }
+    if (kt + 1 < nk) issue(nxt, kt + 1);
+    compute(cur);
+  };
+  if (nk > 0) issue(smem0, 0);
   for (int kt = 0; kt < nk; kt += 2) {
-    step(std::integral_constant<int, 0>{}, kt);
-    if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
+    step(smem0, smem1, kt);
+    if (kt + 1 < nk) step(smem1, smem0, kt + 1);
   }
 
   // Epilogue.  acc[i][j] holds D[n][m] with m = lane&15 (+16j), n = 4(lane>>4)+r (+16i):
