@@ -50,8 +50,11 @@ extern "C" int sn_relu_bwd(const bf16_t* dy, const bf16_t* x, bf16_t* dx, long l
 
 // ---------------- Dropout ----------------
 // keep(i) = philox(key=seed, ctr=(i_lo, i_hi | stream<<16, counter_lo, counter_hi)).x > thr
+// gate (optional, backward only): the in-place ReLU output feeding this dropout — its
+// slope-0 backward mask (gate > 0) is applied here instead of in a separate pass.
 __global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8,
-                               const long long* __restrict__ rng, int stream, uint32_t thr, float scale) {
+                               const long long* __restrict__ rng, int stream, uint32_t thr, float scale,
+                               const bf16_t* __restrict__ gate) {
   const unsigned long long seed = (unsigned long long)rng[0];
   const unsigned long long counter = (unsigned long long)rng[1];
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
@@ -66,17 +69,23 @@ __global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
       uint32_t u = philox4x32(key, ctr).x;
       f[k] = (u > thr) ? f[k] * scale : 0.f;
     }
+    if (gate) {
+      float gv[8];
+      unpack8(reinterpret_cast<const uint4*>(gate)[i], gv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = gv[k] > 0.f ? f[k] : 0.f;
+    }
     reinterpret_cast<uint4*>(y)[i] = pack8(f);
   }
 }
 
 extern "C" int sn_dropout(const bf16_t* x, bf16_t* y, long long n, const long long* rng, long long stream,
-                          float ratio, hipStream_t st) {
+                          float ratio, const bf16_t* gate, hipStream_t st) {
   if (n % 8) return 7;
   uint32_t thr = (uint32_t)((double)4294967295u * (double)ratio);
   float scale = 1.f / (1.f - ratio);
   hipLaunchKernelGGL(dropout_kernel, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, x, y, n / 8, rng,
-                     (int)stream, thr, scale);
+                     (int)stream, thr, scale, gate);
   return SN_CHECK_LAUNCH();
 }
 

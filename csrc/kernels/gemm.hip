@@ -64,6 +64,7 @@ struct SnGemmArgs {
   const float* bias;  // per output column n (offset by g*N), EPI_BF16 only
   int relu;
   int tile;           // 0: 128x128, 1: 256x64
+  const bf16_t* gate; // EPI_BF16: zero outputs where gate (same layout as C) <= 0 (fused ReLU backward)
 };
 
 }  // extern "C"
@@ -343,6 +344,23 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
         if (args.relu) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
+        }
+        if (args.gate) {
+          const bf16_t* gp = args.gate + grp * args.c_gstride + (long long)m * args.ldc + n;
+          float gv[4];
+          if (full && (args.c_gstride & 3) == 0) {
+            const uint2 u = *reinterpret_cast<const uint2*>(gp);
+            gv[0] = __uint_as_float(u.x << 16);
+            gv[1] = __uint_as_float(u.x & 0xffff0000u);
+            gv[2] = __uint_as_float(u.y << 16);
+            gv[3] = __uint_as_float(u.y & 0xffff0000u);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gv[r] = (n + r < args.N) ? bf2f(gp[r]) : 0.f;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (!(gv[r] > 0.f)) o[r] = 0.f;
         }
         if (full) {
           uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));

@@ -13,7 +13,7 @@ struct PoolGeom {
 
 template <bool VEC>
 __global__ void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
-                            PoolGeom g) {
+                            PoolGeom g, int gate) {
   const int cv = VEC ? g.C / 8 : g.C;
   const long long total = (long long)g.N * g.P * g.Q * cv;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -45,6 +45,14 @@ __global__ void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
           if (f > best[0]) { best[0] = f; arg[0] = widx; }
         }
       }
+    // ReLU gate (the pooled input is the output of an in-place slope-0 ReLU whose
+    // backward is folded in here): a window whose max is <= 0 passes no gradient, which
+    // the mask encodes as the impossible window index 255.
+    if (gate) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (!(best[k] > 0.f)) arg[k] = 255;
+    }
     const long long o = pix * g.C + c0;
     if (VEC) {
       *reinterpret_cast<uint4*>(y + o) = pack8(best);
@@ -170,15 +178,16 @@ static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long 
 
 extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long N, long long H, long long W,
                            long long C, long long P, long long Q, long long kh, long long kw, long long sh,
-                           long long sw, long long ph, long long pw, long long method, hipStream_t st) {
+                           long long sw, long long ph, long long pw, long long method, long long gate,
+                           hipStream_t st) {
   PoolGeom g = mkgeom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
-  if (method == 0 && kh * kw > 255) return 6;
+  if (method == 0 && kh * kw > 254) return 6;
   const bool vec = (C % 8) == 0;
   long long total = N * P * Q * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
   if (method == 0) {
-    if (vec) hipLaunchKernelGGL(maxpool_fwd<true>, grid, dim3(256), 0, st, x, y, mask, g);
-    else hipLaunchKernelGGL(maxpool_fwd<false>, grid, dim3(256), 0, st, x, y, mask, g);
+    if (vec) hipLaunchKernelGGL(maxpool_fwd<true>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
+    else hipLaunchKernelGGL(maxpool_fwd<false>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
   } else {
     if (vec) hipLaunchKernelGGL(avepool_fwd<true>, grid, dim3(256), 0, st, x, y, g);
     else hipLaunchKernelGGL(avepool_fwd<false>, grid, dim3(256), 0, st, x, y, g);

@@ -9,11 +9,39 @@
 
 // out (op)= act(sum_s ws[s] + bias)
 //   mode 0: out bf16 = act(sum + bias)     mode 1: out f32 = sum     mode 2: out f32 += sum
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long sstride,
-                                     int rows, int cols, long long ldw, void* out, long long ldo,
-                                     int mode, const float* __restrict__ bias, int relu,
-                                     int groups, long long ws_gstride, long long out_gstride) {
-  const int cols4 = (cols + 3) >> 2;
+// (gate, mode 0: zero where gate <= 0 — a fused slope-0 ReLU backward)
+struct ReduceOut {
+  void* out;
+  long long ldo, out_gstride;
+  int cols, mode, relu;
+  const float* bias;
+  const bf16_t* gate;
+};
+
+SN_DEV void reduce_store(const ReduceOut& o, int g, int r, int c, const float* acc) {
+  if (o.mode == 0) {
+    const long long base = g * o.out_gstride + (long long)r * o.ldo + c;
+    bf16_t* p = reinterpret_cast<bf16_t*>(o.out) + base;
+    for (int k = 0; k < 4; ++k) {
+      if (c + k >= o.cols) break;
+      float v = acc[k] + (o.bias ? o.bias[(long long)g * o.cols + c + k] : 0.f);
+      if (o.relu) v = fmaxf(v, 0.f);
+      if (o.gate && !(bf2f(o.gate[base + k]) > 0.f)) v = 0.f;
+      p[k] = f2bf(v);
+    }
+  } else {
+    float* p = reinterpret_cast<float*>(o.out) + g * o.out_gstride + (long long)r * o.ldo + c;
+    for (int k = 0; k < 4; ++k) {
+      if (c + k >= o.cols) break;
+      p[k] = (o.mode == 2 ? p[k] : 0.f) + acc[k];
+    }
+  }
+}
+
+// Few splits: one thread per 4 output columns, serial over the splits.
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long sstride, int rows,
+                                     long long ldw, long long ws_gstride, ReduceOut o) {
+  const int cols = o.cols, cols4 = (cols + 3) >> 2;
   const long long total = (long long)rows * cols4;
   const int g = blockIdx.y;
   const float* wsg = ws + g * ws_gstride;
@@ -32,53 +60,108 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, l
           if (c + k < cols) acc[k] += p[k];
       }
     }
-    if (mode == 0) {
-      bf16_t* o = reinterpret_cast<bf16_t*>(out) + g * out_gstride + (long long)r * ldo + c;
-      for (int k = 0; k < 4; ++k) {
-        if (c + k >= cols) break;
-        float v = acc[k] + (bias ? bias[(long long)g * cols + c + k] : 0.f);
-        if (relu) v = fmaxf(v, 0.f);
-        o[k] = f2bf(v);
-      }
-    } else {
-      float* o = reinterpret_cast<float*>(out) + g * out_gstride + (long long)r * ldo + c;
-      for (int k = 0; k < 4; ++k) {
-        if (c + k >= cols) break;
-        o[k] = (mode == 2 ? o[k] : 0.f) + acc[k];
+    reduce_store(o, g, r, c, acc);
+  }
+}
+
+// Many splits (e.g. 128-way split-K of a small weight gradient): 16 output float4s per
+// block x 16 split lanes, four slab loads in flight per thread, fixed-order LDS combine.
+// Needs cols % 4 == 0 and ldw % 4 == 0.
+__global__ void __launch_bounds__(256) splitk_reduce_wide(const float* __restrict__ ws, int splits,
+                                                          long long sstride, int rows, long long ldw,
+                                                          long long ws_gstride, ReduceOut o) {
+  __shared__ float4 red[16][16];
+  const int it = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int cols4 = o.cols >> 2;
+  const long long total = (long long)rows * cols4;
+  const long long i = blockIdx.x * 16LL + it;
+  const int g = blockIdx.y;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int r = 0, c = 0;
+  if (i < total) {
+    r = (int)(i / cols4);
+    c = (int)(i - (long long)r * cols4) * 4;
+    const float* p = ws + g * ws_gstride + (long long)r * ldw + c;
+    int s = sl;
+    for (; s + 48 < splits; s += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (s + 16 * u) * sstride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
       }
     }
+    for (; s < splits; s += 16) {
+      float4 v = *reinterpret_cast<const float4*>(p + s * sstride);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[sl][it] = acc;
+  __syncthreads();
+  if (sl == 0 && i < total) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float4 v = red[q][it];
+      a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
+    }
+    reduce_store(o, g, r, c, a);
   }
 }
 
 extern "C" int sn_splitk_reduce(const float* ws, long long splits, long long sstride, long long rows,
                                 long long cols, long long ldw, void* out, long long ldo, long long mode,
                                 const float* bias, long long relu, long long groups,
-                                long long ws_gstride, long long out_gstride, hipStream_t st) {
+                                long long ws_gstride, long long out_gstride, const bf16_t* gate,
+                                hipStream_t st) {
+  ReduceOut o;
+  o.out = out; o.ldo = ldo; o.out_gstride = out_gstride; o.cols = (int)cols; o.mode = (int)mode;
+  o.relu = (int)relu; o.bias = bias; o.gate = gate;
   long long total = rows * ((cols + 3) / 4);
-  dim3 grid(sn_blocks(total, 256, 4096), (unsigned)groups);
-  hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, ws, (int)splits, sstride, (int)rows,
-                     (int)cols, ldw, out, ldo, (int)mode, bias, (int)relu, (int)groups, ws_gstride,
-                     out_gstride);
+  if (splits >= 16 && (cols & 3) == 0 && (ldw & 3) == 0) {
+    dim3 grid((unsigned)((total + 15) / 16), (unsigned)groups);
+    hipLaunchKernelGGL(splitk_reduce_wide, grid, dim3(256), 0, st, ws, (int)splits, sstride, (int)rows, ldw,
+                       ws_gstride, o);
+  } else {
+    dim3 grid(sn_blocks(total, 256, 4096), (unsigned)groups);
+    hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, ws, (int)splits, sstride, (int)rows, ldw,
+                       ws_gstride, o);
+  }
   return SN_CHECK_LAUNCH();
 }
 
 // ---- column sums of a bf16 [rows x cols] matrix (bias gradient) --------------------
-// Pass 1: block b sums rows [b*rpb, (b+1)*rpb) for all columns -> part[b][cols] (f32).
-// Each thread owns 8 consecutive columns (one 16-B load) and strides over rows.
-__global__ void colsum_pass1(const bf16_t* __restrict__ x, long long rows, int cols, long long ld,
-                             long long rpb, float* __restrict__ part) {
-  extern __shared__ float red[];  // [threads][8]
-  const int c8 = (cols + 7) >> 3;
-  const int lanes_per_row = c8;  // threads covering one row
-  const int rows_per_pass = blockDim.x / lanes_per_row;
+// Pass 1: block (b, cb) sums rows [b*rpb, (b+1)*rpb) of the column block cb (CL*8
+// columns) -> part[b][cols] (f32).  256 threads = CL column lanes (8 columns = one 16-B
+// load each) x RL row lanes; four rows in flight per thread.
+__global__ void __launch_bounds__(256) colsum_pass1(const bf16_t* __restrict__ x, long long rows, int cols,
+                                                    long long ld, long long rpb, int CL, float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int RL = 256 / CL;
   const int t = threadIdx.x;
-  const int cc = t % lanes_per_row, rr = t / lanes_per_row;
+  const int cc = t % CL, rr = t / CL;
+  const int c = (blockIdx.y * CL + cc) * 8;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const long long r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  const int c = cc * 8;
-  if (rr < rows_per_pass) {
+  if (c < cols) {
     const bool vec = (c + 7 < cols) && ((ld & 7) == 0);
-    for (long long r = r0 + rr; r < r1; r += rows_per_pass) {
+    long long r = r0 + rr;
+    if (vec) {
+      for (; r + 3 * RL < r1; r += 4 * RL) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(x + (r + u * RL) * ld + c);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float f[8];
+          unpack8(v[u], f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += f[k];
+        }
+      }
+    }
+    for (; r < r1; r += RL) {
       const bf16_t* p = x + r * ld + c;
       if (vec) {
         float f[8];
@@ -92,41 +175,42 @@ __global__ void colsum_pass1(const bf16_t* __restrict__ x, long long rows, int c
     }
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) red[t * 8 + k] = (rr < rows_per_pass) ? acc[k] : 0.f;
+  for (int k = 0; k < 8; ++k) red[t * 8 + k] = acc[k];
   __syncthreads();
-  // tree over rr for fixed cc (deterministic order)
-  if (rr == 0) {
-    for (int q = 1; q < rows_per_pass; ++q)
+  // fixed-order combine over the row lanes (deterministic)
+  if (rr == 0 && c < cols) {
+    for (int q = 1; q < RL; ++q)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += red[(q * lanes_per_row + cc) * 8 + k];
+      for (int k = 0; k < 8; ++k) acc[k] += red[(q * CL + cc) * 8 + k];
     for (int k = 0; k < 8; ++k)
       if (c + k < cols) part[blockIdx.x * (long long)cols + c + k] = acc[k];
   }
 }
 
-// Pass 2: one 256-thread block per group of 64 columns; the 4 waves split the partial
-// rows, lanes own columns (coalesced), fixed-order combine in LDS (deterministic).
+// Pass 2: one 1024-thread block per 64 columns; 16 waves split the partial rows (eight
+// independent loads in flight per lane), lanes own columns (coalesced), fixed-order
+// combine in LDS (deterministic).
 __global__ void __launch_bounds__(1024) colsum_pass2(const float* __restrict__ part, int nparts, int cols, float* out,
                                                      int accumulate) {
   __shared__ float red[16][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;  // 16 waves split the partial rows
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float s0 = 0.f, s1 = 0.f;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c < cols) {
     int p = w;
-    for (; p + 16 < nparts; p += 32) {
-      s0 += part[(long long)p * cols + c];
-      s1 += part[(long long)(p + 16) * cols + c];
+    for (; p + 7 * 16 < nparts; p += 8 * 16) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += part[(long long)(p + u * 16) * cols + c];
     }
-    if (p < nparts) s0 += part[(long long)p * cols + c];
+    for (; p < nparts; p += 16) s[0] += part[(long long)p * cols + c];
   }
-  red[w][lane] = s0 + s1;
+  red[w][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   if (w == 0 && c < cols) {
-    float t = 0.f;
+    float tot = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t += red[k][lane];
-    out[c] = (accumulate ? out[c] : 0.f) + t;
+    for (int k = 0; k < 16; ++k) tot += red[k][lane];
+    out[c] = (accumulate ? out[c] : 0.f) + tot;
   }
 }
 
@@ -134,12 +218,12 @@ __global__ void __launch_bounds__(1024) colsum_pass2(const float* __restrict__ p
 extern "C" int sn_colsum_bf16(const bf16_t* x, long long rows, long long cols, long long ld, float* part,
                               long long nparts, float* out, long long accumulate, hipStream_t st) {
   const int c8 = (int)((cols + 7) / 8);
-  if (c8 > 1024) return 5;
-  int threads = 256;
-  while (threads < c8) threads *= 2;
+  int CL = 1;
+  while (CL < c8 && CL < 64) CL *= 2;
+  const int cblocks = (c8 + CL - 1) / CL;
   long long rpb = (rows + nparts - 1) / nparts;
-  hipLaunchKernelGGL(colsum_pass1, dim3((unsigned)nparts), dim3(threads), threads * 8 * sizeof(float), st, x,
-                     rows, (int)cols, ld, rpb, part);
+  hipLaunchKernelGGL(colsum_pass1, dim3((unsigned)nparts, (unsigned)cblocks), dim3(256), 0, st, x, rows,
+                     (int)cols, ld, rpb, CL, part);
   hipLaunchKernelGGL(colsum_pass2, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st, part, (int)nparts,
                      (int)cols, out, (int)accumulate);
   return SN_CHECK_LAUNCH();

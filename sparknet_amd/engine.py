@@ -43,6 +43,44 @@ def fuse_relu(net) -> int:
         prod.fuse_relu = True
         relu.fused = True
         n += 1
+    fuse_relu_backward(net)
+    return n
+
+
+_GATE_CONSUMERS = ("Convolution", "InnerProduct", "Dropout", "Pooling")
+
+
+def fuse_relu_backward(net) -> int:
+    """Fold the backward of every in-place slope-0 ReLU into the backward of the single
+    layer that consumes its output (Caffe's ReLU backward is a separate pass over the
+    gradient, relu_layer.cu:24-41): conv / inner-product dgrad epilogues, the dropout
+    kernel and the max-pool argmax mask then zero the gradient where the ReLU output is
+    not positive, and the ReLU layer's own backward becomes a no-op.  Returns the count."""
+    n = 0
+    for li, relu in enumerate(net.layers):
+        if relu.type_name != "ReLU" or getattr(relu, "slope", 1.0) != 0.0:
+            continue
+        if net.bottom_ids[li] != net.top_ids[li]:
+            continue
+        blob = net.top_ids[li][0]
+        consumers = [lj for lj in range(li + 1, len(net.layers)) if blob in net.bottom_ids[lj]]
+        if not consumers:
+            continue
+        lc = consumers[0]
+        # later readers are fine only behind an in-place consumer (e.g. relu6 -> drop6 ->
+        # fc7 all on blob "fc6"): they read the consumer's output, not the ReLU's
+        if len(consumers) > 1 and blob not in net.top_ids[lc]:
+            continue
+        cons = net.layers[lc]
+        if cons.type_name not in _GATE_CONSUMERS or len(net.bottom_ids[lc]) != 1:
+            continue
+        if cons.type_name == "Pooling" and (cons.method != 0 or len(net.top_ids[lc]) != 1):
+            continue
+        if blob in getattr(net, "output_blob_ids", ()):
+            continue
+        cons.relu_gate = True
+        relu.bwd_fused = True
+        n += 1
     return n
 
 

@@ -28,6 +28,7 @@ class NeuronLayer(Layer):
 @register("ReLU")
 class ReLULayer(NeuronLayer):
     fused = False  # forward folded into the producer's GEMM epilogue
+    bwd_fused = False  # backward folded into the consumer's backward (gate)
 
     def layer_setup(self, bottoms, tops):
         self.slope = float(self.lp.relu_param.negative_slope)
@@ -38,7 +39,7 @@ class ReLULayer(NeuronLayer):
         tops[0].data = ops.relu_forward(bottoms[0].data, self.slope)
 
     def backward(self, tops, propagate_down, bottoms):
-        if propagate_down[0]:
+        if propagate_down[0] and not self.bwd_fused:
             # in-place: bottom data was overwritten by top data; sign(y) == sign(x) for slope >= 0
             ref = bottoms[0].data
             bottoms[0].diff = ops.relu_backward(tops[0].diff, ref, self.slope)
@@ -46,6 +47,7 @@ class ReLULayer(NeuronLayer):
 
 @register("Dropout")
 class DropoutLayer(NeuronLayer):
+    relu_gate = False  # backward of the in-place ReLU producing the bottom is fused here
     def layer_setup(self, bottoms, tops):
         self.ratio = float(self.lp.dropout_param.dropout_ratio)
         if not 0.0 <= self.ratio < 1.0:
@@ -62,7 +64,10 @@ class DropoutLayer(NeuronLayer):
         if not propagate_down[0]:
             return
         if self.phase == 0 and self.ratio > 0:
-            bottoms[0].diff = ops.dropout_backward(tops[0].diff, self.ratio, self.ctx.rng_state, self.stream)
+            gate = bottoms[0].data if self.relu_gate else None
+            bottoms[0].diff = ops.dropout_backward(tops[0].diff, self.ratio, self.ctx.rng_state, self.stream, gate)
+        elif self.relu_gate:
+            bottoms[0].diff = ops.relu_backward(tops[0].diff, bottoms[0].data)
         elif tops[0] is not bottoms[0]:
             bottoms[0].diff = tops[0].diff
 

@@ -47,6 +47,7 @@ class ConvolutionLayer(Layer):
     min_tops = 1
 
     fuse_relu = False  # set by the net's fusion pass when an in-place ReLU follows
+    relu_gate = False  # ... and when an in-place ReLU PRODUCES the bottom (backward fused into dgrad)
 
     def layer_setup(self, bottoms, tops):
         cp = self.lp.convolution_param
@@ -90,9 +91,10 @@ class ConvolutionLayer(Layer):
     def forward(self, bottoms, tops):
         w = self.weight.compute
         bias = self.bias.data if self.bias is not None else None
-        for b, t in zip(bottoms, tops):
+        self._ws = [{} for _ in bottoms]  # forward -> backward scratch (e.g. folded input)
+        for i, (b, t) in enumerate(zip(bottoms, tops)):
             s = self.spec(b)
-            t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu)
+            t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i])
 
     def backward(self, tops, propagate_down, bottoms):
         w = self.weight.compute
@@ -100,7 +102,9 @@ class ConvolutionLayer(Layer):
         db = self.bias.diff if (self.bias is not None and self.param_grads_needed(1)) else None
         for i, (t, b) in enumerate(zip(tops, bottoms)):
             s = self.spec(b)
-            dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db)
+            gate = b.data if self.relu_gate else None
+            ws = self._ws[i] if i < len(getattr(self, "_ws", ())) else None
+            dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws)
             if propagate_down[i]:
                 b.diff = dx
 
@@ -200,6 +204,8 @@ class PoolingLayer(Layer):
             raise ValueError("Pooling: kernel size is required")
         self.aux = None
 
+    relu_gate = False  # backward of the slope-0 in-place ReLU producing the bottom is fused here
+
     def spec(self, b) -> PoolSpec:
         N, C, H, W = b.shape
         kh, kw = (H, W) if self.global_pooling else (self.kh, self.kw)
@@ -221,7 +227,7 @@ class PoolingLayer(Layer):
             y = _stochastic_test(xf, s).to(x.dtype)
             tops[0].data = y
             return
-        y, self.aux = ops.pool_forward_aux(x, s)
+        y, self.aux = ops.pool_forward_aux(x, s, self.relu_gate)
         tops[0].data = y
         if len(tops) > 1:
             tops[1].data = (self.aux.to(tops[1].dtype) if self.aux is not None
@@ -231,7 +237,8 @@ class PoolingLayer(Layer):
         if not propagate_down[0]:
             return
         s = self.spec(bottoms[0])
-        bottoms[0].diff = ops.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data)
+        bottoms[0].diff = ops.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data,
+                                            self.relu_gate)
 
 
 def _stochastic_test(xf, s: PoolSpec):
@@ -271,6 +278,7 @@ class InnerProductLayer(Layer):
     exact_bottoms = 1
     exact_tops = 1
     fuse_relu = False
+    relu_gate = False
 
     def layer_setup(self, bottoms, tops):
         p = self.lp.inner_product_param
@@ -318,7 +326,8 @@ class InnerProductLayer(Layer):
         x2 = b.data.reshape(M, self.Kdim)
         dw = self.weight.diff if self.param_grads_needed(0) else None
         db = self.bias.diff if (self.bias is not None and self.param_grads_needed(1)) else None
-        dx = ops.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db)
+        gate = b.data if self.relu_gate else None
+        dx = ops.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db, gate)
         if propagate_down[0]:
             b.diff = dx.reshape(b.data.shape)
 

@@ -50,16 +50,18 @@ softmax_backward = _dispatch("softmax_backward")
 accuracy = _dispatch("accuracy")
 
 
-def pool_backward(dy, x, s, aux=None, y=None):
+def pool_backward(dy, x, s, aux=None, y=None, gate=False):
+    """gate=True: x is a slope-0 in-place ReLU output whose backward is fused here (MAX
+    pooling on the GPU encodes it in the forward's argmax mask)."""
     if dy.is_cuda:
-        return _hipmod().pool_backward(dy, x, s, aux, y)
-    return ref.pool_backward(dy, x, s)
+        return _hipmod().pool_backward(dy, x, s, aux, y, gate)
+    return ref.pool_backward(dy, x, s, gate)
 
 
-def pool_forward_aux(x, s):
+def pool_forward_aux(x, s, gate=False):
     """Forward returning (y, aux) where aux is the GPU argmax mask (None on CPU)."""
     if x.is_cuda:
-        return _hipmod().pool_forward_mask(x, s)
+        return _hipmod().pool_forward_mask(x, s, gate)
     return ref.pool_forward(x, s), None
 
 
@@ -70,11 +72,11 @@ def dropout_forward(x, ratio, rng_state, stream):
     return ref.dropout_forward(x, ratio, seed, counter, stream)
 
 
-def dropout_backward(dy, ratio, rng_state, stream):
+def dropout_backward(dy, ratio, rng_state, stream, gate=None):
     if dy.is_cuda:
-        return _hipmod().dropout_backward(dy, ratio, rng_state, stream)
+        return _hipmod().dropout_backward(dy, ratio, rng_state, stream, gate)
     seed, counter = (int(v) for v in rng_state.tolist())
-    return ref.dropout_backward(dy, ratio, seed, counter, stream)
+    return ref.dropout_backward(dy, ratio, seed, counter, stream, gate)
 
 
 def softmax_loss_forward(x2, labels, ignore_label=None, normalize=True, outer_num=None):

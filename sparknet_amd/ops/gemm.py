@@ -24,7 +24,6 @@ OP_DENSE, OP_IM2COL = 0, 1
 EPI_BF16, EPI_F32, EPI_F32_ACC = 0, 1, 2
 BM = BN = 128
 BK = 64
-TARGET_BLOCKS = 512  # 2 blocks per CU on 256 CUs
 
 
 @dataclass
@@ -89,14 +88,36 @@ def choose_tile(M: int, N: int) -> int:
     return 1 if N <= 64 and M >= 256 else 0
 
 
+SLOTS = 512          # resident blocks: 2 per CU (64 KB of LDS each) x 256 CUs
+KTILE_US = 1.25      # measured: one 128x128x64 k-step of one block at full occupancy
+BLOCK_OVERHEAD = 4   # prologue + epilogue of a block, in k-steps
+REDUCE_BW = 5e12     # split-K slab read+write, bytes/s effective (+ one launch)
+
+
+def _cost(tiles: int, ktiles: int, s: int, out_elems: int) -> float:
+    """Modelled microseconds of a GEMM split s ways: whole waves of SLOTS blocks (a wave
+    that is 1 % full costs a full block time) plus the slab reduction."""
+    kt = -(-ktiles // s)
+    t = -(-tiles * s // SLOTS) * (kt + BLOCK_OVERHEAD) * KTILE_US
+    if s > 1:
+        t += (out_elems * 4.0 * (s + 1)) / REDUCE_BW * 1e6 + 3.0
+    return t
+
+
 def choose_splits(M: int, N: int, K: int, groups: int = 1, tile: int = 0) -> tuple[int, int]:
+    """Split-K factor minimising the wave-quantised cost model above: e.g. 54 tiles x 10
+    splits = 540 blocks would run a second, nearly empty wave; 9 splits fits in one."""
     bm, bn = TILES[tile]
     tiles = -(-M // bm) * -(-N // bn) * groups
-    splits = 1
-    if tiles < TARGET_BLOCKS and K > 4 * BK:
-        ws_cap = max(1, (256 << 20) // max(1, 4 * M * N * groups))  # fp32 partial slabs <= 256 MB
-        splits = max(1, min(-(-TARGET_BLOCKS // tiles), K // (4 * BK), 256, ws_cap))
-    kchunk = -(-K // splits)
+    ktiles = -(-K // BK)
+    ws_cap = max(1, (256 << 20) // max(1, 4 * M * N * groups))  # fp32 partial slabs <= 256 MB
+    smax = max(1, min(256, ktiles // 4, ws_cap))
+    best, best_t = 1, _cost(tiles, ktiles, 1, M * N * groups)
+    for s in range(2, smax + 1):
+        t = _cost(tiles, ktiles, s, M * N * groups)
+        if t < best_t * 0.98:
+            best, best_t = s, t
+    kchunk = -(-K // best)
     kchunk = -(-kchunk // BK) * BK
     splits = -(-K // kchunk)
     return splits, kchunk
@@ -104,9 +125,11 @@ def choose_splits(M: int, N: int, K: int, groups: int = 1, tile: int = 0) -> tup
 
 def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
          groups: int = 1, c_gstride: int = 0, bias: torch.Tensor | None = None, relu: bool = False,
-         splits: int | None = None) -> None:
+         splits: int | None = None, gate: torch.Tensor | None = None) -> None:
     """Run one (possibly grouped, split-K) GEMM.  ``epi``: EPI_BF16 (store bf16 with
-    bias/ReLU), EPI_F32 (store), EPI_F32_ACC (accumulate into an fp32 output)."""
+    bias/ReLU; ``gate``: a bf16 tensor laid out like ``out`` — outputs where gate <= 0
+    are zeroed, i.e. a following slope-0 ReLU's backward), EPI_F32 (store), EPI_F32_ACC
+    (accumulate into an fp32 output)."""
     if M == 0 or N == 0:
         return
     sa, a_mc, a_mode = _operand(A)
@@ -119,19 +142,23 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         splits = max(1, -(-K // kchunk))
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
+    gp = 0
+    if gate is not None:
+        assert epi == EPI_BF16 and gate.dtype == torch.bfloat16
+        gp = gate.data_ptr()
     if splits == 1:
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, BK), a_mc, a_mode, b_mc, b_mode, epi,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
-                               bias.data_ptr() if bias is not None else 0, int(relu), tile)
+                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp)
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         return
     ws = torch.empty((groups, splits, M, N), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
-                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0, tile)
+                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0, tile, 0)
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
     _lib.call("splitk_reduce", ws, splits, M * N, M, N, N, out, ldc, mode, bias, int(relu),
-              groups, splits * M * N, c_gstride)
+              groups, splits * M * N, c_gstride, gate)
 
 
 # --- dense helpers ---------------------------------------------------------------------
@@ -162,8 +189,10 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = Non
     return out
 
 
-def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """dx[M,K] = dy[M,N] @ w[N,K] in bf16 (B operand read transposed from LDS)."""
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
+                 gate: torch.Tensor | None = None) -> torch.Tensor:
+    """dx[M,K] = dy[M,N] @ w[N,K] in bf16 (B operand read transposed from LDS);
+    ``gate`` [M,K]: zero dx where gate <= 0 (fused ReLU backward)."""
     M, N = dy.shape
     K = w.shape[1]
     dyp = _pad8(dy, 1)
@@ -177,7 +206,14 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = N
         o = torch.empty((M, Kp), dtype=torch.bfloat16, device=dy.device)
     else:
         o = out
-    gemm(M, Kp, Np, Dense(dyp, Np, True), Dense(wp, Kp, False), o, o.stride(0), epi=EPI_BF16)
+    if gate is not None and (Kp != K or not gate.is_contiguous()):
+        gemm(M, Kp, Np, Dense(dyp, Np, True), Dense(wp, Kp, False), o, o.stride(0), epi=EPI_BF16)
+        o = o[:, :K] * (gate > 0).to(o.dtype)
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+    gemm(M, Kp, Np, Dense(dyp, Np, True), Dense(wp, Kp, False), o, o.stride(0), epi=EPI_BF16, gate=gate)
     if o is not out:
         o = o[:, :K]
         if out is not None:
@@ -207,6 +243,13 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate
 def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = True) -> None:
     """out[N] (+)= sum over rows of a bf16 [M, N] matrix (bias gradient)."""
     M, N = x.shape
-    nparts = max(1, min(1024, M // 64))
+    c8 = -(-N // 8)
+    cl = 1
+    while cl < c8 and cl < 64:
+        cl *= 2
+    cblocks = -(-c8 // cl)
+    rl = 256 // cl
+    # ~1024 blocks in pass 1, at least two rows per row lane
+    nparts = max(1, min(max(1, 1024 // cblocks), -(-M // (2 * rl))))
     part = torch.empty((nparts, N), dtype=torch.float32, device=x.device)
     _lib.call("colsum_bf16", x, M, N, x.stride(0), part, nparts, out, int(accumulate))

@@ -83,7 +83,9 @@ def _s2d_input(x, s: ConvSpec, plan):
     return x2
 
 
-def conv_forward(x, w, b, s: ConvSpec, relu=False):
+def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None):
+    """ws: optional per-layer dict kept from forward to backward (the space-to-depth
+    folded input is stored there so the weight-gradient pass does not rebuild it)."""
     x = _c(x)
     assert x.dtype == BF16 and w.dtype == BF16, (x.dtype, w.dtype)
     plan = _s2d_plan(s)
@@ -91,7 +93,10 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False):
         f, cp, rf, sf, s2 = plan
         w2 = torch.empty((s.K, rf, sf, s2.C), dtype=BF16, device=x.device)
         call("s2d_weight", _c(w), w2, s.K, s.R, s.S, s.C, f, cp, rf, sf)
-        return conv_forward(_s2d_input(x, s, plan), w2, b, s2, relu)
+        x2 = _s2d_input(x, s, plan)
+        if ws is not None:
+            ws["s2d"] = (x.data_ptr(), x._version, x2)
+        return conv_forward(x2, w2, b, s2, relu)
     M = s.N * s.P * s.Q
     y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device)
     if _implicit_ok(s):
@@ -117,7 +122,9 @@ def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
     return out
 
 
-def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None):
+def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None):
+    """gate: optional bf16 NHWC tensor shaped like x; dx is zeroed where gate <= 0
+    (the backward of a slope-0 in-place ReLU that produced x, fused into the dgrad)."""
     dy = _c(dy)
     x = _c(x)
     M = s.N * s.P * s.Q
@@ -128,7 +135,11 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None):
     plan = _s2d_plan(s) if s.Kg % 8 == 0 else None
     if dw is not None and plan is not None:
         f, cp, rf, sf, s2 = plan
-        x2 = _s2d_input(x, s, plan)
+        cached = ws.get("s2d") if ws is not None else None
+        if cached is not None and cached[0] == x.data_ptr() and cached[1] == x._version:
+            x2 = cached[2]
+        else:
+            x2 = _s2d_input(x, s, plan)
         k2 = rf * sf * s2.C
         dw2 = torch.empty((s.K, k2), dtype=torch.float32, device=x.device)
         gemm(s.K, k2, M, Dense(dy2, s.K, kcontig=False), Im2col(x2, _geom(s2), kcontig=False), dw2, k2,
@@ -163,7 +174,8 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None):
         kr2 = s.R * s.S * s.Kg
         A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
         B = Dense(wt.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
-        gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg)
+        gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg,
+             gate=_c(gate) if gate is not None else None)
         return dx
     # generic: dcol = dy_g @ W_g, then col2im (gather, no atomics)
     wp, kpad = _weight_kpad(w, s)
@@ -178,6 +190,8 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None):
         gemm(M, kpad, kgp, Dense(dyg, dyg.stride(0), True), Dense(_c(wg), kpad, False), dcol, kpad, epi=EPI_BF16)
         call("col2im", dcol, dx, s.N, s.H, s.W, s.C, s.P, s.Q, s.R, s.S, s.sh, s.sw, s.ph, s.pw, s.dh, s.dw,
              s.Cg, kpad, g * s.Cg)
+    if gate is not None:
+        dx = relu_backward(dx, gate)
     return dx
 
 
@@ -189,13 +203,15 @@ def linear_forward(x2, w, b, relu=False):
     return linear_fwd(_c(x2), _c(w), b, relu)
 
 
-def linear_backward(dy2, x2, w, need_dx, dw=None, db=None):
+def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None):
     dy2 = _c(dy2)
     if db is not None:
         colsum(dy2, db, accumulate=True)
     if dw is not None:
         linear_wgrad(dy2, _c(x2), dw, accumulate=True)
-    return linear_dgrad(dy2, _c(w)) if need_dx else None
+    if not need_dx:
+        return None
+    return linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)
 
 
 # --------------------------------------------------------------------------------------
@@ -206,11 +222,13 @@ def _pool_args(s: PoolSpec):
     return (s.N, s.H, s.W, s.C, s.P, s.Q, s.kh, s.kw, s.sh, s.sw, s.ph, s.pw, s.method)
 
 
-def pool_forward_mask(x, s: PoolSpec):
+def pool_forward_mask(x, s: PoolSpec, gate: bool = False):
+    """gate=True (MAX only): x is the output of a slope-0 in-place ReLU whose backward is
+    folded into the argmax mask (windows with max <= 0 pass no gradient)."""
     x = _c(x)
     y = torch.empty((s.N, s.P, s.Q, s.C), dtype=BF16, device=x.device)
     mask = torch.empty((s.N, s.P, s.Q, s.C), dtype=torch.uint8, device=x.device) if s.method == POOL_MAX else None
-    call("pool_fwd", x, y, mask, *_pool_args(s))
+    call("pool_fwd", x, y, mask, *_pool_args(s), int(gate and s.method == POOL_MAX))
     return y, mask
 
 
@@ -218,11 +236,13 @@ def pool_forward(x, s: PoolSpec):
     return pool_forward_mask(x, s)[0]
 
 
-def pool_backward(dy, x, s: PoolSpec, mask=None, y=None):
+def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False):
     dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=dy.device)
     if s.method == POOL_MAX and mask is None:
-        _, mask = pool_forward_mask(x, s)
+        _, mask = pool_forward_mask(x, s, gate)
     call("pool_bwd", _c(dy), mask, dx, *_pool_args(s))
+    if gate and s.method != POOL_MAX:
+        dx = relu_backward(dx, x)
     return dx
 
 
@@ -274,12 +294,12 @@ def relu_backward(dy, x, slope=0.0):
     return dx
 
 
-def _dropout(x, ratio, rng_state, stream):
+def _dropout(x, ratio, rng_state, stream, gate=None):
     x = _c(x)
     if x.numel() % 8:
         raise NotImplementedError("dropout on GPU needs element count % 8 == 0")
     y = torch.empty_like(x)
-    call("dropout", x, y, x.numel(), rng_state, int(stream), float(ratio))
+    call("dropout", x, y, x.numel(), rng_state, int(stream), float(ratio), _c(gate) if gate is not None else None)
     return y
 
 
@@ -287,8 +307,8 @@ def dropout_forward(x, ratio, rng_state, stream):
     return _dropout(x, ratio, rng_state, stream)
 
 
-def dropout_backward(dy, ratio, rng_state, stream):
-    return _dropout(dy, ratio, rng_state, stream)
+def dropout_backward(dy, ratio, rng_state, stream, gate=None):
+    return _dropout(dy, ratio, rng_state, stream, gate)
 
 
 def cast_f32_to_bf16(src, dst):

@@ -30,7 +30,7 @@ def _w_oihw(w, s: ConvSpec):
 
 # --- convolution (base_conv_layer.cpp:312-376, conv_layer.cpp) -----------------------
 
-def conv_forward(x, w, b, s: ConvSpec, relu=False):
+def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None):
     y = F.conv2d(nchw(x.float()), _w_oihw(w.float(), s), b.float() if b is not None else None,
                  stride=(s.sh, s.sw), padding=(s.ph, s.pw), dilation=(s.dh, s.dw), groups=s.groups)
     if relu:
@@ -38,7 +38,12 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False):
     return nhwc(y).to(x.dtype)
 
 
-def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None):
+def _gated(dx, gate):
+    """Backward of a slope-0 ReLU whose output is ``gate`` (fused into the producer)."""
+    return dx if gate is None else dx * (gate > 0).to(dx.dtype)
+
+
+def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None):
     dyn = nchw(dy.float())
     xn = nchw(x.float())
     wo = _w_oihw(w.float(), s)
@@ -46,7 +51,7 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None):
     if need_dx:
         dx = torch.nn.grad.conv2d_input(xn.shape, wo, dyn, stride=(s.sh, s.sw), padding=(s.ph, s.pw),
                                         dilation=(s.dh, s.dw), groups=s.groups)
-        dx = nhwc(dx).to(x.dtype)
+        dx = _gated(nhwc(dx).to(x.dtype), gate)
     if dw is not None:
         gw = torch.nn.grad.conv2d_weight(xn, wo.shape, dyn, stride=(s.sh, s.sw), padding=(s.ph, s.pw),
                                          dilation=(s.dh, s.dw), groups=s.groups)
@@ -78,13 +83,15 @@ def linear_forward(x2, w, b, relu=False):
     return y.to(x2.dtype)
 
 
-def linear_backward(dy2, x2, w, need_dx, dw=None, db=None):
+def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None):
     dyf = dy2.float()
     if dw is not None:
         dw += dyf.t() @ x2.float()
     if db is not None:
         db += dyf.sum(0)
-    return (dyf @ w.float()).to(x2.dtype) if need_dx else None
+    if not need_dx:
+        return None
+    return _gated((dyf @ w.float()).to(x2.dtype), gate.reshape(x2.shape) if gate is not None else None)
 
 
 # --- pooling (pooling_layer.cpp / .cu) -------------------------------------------------
@@ -124,11 +131,11 @@ def pool_forward(x, s: PoolSpec):
     return nhwc(y).to(x.dtype)
 
 
-def pool_backward(dy, x, s: PoolSpec):
+def pool_backward(dy, x, s: PoolSpec, gate=False):
     xf = x.float().detach().requires_grad_(True)
     y = _pool_fwd_f32(xf, s)
     (g,) = torch.autograd.grad(y, xf, nchw(dy.float()))
-    return g.to(x.dtype)
+    return _gated(g.to(x.dtype), x if gate else None)
 
 
 # --- LRN (lrn_layer.cpp / .cu) -------------------------------------------------------
@@ -217,8 +224,8 @@ def dropout_forward(x, ratio, seed, counter, stream):
     return (x.float() * m * scale).to(x.dtype)
 
 
-def dropout_backward(dy, ratio, seed, counter, stream):
-    return dropout_forward(dy, ratio, seed, counter, stream)
+def dropout_backward(dy, ratio, seed, counter, stream, gate=None):
+    return _gated(dropout_forward(dy, ratio, seed, counter, stream), gate)
 
 
 # --- softmax / softmax-with-loss (softmax_loss_layer.cpp / .cu) ------------------------

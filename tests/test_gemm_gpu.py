@@ -52,9 +52,39 @@ def test_linear_wgrad(gpu, M, N, K):
     _close(dw, 1 + dy.float().t() @ x.float())
 
 
-def test_colsum(gpu):
+@pytest.mark.parametrize("M,N", [(5000, 96), (256, 4096), (256, 1000), (77, 13), (3000, 700), (100000, 48)])
+def test_colsum(gpu, M, N):
     from sparknet_amd.ops import gemm
-    x = _bf(5000, 96, device=gpu)
-    out = torch.ones(96, device=gpu)
+    x = _bf(M, N, device=gpu)
+    out = torch.ones(N, device=gpu)
     gemm.colsum(x, out)
     _close(out, 1 + x.float().sum(0), 1e-3)
+    gemm.colsum(x, out, accumulate=False)
+    _close(out, x.float().sum(0), 1e-3)
+
+
+@pytest.mark.parametrize("splits", [1, 3, 16, 100])
+def test_forced_splitk_epilogues(gpu, splits):
+    """Split-K through both reduce kernels with every epilogue (bias, ReLU, gate, fp32
+    store / accumulate) against the unsplit fp32 product."""
+    from sparknet_amd.ops import gemm as G
+    M, N, K = 96, 200, 64 * 110
+    x, w = _bf(M, K, device=gpu), _bf(N, K, device=gpu)
+    b = torch.randn(N, device=gpu)
+    gate = _bf(M, N, device=gpu)
+    ref = x.float() @ w.float().t()
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    G.gemm(M, N, K, G.Dense(x, K, True), G.Dense(w, K, True), y, N, epi=G.EPI_BF16, bias=b, relu=True,
+           splits=splits, gate=gate)
+    _close(y, torch.relu(ref + b) * (gate.float() > 0))
+    acc = torch.ones(M, N, device=gpu)
+    G.gemm(M, N, K, G.Dense(x, K, True), G.Dense(w, K, True), acc, N, epi=G.EPI_F32_ACC, splits=splits)
+    _close(acc, 1 + ref)
+
+
+def test_linear_dgrad_gate(gpu):
+    from sparknet_amd.ops import gemm
+    dy, w = _bf(256, 512, device=gpu), _bf(512, 384, device=gpu)
+    gate = _bf(256, 384, device=gpu)
+    dx = gemm.linear_dgrad(dy, w, gate=gate)
+    _close(dx, (dy.float() @ w.float()) * (gate.float() > 0))

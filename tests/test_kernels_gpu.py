@@ -114,6 +114,25 @@ def test_relu_dropout(gpu):
     close(y, yr, 1e-2)
     keep = (y != 0).float().mean().item()
     assert 0.45 < keep < 0.55
+    # fused ReLU backward: gate = ReLU output (after in-place dropout)
+    gate = hip.relu_forward(x, 0.0)
+    dx = hip.dropout_backward(dy, 0.5, rng, 3, gate)
+    close(dx, ref.dropout_backward(dy.cpu(), 0.5, 1234567, 42, 3, gate.cpu()), 1e-2)
+
+
+@pytest.mark.parametrize("geo", [(2, 55, 55, 96, 3, 2, 0), (2, 13, 13, 256, 3, 2, 0), (2, 9, 9, 3, 2, 2, 0)])
+def test_maxpool_relu_gate(gpu, geo):
+    """Max pooling over a ReLU output with the ReLU backward folded into the argmax mask:
+    windows whose max is 0 pass no gradient."""
+    from sparknet_amd.ops import hip
+    N, H, W, Cc, k, st, pd = geo
+    s = PoolSpec(N, H, W, Cc, k, k, st, st, pd, pd, POOL_MAX)
+    x = torch.relu(rnd(N, H, W, Cc).float() - 0.9).to(torch.bfloat16)  # many all-zero windows
+    y, mask = hip.pool_forward_mask(x, s, gate=True)
+    close(y, ref.pool_forward(x, s), 1e-2)
+    dy = rnd(N, s.P, s.Q, Cc)
+    close(hip.pool_backward(dy, x, s, mask, gate=True), ref.pool_backward(dy, x, s, gate=True), 1e-2)
+    close(hip.pool_backward(dy, x, s, None, gate=True), ref.pool_backward(dy, x, s, gate=True), 1e-2)
 
 
 def test_softmax_loss_and_accuracy(gpu):

@@ -184,3 +184,39 @@ def test_loss_weight_scales_gradient():
         grads.append(net.flat_diff.clone())
     scale = grads[0].abs().max()
     assert torch.allclose(grads[1], 2.5 * grads[0], rtol=1e-3, atol=1e-5 * float(scale))
+
+
+def _caffenet_tiny(ratio=0.5):
+    n = models.caffenet(train_batch=2, test_batch=2, crop=67, classes=7)
+    for l in n.layer:
+        if l.type == "Dropout":
+            l.dropout_param.dropout_ratio = ratio
+        if l.type == "InnerProduct" and l.name in ("fc6", "fc7"):
+            l.inner_product_param.num_output = 16
+    return n
+
+
+def _grads_with_fusion(netparam, fuse, device="cpu"):
+    from sparknet_amd.engine import fuse_relu
+    net = Net(netparam, phase=proto.TRAIN, seed=11, device=device)
+    counts = (0, 0)
+    if fuse:
+        nf = fuse_relu(net)  # also runs the backward (gate) fusion pass
+        counts = (nf, sum(1 for l in net.layers if getattr(l, "bwd_fused", False)))
+    g = torch.Generator().manual_seed(9)
+    net.blob_by_name("data").set_nchw(torch.randn(2, 3, 67, 67, generator=g))
+    net.blob_by_name("label").set_nchw(torch.tensor([[1.0], [5.0]]))
+    net.clear_param_diffs()
+    loss = net.forward_backward()
+    return float(loss), net.flat_diff.detach().cpu().clone(), counts
+
+
+def test_relu_forward_backward_fusion_matches_unfused():
+    """ReLU folded into the producer's epilogue (forward) and into the consumer's backward
+    (dgrad gate / max-pool mask / dropout gate) gives the unfused gradients."""
+    n = _caffenet_tiny()
+    l0, g0, _ = _grads_with_fusion(n, False)
+    l1, g1, counts = _grads_with_fusion(n, True)
+    assert counts == (7, 7), counts  # relu1..7 forward-fused; all 7 backward-fused
+    assert abs(l0 - l1) < 1e-5 * max(1.0, abs(l0))
+    assert torch.allclose(g0, g1, rtol=1e-5, atol=1e-6 * float(g0.abs().max()))
