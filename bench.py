@@ -59,7 +59,7 @@ def main():
     from sparknet_amd import models
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.data.prefetch import DeviceFeeder, SyntheticSource
-    from sparknet_amd.engine import LocalSGDTrainer, fuse_relu
+    from sparknet_amd.engine import LocalSGDTrainer, fuse_input_fold, fuse_relu
     from sparknet_amd.ops import _lib
     from sparknet_amd.parallel import Comm
 
@@ -77,6 +77,7 @@ def main():
     src = SyntheticSource(B, C, HW, HW, classes=classes, pool=3, seed=rank)
     feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
                           mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev)
+    fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph)
     trainer.broadcast_initial()
 
@@ -128,7 +129,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
-                "hipgraph": not args.no_graph,
+                "hipgraph": not args.no_graph, "fused_input_fold": fused_fold,
                 "final_loss": round(final_loss, 4),
             },
         }

@@ -60,6 +60,95 @@ extern "C" int sn_augment(const uint8_t* src, bf16_t* dst, long long N, long lon
   return SN_CHECK_LAUNCH();
 }
 
+// Fused augment + space-to-depth fold for an input layer whose only consumer is a
+// stride-f convolution on the S2D path (see s2d_input in eltwise.hip): writes the folded
+// bf16 tensor x2 [N][Hs2][Ws2][f*f*Cp] straight from the uint8 planar source, so the
+// NHWC crop is never materialised (one pass instead of augment + s2d_input).  Same
+// Philox crop / mirror draw as augment_kernel, so both produce identical samples.
+// One thread per folded output pixel (the Philox draw is amortised over its f*f*Cp
+// channels); F / CP are compile-time for the common RGB cases so the channel ->
+// (dy, dx, c) decode is shifts, with a runtime fallback.
+template <int F, int CP, int MM>
+__global__ void augment_s2d_kernel(const uint8_t* __restrict__ src, bf16_t* __restrict__ x2, int N, int C, int Hs,
+                                   int Ws, int crop_h, int crop_w, const float* __restrict__ mean, int mean_mode,
+                                   float scale, const long long* __restrict__ rng, int train, int mirror, int H2,
+                                   int W2, int f_rt, int cp_rt, int ph, int pw) {
+  const int f = F ? F : f_rt, Cp = CP ? CP : cp_rt;
+  const int cv = f * f * Cp / 8;
+  const long long total = (long long)N * H2 * W2;
+  const unsigned long long seed = rng ? (unsigned long long)rng[0] : 0ull;
+  const unsigned long long counter = rng ? (unsigned long long)rng[1] : 0ull;
+  for (long long pix = blockIdx.x * (long long)blockDim.x + threadIdx.x; pix < total;
+       pix += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(pix % W2), r = (int)((pix / W2) % H2), n = (int)(pix / ((long long)W2 * H2));
+    int ho, wo, mir;
+    if (train) {
+      uint4 u = philox4x32(make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)),
+                           make_uint4((uint32_t)n, 0xA5A50000u, (uint32_t)counter, (uint32_t)(counter >> 32)));
+      ho = (int)(u.x % (uint32_t)(Hs - crop_h + 1));
+      wo = (int)(u.y % (uint32_t)(Ws - crop_w + 1));
+      mir = mirror ? (int)(u.z & 1u) : 0;
+    } else {
+      ho = (Hs - crop_h) / 2;
+      wo = (Ws - crop_w) / 2;
+      mir = 0;
+    }
+    uint4* out = reinterpret_cast<uint4*>(x2) + pix * cv;
+#pragma unroll
+    for (int ch = 0; ch < cv; ++ch) {
+      float v[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int e = ch * 8 + t;
+        const int d = e / Cp, c = e - d * Cp;
+        const int h = r * f + d / f - ph, w = j * f + d % f - pw;  // crop coordinates
+        // branch-free: load from a clamped in-image address, then select (a load under a
+        // per-element condition makes hipcc wait vmcnt(0) per element)
+        const bool ok = c < C && (unsigned)h < (unsigned)crop_h && (unsigned)w < (unsigned)crop_w;
+        const int hc = min(max(h, 0), crop_h - 1), wc = min(max(w, 0), crop_w - 1), cc = min(c, C - 1);
+        const int sh = hc + ho, sw = (mir ? (crop_w - 1 - wc) : wc) + wo;
+        float x = (float)src[(((long long)n * C + cc) * Hs + sh) * Ws + sw];
+        if (MM == 1) x -= mean[cc];  // mean mode is a template parameter: no per-element branch
+        if (MM == 2) x -= mean[((long long)cc * Hs + sh) * Ws + sw];
+        x = ok ? x * scale : 0.f;
+        v[t] = x;
+      }
+      out[ch] = pack8(v);
+    }
+  }
+}
+
+extern "C" int sn_augment_s2d(const uint8_t* src, bf16_t* x2, long long N, long long C, long long Hs, long long Ws,
+                              long long crop_h, long long crop_w, const float* mean, long long mean_mode, float scale,
+                              const long long* rng, long long train, long long mirror, long long H2, long long W2,
+                              long long f, long long Cp, long long ph, long long pw, hipStream_t st) {
+  if (crop_h > Hs || crop_w > Ws || (f * f * Cp) % 8 || Cp < C) return 9;
+  long long total = N * H2 * W2;
+  dim3 grid(sn_blocks(total, 256, 16384));
+#define SN_AUG_S2D_MM(FF, CC, MM)                                                                               \
+  hipLaunchKernelGGL((augment_s2d_kernel<FF, CC, MM>), grid, dim3(256), 0, st, src, x2, (int)N, (int)C, (int)Hs, (int)Ws, \
+                     (int)crop_h, (int)crop_w, mean, (int)mean_mode, scale, rng, (int)train, (int)mirror, (int)H2,     \
+                     (int)W2, (int)f, (int)Cp, (int)ph, (int)pw)
+#define SN_AUG_S2D(FF, CC)              \
+  do {                                  \
+    if (mean_mode == 1)                 \
+      SN_AUG_S2D_MM(FF, CC, 1);         \
+    else if (mean_mode == 2)            \
+      SN_AUG_S2D_MM(FF, CC, 2);         \
+    else                                \
+      SN_AUG_S2D_MM(FF, CC, 0);         \
+  } while (0)
+  if (f == 4 && Cp == 3)  // AlexNet / CaffeNet conv1: 11x11 stride 4 on RGB -> 3x3 on 48 channels
+    SN_AUG_S2D(4, 3);
+  else if (f == 2 && Cp == 4)  // GoogLeNet / ResNet conv1: 7x7 stride 2 on RGB -> 4x4 on 16 channels
+    SN_AUG_S2D(2, 4);
+  else
+    SN_AUG_S2D(0, 0);
+#undef SN_AUG_S2D
+#undef SN_AUG_S2D_MM
+  return SN_CHECK_LAUNCH();
+}
+
 // labels: uint8/int32 -> float (JavaData label blob is [B, 1] float, ProtoLoader.scala:53)
 __global__ void labels_kernel(const int* __restrict__ src, float* __restrict__ dst, int n) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -276,7 +276,9 @@ __global__ void s2d_input(const bf16_t* __restrict__ x, bf16_t* __restrict__ x2,
         const int d = e / Cp, c = e - d * Cp;
         const int h = r * f + d / f - ph, w = j * f + d % f - pw;
         const bool v = c < C && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-        v2[u] = v ? x[(((long long)n * H + h) * W + w) * C + c] : (bf16_t)0;
+        const int hc = min(max(h, 0), H - 1), wc = min(max(w, 0), W - 1), cc = min(c, C - 1);
+        const bf16_t ld = x[(((long long)n * H + hc) * W + wc) * C + cc];  // unconditional load
+        v2[u] = v ? ld : (bf16_t)0;
       }
       w32[t / 2] = (uint32_t)v2[0] | ((uint32_t)v2[1] << 16);
     }

@@ -125,6 +125,7 @@ class DeviceFeeder:
         self.slots = [(torch.empty(self.shape, dtype=torch.uint8, device=self.device),
                        torch.empty((N,), dtype=torch.int32, device=self.device)) for _ in range(slots)]
         self.events = [None] * slots
+        self.fold = None  # (x2, plan, ConvSpec) when fused with the first conv's S2D fold
         self.k = 0
         self._pending = None
         if not isinstance(source, SyntheticSource):
@@ -169,8 +170,13 @@ class DeviceFeeder:
             self._stage_cpu(src, lab)
             return
         from ..ops import hip
-        hip.augment(src, self.data_blob.data, self.crop, self.mean, self.mean_mode, self.scale, self.rng_state,
-                    self.train, self.mirror)
+        if self.fold is not None:
+            x2, plan, spec = self.fold
+            hip.augment_s2d(src, x2, self.crop, plan, spec, self.mean, self.mean_mode, self.scale, self.rng_state,
+                            self.train, self.mirror)
+        else:
+            hip.augment(src, self.data_blob.data, self.crop, self.mean, self.mean_mode, self.scale,
+                        self.rng_state, self.train, self.mirror)
         _lib.call("labels_to_float", lab, self.label_blob.data, lab.numel())
 
     def _stage_cpu(self, src, lab) -> None:

@@ -84,6 +84,35 @@ def fuse_relu_backward(net) -> int:
     return n
 
 
+def fuse_input_fold(net, feeder) -> bool:
+    """If the feeder's data blob is consumed only by a strided low-channel convolution on
+    the space-to-depth path (AlexNet/CaffeNet conv1), make the feeder write the folded
+    tensor directly (one fused augment + fold kernel) and the convolution read it.  The
+    NHWC data blob is then no longer written during training steps.  GPU only."""
+    if feeder is None or feeder.device.type != "cuda":
+        return False
+    from .ops import hip
+    try:
+        bid = net.blob_names.index(feeder.data_blob.name)
+    except (AttributeError, ValueError):
+        return False
+    consumers = [li for li, b in enumerate(net.bottom_ids) if bid in b]
+    if len(consumers) != 1:
+        return False
+    conv = net.layers[consumers[0]]
+    if conv.type_name != "Convolution" or net.bottom_ids[consumers[0]].index(bid) != 0:
+        return False
+    spec = conv.spec(feeder.data_blob)
+    plan = hip.s2d_plan(spec)
+    if plan is None or spec.H != feeder.crop or spec.C != feeder.shape[1]:
+        return False
+    s2 = plan[4]
+    x2 = torch.empty((spec.N, s2.H, s2.W, s2.C), dtype=torch.bfloat16, device=feeder.device)
+    feeder.fold = (x2, plan, spec)
+    conv.folded_input = x2
+    return True
+
+
 class GraphStep:
     """One captured solver iteration (iter_size = 1)."""
 

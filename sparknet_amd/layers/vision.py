@@ -48,6 +48,7 @@ class ConvolutionLayer(Layer):
 
     fuse_relu = False  # set by the net's fusion pass when an in-place ReLU follows
     relu_gate = False  # ... and when an in-place ReLU PRODUCES the bottom (backward fused into dgrad)
+    folded_input = None  # S2D-folded bottom 0 written by a fused augment (engine.fuse_input_fold)
 
     def layer_setup(self, bottoms, tops):
         cp = self.lp.convolution_param
@@ -94,7 +95,8 @@ class ConvolutionLayer(Layer):
         self._ws = [{} for _ in bottoms]  # forward -> backward scratch (e.g. folded input)
         for i, (b, t) in enumerate(zip(bottoms, tops)):
             s = self.spec(b)
-            t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i])
+            folded = self.folded_input if i == 0 else None
+            t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i], folded=folded)
 
     def backward(self, tops, propagate_down, bottoms):
         w = self.weight.compute

@@ -83,9 +83,11 @@ def _s2d_input(x, s: ConvSpec, plan):
     return x2
 
 
-def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None):
+def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None):
     """ws: optional per-layer dict kept from forward to backward (the space-to-depth
-    folded input is stored there so the weight-gradient pass does not rebuild it)."""
+    folded input is stored there so the weight-gradient pass does not rebuild it).
+    folded: the S2D-folded input already produced upstream (fused augment + fold); x is
+    then not read."""
     x = _c(x)
     assert x.dtype == BF16 and w.dtype == BF16, (x.dtype, w.dtype)
     plan = _s2d_plan(s)
@@ -93,7 +95,7 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None):
         f, cp, rf, sf, s2 = plan
         w2 = torch.empty((s.K, rf, sf, s2.C), dtype=BF16, device=x.device)
         call("s2d_weight", _c(w), w2, s.K, s.R, s.S, s.C, f, cp, rf, sf)
-        x2 = _s2d_input(x, s, plan)
+        x2 = folded if folded is not None else _s2d_input(x, s, plan)
         if ws is not None:
             ws["s2d"] = (x.data_ptr(), x._version, x2)
         return conv_forward(x2, w2, b, s2, relu)
@@ -420,6 +422,22 @@ def scale_shadow(flat, shadow, scale: float):
 # --------------------------------------------------------------------------------------
 # Data augmentation
 # --------------------------------------------------------------------------------------
+
+def s2d_plan(s: ConvSpec):
+    return _s2d_plan(s)
+
+
+def augment_s2d(src_u8, x2, crop, plan, s: ConvSpec, mean=None, mean_mode=0, scale=1.0, rng_state=None,
+                train=True, mirror=False):
+    """Fused augment + space-to-depth fold into x2 (see conv_forward(folded=...))."""
+    N, Cc, Hs, Ws = src_u8.shape
+    f, cp, rf, sf, s2 = plan
+    assert tuple(x2.shape) == (N, s2.H, s2.W, s2.C) and x2.dtype == BF16 and x2.is_contiguous()
+    assert s.C == Cc and s.H == crop and s.W == crop
+    call("augment_s2d", _c(src_u8), x2, N, Cc, Hs, Ws, crop, crop, mean, int(mean_mode), float(scale), rng_state,
+         int(train), int(mirror), s2.H, s2.W, f, cp, s.ph, s.pw)
+    return x2
+
 
 def augment(src_u8, dst, crop, mean=None, mean_mode=0, scale=1.0, rng_state=None, train=True, mirror=False,
             offs_out=None):

@@ -30,7 +30,7 @@ def _w_oihw(w, s: ConvSpec):
 
 # --- convolution (base_conv_layer.cpp:312-376, conv_layer.cpp) -----------------------
 
-def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None):
+def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None):
     y = F.conv2d(nchw(x.float()), _w_oihw(w.float(), s), b.float() if b is not None else None,
                  stride=(s.sh, s.sw), padding=(s.ph, s.pw), dilation=(s.dh, s.dw), groups=s.groups)
     if relu:

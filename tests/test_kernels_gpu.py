@@ -211,3 +211,24 @@ def test_cast_and_augment(gpu):
             crop = crop.flip(-1)
         expect = ((crop - mean.view(3, 1, 1)) * 0.5).permute(1, 2, 0)
         close(out[n], expect, 1e-2)
+
+
+@pytest.mark.parametrize("mean_mode", [1, 2])
+@pytest.mark.parametrize("ksp", [(11, 4, 0), (7, 2, 3)])
+def test_augment_s2d_equals_augment_then_fold(gpu, mean_mode, ksp):
+    """The fused augment + space-to-depth kernel is bitwise the two-pass result."""
+    from sparknet_amd.ops import hip
+    N, crop = 3, 35
+    img = torch.randint(0, 256, (N, 3, 40, 44), dtype=torch.uint8, device="cuda")
+    mean = (torch.rand(3, device="cuda") * 200) if mean_mode == 1 else (torch.rand(3, 40, 44, device="cuda") * 200)
+    rng = torch.tensor([11, 5], dtype=torch.int64, device="cuda")
+    k, st, pd = ksp
+    s = ConvSpec(N, crop, crop, 3, 16, k, k, st, st, pd, pd)
+    plan = hip.s2d_plan(s)
+    assert plan is not None
+    nhwc = torch.empty((N, crop, crop, 3), dtype=torch.bfloat16, device="cuda")
+    hip.augment(img, nhwc, crop, mean, mean_mode, 0.25, rng, True, True)
+    ref2 = hip._s2d_input(nhwc, s, plan)
+    x2 = torch.empty_like(ref2)
+    hip.augment_s2d(img, x2, crop, plan, s, mean, mean_mode, 0.25, rng, True, True)
+    assert torch.equal(x2, ref2)
