@@ -57,6 +57,29 @@ SN_DEV int fdiv(int n, int d, float inv) {
   return q;
 }
 
+// Exact unsigned 32-bit division by a runtime-invariant divisor (multiply-high + shift,
+// Granlund-Montgomery): NHWC index decodes in the elementwise kernels otherwise compile
+// to 64-bit division loops of ~100 instructions each.
+struct FDiv {
+  uint32_t d, m;
+  int l;
+};
+
+static inline FDiv make_fdiv(uint32_t d) {
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  FDiv f;
+  f.d = d;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+  f.l = l;
+  return f;
+}
+
+SN_DEV uint32_t udiv(uint32_t n, const FDiv& f) {
+  const uint32_t t = __umulhi(n, f.m);
+  return (uint32_t)(((uint64_t)t + n) >> f.l);
+}
+
 SN_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

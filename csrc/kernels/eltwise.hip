@@ -305,7 +305,7 @@ __global__ void s2d_weight(const bf16_t* __restrict__ w, bf16_t* __restrict__ w2
 
 // dW [K][R][S][C] (f32) += fold(dW2 [K][Rf][Sf][f*f*Cp] (f32))
 __global__ void s2d_weight_grad(const float* __restrict__ dw2, float* __restrict__ dw, int K, int R, int S, int C,
-                                int f, int Cp, int Rf, int Sf) {
+                                int f, int Cp, int Rf, int Sf, int accumulate) {
   const long long total = (long long)K * R * S * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     int c = (int)(i % C);
@@ -314,7 +314,8 @@ __global__ void s2d_weight_grad(const float* __restrict__ dw2, float* __restrict
     const int r = (int)(t % R);
     const int k = (int)(t / R);
     const int rf = r / f, dy = r % f, sf = s / f, dx = s % f;
-    dw[i] += dw2[(((long long)k * Rf + rf) * Sf + sf) * (f * f * Cp) + (dy * f + dx) * Cp + c];
+    const float g = dw2[(((long long)k * Rf + rf) * Sf + sf) * (f * f * Cp) + (dy * f + dx) * Cp + c];
+    dw[i] = accumulate ? dw[i] + g : g;
   }
 }
 
@@ -336,8 +337,9 @@ extern "C" int sn_s2d_weight(const bf16_t* w, bf16_t* w2, long long K, long long
 }
 
 extern "C" int sn_s2d_weight_grad(const float* dw2, float* dw, long long K, long long R, long long S, long long C,
-                                  long long f, long long Cp, long long Rf, long long Sf, hipStream_t st) {
+                                  long long f, long long Cp, long long Rf, long long Sf, long long accumulate,
+                                  hipStream_t st) {
   hipLaunchKernelGGL(s2d_weight_grad, dim3(sn_blocks(K * R * S * C, 256, 16384)), dim3(256), 0, st, dw2, dw, (int)K,
-                     (int)R, (int)S, (int)C, (int)f, (int)Cp, (int)Rf, (int)Sf);
+                     (int)R, (int)S, (int)C, (int)f, (int)Cp, (int)Rf, (int)Sf, (int)accumulate);
   return SN_CHECK_LAUNCH();
 }

@@ -20,21 +20,28 @@
 struct LrnP {
   int N, H, W, C, size, pre;
   float alpha, beta, k;
+  FDiv fcv;  // C / 8
 };
 
 SN_DEV float powneg(float s, float beta) { return __expf(-beta * __logf(s)); }
 
-// Load the 24 channels [c0-8, c0+16) of a pixel as fp32 (zeros outside [0, C)).
+// Load the 24 channels [c0-8, c0+16) of a pixel as fp32 (zeros outside [0, C)).  The
+// three 16-B loads are unconditional (clamped chunk index) and masked afterwards, so
+// they are all in flight together.
 SN_DEV void load24(const bf16_t* row, int c0, int C, float* v) {
+  uint4 raw[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    int c = c0 - 8 + 8 * j;
-    if (c >= 0 && c < C) {
-      unpack8(*reinterpret_cast<const uint4*>(row + c), v + 8 * j);
-    } else {
+    const int c = min(max(c0 - 8 + 8 * j, 0), C - 8);
+    raw[j] = *reinterpret_cast<const uint4*>(row + c);
+  }
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[8 * j + t] = 0.f;
-    }
+  for (int j = 0; j < 3; ++j) {
+    const int c = c0 - 8 + 8 * j;
+    const bool ok = c >= 0 && c < C;
+    unpack8(raw[j], v + 8 * j);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[8 * j + t] = ok ? v[8 * j + t] : 0.f;
   }
 }
 
@@ -46,8 +53,9 @@ __global__ void lrn_across_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict_
   const float a = p.alpha / p.size;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * 8;
-    const bf16_t* row = x + (i / cv) * p.C;
+    const uint32_t pix = udiv((uint32_t)i, p.fcv);
+    const int c0 = (int)((uint32_t)i - pix * cv) * 8;
+    const bf16_t* row = x + (long long)pix * p.C;
     float v[24];
     load24(row, c0, p.C, v);
     float o[8];
@@ -62,7 +70,7 @@ __global__ void lrn_across_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict_
       float sc = p.k + a * s;
       o[t] = v[8 + t] * powneg(sc, p.beta);
     }
-    *reinterpret_cast<uint4*>(y + (i / cv) * p.C + c0) = pack8(o);
+    *reinterpret_cast<uint4*>(y + (long long)pix * p.C + c0) = pack8(o);
   }
 }
 
@@ -76,8 +84,9 @@ __global__ void lrn_across_bwd(const bf16_t* __restrict__ x, const bf16_t* __res
   const float cache_ratio = 2.f * p.alpha * p.beta / p.size;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * 8;
-    const long long base = (i / cv) * p.C;
+    const uint32_t pix = udiv((uint32_t)i, p.fcv);
+    const int c0 = (int)((uint32_t)i - pix * cv) * 8;
+    const long long base = (long long)pix * p.C;
     float xv[24], gv[24];
     load24(x + base, c0, p.C, xv);
     load24(dy + base, c0, p.C, gv);
@@ -223,12 +232,14 @@ static LrnP mk(long long N, long long H, long long W, long long C, long long siz
   LrnP p;
   p.N = (int)N; p.H = (int)H; p.W = (int)W; p.C = (int)C; p.size = (int)size; p.pre = (int)((size - 1) / 2);
   p.alpha = alpha; p.beta = beta; p.k = k;
+  p.fcv = make_fdiv((uint32_t)(C % 8 == 0 ? C / 8 : 1));
   return p;
 }
 
 extern "C" int sn_lrn_across_fwd(const bf16_t* x, bf16_t* y, long long N, long long H, long long W, long long C,
                                  long long size, float alpha, float beta, float k, hipStream_t st) {
   LrnP p = mk(N, H, W, C, size, alpha, beta, k);
+  if (N * H * W * C >= (1ll << 32)) return 8;  // 32-bit index decode
   dim3 g8(sn_blocks(N * H * W * (C / 8), 256, 16384));
   if (C % 8 == 0 && size == 3) {
     hipLaunchKernelGGL(lrn_across_fwd<3>, g8, dim3(256), 0, st, x, y, p);
@@ -248,6 +259,7 @@ extern "C" int sn_lrn_across_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, 
                                  long long W, long long C, long long size, float alpha, float beta, float k,
                                  hipStream_t st) {
   LrnP p = mk(N, H, W, C, size, alpha, beta, k);
+  if (N * H * W * C >= (1ll << 32)) return 8;  // 32-bit index decode
   dim3 g8(sn_blocks(N * H * W * (C / 8), 256, 16384));
   if (C % 8 == 0 && size == 3) {
     hipLaunchKernelGGL(lrn_across_bwd<3>, g8, dim3(256), 0, st, x, dy, dx, p);

@@ -9,6 +9,7 @@
 
 struct PoolGeom {
   int N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw;
+  FDiv fcv, fW, fH, fQ, fP, fsh, fsw;  // cv = channel chunks per pixel (C/8 or C)
 };
 
 template <bool VEC>
@@ -18,11 +19,9 @@ __global__ void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
   const long long total = (long long)g.N * g.P * g.Q * cv;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * (VEC ? 8 : 1);
-    long long pix = i / cv;
-    const int q = (int)(pix % g.Q);
-    const int p = (int)((pix / g.Q) % g.P);
-    const int n = (int)(pix / ((long long)g.Q * g.P));
+    const uint32_t pix = udiv((uint32_t)i, g.fcv), pq = udiv(pix, g.fQ), n = udiv(pq, g.fP);
+    const int c0 = (int)((uint32_t)i - pix * cv) * (VEC ? 8 : 1);
+    const int q = (int)(pix - pq * g.Q), p = (int)(pq - n * g.P);
     const int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
     const int he = min(hs + g.kh, g.H), we = min(ws + g.kw, g.W);
     const int h0 = max(hs, 0), w0 = max(ws, 0);
@@ -53,7 +52,7 @@ __global__ void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
       for (int k = 0; k < 8; ++k)
         if (!(best[k] > 0.f)) arg[k] = 255;
     }
-    const long long o = pix * g.C + c0;
+    const long long o = (long long)pix * g.C + c0;
     if (VEC) {
       *reinterpret_cast<uint4*>(y + o) = pack8(best);
       if (mask) {
@@ -75,11 +74,9 @@ __global__ void avepool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
   const long long total = (long long)g.N * g.P * g.Q * cv;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * (VEC ? 8 : 1);
-    long long pix = i / cv;
-    const int q = (int)(pix % g.Q);
-    const int p = (int)((pix / g.Q) % g.P);
-    const int n = (int)(pix / ((long long)g.Q * g.P));
+    const uint32_t pix = udiv((uint32_t)i, g.fcv), pq = udiv(pix, g.fQ), n = udiv(pq, g.fP);
+    const int c0 = (int)((uint32_t)i - pix * cv) * (VEC ? 8 : 1);
+    const int q = (int)(pix - pq * g.Q), p = (int)(pq - n * g.P);
     int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
     int he = min(hs + g.kh, g.H + g.ph), we = min(ws + g.kw, g.W + g.pw);
     const float inv = 1.f / (float)((he - hs) * (we - ws));
@@ -97,7 +94,7 @@ __global__ void avepool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
           acc[0] += bf2f(src[0]);
         }
       }
-    const long long o = pix * g.C + c0;
+    const long long o = (long long)pix * g.C + c0;
     if (VEC) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] *= inv;
@@ -117,16 +114,14 @@ __global__ void pool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restric
   const long long total = (long long)g.N * g.H * g.W * cv;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * (VEC ? 8 : 1);
-    long long pix = i / cv;
-    const int w = (int)(pix % g.W);
-    const int h = (int)((pix / g.W) % g.H);
-    const int n = (int)(pix / ((long long)g.W * g.H));
+    const uint32_t pix = udiv((uint32_t)i, g.fcv), ph_ = udiv(pix, g.fW), n = udiv(ph_, g.fH);
+    const int c0 = (int)((uint32_t)i - pix * cv) * (VEC ? 8 : 1);
+    const int w = (int)(pix - ph_ * g.W), h = (int)(ph_ - n * g.H);
     const int hp = h + g.ph, wp = w + g.pw;
-    const int p0 = hp < g.kh ? 0 : (hp - g.kh) / g.sh + 1;
-    const int p1 = min(hp / g.sh + 1, g.P);
-    const int q0 = wp < g.kw ? 0 : (wp - g.kw) / g.sw + 1;
-    const int q1 = min(wp / g.sw + 1, g.Q);
+    const int p0 = hp < g.kh ? 0 : (int)udiv((uint32_t)(hp - g.kh), g.fsh) + 1;
+    const int p1 = min((int)udiv((uint32_t)hp, g.fsh) + 1, g.P);
+    const int q0 = wp < g.kw ? 0 : (int)udiv((uint32_t)(wp - g.kw), g.fsw) + 1;
+    const int q1 = min((int)udiv((uint32_t)wp, g.fsw) + 1, g.Q);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int p = p0; p < p1; ++p)
       for (int q = q0; q < q1; ++q) {
@@ -160,11 +155,123 @@ __global__ void pool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restric
           }
         }
       }
-    const long long o = pix * g.C + c0;
+    const long long o = (long long)pix * g.C + c0;
     if (VEC)
       *reinterpret_cast<uint4*>(dx + o) = pack8(acc);
     else
       dx[o] = f2bf(acc[0]);
+  }
+}
+
+// ---- fixed-window fast paths (VEC, compile-time window) --------------------------------
+// Same semantics as the generic kernels above, but every window load is issued up front
+// from a clamped in-bounds address and masked afterwards: a load inside a data-dependent
+// loop / branch makes hipcc wait vmcnt(0) per element (one L2 round trip each).
+
+template <int KH, int KW>
+__global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                              PoolGeom g, int gate) {
+  const int cv = g.C / 8;
+  const long long total = (long long)g.N * g.P * g.Q * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t pix = udiv((uint32_t)i, g.fcv), pq = udiv(pix, g.fQ), n = udiv(pq, g.fP);
+    const int c0 = (int)((uint32_t)i - pix * cv) * 8;
+    const int q = (int)(pix - pq * g.Q), p = (int)(pq - n * g.P);
+    const int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
+    uint4 v[KH * KW];
+    bool ok[KH * KW];
+#pragma unroll
+    for (int a = 0; a < KH; ++a)
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
+        const int h = hs + a, w = ws + b;
+        ok[a * KW + b] = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+        const int hc = min(max(h, 0), g.H - 1), wc = min(max(w, 0), g.W - 1);
+        v[a * KW + b] = *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + hc) * g.W + wc) * g.C + c0);
+      }
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+#pragma unroll
+    for (int widx = 0; widx < KH * KW; ++widx) {
+      float f[8];
+      unpack8(v[widx], f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (ok[widx] && f[k] > best[k]) { best[k] = f[k]; arg[k] = widx; }
+    }
+    if (gate) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (!(best[k] > 0.f)) arg[k] = 255;
+    }
+    const long long o = (long long)pix * g.C + c0;
+    *reinterpret_cast<uint4*>(y + o) = pack8(best);
+    if (mask) {
+      uint2 m;
+      m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+      m.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+      *reinterpret_cast<uint2*>(mask + o) = m;
+    }
+  }
+}
+
+// NH x NW = max number of windows covering one input pixel (ceil(k / stride) per axis).
+template <int NH, int NW, bool MAX>
+__global__ void pool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
+                           PoolGeom g) {
+  const int cv = g.C / 8;
+  const long long total = (long long)g.N * g.H * g.W * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t pix = udiv((uint32_t)i, g.fcv), ph_ = udiv(pix, g.fW), n = udiv(ph_, g.fH);
+    const int c0 = (int)((uint32_t)i - pix * cv) * 8;
+    const int w = (int)(pix - ph_ * g.W), h = (int)(ph_ - n * g.H);
+    const int hp = h + g.ph, wp = w + g.pw;
+    const int p0 = hp < g.kh ? 0 : (int)udiv((uint32_t)(hp - g.kh), g.fsh) + 1;
+    const int p1 = min((int)udiv((uint32_t)hp, g.fsh) + 1, g.P);
+    const int q0 = wp < g.kw ? 0 : (int)udiv((uint32_t)(wp - g.kw), g.fsw) + 1;
+    const int q1 = min((int)udiv((uint32_t)wp, g.fsw) + 1, g.Q);
+    uint4 dv[NH * NW];
+    uint2 mv[NH * NW];
+    bool ok[NH * NW];
+#pragma unroll
+    for (int a = 0; a < NH; ++a)
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        const int p = p0 + a, q = q0 + b;
+        ok[a * NW + b] = p < p1 && q < q1;
+        const int pc = min(p, g.P - 1), qc = min(q, g.Q - 1);
+        const long long o = (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0;
+        dv[a * NW + b] = *reinterpret_cast<const uint4*>(dy + o);
+        if (MAX) mv[a * NW + b] = *reinterpret_cast<const uint2*>(mask + o);
+      }
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int a = 0; a < NH; ++a)
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        const int t = a * NW + b;
+        const int p = p0 + a, q = q0 + b;
+        const int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
+        float f[8];
+        unpack8(dv[t], f);
+        if (MAX) {
+          const int widx = (h - hs) * g.kw + (w - ws);
+          const uint32_t mw[2] = {mv[t].x, mv[t].y};
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (ok[t] && (int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == widx) acc[k] += f[k];
+        } else {
+          const int he = min(hs + g.kh, g.H + g.ph), we = min(ws + g.kw, g.W + g.pw);
+          const float scale = ok[t] ? 1.f / (float)((he - hs) * (we - ws)) : 0.f;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += f[k] * scale;
+        }
+      }
+    *reinterpret_cast<uint4*>(dx + (long long)pix * g.C + c0) = pack8(acc);
   }
 }
 
@@ -173,6 +280,10 @@ static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long 
   PoolGeom g;
   g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C; g.P = (int)P; g.Q = (int)Q;
   g.kh = (int)kh; g.kw = (int)kw; g.sh = (int)sh; g.sw = (int)sw; g.ph = (int)ph; g.pw = (int)pw;
+  g.fcv = make_fdiv((uint32_t)((C % 8) == 0 ? C / 8 : C));
+  g.fW = make_fdiv((uint32_t)W); g.fH = make_fdiv((uint32_t)H);
+  g.fQ = make_fdiv((uint32_t)Q); g.fP = make_fdiv((uint32_t)P);
+  g.fsh = make_fdiv((uint32_t)sh); g.fsw = make_fdiv((uint32_t)sw);
   return g;
 }
 
@@ -182,10 +293,14 @@ extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long 
                            hipStream_t st) {
   PoolGeom g = mkgeom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
   if (method == 0 && kh * kw > 254) return 6;
+  if (N * H * W * C >= (1ll << 32)) return 8;  // 32-bit index decode
   const bool vec = (C % 8) == 0;
   long long total = N * P * Q * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
-  if (method == 0) {
+  if (method == 0 && vec && kh == kw && (kh == 2 || kh == 3)) {
+    if (kh == 3) hipLaunchKernelGGL((maxpool_fwd_k<3, 3>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
+    else hipLaunchKernelGGL((maxpool_fwd_k<2, 2>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
+  } else if (method == 0) {
     if (vec) hipLaunchKernelGGL(maxpool_fwd<true>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
     else hipLaunchKernelGGL(maxpool_fwd<false>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
   } else {
@@ -199,10 +314,22 @@ extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, lo
                            long long C, long long P, long long Q, long long kh, long long kw, long long sh,
                            long long sw, long long ph, long long pw, long long method, hipStream_t st) {
   PoolGeom g = mkgeom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  if (N * H * W * C >= (1ll << 32)) return 8;  // 32-bit index decode
   const bool vec = (C % 8) == 0;
   long long total = N * H * W * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
-  if (method == 0) {
+  const long long nh = (kh + sh - 1) / sh, nw = (kw + sw - 1) / sw;
+  if (vec && nh == nw && nh >= 1 && nh <= 3) {
+#define SN_POOL_BWD_K(NN)                                                                             \
+  do {                                                                                                \
+    if (method == 0) hipLaunchKernelGGL((pool_bwd_k<NN, NN, true>), grid, dim3(256), 0, st, dy, mask, dx, g);  \
+    else hipLaunchKernelGGL((pool_bwd_k<NN, NN, false>), grid, dim3(256), 0, st, dy, mask, dx, g);             \
+  } while (0)
+    if (nh == 1) SN_POOL_BWD_K(1);
+    else if (nh == 2) SN_POOL_BWD_K(2);
+    else SN_POOL_BWD_K(3);
+#undef SN_POOL_BWD_K
+  } else if (method == 0) {
     if (vec) hipLaunchKernelGGL((pool_bwd<true, true>), grid, dim3(256), 0, st, dy, mask, dx, g);
     else hipLaunchKernelGGL((pool_bwd<false, true>), grid, dim3(256), 0, st, dy, mask, dx, g);
   } else {

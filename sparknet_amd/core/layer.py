@@ -171,6 +171,20 @@ class Layer:
     def param_grads_needed(self, i: int) -> bool:
         return i < len(self.param_propagate_down) and self.param_propagate_down[i]
 
+    supports_grad_overwrite = False  # backward honours grad_overwrite() (see Net.clear_param_diffs)
+
+    def grad_overwrite(self, i: int) -> bool:
+        """True when param i's gradient buffer was lazily cleared and this is its first
+        write of the pass: the caller must store, not accumulate."""
+        st = self.ctx.stale_diffs
+        if not st:
+            return False
+        off = self.params[i].offset
+        if off in st:
+            st.discard(off)
+            return True
+        return False
+
     def __repr__(self):
         return f"<{self.type_name} {self.name!r}>"
 

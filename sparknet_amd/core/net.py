@@ -40,6 +40,9 @@ class NetContext:
     # Philox state for in-kernel RNG (dropout): [seed, counter] on the net's device.
     rng_state: torch.Tensor = field(default=None)
     layer_counter: int = 0
+    # flat offsets of params whose gradient buffer was NOT cleared (lazy clear): the first
+    # backward contribution overwrites instead of accumulating (Layer.grad_overwrite)
+    stale_diffs: set = field(default_factory=set)
 
     def next_stream_id(self) -> int:
         self.layer_counter += 1
@@ -484,9 +487,56 @@ class Net:
         for li, layer in enumerate(self.layers):
             layer.reshape(self.bottom_vecs[li], self.top_vecs[li])
 
-    def clear_param_diffs(self) -> None:
-        if self.flat_diff is not None:
+    def clear_param_diffs(self, lazy: bool = False) -> None:
+        """Net::ClearParamDiffs.  lazy=True skips the memset for params whose every user
+        layer can overwrite its gradient on first write (Convolution / InnerProduct:
+        their wgrad GEMM stores instead of read-modify-writes); the rest are zeroed.
+        Pair with :meth:`finish_param_diffs` after the last backward."""
+        if self.flat_diff is None:
+            return
+        st = self.ctx.stale_diffs
+        st.clear()
+        if not lazy:
             self.flat_diff.zero_()
+            return
+        ok = self._overwrite_ok()
+        for off, cnt in self._zero_ranges(ok):
+            self.flat_diff[off:off + cnt].zero_()
+        st.update(o for o, good in ok.items() if good)
+
+    def finish_param_diffs(self) -> None:
+        """Zero the gradients of lazily-cleared params that no backward wrote (e.g. a
+        layer whose backward was pruned this pass)."""
+        st = self.ctx.stale_diffs
+        if st:
+            for p in self.learnable_params:
+                if p.offset in st:
+                    p.diff.zero_()
+            st.clear()
+
+    def _overwrite_ok(self) -> dict:
+        if getattr(self, "_ow_cache", None) is None:
+            ok = {p.offset: True for p in self.learnable_params}
+            for layer in self.layers:
+                good = getattr(layer, "supports_grad_overwrite", False)
+                for p in layer.params:
+                    if not good:
+                        ok[p.offset] = False
+            self._ow_cache = ok
+        return self._ow_cache
+
+    def _zero_ranges(self, ok: dict):
+        """Contiguous flat ranges covering every param that must be zeroed eagerly."""
+        ranges = []
+        for p in sorted(self.learnable_params, key=lambda q: q.offset):
+            if ok.get(p.offset, False):
+                continue
+            seg = -(-p.count // PARAM_ALIGN) * PARAM_ALIGN
+            if ranges and ranges[-1][0] + ranges[-1][1] == p.offset:
+                ranges[-1][1] += seg
+            else:
+                ranges.append([p.offset, seg])
+        return ranges
 
     def update(self) -> None:
         """Net::Update: data -= diff for every owner param (plain Blob::Update)."""

@@ -203,7 +203,7 @@ class Solver:
     def iteration(self):
         """One training iteration minus bookkeeping: returns the device loss."""
         net = self.net
-        net.clear_param_diffs()
+        net.clear_param_diffs(lazy=True)
         for cb in self.callbacks:
             getattr(cb, "on_start", lambda: None)()
         loss = None
@@ -212,6 +212,7 @@ class Solver:
             loss = l if loss is None else loss + l
             from .. import ops
             ops.advance_rng(net.ctx.rng_state)
+        net.finish_param_diffs()
         if self.param.iter_size > 1:
             loss = loss / self.param.iter_size
         for cb in self.callbacks:

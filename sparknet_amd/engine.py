@@ -126,8 +126,9 @@ class GraphStep:
     def _body(self):
         s = self.solver
         net = s.net
-        net.clear_param_diffs()
+        net.clear_param_diffs(lazy=True)
         loss = net.forward_backward()
+        net.finish_param_diffs()
         ops.advance_rng(net.ctx.rng_state)
         s.update_params()
         return loss

@@ -98,6 +98,8 @@ class ConvolutionLayer(Layer):
             folded = self.folded_input if i == 0 else None
             t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i], folded=folded)
 
+    supports_grad_overwrite = True
+
     def backward(self, tops, propagate_down, bottoms):
         w = self.weight.compute
         dw = self.weight.diff if self.param_grads_needed(0) else None
@@ -106,7 +108,10 @@ class ConvolutionLayer(Layer):
             s = self.spec(b)
             gate = b.data if self.relu_gate else None
             ws = self._ws[i] if i < len(getattr(self, "_ws", ())) else None
-            dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws)
+            dw_acc = not (dw is not None and self.grad_overwrite(0))
+            db_acc = not (db is not None and self.grad_overwrite(1))
+            dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws,
+                                   dw_acc=dw_acc, db_acc=db_acc)
             if propagate_down[i]:
                 b.diff = dx
 
@@ -281,6 +286,7 @@ class InnerProductLayer(Layer):
     exact_tops = 1
     fuse_relu = False
     relu_gate = False
+    supports_grad_overwrite = True
 
     def layer_setup(self, bottoms, tops):
         p = self.lp.inner_product_param
@@ -329,7 +335,10 @@ class InnerProductLayer(Layer):
         dw = self.weight.diff if self.param_grads_needed(0) else None
         db = self.bias.diff if (self.bias is not None and self.param_grads_needed(1)) else None
         gate = b.data if self.relu_gate else None
-        dx = ops.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db, gate)
+        dw_acc = not (dw is not None and self.grad_overwrite(0))
+        db_acc = not (db is not None and self.grad_overwrite(1))
+        dx = ops.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db, gate,
+                                 dw_acc=dw_acc, db_acc=db_acc)
         if propagate_down[0]:
             b.diff = dx.reshape(b.data.shape)
 

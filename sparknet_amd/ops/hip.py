@@ -124,15 +124,18 @@ def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
     return out
 
 
-def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None):
+def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
+                  dw_acc=True, db_acc=True):
     """gate: optional bf16 NHWC tensor shaped like x; dx is zeroed where gate <= 0
-    (the backward of a slope-0 in-place ReLU that produced x, fused into the dgrad)."""
+    (the backward of a slope-0 in-place ReLU that produced x, fused into the dgrad).
+    dw_acc / db_acc False: overwrite the gradient instead of accumulating (its buffer
+    was not cleared, see Net.clear_param_diffs(lazy=True))."""
     dy = _c(dy)
     x = _c(x)
     M = s.N * s.P * s.Q
     dy2 = dy.view(M, s.K)
     if db is not None:
-        colsum(dy2, db, accumulate=True)
+        colsum(dy2, db, accumulate=db_acc)
     kred = s.R * s.S * s.Cg
     plan = _s2d_plan(s) if s.Kg % 8 == 0 else None
     if dw is not None and plan is not None:
@@ -146,13 +149,14 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
         dw2 = torch.empty((s.K, k2), dtype=torch.float32, device=x.device)
         gemm(s.K, k2, M, Dense(dy2, s.K, kcontig=False), Im2col(x2, _geom(s2), kcontig=False), dw2, k2,
              epi=EPI_F32)
-        call("s2d_weight_grad", dw2, dw, s.K, s.R, s.S, s.C, f, cp, rf, sf)
+        call("s2d_weight_grad", dw2, dw, s.K, s.R, s.S, s.C, f, cp, rf, sf, int(dw_acc))
         dw = None
     if dw is not None:
         if _implicit_ok(s) and s.Kg % 8 == 0:
             A = Dense(dy2, s.K, kcontig=False, gstride=s.Kg)
             B = Im2col(x, _geom(s), kcontig=False, gstride=s.Cg)
-            gemm(s.Kg, kred, M, A, B, dw, kred, epi=EPI_F32_ACC, groups=s.groups, c_gstride=s.Kg * kred)
+            gemm(s.Kg, kred, M, A, B, dw, kred, epi=EPI_F32_ACC if dw_acc else EPI_F32, groups=s.groups,
+                 c_gstride=s.Kg * kred)
         else:
             kpad = _round8(kred)
             kgp = _round8(s.Kg)
@@ -164,7 +168,10 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
                 tmp = torch.zeros((kgp, kpad), dtype=torch.float32, device=x.device)
                 gemm(kgp, kpad, M, Dense(dyg, dyg.stride(0), False), Dense(col, kpad, False), tmp, kpad,
                      epi=EPI_F32)
-                dw2[g * s.Kg:(g + 1) * s.Kg].add_(tmp[:s.Kg, :kred])
+                if dw_acc:
+                    dw2[g * s.Kg:(g + 1) * s.Kg].add_(tmp[:s.Kg, :kred])
+                else:
+                    dw2[g * s.Kg:(g + 1) * s.Kg].copy_(tmp[:s.Kg, :kred])
     if not need_dx:
         return None
     dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
@@ -205,12 +212,12 @@ def linear_forward(x2, w, b, relu=False):
     return linear_fwd(_c(x2), _c(w), b, relu)
 
 
-def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None):
+def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=True, db_acc=True):
     dy2 = _c(dy2)
     if db is not None:
-        colsum(dy2, db, accumulate=True)
+        colsum(dy2, db, accumulate=db_acc)
     if dw is not None:
-        linear_wgrad(dy2, _c(x2), dw, accumulate=True)
+        linear_wgrad(dy2, _c(x2), dw, accumulate=dw_acc)
     if not need_dx:
         return None
     return linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)

@@ -43,7 +43,15 @@ def _gated(dx, gate):
     return dx if gate is None else dx * (gate > 0).to(dx.dtype)
 
 
-def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None):
+def _acc(dst, val, accumulate):
+    if accumulate:
+        dst += val
+    else:
+        dst.copy_(val)
+
+
+def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
+                  dw_acc=True, db_acc=True):
     dyn = nchw(dy.float())
     xn = nchw(x.float())
     wo = _w_oihw(w.float(), s)
@@ -55,9 +63,9 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
     if dw is not None:
         gw = torch.nn.grad.conv2d_weight(xn, wo.shape, dyn, stride=(s.sh, s.sw), padding=(s.ph, s.pw),
                                          dilation=(s.dh, s.dw), groups=s.groups)
-        dw += gw.permute(0, 2, 3, 1).reshape(dw.shape)
+        _acc(dw, gw.permute(0, 2, 3, 1).reshape(dw.shape), dw_acc)
     if db is not None:
-        db += dyn.sum(dim=(0, 2, 3))
+        _acc(db, dyn.sum(dim=(0, 2, 3)), db_acc)
     return dx
 
 
@@ -83,12 +91,12 @@ def linear_forward(x2, w, b, relu=False):
     return y.to(x2.dtype)
 
 
-def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None):
+def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=True, db_acc=True):
     dyf = dy2.float()
     if dw is not None:
-        dw += dyf.t() @ x2.float()
+        _acc(dw, dyf.t() @ x2.float(), dw_acc)
     if db is not None:
-        db += dyf.sum(0)
+        _acc(db, dyf.sum(0), db_acc)
     if not need_dx:
         return None
     return _gated((dyf @ w.float()).to(x2.dtype), gate.reshape(x2.shape) if gate is not None else None)

@@ -77,7 +77,8 @@ def test_linear(gpu, M, K, N):
 
 @pytest.mark.parametrize("method", [POOL_MAX, POOL_AVE])
 @pytest.mark.parametrize("geo", [(2, 55, 55, 96, 3, 2, 0), (2, 32, 32, 32, 3, 2, 0), (2, 8, 8, 24, 3, 2, 1),
-                                 (2, 7, 7, 16, 7, 1, 0), (2, 6, 6, 3, 2, 2, 0)])
+                                 (2, 7, 7, 16, 7, 1, 0), (2, 6, 6, 3, 2, 2, 0), (2, 9, 9, 16, 3, 1, 1),
+                                 (2, 8, 8, 16, 2, 2, 0), (2, 13, 13, 32, 3, 2, 1)])
 def test_pool(gpu, method, geo):
     from sparknet_amd.ops import hip
     N, H, W, Cc, k, st, pd = geo

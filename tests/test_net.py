@@ -220,3 +220,32 @@ def test_relu_forward_backward_fusion_matches_unfused():
     assert counts == (7, 7), counts  # relu1..7 forward-fused; all 7 backward-fused
     assert abs(l0 - l1) < 1e-5 * max(1.0, abs(l0))
     assert torch.allclose(g0, g1, rtol=1e-5, atol=1e-6 * float(g0.abs().max()))
+
+
+def test_lazy_gradient_clear_matches_memset():
+    """clear_param_diffs(lazy=True) + first-write overwrite == memset + accumulate, with
+    garbage left in the buffer, two accumulated passes (iter_size), a frozen layer and a
+    shared parameter."""
+    n = models.cifar10_quick(train_batch=2, test_batch=2)
+    for l in n.layer:
+        if l.name == "conv2":
+            l.param[0].lr_mult = 0.0  # frozen weight: its diff must come out zero
+            l.param[1].lr_mult = 0.0
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 3, 32, 32, generator=g)
+    y = torch.tensor([[1.0], [7.0]])
+    out = []
+    for lazy in (False, True):
+        net = Net(n, phase=proto.TRAIN, seed=5)
+        net.blob_by_name("data").set_nchw(x)
+        net.blob_by_name("label").set_nchw(y)
+        net.flat_diff.normal_()  # stale garbage
+        net.clear_param_diffs(lazy=lazy)
+        for _ in range(2):
+            net.forward_backward()
+        net.finish_param_diffs()
+        # compare the param segments (the alignment padding is never written by layers)
+        out.append(torch.cat([p.diff.reshape(-1) for p in net.learnable_params]))
+        frozen = net.layer_by_name("conv2").params
+    assert torch.allclose(out[0], out[1], rtol=1e-6, atol=1e-7)
+    assert all(float(p.diff.abs().max()) == 0.0 for p in frozen)
