@@ -28,9 +28,22 @@ def main(argv=None):
     if args.data and not args.synthetic:
         ld = CifarLoader(args.data, seed=args.seed)
         mean = ld.mean_image()  # full mean image (the reference computed it, then ignored it)
-        ti, tl = ld.tensors(train=True)
-        a, b = shard_range(ti.shape[0], rank, world)
-        train = (ti[a:b], tl[a:b])
+        files = [os.path.join(args.data, f"data_batch_{i}.bin") for i in range(1, 6)]
+        files = [f for f in files if os.path.exists(f)]
+        if args.native_loader and files:
+            # native pipeline: mmap'd records, SparkNet window sampler, worker threads,
+            # pinned ring (csrc/runtime/loader.cpp); sharding is done by the loader
+            from ..data.native import SAMPLER_WINDOW, NativeLoader
+            first = 0
+            if args.resume:  # continue the batch stream where the checkpointed run stopped
+                from ..utils.checkpoint import read_round_sidecar
+                first = read_round_sidecar(args.resume + ".json")["round"] * args.tau
+            train = NativeLoader.cifar10(files, args.batch, sampler=SAMPLER_WINDOW, tau=args.tau, rank=rank,
+                                         world=world, seed=args.seed * 101 + rank, threads=2, first_batch=first)
+        else:
+            ti, tl = ld.tensors(train=True)
+            a, b = shard_range(ti.shape[0], rank, world)
+            train = (ti[a:b], tl[a:b])
         vi, vl = ld.tensors(train=False)
         a, b = shard_range(vi.shape[0], rank, world)
         test = (vi[a:b], vl[a:b])

@@ -91,7 +91,10 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
         start_round = side["round"]
         log.log(f"resumed from {args.resume} at round {start_round}")
 
-    if train_data is not None:
+    from ..data.native import NativeLoader
+    if isinstance(train_data, NativeLoader):
+        src = train_data
+    elif train_data is not None:
         src = WindowedSource(train_data[0], train_data[1], args.batch, args.tau, seed=args.seed * 101 + rank)
     else:
         src = SyntheticSource(args.batch, C, H, W, classes=classes, pool=4, seed=args.seed * 101 + rank)

@@ -39,7 +39,11 @@ HIP_FLAGS = [
     "-munsafe-fp-atomics",
     f"-I{CSRC / 'kernels'}",
 ]
-CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", f"-I{CSRC / 'runtime'}"]
+# host C++ runtime: g++ against the HIP runtime API (hipHostMalloc / hipMemcpyAsync /
+# events); the HIP platform macro selects the AMD backend of the runtime headers.
+CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", f"-I{CSRC / 'runtime'}",
+             "-D__HIP_PLATFORM_AMD__=1", f"-I{ROCM}/include"]
+RUNTIME_LINK = [f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"]
 
 KERNEL_LIB = LIBDIR / "libsn_kernels.so"
 RUNTIME_LIB = LIBDIR / "libsn_runtime.so"
@@ -95,7 +99,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         out["kernels"] = str(KERNEL_LIB)
     if cpp_objs:
         if force or _stale(RUNTIME_LIB, cpp_objs):
-            _run(["g++", "-shared", "-fPIC", "-pthread", *map(str, cpp_objs), "-o", str(RUNTIME_LIB)])
+            _run(["g++", "-shared", "-fPIC", "-pthread", *map(str, cpp_objs), *RUNTIME_LINK, "-o",
+                  str(RUNTIME_LIB)])
         out["runtime"] = str(RUNTIME_LIB)
     if verbose:
         print(out)

@@ -109,8 +109,14 @@ class DeviceFeeder:
         self.source = source
         self.data_blob, self.label_blob = data_blob, label_blob
         self.device = torch.device(device)
-        x0, y0 = source.batches[0] if isinstance(source, SyntheticSource) else source.next_batch()
-        self.shape = tuple(x0.shape)
+        from .native import NativeLoader
+        self.native = isinstance(source, NativeLoader)
+        if self.native:
+            x0 = y0 = None
+            self.shape = tuple(source.shape)
+        else:
+            x0, y0 = source.batches[0] if isinstance(source, SyntheticSource) else source.next_batch()
+            self.shape = tuple(x0.shape)
         N, C, H, W = self.shape
         self.crop = crop or H
         self.scale, self.mirror, self.train = scale, mirror, train
@@ -128,13 +134,16 @@ class DeviceFeeder:
         self.fold = None  # (x2, plan, ConvSpec) when fused with the first conv's S2D fold
         self.k = 0
         self._pending = None
-        if not isinstance(source, SyntheticSource):
+        if not isinstance(source, SyntheticSource) and not self.native:
             self._first = (x0, y0)
         else:
             self._first = None
 
     def prefetch(self) -> None:
         """Issue the H2D copy of the next host batch into the next slot (copy stream)."""
+        if self.native:
+            self._prefetch_native()
+            return
         if self._first is not None:
             x, y = self._first
             self._first = None
@@ -154,6 +163,23 @@ class DeviceFeeder:
         else:
             dx.copy_(x)
             dy.copy_(y)
+        self._pending = slot
+        self.k += 1
+
+    def _prefetch_native(self) -> None:
+        """Native pipeline: the C++ loader issues the H2D copy of its next pinned slot."""
+        slot = self.k % len(self.slots)
+        dx, dy = self.slots[slot]
+        if self.copy_stream is not None:
+            self.copy_stream.wait_stream(torch.cuda.current_stream(self.device))
+            self.source.next_to_device(dx, dy, self.copy_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+            self.events[slot] = ev
+        else:
+            _, x, y = self.source.next_host()
+            dx.copy_(torch.from_numpy(x))
+            dy.copy_(torch.from_numpy(y))
         self._pending = slot
         self.k += 1
 
