@@ -142,6 +142,8 @@ extern "C" int sn_augment_s2d(const uint8_t* src, bf16_t* x2, long long N, long 
     SN_AUG_S2D(4, 3);
   else if (f == 2 && Cp == 4)  // GoogLeNet / ResNet conv1: 7x7 stride 2 on RGB -> 4x4 on 16 channels
     SN_AUG_S2D(2, 4);
+  else if (f == 1 && Cp == 8)  // stride-1 input conv (VGG conv1_1, CIFAR conv1): channels padded to 8
+    SN_AUG_S2D(1, 8);
   else
     SN_AUG_S2D(0, 0);
 #undef SN_AUG_S2D

@@ -114,14 +114,20 @@ extern "C" int sn_cast_f32_bf16(const float* src, bf16_t* dst, long long n, hipS
   return SN_CHECK_LAUNCH();
 }
 
-// out = sum_k in_k (k < 8), bf16
+// out = sum_k in_k (k <= 8), bf16 with fp32 accumulation; K is a template parameter so
+// the K loads of an iteration are issued together.
 struct Ptrs8 { const bf16_t* p[8]; };
-__global__ void sum_bf16(Ptrs8 in, int k, bf16_t* __restrict__ out, long long n8) {
+template <int K>
+__global__ void sum_bf16(Ptrs8 in, bf16_t* __restrict__ out, long long n8) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    uint4 v[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = reinterpret_cast<const uint4*>(in.p[j])[i];
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int j = 0; j < k; ++j) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
       float f[8];
-      unpack8(reinterpret_cast<const uint4*>(in.p[j])[i], f);
+      unpack8(v[j], f);
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] += f[t];
     }
@@ -133,7 +139,14 @@ extern "C" int sn_sum_bf16(const bf16_t* const* ptrs, long long k, bf16_t* out, 
   if (n % 8 || k > 8 || k < 1) return 7;
   Ptrs8 in;
   for (int j = 0; j < 8; ++j) in.p[j] = j < k ? ptrs[j] : nullptr;
-  hipLaunchKernelGGL(sum_bf16, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, in, (int)k, out, n / 8);
+  const dim3 grid(sn_blocks(n / 8, 256, 16384));
+  switch (k) {
+#define SN_SUM_CASE(KK) \
+  case KK: hipLaunchKernelGGL(sum_bf16<KK>, grid, dim3(256), 0, st, in, out, n / 8); break;
+    SN_SUM_CASE(1) SN_SUM_CASE(2) SN_SUM_CASE(3) SN_SUM_CASE(4)
+    SN_SUM_CASE(5) SN_SUM_CASE(6) SN_SUM_CASE(7) SN_SUM_CASE(8)
+#undef SN_SUM_CASE
+  }
   return SN_CHECK_LAUNCH();
 }
 

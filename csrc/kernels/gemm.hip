@@ -14,16 +14,18 @@
 //   MC : [rows = K] x [cols = M (or N)]   (reduction dim strided)     -> ds_read_b64_tr_b16
 // so NT / NN / TN products all stage their tiles straight from global memory without a
 // transpose pass: the transposition happens in the LDS read (CDNA4 tr_b16).
-// A virtual matrix is either DENSE (ptr + row*ld + col) or IM2COL: the implicit
-// [N*P*Q pixels] x [R*S*Cg] patch matrix of an NHWC tensor, gathered on the fly with
-// zero-fill for padding — no column buffer in HBM.
+// A virtual matrix is DENSE (ptr + row*ld + col), IM2COL (the implicit [N*P*Q pixels] x
+// [R*S*Cg] patch matrix of an NHWC tensor, gathered on the fly with zero-fill for
+// padding — no column buffer in HBM) or FLIPW (conv weights read flipped / transposed
+// for the data gradient).
 //
 // Block tile BM x BN x 64 with 256 threads = 4 waves, each wave owning a 64x64 output
 // sub-tile (4x4 MFMA tiles): (BM, BN) = (128, 128) or (256, 64) for skinny N (e.g.
-// 48-channel grouped dgrad).  LDS double buffered with XOR swizzles that make both the
-// b128 row reads and the tr_b16 transposed reads bank-conflict free, register-staged
-// global->LDS copies issued one tile ahead (load early / write late), XCD-aware
-// bijective block remap.
+// 48-channel grouped dgrad).  Tiles are staged by LDS-DMA (global_load_lds_dwordx4) into
+// two LDS stages held in two distinct __shared__ objects, XOR-swizzled on the source
+// side so both the b128 row reads and the tr_b16 transposed reads are bank-conflict
+// free; the DMA of tile k+1 runs under the MFMAs of tile k; XCD-aware bijective block
+// remap; fused bias / ReLU / ReLU-backward-gate epilogue; deterministic split-K.
 #include "common.h"
 
 #include <type_traits>
@@ -32,7 +34,10 @@ namespace {
 
 constexpr int BK = 64, NTHR = 256;
 
-enum { OP_DENSE = 0, OP_IM2COL = 1 };
+// OP_FLIPW (MC only): the dgrad B operand read straight from conv weights W[K][R][S][Cg]:
+// row k = tap * Kg + kout, col = c  ->  W[g*Kg + kout][R-1-r][S-1-s][c]  (flipped taps,
+// transposed channels) with geometry fields R, S, Cg and C := Kg — no flip pass over W.
+enum { OP_DENSE = 0, OP_IM2COL = 1, OP_FLIPW = 2 };
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2 };
 
 }  // namespace
@@ -63,7 +68,7 @@ struct SnGemmArgs {
   long long ldc, c_gstride, c_split_stride;
   const float* bias;  // per output column n (offset by g*N), EPI_BF16 only
   int relu;
-  int tile;           // 0: 128x128, 1: 256x64
+  int tile;           // 0: 128x128, 1: 256x64 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages)
   const bf16_t* gate; // EPI_BF16: zero outputs where gate (same layout as C) <= 0 (fused ReLU backward)
 };
 
@@ -97,12 +102,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 // maps to that slot.  Lanes outside the matrix read a zero page.
 //   KC: [TILE rows][64 k], 8 chunks per row, 8 rows per instruction.
 //   MC: [64 k rows][TILE cols], TILE/8 chunks per row.
-template <int MC, int MODE, int TILE>
+template <int MC, int MODE, int TILE, int NW>
 struct GStager {
-  static constexpr int NI = TILE / 32;            // wave-instructions per wave per tile
+  static constexpr int NI = TILE / (8 * NW);      // wave-instructions per wave per tile
   static constexpr int CPL = MC ? TILE / 8 : 8;   // 16-B chunks per LDS row
   static constexpr int RPI = 64 / CPL;            // LDS rows per wave-instruction
-  static_assert(NI % 2 == 0, "KC chunk pattern repeats with period 2 in j");
+  static_assert(NI >= 1 && (MC || NI % 2 == 0), "KC chunk pattern repeats with period 2 in j");
   const bf16_t* base;
   long long ld;
   SnConvGeom g;
@@ -113,19 +118,20 @@ struct GStager {
   bool pv[NI];
   int cr[NI], cs[NI], cc[NI];  // MC+IM2COL: column decode (cols fixed across k)
   bool cv[NI];
-  float invPQ, invQ, invCg, invS;
+  float invPQ, invQ, invCg, invS, invKg;
 
   SN_DEV void init(const SnOperand& op, int grp, int wave, int lane, int tile_row0, int rows_lim,
                    int tile_col0, int cols_lim) {
     ld = op.ld;
     g = op.g;
-    if (MODE == OP_DENSE) {
+    if (MODE != OP_IM2COL) {
       base = op.ptr + (long long)grp * op.gstride;
       coff = 0;
     } else {
       base = op.ptr;
       coff = (int)(grp * op.gstride);
     }
+    invKg = MODE == OP_FLIPW ? 1.f / (float)g.C : 0.f;
     invPQ = 1.f / (float)(g.P * g.Q);
     invQ = 1.f / (float)g.Q;
     invCg = 1.f / (float)g.Cg;
@@ -156,9 +162,13 @@ struct GStager {
     }
   }
 
+  // The DMA is issued from inline asm so the compiler's wait-count pass does not see an
+  // LDS write it cannot disambiguate (it would drain vmcnt(0) before the next ds_read);
+  // every wait on these DMAs is explicit in the K-loop (counted vmcnt + barrier).
   SN_DEV void dma(const bf16_t* src, bool valid, char* lds) {
     const void* s = valid ? (const void*)src : (const void*)g_zero16;
-    __builtin_amdgcn_global_load_lds(s, (lds_void*)lds, 16, 0, 0);
+    const uint32_t m0 = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(s) : "memory");
   }
 
   // Issue the LDS-DMA of the tile whose first reduction index is k_tile into `lds`.
@@ -197,6 +207,17 @@ struct GStager {
         for (int j = 0; j < NI; ++j) {
           int k = k_tile + rr[j], col = tile_rc0 + ch[j] * 8;
           dma(base + (long long)k * ld + col, k < k_lim && col < rc_lim, dst + j * 1024);
+        }
+      } else if (MODE == OP_FLIPW) {
+        const int RS = g.R * g.S;
+        const long long rowlen = (long long)RS * g.Cg;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          int k = k_tile + rr[j], col = tile_rc0 + ch[j] * 8;
+          int tap = fdiv(k, g.C, invKg), kout = k - tap * g.C;
+          bool v = k < k_lim && col < rc_lim;
+          long long off = v ? (long long)kout * rowlen + (long long)(RS - 1 - tap) * g.Cg + col : 0;
+          dma(base + off, v, dst + j * 1024);
         }
       } else {
         const int PQ = g.P * g.Q;
@@ -243,16 +264,27 @@ SN_DEV bf16x8_t read_frag(const char* lds, int x0, int s, int lane) {
   }
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN>
-__global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
+// s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= N only.
+constexpr int waitcnt_vm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
+
+// NW waves (4 or 8), each owning a 64x64 output sub-tile; NS LDS stages (2 or 3).
+//   NS = 2: one barrier per K-step, DMA of tile k+1 under the MFMAs of tile k (vmcnt(0)).
+//   NS = 3: two tiles in flight; each K-step waits with a COUNTED vmcnt for its own tile
+//           only and uses a raw s_barrier (no fence), so the DMA of tile k+1 keeps
+//           flying across the barrier while tile k+2 is issued (cdna_hip_programming
+//           "Pipelining across barriers").
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS>
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmArgs args) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int WN = BN / 64, WM = 4 / WN;  // waves along N / M (64x64 per wave)
-  static_assert(WM * 64 == BM, "tile/wave layout mismatch");
-  // Two distinct LDS objects (one per stage): the compiler's alias scopes then prove that
-  // the ds_reads of one stage do not depend on the DMA in flight into the other, so it
+  constexpr int WN = BN / 64, WM = NW / WN;  // waves along N / M (64x64 per wave)
+  static_assert(WM * 64 == BM && WM * WN == NW, "tile/wave layout mismatch");
+  static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
+  // Distinct LDS objects (one per stage): the compiler's alias scopes then prove that
+  // the ds_reads of one stage do not depend on the DMA in flight into another, so it
   // does not drain vmcnt before every k-step's first ds_read.
   __shared__ __attribute__((aligned(16))) char smem0[STAGE];
   __shared__ __attribute__((aligned(16))) char smem1[STAGE];
+  __shared__ __attribute__((aligned(16))) char smem2[NS == 3 ? STAGE : 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (args.M + BM - 1) / BM;
 
@@ -271,8 +303,10 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
   const int k1 = min(args.K, k0 + args.kchunk);
 
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  GStager<AMC, AMODE, BM> sa;
-  GStager<BMC, BMODE, BN> sb;
+  using SA = GStager<AMC, AMODE, BM, NW>;
+  using SB = GStager<BMC, BMODE, BN, NW>;
+  SA sa;
+  SB sb;
   sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M);
   sb.init(args.B, grp, wv, lane, n_blk, args.N, n_blk, args.N);
 
@@ -287,37 +321,63 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
 
   auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
+    bf16x8_t fa[2][4], fb[2][4];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8_t fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fb[i] = read_frag<BMC, BN>(lb, wn0 + 16 * i, s, lane);
+      for (int i = 0; i < 4; ++i) fb[s][i] = read_frag<BMC, BN>(lb, wn0 + 16 * i, s, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
+      for (int i = 0; i < 4; ++i) fa[s][i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][i], fa[s][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   };
   auto issue = [&](char* st, int kt) {
     sa.issue(st, wv, k0 + kt * BK, k1, m_blk, args.M);
     sb.issue(st + A_BYTES, wv, k0 + kt * BK, k1, n_blk, args.N);
   };
-  // One barrier per K-step: retire this wave's DMA of tile kt, barrier (all waves' DMAs
-  // landed AND all reads of the other stage from step kt-1 are done), then start the DMA
-  // of tile kt+1 into the other stage and run the MFMAs of tile kt under it.
-  auto step = [&](char* cur, char* nxt, int kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < nk) issue(nxt, kt + 1);
-    compute(cur);
-  };
-  if (nk > 0) issue(smem0, 0);
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(smem0, smem1, kt);
-    if (kt + 1 < nk) step(smem1, smem0, kt + 1);
+  if (NS == 2) {
+    // One barrier per K-step: retire this wave's DMA of tile kt, barrier (all waves' DMAs
+    // landed AND all reads of the other stage from step kt-1 are done), then start the
+    // DMA of tile kt+1 into the other stage and run the MFMAs of tile kt under it.
+    auto step = [&](char* cur, char* nxt, int kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < nk) issue(nxt, kt + 1);
+      compute(cur);
+    };
+    if (nk > 0) issue(smem0, 0);
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(smem0, smem1, kt);
+      if (kt + 1 < nk) step(smem1, smem0, kt + 1);
+    }
+  } else {
+    constexpr int PER_TILE = SA::NI + SB::NI;  // LDS-DMA instructions per wave per tile
+    auto step = [&](char* cur, char* nxt2, int kt) {
+      // retire tile kt; tile kt+1 (if any) stays in flight
+      if (kt + 1 < nk)
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(PER_TILE));
+      else
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // all waves: tile kt landed, stage of tile kt-1 free
+      if (kt + 2 < nk) issue(nxt2, kt + 2);
+      compute(cur);
+    };
+    if (nk > 0) issue(smem0, 0);
+    if (nk > 1) issue(smem1, 1);
+    for (int kt = 0; kt < nk; kt += 3) {
+      step(smem0, smem2, kt);
+      if (kt + 1 < nk) step(smem1, smem0, kt + 1);
+      if (kt + 2 < nk) step(smem2, smem1, kt + 2);
+    }
   }
 
   // Epilogue.  acc[i][j] holds D[n][m] with m = lane&15 (+16j), n = 4(lane>>4)+r (+16i):
@@ -396,17 +456,20 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_kernel(SnGemmArgs args) {
   }
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN>
+template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS>
 int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN>), grid, dim3(NTHR), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS>), grid, dim3(NW * 64), 0,
+                         st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN>), grid, dim3(NTHR), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS>), grid, dim3(NW * 64), 0,
+                         st, a);
       break;
     case EPI_F32_ACC:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN>), grid, dim3(NTHR), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS>), grid, dim3(NW * 64),
+                         0, st, a);
       break;
     default:
       return 2;
@@ -414,20 +477,23 @@ int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   return SN_CHECK_LAUNCH();
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NW, int NS>
 int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.splits, a.groups);
   const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
   switch (key) {
-    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, BM, BN>(a, grid, stream);    // NT dense
-    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, BM, BN>(a, grid, stream);   // conv fwd/dgrad
-    case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE, BM, BN>(a, grid, stream);    // NN dense
-    case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE, BM, BN>(a, grid, stream);    // TN dense
-    case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL, BM, BN>(a, grid, stream);   // conv wgrad
-    case 0b1000: return launch_epi<1, OP_DENSE, 0, OP_DENSE, BM, BN>(a, grid, stream);
-    default: return 4;
+    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, BM, BN, NW, NS>(a, grid, stream);   // NT dense
+    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, BM, BN, NW, NS>(a, grid, stream);  // conv fwd/dgrad
+    case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE, BM, BN, NW, NS>(a, grid, stream);   // NN dense
+    case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE, BM, BN, NW, NS>(a, grid, stream);   // TN dense
+    case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL, BM, BN, NW, NS>(a, grid, stream);  // conv wgrad
+    case 0b1000: return launch_epi<1, OP_DENSE, 0, OP_DENSE, BM, BN, NW, NS>(a, grid, stream);
+    default: break;
   }
+  if (a.a_mc == 0 && a.a_mode == OP_IM2COL && a.b_mc == 1 && a.b_mode == OP_FLIPW)  // conv dgrad
+    return launch_epi<0, OP_IM2COL, 1, OP_FLIPW, BM, BN, NW, NS>(a, grid, stream);
+  return 4;
 }
 
 }  // namespace
@@ -436,6 +502,10 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   const SnGemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
   if (a.kchunk <= 0 || (a.kchunk % BK) != 0) return 3;
-  if (a.tile == 1) return launch_tile<256, 64>(a, stream);
-  return launch_tile<128, 128>(a, stream);
+  switch (a.tile) {
+    case 1: return launch_tile<256, 64, 4, 2>(a, stream);    // skinny N
+    case 2: return launch_tile<256, 128, 8, 3>(a, stream);   // 8 waves, 3-stage pipeline
+    case 3: return launch_tile<128, 256, 8, 3>(a, stream);
+    default: return launch_tile<128, 128, 4, 2>(a, stream);
+  }
 }

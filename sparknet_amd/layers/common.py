@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import torch
 
+from .. import ops
 from ..core.layer import Layer, register
 
 
@@ -41,9 +42,15 @@ class SplitLayer(Layer):
         if len(tops) == 1:
             bottoms[0].diff = tops[0].diff
             return
-        acc = tops[0].diff.float() if tops[0].dtype != torch.float32 else tops[0].diff.clone()
-        for t in tops[1:]:
-            acc = acc + t.diff.float()
+        diffs = [t.diff for t in tops]
+        d0 = diffs[0]
+        if d0.is_cuda and d0.dtype == torch.bfloat16 and d0.numel() % 8 == 0:
+            # one fused fp32-accumulating pass over all top diffs (HIP sum_bf16)
+            bottoms[0].diff = ops.sum_bf16(diffs)
+            return
+        acc = d0.float() if d0.dtype != torch.float32 else d0.clone()
+        for d in diffs[1:]:
+            acc = acc + d.float()
         bottoms[0].diff = acc.to(bottoms[0].dtype)
 
 

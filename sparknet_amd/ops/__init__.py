@@ -87,6 +87,11 @@ def softmax_loss_backward(prob, labels, loss_weight, norm, ignore_label=None, dt
     return _impl(prob).softmax_loss_backward(prob, labels, loss_weight, norm, ignore_label, dtype)
 
 
+def sum_bf16(tensors):
+    """Elementwise sum of same-shape bf16 device tensors (fp32 accumulation)."""
+    return _hipmod().sum_bf16([t.contiguous() for t in tensors])
+
+
 def cast_f32_to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
     if src.is_cuda:
         _hipmod().cast_f32_to_bf16(src, dst)

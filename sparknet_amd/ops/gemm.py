@@ -14,13 +14,14 @@ an fp32 workspace and are combined by a deterministic reduce kernel.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import torch
 
 from . import _lib
 
-OP_DENSE, OP_IM2COL = 0, 1
+OP_DENSE, OP_IM2COL, OP_FLIPW = 0, 1, 2
 EPI_BF16, EPI_F32, EPI_F32_ACC = 0, 1, 2
 BM = BN = 128
 BK = 64
@@ -65,7 +66,23 @@ class Im2col:
     gstride: int = 0  # channels between groups
 
 
+@dataclass
+class FlipW:
+    """Conv weights w [K][R][S][Cg] (bf16) read as the dgrad B operand:
+    B_g(n = c, k = tap * Kg + kout) = w[g*Kg + kout][R-1-r][S-1-s][c]  (MC layout)."""
+    w: torch.Tensor
+    Kg: int
+    R: int
+    S: int
+    Cg: int
+
+
 def _operand(op) -> tuple[_lib.SnOperand, int, int]:
+    if isinstance(op, FlipW):
+        assert op.w.dtype == torch.bfloat16 and op.w.is_contiguous() and op.Cg % 8 == 0
+        g = _lib.SnConvGeom(0, 0, 0, op.Kg, 1, 1, op.R, op.S, 1, 1, 0, 0, 1, 1, op.Cg)
+        s = _lib.SnOperand(op.w.data_ptr(), 0, op.Kg * op.R * op.S * op.Cg, g)
+        return s, 1, OP_FLIPW
     if isinstance(op, Dense):
         assert op.t.dtype == torch.bfloat16, op.t.dtype
         assert op.t.data_ptr() % 16 == 0 and op.ld % 8 == 0, "dense operand must be 16-B aligned"
@@ -80,7 +97,8 @@ def _operand(op) -> tuple[_lib.SnOperand, int, int]:
     return s, 0 if op.kcontig else 1, OP_IM2COL
 
 
-TILES = {0: (128, 128), 1: (256, 64)}
+TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256)}
+_FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
 
 
 def choose_tile(M: int, N: int) -> int:
@@ -134,7 +152,7 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         return
     sa, a_mc, a_mode = _operand(A)
     sb, b_mc, b_mode = _operand(B)
-    tile = choose_tile(M, N)
+    tile = choose_tile(M, N) if _FORCE_TILE < 0 else _FORCE_TILE
     if splits is None:
         splits, kchunk = choose_splits(M, N, K, groups, tile)
     else:

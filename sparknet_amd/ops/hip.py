@@ -12,12 +12,13 @@ import ctypes as C
 import torch
 
 from . import _lib
-from .gemm import (EPI_BF16, EPI_F32, EPI_F32_ACC, ConvGeom, Dense, Im2col, colsum, gemm,
+from .gemm import (EPI_BF16, EPI_F32, EPI_F32_ACC, ConvGeom, Dense, FlipW, Im2col, colsum, gemm,
                    linear_dgrad, linear_fwd, linear_wgrad)
 from .spec import POOL_MAX, ConvSpec, PoolSpec
 
 call = _lib.call
 BF16 = torch.bfloat16
+DGRAD_INPLACE_WEIGHTS = False  # conv dgrad: read W via the FLIPW operand instead of a flip pass
 
 
 def _c(t: torch.Tensor) -> torch.Tensor:
@@ -61,9 +62,13 @@ def _geom(s: ConvSpec) -> ConvGeom:
 
 
 def _s2d_plan(s: ConvSpec):
-    """Space-to-depth fold for strided, low-channel, ungrouped convs (input layers):
-    returns (f, Cp, Rf, Sf, folded ConvSpec) or None."""
-    if _implicit_ok(s) or s.groups != 1 or s.sh != s.sw or s.sh < 2 or s.dh != 1 or s.dw != 1:
+    """Space-to-depth fold for low-channel, ungrouped convs (input layers): returns
+    (f, Cp, Rf, Sf, folded ConvSpec) or None.  Stride f >= 2 folds f x f pixels into the
+    channels (AlexNet conv1: 3 -> 48 channels, 11x11/4 -> 3x3/1); stride 1 is the f = 1
+    case — channels zero-padded to 8 and the spatial padding materialised (VGG conv1_1,
+    LeNet / CIFAR conv1) — so every input conv runs on the implicit-GEMM path instead of
+    an explicit im2col buffer."""
+    if _implicit_ok(s) or s.groups != 1 or s.sh != s.sw or s.dh != 1 or s.dw != 1:
         return None
     f = s.sh
     cp = s.C
@@ -176,13 +181,19 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
         return None
     dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
     if s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0:
-        # dgrad == forward conv of dy with flipped / transposed weights, pad' = R-1-pad
-        wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
-        call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
+        # dgrad == forward conv of dy with flipped / transposed weights, pad' = R-1-pad.
+        # A flip pass + KC (ds_read_b128) B operand measures faster than reading the
+        # weights in place through the FLIPW operand (MC, tr_b16 reads): 81k vs 86k img/s
+        # on CaffeNet; FLIPW stays available via DGRAD_INPLACE_WEIGHTS.
         g2 = ConvGeom(s.N, s.P, s.Q, s.K, s.H, s.W, s.R, s.S, 1, 1, s.R - 1 - s.ph, s.S - 1 - s.pw, 1, 1, s.Kg)
         kr2 = s.R * s.S * s.Kg
         A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
-        B = Dense(wt.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
+        if DGRAD_INPLACE_WEIGHTS:
+            B = FlipW(_c(w), s.Kg, s.R, s.S, s.Cg)
+        else:
+            wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
+            call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
+            B = Dense(wt.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
         gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg,
              gate=_c(gate) if gate is not None else None)
         return dx

@@ -59,6 +59,19 @@ def test_conv(gpu, case):
     close(db, db_r, 1e-3, what="bias")
 
 
+@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[8]])
+def test_conv_dgrad_inplace_weights(gpu, case, monkeypatch):
+    """dgrad reading W through the FLIPW operand (no flip pass) == the reference."""
+    from sparknet_amd.ops import hip
+    monkeypatch.setattr(hip, "DGRAD_INPLACE_WEIGHTS", True)
+    N, H, W, Cc, K, R, S, st, pd, g = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    x = rnd(N, H, W, Cc)
+    w = rnd(K, R, S, Cc // g, scale=0.2)
+    dy = rnd(N, s.P, s.Q, K)
+    close(hip.conv_backward(dy, x, w, s, True), ref.conv_backward(dy, x, w, s, True), what="dgrad")
+
+
 @pytest.mark.parametrize("M,K,N", [(256, 9216, 4096), (64, 800, 500), (100, 64, 10)])
 def test_linear(gpu, M, K, N):
     from sparknet_amd.ops import hip
@@ -215,7 +228,7 @@ def test_cast_and_augment(gpu):
 
 
 @pytest.mark.parametrize("mean_mode", [1, 2])
-@pytest.mark.parametrize("ksp", [(11, 4, 0), (7, 2, 3)])
+@pytest.mark.parametrize("ksp", [(11, 4, 0), (7, 2, 3), (3, 1, 1)])
 def test_augment_s2d_equals_augment_then_fold(gpu, mean_mode, ksp):
     """The fused augment + space-to-depth kernel is bitwise the two-pass result."""
     from sparknet_amd.ops import hip
@@ -233,3 +246,10 @@ def test_augment_s2d_equals_augment_then_fold(gpu, mean_mode, ksp):
     x2 = torch.empty_like(ref2)
     hip.augment_s2d(img, x2, crop, plan, s, mean, mean_mode, 0.25, rng, True, True)
     assert torch.equal(x2, ref2)
+
+
+@pytest.mark.parametrize("k", [2, 3, 8, 11])
+def test_sum_bf16(gpu, k):
+    from sparknet_amd.ops import hip
+    xs = [rnd(3, 5, 8) for _ in range(k)]
+    close(hip.sum_bf16(xs), sum(x.float() for x in xs), 1e-2)
