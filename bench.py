@@ -33,6 +33,8 @@ def parse():
     p.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the model's train batch)")
     p.add_argument("--tau", type=int, default=50)
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--overlap-update", action="store_true",
+                   help="run large layers' solver updates on a side stream during backward")
     p.add_argument("--profile-steps", type=int, default=0)
     return p.parse_args()
 
@@ -80,7 +82,8 @@ def main():
     feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
                           scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev)
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
-    trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph)
+    trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph,
+                              overlap_update=args.overlap_update)
     trainer.broadcast_initial()
 
     # warmup (includes hipGraph capture and one averaging collective to set up RCCL)

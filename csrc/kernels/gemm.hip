@@ -114,8 +114,8 @@ struct GStager {
   int coff;
   int rr[NI];  // tile-relative LDS row of this lane in instruction j
   int ch[NI];  // logical 16-B chunk this lane fetches in instruction j
-  int pn[NI], ph[NI], pw[NI];  // KC+IM2COL: pixel decode (rows fixed across k)
-  bool pv[NI];
+  int rowoff[NI], ph[NI], pw[NI];  // KC+IM2COL: pixel decode (rows fixed across k); rowoff =
+  bool pv[NI];                     // element offset of the (h=ph, w=pw) corner, may be < 0
   int cr[NI], cs[NI], cc[NI];  // MC+IM2COL: column decode (cols fixed across k)
   bool cv[NI];
   float invPQ, invQ, invCg, invS, invKg;
@@ -147,9 +147,9 @@ struct GStager {
         pv[j] = pix < rows_lim;
         int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
         int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
-        pn[j] = n * g.H;
         ph[j] = p * g.sh - g.ph;
         pw[j] = q * g.sw - g.pw;
+        rowoff[j] = ((n * g.H + ph[j]) * g.W + pw[j]) * g.C + coff;  // host guarantees < 2^31 elements
       }
       if (MODE == OP_IM2COL && MC) {
         int col = tile_col0 + ch[j] * 8;
@@ -182,23 +182,42 @@ struct GStager {
           dma(base + (long long)row * ld + k, row < rc_lim && k < k_lim, dst + j * 1024);
         }
       } else {
-        int kk[2], cch[2], dh[2], dw[2];
+        // k = (tap, c), c innermost.  k_tile is wave-uniform: decode it once on the scalar
+        // unit, then each lane adds its chunk (< 64 channels), which crosses at most one
+        // tap boundary when Cg >= 64 — no per-lane division on the fast path.
+        const int tap0 = k_tile / g.Cg, c0 = k_tile - tap0 * g.Cg;
+        const int r0 = tap0 / g.S, s0 = tap0 - r0 * g.S;
+        int kv[2], dh[2], dw[2], toff[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-          kk[e] = k_tile + ch[e] * 8;
-          int tap = fdiv(kk[e], g.Cg, invCg);
-          cch[e] = kk[e] - tap * g.Cg;
-          int r = fdiv(tap, g.S, invS), s = tap - r * g.S;
+          int c = c0 + ch[e] * 8, r = r0, s = s0;
+          if (g.Cg >= 64) {
+            if (c >= g.Cg) {
+              c -= g.Cg;
+              s += 1;
+              if (s == g.S) {
+                s = 0;
+                r += 1;
+              }
+            }
+          } else {
+            const int kk = k_tile + ch[e] * 8;
+            const int tap = fdiv(kk, g.Cg, invCg);
+            c = kk - tap * g.Cg;
+            r = fdiv(tap, g.S, invS);
+            s = tap - r * g.S;
+          }
+          kv[e] = k_tile + ch[e] * 8 < k_lim;
           dh[e] = r * g.dh;
           dw[e] = s * g.dw;
+          toff[e] = (dh[e] * g.W + dw[e]) * g.C + c;
         }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           const int e = j & 1;
-          int h = ph[j] + dh[e], w = pw[j] + dw[e];
-          bool v = kk[e] < k_lim && pv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          long long off = ((long long)(pn[j] + h) * g.W + w) * g.C + coff + cch[e];
-          dma(base + off, v, dst + j * 1024);
+          const int h = ph[j] + dh[e], w = pw[j] + dw[e];
+          const bool v = kv[e] && pv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          dma(base + (rowoff[j] + toff[e]), v, dst + j * 1024);
         }
       }
     } else {

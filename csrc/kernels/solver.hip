@@ -22,10 +22,13 @@ __global__ void __launch_bounds__(256) solver_update_kernel(float* __restrict__ 
                                                             bf16_t* __restrict__ shadow,
                                                             const long long* __restrict__ chunk_pos,
                                                             const float* __restrict__ chunk_mult,
-                                                            const float* __restrict__ hyper) {
-  const long long start = chunk_pos[2 * blockIdx.x];
-  const int count = (int)chunk_pos[2 * blockIdx.x + 1];
-  const float lr_mult = chunk_mult[2 * blockIdx.x], decay_mult = chunk_mult[2 * blockIdx.x + 1];
+                                                            const float* __restrict__ hyper, int nchunks) {
+  // a grid smaller than the chunk table loops over it (a background update running next to
+  // the backward GEMMs on a side stream takes only a slice of the CUs)
+  for (int cid = blockIdx.x; cid < nchunks; cid += gridDim.x) {
+  const long long start = chunk_pos[2 * cid];
+  const int count = (int)chunk_pos[2 * cid + 1];
+  const float lr_mult = chunk_mult[2 * cid], decay_mult = chunk_mult[2 * cid + 1];
   const float rate = hyper[H_LR] * lr_mult;
   const float mom = hyper[H_MOM];
   const float decay = hyper[H_WD] * decay_mult;
@@ -80,6 +83,7 @@ __global__ void __launch_bounds__(256) solver_update_kernel(float* __restrict__ 
     if (KIND >= 4) *reinterpret_cast<float4*>(h1 + o) = make_float4(B[0], B[1], B[2], B[3]);
     if (SHADOW) *reinterpret_cast<uint2*>(shadow + o) = make_uint2(pack2(W[0], W[1]), pack2(W[2], W[3]));
   }
+  }
 }
 
 // deterministic sum of squares of the flat gradient -> hyper[H_SUMSQ]
@@ -116,45 +120,47 @@ __global__ void sumsq_pass2(const float* __restrict__ part, int nparts, float* _
 
 template <int KIND, bool L1, bool CLIP>
 static void launch3(bool shadow, dim3 grid, hipStream_t st, float* w, const float* g, float* h0, float* h1,
-                    bf16_t* sh, const long long* cp, const float* cm, const float* hyper) {
+                    bf16_t* sh, const long long* cp, const float* cm, const float* hyper, int n) {
   if (shadow)
     hipLaunchKernelGGL((solver_update_kernel<KIND, L1, CLIP, true>), grid, dim3(256), 0, st, w, g, h0, h1, sh, cp, cm,
-                       hyper);
+                       hyper, n);
   else
     hipLaunchKernelGGL((solver_update_kernel<KIND, L1, CLIP, false>), grid, dim3(256), 0, st, w, g, h0, h1, sh, cp,
-                       cm, hyper);
+                       cm, hyper, n);
 }
 
 template <int KIND>
 static void launch_kind(bool l1, bool clip, bool shadow, dim3 grid, hipStream_t st, float* w, const float* g,
-                        float* h0, float* h1, bf16_t* sh, const long long* cp, const float* cm, const float* hyper) {
+                        float* h0, float* h1, bf16_t* sh, const long long* cp, const float* cm, const float* hyper,
+                        int n) {
   if (l1) {
-    if (clip) launch3<KIND, true, true>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper);
-    else launch3<KIND, true, false>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper);
+    if (clip) launch3<KIND, true, true>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n);
+    else launch3<KIND, true, false>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n);
   } else {
-    if (clip) launch3<KIND, false, true>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper);
-    else launch3<KIND, false, false>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper);
+    if (clip) launch3<KIND, false, true>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n);
+    else launch3<KIND, false, false>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n);
   }
 }
 
 extern "C" int sn_solver_update(long long kind, float* w, const float* g, float* h0, float* h1, bf16_t* shadow,
                                 const long long* chunk_pos, const float* chunk_mult, long long nchunks,
                                 float* hyper, long long l1, long long clip, float* part, long long nparts,
-                                long long total, hipStream_t st) {
+                                long long total, long long grid_limit, hipStream_t st) {
   if (nchunks <= 0) return 0;
   if (clip) {
     hipLaunchKernelGGL(sumsq_pass1, dim3((unsigned)nparts), dim3(256), 0, st, g, total, part);
     hipLaunchKernelGGL(sumsq_pass2, dim3(1), dim3(1024), 0, st, part, (int)nparts, hyper);
   }
-  dim3 grid((unsigned)nchunks);
+  dim3 grid((unsigned)(grid_limit > 0 && grid_limit < nchunks ? grid_limit : nchunks));
   bool sh = shadow != nullptr;
+  const int n = (int)nchunks;
   switch (kind) {
-    case 0: launch_kind<0>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper); break;
-    case 1: launch_kind<1>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper); break;
-    case 2: launch_kind<2>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper); break;
-    case 3: launch_kind<3>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper); break;
-    case 4: launch_kind<4>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper); break;
-    case 5: launch_kind<5>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper); break;
+    case 0: launch_kind<0>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
+    case 1: launch_kind<1>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
+    case 2: launch_kind<2>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
+    case 3: launch_kind<3>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
+    case 4: launch_kind<4>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
+    case 5: launch_kind<5>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
     default: return 8;
   }
   return SN_CHECK_LAUNCH();

@@ -211,6 +211,7 @@ class Net:
         self.layer_names: list[str] = []
         self.bottom_vecs: list[list[Blob]] = []
         self.top_vecs: list[list[Blob]] = []
+        self.backward_hooks: list = []  # callables(layer_index) run after each layer's backward
         self.bottom_ids: list[list[int]] = []
         self.top_ids: list[list[int]] = []
         self.bottom_need_backward: list[list[bool]] = []
@@ -474,6 +475,8 @@ class Net:
                                          self.bottom_vecs[li])
                 if self.debug_info:
                     self._debug_backward(li)
+            for hook in self.backward_hooks:  # e.g. overlapped per-layer solver update
+                hook(li)
 
     def backward(self) -> None:
         self.backward_from_to(len(self.layers) - 1, 0)

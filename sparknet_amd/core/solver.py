@@ -189,6 +189,45 @@ class Solver:
         self.update_params()
         return rate
 
+    # -- overlapped update (graph path) ---------------------------------------------------
+    def overlap_eligible(self) -> bool:
+        """Per-layer updates may run while backward continues only when every update is
+        local to its own parameters: no gradient clipping (global norm), no gradient
+        accumulation over iter_size passes, no gradient callbacks (sync-SGD all-reduce)."""
+        return (self.device.type == "cuda" and self.param.clip_gradients <= 0 and self.param.iter_size <= 1
+                and not self.callbacks)
+
+    def overlap_plan(self, min_group: int = 1) -> tuple[dict, list]:
+        """({layer index: [segments]}, late segments): a param's segment joins the group of
+        the LAST layer (in backward order) that writes its gradient; params whose gradient
+        is not written by backward (frozen / pruned) are updated after the pass."""
+        net = self.net
+        seg_of = {seg[0]: seg for seg in self.segments}
+        final, late = {}, set()
+        for li, layer in enumerate(net.layers):
+            for i, p in enumerate(layer.params):
+                if p.offset not in seg_of:
+                    continue
+                if not net.layer_need_backward[li] or not layer.param_grads_needed(i):
+                    late.add(p.offset)
+                final[p.offset] = min(final.get(p.offset, li), li)
+        groups: dict = {}
+        for off, li in final.items():
+            if off not in late:
+                groups.setdefault(li, []).append(seg_of[off])
+        # only large groups are worth a fork/join on the side stream (each costs ~10 us of
+        # graph synchronisation); the rest are updated after the backward pass
+        big = {li: segs for li, segs in groups.items() if sum(sg[1] for sg in segs) >= min_group}
+        rest = [seg_of[o] for o in seg_of if not any(o == sg[0] for segs in big.values() for sg in segs)]
+        return big, rest
+
+    def update_params_segments(self, tables, grid_limit: int = 0) -> None:
+        from .. import ops
+        net = self.net
+        ops.solver_update(SOLVER_KINDS[self.type], net.flat_data, net.flat_diff, self.history,
+                          net.flat_compute if net.flat_compute is not net.flat_data else None,
+                          tables, self.hyper, self.param.regularization_type == "L1", False, grid_limit)
+
     def update_params(self) -> None:
         from .. import ops
         l1 = self.param.regularization_type == "L1"

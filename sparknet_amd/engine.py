@@ -113,24 +113,73 @@ def fuse_input_fold(net, feeder) -> bool:
     return True
 
 
+class OverlappedUpdate:
+    """Runs each layer's fused solver update on a side stream as soon as backward has
+    produced that layer's final gradients, so the bandwidth-bound update (CaffeNet: 61 M
+    params, ~1.3 GB of traffic, fc6-fc8 first) overlaps the compute-bound conv backward
+    GEMMs.  Caffe applies the update only after the whole backward pass
+    (solver.cpp:237-240 -> sgd_solver.cpp:102-116); the result is identical because each
+    parameter's update reads only its own gradient and history."""
+
+    MIN_GROUP = 1 << 22   # params: smaller layers are updated after the backward pass
+    GRID = 128            # background update blocks (a slice of the 256 CUs)
+
+    def __init__(self, solver: Solver, min_group: int | None = None):
+        self.solver = solver
+        groups, rest = solver.overlap_plan(self.MIN_GROUP if min_group is None else min_group)
+        dev = solver.device
+        self.tables = {li: ops.solver_tables(segs, solver.net.num_param_elems, dev) for li, segs in groups.items()}
+        self.rest = ops.solver_tables(rest, solver.net.num_param_elems, dev) if rest else None
+        self.side = torch.cuda.Stream(dev)
+        self.active = False
+
+    def hook(self, li: int) -> None:
+        t = self.tables.get(li)
+        if t is None or not self.active:
+            return
+        main = torch.cuda.current_stream(self.solver.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.solver.update_params_segments(t, grid_limit=self.GRID)
+
+    def begin(self) -> None:
+        self.active = True
+
+    def end(self) -> None:
+        """After backward + finish_param_diffs: late params, then join the side stream."""
+        self.active = False
+        if self.rest is not None:
+            self.solver.update_params_segments(self.rest)
+        torch.cuda.current_stream(self.solver.device).wait_stream(self.side)
+
+
 class GraphStep:
     """One captured solver iteration (iter_size = 1)."""
 
-    def __init__(self, solver: Solver, warmup: int = 2, pre=None):
+    def __init__(self, solver: Solver, warmup: int = 2, pre=None, overlap: bool = True):
         self.solver = solver
         self.pre = pre  # callable run (eagerly) before each replay, e.g. feeder.stage
         self.graph = None
         self.loss = None
         self.warmup = warmup
+        self.overlap = None
+        if overlap and solver.overlap_eligible():
+            self.overlap = OverlappedUpdate(solver)
+            solver.net.backward_hooks.append(self.overlap.hook)
 
     def _body(self):
         s = self.solver
         net = s.net
         net.clear_param_diffs(lazy=True)
+        if self.overlap is not None:
+            self.overlap.begin()
         loss = net.forward_backward()
         net.finish_param_diffs()
         ops.advance_rng(net.ctx.rng_state)
-        s.update_params()
+        if self.overlap is not None:
+            self.overlap.end()
+        else:
+            s.update_params()
         return loss
 
     def capture(self) -> None:
@@ -174,14 +223,14 @@ class LocalSGDTrainer:
     """tau local steps + weight averaging per round (SparkNet's model averaging)."""
 
     def __init__(self, solver: Solver, comm=None, tau: int = 50, feeder=None, use_graph: bool = True,
-                 log_every: int = 0):
+                 log_every: int = 0, overlap_update: bool = False):
         self.solver = solver
         self.comm = comm
         self.tau = tau
         self.feeder = feeder
         self.round = 0
         self.use_graph = use_graph and solver.device.type == "cuda"
-        self.step_fn = GraphStep(solver, pre=self._pre) if self.use_graph else None
+        self.step_fn = GraphStep(solver, pre=self._pre, overlap=overlap_update) if self.use_graph else None
         self.log_every = log_every
         self.times = {"compute": 0.0, "allreduce": 0.0}
 

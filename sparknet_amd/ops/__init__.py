@@ -120,9 +120,10 @@ def solver_tables(segments, total: int, device) -> dict:
     return {"lr": lr, "decay": dc}
 
 
-def solver_update(kind, data, diff, history, compute, tables, hyper, l1: bool, clip: bool) -> None:
+def solver_update(kind, data, diff, history, compute, tables, hyper, l1: bool, clip: bool,
+                  grid_limit: int = 0) -> None:
     if data.is_cuda:
-        _hipmod().solver_update(kind, data, diff, history, compute, tables, hyper, l1, clip)
+        _hipmod().solver_update(kind, data, diff, history, compute, tables, hyper, l1, clip, grid_limit)
         return
     h = hyper.tolist()
     ref.solver_update_ref(kind, data, diff, history, tables["lr"], tables["decay"], h, l1, clip)

@@ -93,6 +93,7 @@ def _operand(op) -> tuple[_lib.SnOperand, int, int]:
     assert g.Cg % 8 == 0 and g.C % 8 == 0, "implicit conv needs channels % 8 == 0"
     # the kernel's fp32-reciprocal index division is exact below 2^24
     assert g.N * g.P * g.Q < (1 << 24) and g.N * g.H * g.W < (1 << 24), "conv too large for one launch"
+    assert op.x.numel() < (1 << 31), "implicit conv uses 32-bit element offsets"
     s = _lib.SnOperand(op.x.data_ptr(), 0, op.gstride, g.c_struct())
     return s, 0 if op.kcontig else 1, OP_IM2COL
 

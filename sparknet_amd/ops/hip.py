@@ -426,11 +426,11 @@ def solver_tables(segments, total: int, device) -> dict:
     }
 
 
-def solver_update(kind, data, diff, history, compute, tables, hyper, l1, clip):
+def solver_update(kind, data, diff, history, compute, tables, hyper, l1, clip, grid_limit=0):
     h0 = history[0]
     h1 = history[1] if len(history) > 1 else history[0]
     call("solver_update", int(kind), data, diff, h0, h1, compute, tables["pos"], tables["mult"], tables["n"],
-         hyper, int(l1), int(clip), tables["part"], tables["part"].numel(), tables["total"])
+         hyper, int(l1), int(clip), tables["part"], tables["part"].numel(), tables["total"], int(grid_limit))
 
 
 def scale_shadow(flat, shadow, scale: float):
