@@ -217,11 +217,11 @@ class Loader {
     for (auto& s : slots_) {
       if (cfg_.pinned) {
         if (s.ev) {
-          hipEventSynchronize(s.ev);
-          hipEventDestroy(s.ev);
+          (void)hipEventSynchronize(s.ev);
+          (void)hipEventDestroy(s.ev);
         }
-        if (s.img) hipHostFree(s.img);
-        if (s.lab) hipHostFree(s.lab);
+        if (s.img) (void)hipHostFree(s.img);
+        if (s.lab) (void)hipHostFree(s.lab);
       } else {
         std::free(s.img);
         std::free(s.lab);
@@ -347,7 +347,7 @@ class Loader {
         s.state = FILLING;
       }
       if (s.ev && s.ev_pending) {  // the previous occupant's H2D copy must have landed
-        hipEventSynchronize(s.ev);
+        (void)hipEventSynchronize(s.ev);
         s.ev_pending = false;
       }
       auto t0 = std::chrono::steady_clock::now();

@@ -50,12 +50,9 @@ def evaluate(solver, feeder, n_batches: int, comm) -> tuple[list[float], list[st
     over ranks (CifarApp.scala:101-116, Solver::TestAndStoreResult)."""
     tn = solver.test_nets[0]
     acc = None
-    for _ in range(n_batches):
-        feeder.stage()
-        feeder.prefetch()
-        tn.forward()
-        v = torch.stack([b.data.float().sum() for b in tn.output_blobs])
-        acc = v if acc is None else acc + v
+    from ..utils.trace import trace_range
+    with trace_range("eval"):
+        acc = _eval_batches(tn, feeder, n_batches)
     scores = acc.cpu().tolist() if acc is not None else [0.0] * len(tn.output_blobs)
     total = n_batches
     if comm is not None and comm.world_size > 1:
@@ -63,6 +60,17 @@ def evaluate(solver, feeder, n_batches: int, comm) -> tuple[list[float], list[st
                                        if solver.device.type == "cuda" else None)
         total = int(scores.pop())
     return scores, [b.name for b in tn.output_blobs], total
+
+
+def _eval_batches(tn, feeder, n_batches):
+    acc = None
+    for _ in range(n_batches):
+        feeder.stage()
+        feeder.prefetch()
+        tn.forward()
+        v = torch.stack([b.data.float().sum() for b in tn.output_blobs])
+        acc = v if acc is None else acc + v
+    return acc
 
 
 def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: bool, classes: int,

@@ -21,6 +21,7 @@ import torch
 
 from . import ops
 from .core.solver import Solver
+from .utils.trace import trace_range
 
 log = logging.getLogger("sparknet_amd.engine")
 
@@ -236,8 +237,9 @@ class LocalSGDTrainer:
 
     def _pre(self):
         if self.feeder is not None:
-            self.feeder.stage()
-            self.feeder.prefetch()
+            with trace_range("data"):
+                self.feeder.stage()
+                self.feeder.prefetch()
 
     def broadcast_initial(self) -> None:
         """All ranks start from rank 0's initial weights (CifarApp.scala:92)."""
@@ -245,16 +247,18 @@ class LocalSGDTrainer:
             self.comm.broadcast_params(self.solver.net)
 
     def local_step(self):
-        if self.use_graph:
-            return self.step_fn.step()
-        self._pre()
-        loss = self.solver.iteration()
-        self.solver.iter += 1
-        return loss
+        with trace_range("compute"):
+            if self.use_graph:
+                return self.step_fn.step()
+            self._pre()
+            loss = self.solver.iteration()
+            self.solver.iter += 1
+            return loss
 
     def average(self) -> None:
         if self.comm is not None and self.comm.world_size > 1:
-            self.comm.average_params(self.solver.net)
+            with trace_range("allreduce"):
+                self.comm.average_params(self.solver.net)
 
     def run_round(self):
         loss = None

@@ -16,6 +16,9 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _LIBDIR = Path(__file__).resolve().parent.parent / "lib"
+# SN_DEBUG_SYNC=1: synchronise after every native launch and name the failing kernel
+# (Caffe's CUDA_POST_KERNEL_CHECK under a blocking-launch debug mode)
+DEBUG_SYNC = os.environ.get("SN_DEBUG_SYNC", "0") == "1"
 _kern = None
 _rt = None
 
@@ -103,6 +106,15 @@ def call(name: str, *args):
     conv.append(C.c_void_p(stream_ptr()))
     fn.restype = C.c_int
     check(fn(*conv), name)
+    if DEBUG_SYNC:
+        debug_sync(name)
+
+
+def debug_sync(name: str) -> None:
+    try:
+        torch.cuda.synchronize()
+    except RuntimeError as e:  # a fault inside the kernel surfaces here
+        raise RuntimeError(f"sparknet_amd kernel '{name}' faulted: {e}") from e
 
 
 def loaded_libraries() -> list[str]:

@@ -170,6 +170,8 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
                                bias.data_ptr() if bias is not None else 0, int(relu), tile, gp)
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
+        if _lib.DEBUG_SYNC:
+            _lib.debug_sync("gemm")
         return
     ws = torch.empty((groups, splits, M, N), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,

@@ -124,15 +124,75 @@ class Comm:
             dist.destroy_process_group()
 
 
+def grad_buckets(net, bucket_bytes: int):
+    """Plan the overlapped gradient all-reduce: ({layer index: [(start, end), ...]}, late
+    ranges).  A parameter's gradient is final after the backward of the LAST layer (in
+    backward order) that writes it; parameters are packed in backward order into
+    contiguous flat ranges of >= ``bucket_bytes`` that are launched from the backward
+    hook of the layer completing them.  Gradients that backward does not write (frozen /
+    pruned layers, zeroed by Net.finish_param_diffs) form the late ranges."""
+    from ..core.net import PARAM_ALIGN
+    users, late = {}, set()
+    for li, layer in enumerate(net.layers):
+        for i, p in enumerate(layer.params):
+            users[p.offset] = min(users.get(p.offset, li), li)
+            if not net.layer_need_backward[li] or not layer.param_grads_needed(i):
+                late.add(p.offset)
+    seg = {p.offset: -(-p.count // PARAM_ALIGN) * PARAM_ALIGN for p in net.learnable_params}
+    order = sorted((o for o in seg if o in users and o not in late), key=lambda o: (-users[o], -o))
+    plan, cur, cur_bytes = {}, [], 0
+
+    def close(at_layer):
+        nonlocal cur, cur_bytes
+        if not cur:
+            return
+        lo, hi = min(cur), max(o + seg[o] for o in cur)
+        ranges = [(lo, hi)] if hi - lo == sum(seg[o] for o in cur) else [(o, o + seg[o]) for o in sorted(cur)]
+        plan.setdefault(at_layer, []).extend(ranges)
+        cur, cur_bytes = [], 0
+
+    for k, o in enumerate(order):
+        cur.append(o)
+        cur_bytes += seg[o] * 4
+        nxt = order[k + 1] if k + 1 < len(order) else None
+        if cur_bytes >= bucket_bytes or nxt is None or (users[nxt] != users[o] and cur_bytes >= bucket_bytes):
+            close(users[o])
+    late_ranges = [(o, o + seg[o]) for o in sorted(seg) if o in late or o not in users]
+    return plan, late_ranges
+
+
 class SyncSGDCallback:
     """Solver callback for synchronous gradient all-reduce (Caffe P2PSync semantics:
-    N ranks x batch B == 1 rank x batch N*B, test_gradient_based_solver.cpp:455-490)."""
+    N ranks x batch B == 1 rank x batch N*B, test_gradient_based_solver.cpp:455-490).
 
-    def __init__(self, comm: Comm, net):
+    With ``overlap`` (default) the flat gradient buffer is all-reduced in buckets
+    launched asynchronously from the backward pass as soon as each bucket's gradients
+    are final (fc8/fc7/fc6 first in CaffeNet), so the collective runs under the remaining
+    backward GEMMs; ``on_gradients_ready`` waits for them, reduces the rest and scales by
+    1/N."""
+
+    def __init__(self, comm: Comm, net, overlap: bool = True, bucket_bytes: int = 32 << 20):
         self.comm, self.net = comm, net
+        self.works = []
+        self.plan = None
+        if overlap and comm.world_size > 1:
+            self.plan, self.late = grad_buckets(net, bucket_bytes)
+            net.backward_hooks.append(self._hook)
 
     def on_start(self):
-        pass
+        self.works = []
+
+    def _hook(self, li: int) -> None:
+        for s, e in self.plan.get(li, ()):
+            self.works.append(dist.all_reduce(self.net.flat_diff[s:e], op=dist.ReduceOp.SUM, async_op=True))
 
     def on_gradients_ready(self):
-        self.comm.allreduce_grads(self.net, average=True)
+        if self.plan is None:
+            self.comm.allreduce_grads(self.net, average=True)
+            return
+        for w in self.works:
+            w.wait()
+        self.works = []
+        for s, e in self.late:
+            dist.all_reduce(self.net.flat_diff[s:e], op=dist.ReduceOp.SUM)
+        self.net.flat_diff.mul_(1.0 / self.comm.world_size)

@@ -143,3 +143,53 @@ def _worker_misc(rank, world, port, q):
 def test_collective_helpers():
     for rank, s, g, m in _run(_worker_misc):
         assert s == [3.0, 20.0] and g == [0, 5] and m == 1.0
+
+
+def _multilayer_solver(seed):
+    from sparknet_amd.core.solver import Solver
+    net = proto.parse_prototxt("""
+      name: "ml"
+      layer { name: "data" type: "JavaData" top: "data" java_data_param { shape { dim: 4 dim: 3 dim: 6 dim: 6 } } }
+      layer { name: "label" type: "JavaData" top: "label" java_data_param { shape { dim: 4 dim: 1 } } }
+      layer { name: "conv" type: "Convolution" bottom: "data" top: "conv"
+        param { lr_mult: 0 } param { lr_mult: 0 }
+        convolution_param { num_output: 4 kernel_size: 3 weight_filler { type: "gaussian" std: 0.3 } } }
+      layer { name: "ip1" type: "InnerProduct" bottom: "conv" top: "ip1"
+        inner_product_param { num_output: 8 weight_filler { type: "gaussian" std: 0.3 } } }
+      layer { name: "relu" type: "ReLU" bottom: "ip1" top: "ip1" }
+      layer { name: "ip2" type: "InnerProduct" bottom: "ip1" top: "ip2"
+        inner_product_param { num_output: 3 weight_filler { type: "gaussian" std: 0.3 } } }
+      layer { name: "loss" type: "SoftmaxWithLoss" bottom: "ip2" bottom: "label" top: "loss" }
+    """)
+    sp = proto.SolverParameter(base_lr=0.1, lr_policy="fixed", momentum=0.9, weight_decay=0.001)
+    sp.net_param.CopyFrom(net)
+    return Solver(sp, device="cpu", seed=seed)
+
+
+def _worker_bucketed(rank, world, port, q):
+    _init(rank, world, port)
+    from sparknet_amd.parallel import Comm, SyncSGDCallback
+    from sparknet_amd.parallel.comm import grad_buckets
+    comm = Comm()
+    out = []
+    for overlap in (False, True):
+        s = _multilayer_solver(seed=0)
+        cb = SyncSGDCallback(comm, s.net, overlap=overlap, bucket_bytes=64)
+        s.add_callback(cb)
+        for step in range(3):
+            g = torch.Generator().manual_seed(1000 + 10 * step + rank)
+            s.net.layer_by_name("data").feed(torch.randn(4, 3, 6, 6, generator=g))
+            s.net.layer_by_name("label").feed(torch.randint(0, 3, (4, 1), generator=g).float())
+            s.step(1)
+        out.append(s.net.flat_data.tolist())
+    plan, late = grad_buckets(s.net, 64)
+    q.put((rank, out, sum(len(v) for v in plan.values()), len(late)))
+    comm.close()
+
+
+def test_bucketed_overlapped_grad_allreduce_matches_flat():
+    res = _run(_worker_bucketed)
+    for rank, (flat, bucketed), nb, nlate in res:
+        assert nb >= 3 and nlate == 2, (nb, nlate)  # ip2 w/b, ip1 w/b buckets; frozen conv w/b late
+        assert flat == bucketed
+    assert res[0][1][1] == res[1][1][1]

@@ -249,3 +249,20 @@ def test_lazy_gradient_clear_matches_memset():
         frozen = net.layer_by_name("conv2").params
     assert torch.allclose(out[0], out[1], rtol=1e-6, atol=1e-7)
     assert all(float(p.diff.abs().max()) == 0.0 for p in frozen)
+
+
+def test_random_init_gives_chance_accuracy():
+    """CifarSpec (src/test/scala/libs/CifarSpec.scala:10-94): a random-init cifar10_full on
+    CIFAR-shaped data scores chance — sum over 10 test batches of accuracy x 100 lies in
+    [70, 130].  Synthetic images / labels stand in for the CIFAR test set."""
+    net = Net(models.cifar10_full(train_batch=100, test_batch=100), phase=proto.TEST, seed=1)
+    g = torch.Generator().manual_seed(4)
+    total = 0.0
+    for _ in range(10):
+        x = torch.randint(0, 256, (100, 3, 32, 32), generator=g).float() - 120.0
+        y = torch.randint(0, 10, (100, 1), generator=g).float()
+        net.blob_by_name("data").set_nchw(x)
+        net.blob_by_name("label").set_nchw(y)
+        net.forward()
+        total += float(net.blob_by_name("accuracy").data.reshape(-1)[0])
+    assert 70 <= total * 100 <= 130, total * 100

@@ -91,3 +91,12 @@ def test_overlapped_update_matches_serial(gpu):
     assert s0.iter == s1.iter
     assert torch.equal(s0.net.flat_data, s1.net.flat_data)
     assert torch.equal(s0.history[0], s1.history[0])
+
+
+def test_training_is_bitwise_deterministic(gpu):
+    """Fixed Philox seeds + atomics-free reductions (split-K slabs, colsum, solver): two
+    identical graph-captured runs end with bitwise-identical weights and momentum."""
+    a, _ = _graph_solver(False)
+    b, _ = _graph_solver(False)
+    assert torch.equal(a.net.flat_data, b.net.flat_data)
+    assert torch.equal(a.history[0], b.history[0])
