@@ -1,0 +1,53 @@
+// libsn_core — C ABI over the sparknet_amd engine, the counterpart of SparkNet's
+// libccaffe (libccaffe/ccaffe.h, libccaffe/ccaffe.cpp:22-296) for non-Python callers
+// (C/C++, or the JVM through JNA as in CaffeLibrary.java:8-76).
+//
+// Every function returns 0 on success and non-zero on failure (sn_last_error() then
+// describes the failure), except where a count / pointer is returned.  Handles are
+// thread-compatible: calls may come from any thread, one call at a time per handle.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// java_callback_t (CaffeLibrary.java:12-14): fill `buf` (batch x shape[1..] floats,
+// logical NCHW) for the next minibatch.
+typedef void (*sn_data_callback_t)(float* buf, int batch, int ndims, const int* shape, void* user);
+
+const char* sn_last_error(void);
+
+void* sn_create_state(void);
+void sn_destroy_state(void* state);
+int sn_set_device(void* state, int device);  // -1 = CPU reference path
+int sn_load_solver_from_protobuf(void* state, const char* bytes, int len);  // serialized SolverParameter
+int sn_load_net_from_protobuf(void* state, const char* bytes, int len);     // serialized NetParameter (TEST)
+int sn_set_train_data_callback(void* state, int layer_index, sn_data_callback_t cb, void* user);
+int sn_set_test_data_callback(void* state, int layer_index, sn_data_callback_t cb, void* user);
+
+int sn_forward(void* state, float* loss);
+int sn_backward(void* state);
+int sn_solver_step(void* state, int iters);
+int sn_solver_test(void* state, int iters);  // returns the number of scores (>= 0) or -1
+float sn_get_test_score(void* state, int index);
+
+long long sn_num_params(void* state);  // flat fp32 parameter count (incl. alignment padding)
+int sn_get_weights(void* state, float* out, long long n);
+int sn_set_weights(void* state, const float* in, long long n);
+void* sn_weights_device_ptr(void* state);  // flat fp32 master buffer (device memory on GPU)
+
+int sn_save_weights_to_file(void* state, const char* path);  // .caffemodel
+int sn_load_weights_from_file(void* state, const char* path);
+int sn_restore_solver_from_file(void* state, const char* path);  // .solverstate
+
+int sn_num_layers(void* state);
+int sn_layer_name(void* state, int index, char* buf, int buflen);
+
+int sn_parse_net_prototxt(const char* path, char** out, int* len);     // -> serialized bytes
+int sn_parse_solver_prototxt(const char* path, char** out, int* len);  // (free with sn_free)
+void sn_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,6 +1,6 @@
 """In-tree builder for the native parts of sparknet_amd.
 
-Two shared libraries are produced inside the package (so they travel with the repo
+Three shared libraries are produced inside the package (so they travel with the repo
 snapshot to a GPU box and are what the Python processes load):
 
 * ``sparknet_amd/lib/libsn_kernels.so`` — every ``csrc/kernels/*.hip`` file compiled by
@@ -8,8 +8,10 @@ snapshot to a GPU box and are what the Python processes load):
   fused solver updates, data augmentation ...).  C ABI, launched through ctypes on
   torch's current HIP stream.
 * ``sparknet_amd/lib/libsn_runtime.so`` — host C++ runtime (``csrc/runtime/*.cpp``):
-  prototxt-independent pieces of the engine that the reference keeps native
-  (data prefetch ring / worker threads, BlobProto packing, timers).
+  the native minibatch pipeline (mmap'd record sources, samplers, worker threads,
+  pinned ring, async H2D copies).
+* ``sparknet_amd/lib/libsn_core.so`` — the C ABI over the engine (``csrc/core``), the
+  counterpart of SparkNet's libccaffe for C / C++ / JVM (JNA) hosts.
 
 The builder is incremental (mtime based) and compiles translation units in parallel.
 ``python -m sparknet_amd.build_native`` or ``__graft_entry__.build()`` drive it.
@@ -47,10 +49,20 @@ RUNTIME_LINK = [f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"]
 
 KERNEL_LIB = LIBDIR / "libsn_kernels.so"
 RUNTIME_LIB = LIBDIR / "libsn_runtime.so"
+CORE_LIB = LIBDIR / "libsn_core.so"
+
+
+def _python_flags() -> tuple[list[str], list[str]]:
+    """Compile / link flags for embedding CPython (libsn_core)."""
+    import sysconfig
+    inc = sysconfig.get_paths()["include"]
+    libdir = sysconfig.get_config_var("LIBDIR") or "/usr/lib"
+    ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+    return [f"-I{inc}"], [f"-L{libdir}", f"-lpython{ver}", f"-Wl,-rpath,{libdir}", "-ldl"]
 
 
 def _deps(src: Path) -> list[Path]:
-    hdrs = list((CSRC / "kernels").glob("*.h")) + list((CSRC / "runtime").glob("*.h"))
+    hdrs = [h for d in ("kernels", "runtime", "core") for h in (CSRC / d).glob("*.h")]
     return [src] + hdrs
 
 
@@ -67,14 +79,14 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
-def _compile(src: Path, hip: bool) -> Path:
-    obj = OBJDIR / (src.stem + (".hip.o" if hip else ".cpp.o"))
+def _compile(src: Path, hip: bool, extra: list[str] | None = None) -> Path:
+    obj = OBJDIR / (src.parent.name + "_" + src.stem + (".hip.o" if hip else ".cpp.o"))
     if _stale(obj, _deps(src)):
         obj.parent.mkdir(parents=True, exist_ok=True)
         if hip:
             cmd = [HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)]
         else:
-            cmd = ["g++", *CXX_FLAGS, "-c", str(src), "-o", str(obj)]
+            cmd = ["g++", *CXX_FLAGS, *(extra or []), "-c", str(src), "-o", str(obj)]
         _run(cmd)
     return obj
 
@@ -88,9 +100,12 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     jobs = jobs or min(8, os.cpu_count() or 4)
     hip_srcs = sorted((CSRC / "kernels").glob("*.hip"))
     cpp_srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    core_srcs = sorted((CSRC / "core").glob("*.cpp"))
+    py_inc, py_link = _python_flags()
     with cf.ThreadPoolExecutor(jobs) as ex:
         hip_objs = list(ex.map(lambda s: _compile(s, True), hip_srcs))
         cpp_objs = list(ex.map(lambda s: _compile(s, False), cpp_srcs))
+        core_objs = list(ex.map(lambda s: _compile(s, False, [*py_inc, f"-I{CSRC / 'core'}"]), core_srcs))
     out = {}
     if hip_objs:
         if force or _stale(KERNEL_LIB, hip_objs):
@@ -102,6 +117,10 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
             _run(["g++", "-shared", "-fPIC", "-pthread", *map(str, cpp_objs), *RUNTIME_LINK, "-o",
                   str(RUNTIME_LIB)])
         out["runtime"] = str(RUNTIME_LIB)
+    if core_objs:
+        if force or _stale(CORE_LIB, core_objs):
+            _run(["g++", "-shared", "-fPIC", "-pthread", *map(str, core_objs), *py_link, "-o", str(CORE_LIB)])
+        out["core"] = str(CORE_LIB)
     if verbose:
         print(out)
     return out

@@ -1,0 +1,84 @@
+"""libsn_core — the C ABI replacing SparkNet's libccaffe (libccaffe/ccaffe.cpp:22-296).
+A C host program (tests/native/core_demo.c) trains through it with callback-fed data,
+tests, and round-trips flat weights and a .caffemodel; the same library is also driven
+from Python through ctypes (interpreter already running, GIL handed over)."""
+import ctypes as C
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from sparknet_amd import build_native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "sparknet_amd", "lib")
+SOLVER = os.path.join(ROOT, "tests", "native", "core_solver.prototxt")
+
+
+@pytest.fixture(scope="module")
+def core_lib():
+    out = build_native.build()
+    assert "core" in out
+    return out["core"]
+
+
+def _c_host_program(tmp_path, device):
+    if shutil.which("gcc") is None:
+        pytest.skip("no C compiler")
+    exe = tmp_path / "core_demo"
+    r = subprocess.run(["gcc", "-std=c11", "-O1", f"-I{ROOT}/csrc/core", f"{ROOT}/tests/native/core_demo.c",
+                        f"-L{LIB}", "-lsn_core", f"-Wl,-rpath,{LIB}", "-lm", "-o", str(exe)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ)
+    if device < 0:
+        env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([str(exe), SOLVER, str(tmp_path / "w.caffemodel"), str(device)], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout, r.stderr[-3000:])
+    assert "layers=7 layer2=conv1" in r.stdout and "callbacks=6" in r.stdout
+
+
+def test_c_host_program(core_lib, tmp_path):
+    _c_host_program(tmp_path, -1)
+
+
+
+CB = C.CFUNCTYPE(None, C.POINTER(C.c_float), C.c_int, C.c_int, C.POINTER(C.c_int), C.c_void_p)
+
+
+def test_ctypes_inside_python(core_lib, tmp_path):
+    lib = C.CDLL(core_lib)
+    lib.sn_create_state.restype = C.c_void_p
+    lib.sn_last_error.restype = C.c_char_p
+    lib.sn_num_params.restype = C.c_longlong
+    for f in ("sn_set_device", "sn_load_solver_from_protobuf", "sn_set_train_data_callback", "sn_solver_step",
+              "sn_get_weights", "sn_parse_solver_prototxt"):
+        getattr(lib, f).restype = C.c_int
+    st = C.c_void_p(lib.sn_create_state())
+    assert st.value, lib.sn_last_error()
+    buf, n = C.c_char_p(), C.c_int()
+    assert lib.sn_parse_solver_prototxt(SOLVER.encode(), C.byref(buf), C.byref(n)) == 0
+    assert lib.sn_set_device(st, -1) == 0
+    assert lib.sn_load_solver_from_protobuf(st, buf, n) == 0, lib.sn_last_error()
+    seen = []
+
+    def fill(p, batch, nd, shape, user):
+        cnt = int(np.prod([shape[i] for i in range(nd)]))
+        arr = np.ctypeslib.as_array(p, shape=(cnt,))
+        arr[:] = np.linspace(-1, 1, cnt, dtype=np.float32) if nd == 4 else (np.arange(cnt) % 3)
+        seen.append(nd)
+
+    cb = CB(fill)
+    assert lib.sn_set_train_data_callback(st, 0, cb, None) == 0
+    assert lib.sn_set_train_data_callback(st, 1, cb, None) == 0
+    assert lib.sn_solver_step(st, 3) == 0, lib.sn_last_error()
+    assert sorted(set(seen)) == [2, 4] and len(seen) == 6
+    nparam = lib.sn_num_params(st)
+    w = (C.c_float * nparam)()
+    assert lib.sn_get_weights(st, w, C.c_longlong(nparam)) == 0
+    assert np.isfinite(np.frombuffer(w, dtype=np.float32)).all()
+    lib.sn_free(buf)
+    lib.sn_destroy_state(st)
