@@ -338,6 +338,10 @@ class Solver:
         if d:
             os.makedirs(d, exist_ok=True)
         from ..utils.checkpoint import save_caffemodel
+        if self.param.HasField("snapshot_format") and self.param.snapshot_format == 0:
+            # HDF5 snapshots (sgd_solver.cpp:257-298) need h5py, which this environment
+            # lacks; the binaryproto pair holds the same state
+            log.warning("snapshot_format HDF5 is not available; writing binaryproto snapshots")
         save_caffemodel(self.net, model, write_diff=self.param.snapshot_diff)
         proto.write_binary(state, self.solver_state(model))
         log.info("Snapshotting to %s / %s", model, state)

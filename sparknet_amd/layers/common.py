@@ -618,3 +618,35 @@ class SPPLayer(Layer):
             g += ops.ref.pool_backward(dy, b.data.float(), s)
             off += n
         b.diff = g.to(b.dtype)
+
+
+@register("Python")
+class PythonLayer(Layer):
+    """User-defined layer in Python (caffe/include/caffe/python_layer.hpp:14,
+    layer_factory.cpp:202-214): ``python_param { module: "m" layer: "Cls" param_str: "..." }``
+    imports ``m.Cls`` and drives it with pycaffe's Layer protocol — ``setup(bottom, top)``,
+    ``reshape(bottom, top)``, ``forward(bottom, top)``, ``backward(top, propagate_down,
+    bottom)`` — where bottom / top are this engine's blobs (``.data`` / ``.diff`` tensors,
+    ``.reshape(shape)``) and ``self.param_str`` holds the string parameter."""
+
+    def layer_setup(self, bottoms, tops):
+        import importlib
+        pp = self.lp.python_param
+        if not pp.module or not pp.layer:
+            raise ValueError(f"Python layer {self.name!r} needs python_param.module and .layer")
+        cls = getattr(importlib.import_module(pp.module), pp.layer)
+        self.impl = cls()
+        self.impl.param_str = pp.param_str
+        self.impl.phase = self.phase
+        if hasattr(self.impl, "setup"):
+            self.impl.setup(bottoms, tops)
+
+    def reshape(self, bottoms, tops):
+        self.impl.reshape(bottoms, tops)
+
+    def forward(self, bottoms, tops):
+        self.impl.forward(bottoms, tops)
+
+    def backward(self, tops, propagate_down, bottoms):
+        if hasattr(self.impl, "backward"):
+            self.impl.backward(tops, list(propagate_down), bottoms)

@@ -266,3 +266,21 @@ def test_random_init_gives_chance_accuracy():
         net.forward()
         total += float(net.blob_by_name("accuracy").data.reshape(-1)[0])
     assert 70 <= total * 100 <= 130, total * 100
+
+
+def test_python_layer():
+    """python_param user layer (pycaffe protocol) inside a net, forward and backward."""
+    n = proto.parse_prototxt("""
+      name: "py"
+      force_backward: true
+      layer { name: "x" type: "Input" top: "x" java_data_param { shape { dim: 2 dim: 3 } } }
+      layer { name: "s" type: "Python" bottom: "x" top: "y"
+              python_param { module: "pylayers.scale_layer" layer: "ScaleByParam" param_str: "2.5" } }
+      layer { name: "loss" type: "EuclideanLoss" bottom: "y" bottom: "x" top: "loss" }
+    """)
+    net = Net(n, phase=proto.TRAIN)
+    x = torch.randn(2, 3)
+    net.blob_by_name("x").set_nchw(x)
+    loss = net.forward_backward()
+    assert torch.allclose(net.blob_by_name("y").data, 2.5 * x)
+    assert abs(float(loss) - float(((1.5 * x) ** 2).sum() / 2 / 2)) < 1e-5
