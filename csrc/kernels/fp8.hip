@@ -1,0 +1,83 @@
+// FP8 (OCP e4m3) quantisation with per-tensor delayed scaling for the fp8 forward GEMMs
+// (VGG-16 fp8 configuration, SURVEY §7.6-3: fp32 masters, fp32 accumulation, per-tensor
+// scales from an amax history).
+//
+// A scale slot is float[4]: [0] quantisation scale s (x_fp8 = sat(x * s)), [1] amax of the
+// tensors quantised with this slot since the last update (float bits, atomicMax),
+// [2] dequantisation factor 1/s (read by the GEMM epilogue), [3] unused.
+// fp8_update_scales (once per iteration, inside the captured graph) turns the running
+// amax into the next iteration's scale: s = 448 / amax (e4m3 max normal = 448).
+#include "common.h"
+
+namespace {
+
+constexpr float E4M3_MAX = 448.f;
+
+SN_DEV uint32_t pack4_fp8(float a, float b, float c, float d) {
+  int w = 0;
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
+__global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q,
+                                                        long long n16, float* __restrict__ slot) {
+  const float sc = slot[0];
+  float amax = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x) {
+    const uint4 a = reinterpret_cast<const uint4*>(x)[2 * i];
+    const uint4 b = reinterpret_cast<const uint4*>(x)[2 * i + 1];
+    float f[16];
+    unpack8(a, f);
+    unpack8(b, f + 8);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      amax = fmaxf(amax, fabsf(f[k]));
+      f[k] = fminf(fmaxf(f[k] * sc, -E4M3_MAX), E4M3_MAX);
+    }
+    uint4 o;
+    o.x = pack4_fp8(f[0], f[1], f[2], f[3]);
+    o.y = pack4_fp8(f[4], f[5], f[6], f[7]);
+    o.z = pack4_fp8(f[8], f[9], f[10], f[11]);
+    o.w = pack4_fp8(f[12], f[13], f[14], f[15]);
+    reinterpret_cast<uint4*>(q)[i] = o;
+  }
+  // one atomic per block (a per-wave atomic on one address serialises ~30k updates)
+  __shared__ float red[4];
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (amax > 0.f)  // amax >= 0: uint order == float order
+      atomicMax(reinterpret_cast<unsigned int*>(slot + 1), __float_as_uint(amax));
+  }
+}
+
+__global__ void fp8_update_scales_kernel(float* __restrict__ slots, int n, float margin) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float* s = slots + 4 * i;
+  const float amax = s[1];
+  if (amax > 0.f) {
+    const float sc = E4M3_MAX / (amax * margin);
+    s[0] = sc;
+    s[2] = 1.f / sc;
+  }
+  s[1] = 0.f;
+}
+
+}  // namespace
+
+extern "C" int sn_quant_fp8(const bf16_t* x, uint8_t* q, long long n, float* slot, hipStream_t st) {
+  if (n % 16) return 7;
+  hipLaunchKernelGGL(quant_fp8_kernel, dim3(sn_blocks(n / 16, 256, 1024)), dim3(256), 0, st, x, q, n / 16, slot);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_fp8_update_scales(float* slots, long long n, float margin, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, slots, (int)n,
+                     margin);
+  return SN_CHECK_LAUNCH();
+}

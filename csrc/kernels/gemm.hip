@@ -70,6 +70,9 @@ struct SnGemmArgs {
   int relu;
   int tile;           // 0: 128x128, 1: 256x64 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages)
   const bf16_t* gate; // EPI_BF16: zero outputs where gate (same layout as C) <= 0 (fused ReLU backward)
+  int fp8;            // operands are e4m3 bytes (K-contiguous only); k counts fp8 elements
+  const float* deq_a; // fp8: dequantisation factors (1 / quantisation scale) of A and B, device scalars
+  const float* deq_b;
 };
 
 }  // extern "C"
@@ -102,13 +105,15 @@ typedef __attribute__((address_space(3))) void lds_void;
 // maps to that slot.  Lanes outside the matrix read a zero page.
 //   KC: [TILE rows][64 k], 8 chunks per row, 8 rows per instruction.
 //   MC: [64 k rows][TILE cols], TILE/8 chunks per row.
-template <int MC, int MODE, int TILE, int NW>
+template <int MC, int MODE, int TILE, int NW, int ES = 2>
 struct GStager {
   static constexpr int NI = TILE / (8 * NW);      // wave-instructions per wave per tile
   static constexpr int CPL = MC ? TILE / 8 : 8;   // 16-B chunks per LDS row
   static constexpr int RPI = 64 / CPL;            // LDS rows per wave-instruction
+  static constexpr int EPC = 16 / ES;             // elements per 16-B chunk (8 bf16, 16 fp8)
   static_assert(NI >= 1 && (MC || NI % 2 == 0), "KC chunk pattern repeats with period 2 in j");
-  const bf16_t* base;
+  static_assert(ES == 2 || !MC, "fp8 operands are K-contiguous");
+  const char* base;  // element offsets below are scaled by ES
   long long ld;
   SnConvGeom g;
   int coff;
@@ -125,10 +130,10 @@ struct GStager {
     ld = op.ld;
     g = op.g;
     if (MODE != OP_IM2COL) {
-      base = op.ptr + (long long)grp * op.gstride;
+      base = reinterpret_cast<const char*>(op.ptr) + (long long)grp * op.gstride * ES;
       coff = 0;
     } else {
-      base = op.ptr;
+      base = reinterpret_cast<const char*>(op.ptr);
       coff = (int)(grp * op.gstride);
     }
     invKg = MODE == OP_FLIPW ? 1.f / (float)g.C : 0.f;
@@ -165,7 +170,7 @@ struct GStager {
   // The DMA is issued from inline asm so the compiler's wait-count pass does not see an
   // LDS write it cannot disambiguate (it would drain vmcnt(0) before the next ds_read);
   // every wait on these DMAs is explicit in the K-loop (counted vmcnt + barrier).
-  SN_DEV void dma(const bf16_t* src, bool valid, char* lds) {
+  SN_DEV void dma(const char* src, bool valid, char* lds) {
     const void* s = valid ? (const void*)src : (const void*)g_zero16;
     const uint32_t m0 = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(s) : "memory");
@@ -178,20 +183,20 @@ struct GStager {
       if (MODE == OP_DENSE) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          int row = tile_rc0 + rr[j], k = k_tile + ch[j] * 8;
-          dma(base + (long long)row * ld + k, row < rc_lim && k < k_lim, dst + j * 1024);
+          int row = tile_rc0 + rr[j], k = k_tile + ch[j] * EPC;
+          dma(base + ((long long)row * ld + k) * ES, row < rc_lim && k < k_lim, dst + j * 1024);
         }
       } else {
         // k = (tap, c), c innermost.  k_tile is wave-uniform: decode it once on the scalar
-        // unit, then each lane adds its chunk (< 64 channels), which crosses at most one
-        // tap boundary when Cg >= 64 — no per-lane division on the fast path.
+        // unit, then each lane adds its chunk (< 8*EPC channels), which crosses at most one
+        // tap boundary when Cg >= 8*EPC — no per-lane division on the fast path.
         const int tap0 = k_tile / g.Cg, c0 = k_tile - tap0 * g.Cg;
         const int r0 = tap0 / g.S, s0 = tap0 - r0 * g.S;
         int kv[2], dh[2], dw[2], toff[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-          int c = c0 + ch[e] * 8, r = r0, s = s0;
-          if (g.Cg >= 64) {
+          int c = c0 + ch[e] * EPC, r = r0, s = s0;
+          if (g.Cg >= 8 * EPC) {
             if (c >= g.Cg) {
               c -= g.Cg;
               s += 1;
@@ -201,13 +206,13 @@ struct GStager {
               }
             }
           } else {
-            const int kk = k_tile + ch[e] * 8;
+            const int kk = k_tile + ch[e] * EPC;
             const int tap = fdiv(kk, g.Cg, invCg);
             c = kk - tap * g.Cg;
             r = fdiv(tap, g.S, invS);
             s = tap - r * g.S;
           }
-          kv[e] = k_tile + ch[e] * 8 < k_lim;
+          kv[e] = k_tile + ch[e] * EPC < k_lim;
           dh[e] = r * g.dh;
           dw[e] = s * g.dw;
           toff[e] = (dh[e] * g.W + dw[e]) * g.C + c;
@@ -217,7 +222,7 @@ struct GStager {
           const int e = j & 1;
           const int h = ph[j] + dh[e], w = pw[j] + dw[e];
           const bool v = kv[e] && pv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          dma(base + (rowoff[j] + toff[e]), v, dst + j * 1024);
+          dma(base + (long long)(rowoff[j] + toff[e]) * ES, v, dst + j * 1024);
         }
       }
     } else {
@@ -225,7 +230,7 @@ struct GStager {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           int k = k_tile + rr[j], col = tile_rc0 + ch[j] * 8;
-          dma(base + (long long)k * ld + col, k < k_lim && col < rc_lim, dst + j * 1024);
+          dma(base + ((long long)k * ld + col) * 2, k < k_lim && col < rc_lim, dst + j * 1024);
         }
       } else if (MODE == OP_FLIPW) {
         const int RS = g.R * g.S;
@@ -236,7 +241,7 @@ struct GStager {
           int tap = fdiv(k, g.C, invKg), kout = k - tap * g.C;
           bool v = k < k_lim && col < rc_lim;
           long long off = v ? (long long)kout * rowlen + (long long)(RS - 1 - tap) * g.Cg + col : 0;
-          dma(base + off, v, dst + j * 1024);
+          dma(base + off * 2, v, dst + j * 1024);
         }
       } else {
         const int PQ = g.P * g.Q;
@@ -249,7 +254,7 @@ struct GStager {
           int w = q * g.sw - g.pw + cs[j] * g.dw;
           bool v = cv[j] && pix < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
           long long off = ((long long)(n * g.H + h) * g.W + w) * g.C + coff + cc[j];
-          dma(base + off, v, dst + j * 1024);
+          dma(base + off * 2, v, dst + j * 1024);
         }
       }
     }
@@ -292,9 +297,22 @@ constexpr int waitcnt_vm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n 
 //           only and uses a raw s_barrier (no fence), so the DMA of tile k+1 keeps
 //           flying across the barrier while tile k+2 is issued (cdna_hip_programming
 //           "Pipelining across barriers").
-template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS>
+// fp8 (e4m3) fragment of a 16-row subtile for v_mfma_scale_f32_16x16x128_f8f6f4: lane l
+// holds X[x0 + (l&15)][32(l>>4) + j], j = 0..31 — two 16-B chunks of the 128-B KC row.
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+SN_DEV i32x8 read_frag8(const char* lds, int x0, int lane) {
+  const int row = x0 + (lane & 15), kc = 2 * (lane >> 4);
+  const uint4 v0 = *reinterpret_cast<const uint4*>(lds + kc_off(row, kc));
+  const uint4 v1 = *reinterpret_cast<const uint4*>(lds + kc_off(row, kc + 1));
+  i32x8 r = {(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+  return r;
+}
+
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, bool FP8 = false>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmArgs args) {
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
+  constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   constexpr int WN = BN / 64, WM = NW / WN;  // waves along N / M (64x64 per wave)
   static_assert(WM * 64 == BM && WM * WN == NW, "tile/wave layout mismatch");
   static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
@@ -322,8 +340,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   const int k1 = min(args.K, k0 + args.kchunk);
 
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  using SA = GStager<AMC, AMODE, BM, NW>;
-  using SB = GStager<BMC, BMODE, BN, NW>;
+  using SA = GStager<AMC, AMODE, BM, NW, ES>;
+  using SB = GStager<BMC, BMODE, BN, NW, ES>;
   SA sa;
   SB sb;
   sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M);
@@ -336,10 +354,26 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int wm0 = (wave % WM) * 64, wn0 = (wave / WM) * 64;
-  const int nk = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
+  const int nk = k1 > k0 ? (k1 - k0 + BKE - 1) / BKE : 0;
 
   auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
+    if constexpr (FP8) {
+      i32x8 fa8[4], fb8[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fb8[i] = read_frag8(lb, wn0 + 16 * i, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa8[i] = read_frag8(la, wm0 + 16 * i, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)  // formats 0/0 = e4m3 x e4m3, block scales 2^0 (E8M0 127)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa8[j], acc[i][j], 0, 0, 0, 127, 0,
+                                                                        127);
+      __builtin_amdgcn_s_setprio(0);
+      return;
+    }
     bf16x8_t fa[2][4], fb[2][4];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -359,8 +393,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
     __builtin_amdgcn_s_setprio(0);
   };
   auto issue = [&](char* st, int kt) {
-    sa.issue(st, wv, k0 + kt * BK, k1, m_blk, args.M);
-    sb.issue(st + A_BYTES, wv, k0 + kt * BK, k1, n_blk, args.N);
+    sa.issue(st, wv, k0 + kt * BKE, k1, m_blk, args.M);
+    sb.issue(st + A_BYTES, wv, k0 + kt * BKE, k1, n_blk, args.N);
   };
   if (NS == 2) {
     // One barrier per K-step: retire this wave's DMA of tile kt, barrier (all waves' DMAs
@@ -412,6 +446,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
       if (n >= args.N) continue;
       const bool full = (n + 3 < args.N) && ((args.ldc & 3) == 0);
       f32x4 v = acc[i][j];
+      if (FP8) v = v * (args.deq_a[0] * args.deq_b[0]);  // per-tensor fp8 scales
       if (EPI == EPI_BF16) {
         bf16_t* C = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride + (long long)m * args.ldc;
         float o[4] = {v[0], v[1], v[2], v[3]};
@@ -515,11 +550,34 @@ int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
   return 4;
 }
 
+template <int AMODE>
+int launch_fp8(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
+  switch (a.epi) {
+    case EPI_BF16:
+      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_BF16, 128, 128, 4, 2, true>), grid, dim3(256), 0, st, a);
+      break;
+    case EPI_F32:
+      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_F32, 128, 128, 4, 2, true>), grid, dim3(256), 0, st, a);
+      break;
+    default:
+      return 2;
+  }
+  return SN_CHECK_LAUNCH();
+}
+
 }  // namespace
 
 extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   const SnGemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
+  if (a.fp8) {
+    // e4m3 forward products: A (dense or implicit im2col) and B dense, both K-contiguous
+    if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || a.a_mc || a.b_mc || a.b_mode != OP_DENSE || !a.deq_a || !a.deq_b)
+      return 3;
+    const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
+    dim3 grid(tiles, a.splits, a.groups);
+    return a.a_mode == OP_IM2COL ? launch_fp8<OP_IM2COL>(a, grid, stream) : launch_fp8<OP_DENSE>(a, grid, stream);
+  }
   if (a.kchunk <= 0 || (a.kchunk % BK) != 0) return 3;
   switch (a.tile) {
     case 1: return launch_tile<256, 64, 4, 2>(a, stream);    // skinny N

@@ -77,20 +77,26 @@ class FlipW:
     Cg: int
 
 
-def _operand(op) -> tuple[_lib.SnOperand, int, int]:
+FP8 = torch.uint8  # e4m3 bytes (torch.float8_e4m3fn tensors are viewed as uint8)
+
+
+def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
+    elt = FP8 if fp8 else torch.bfloat16
     if isinstance(op, FlipW):
         assert op.w.dtype == torch.bfloat16 and op.w.is_contiguous() and op.Cg % 8 == 0
         g = _lib.SnConvGeom(0, 0, 0, op.Kg, 1, 1, op.R, op.S, 1, 1, 0, 0, 1, 1, op.Cg)
         s = _lib.SnOperand(op.w.data_ptr(), 0, op.Kg * op.R * op.S * op.Cg, g)
         return s, 1, OP_FLIPW
     if isinstance(op, Dense):
-        assert op.t.dtype == torch.bfloat16, op.t.dtype
-        assert op.t.data_ptr() % 16 == 0 and op.ld % 8 == 0, "dense operand must be 16-B aligned"
+        assert op.t.dtype == elt, (op.t.dtype, elt)
+        assert op.t.data_ptr() % 16 == 0 and (op.ld * op.t.element_size()) % 16 == 0, \
+            "dense operand must be 16-B aligned"
         s = _lib.SnOperand(op.t.data_ptr(), op.ld, op.gstride, _lib.SnConvGeom())
         return s, 0 if op.kcontig else 1, OP_DENSE
-    assert op.x.dtype == torch.bfloat16 and op.x.is_contiguous()
+    assert op.x.dtype == elt and op.x.is_contiguous()
     g = op.geom
-    assert g.Cg % 8 == 0 and g.C % 8 == 0, "implicit conv needs channels % 8 == 0"
+    cm = 16 if fp8 else 8
+    assert g.Cg % cm == 0 and g.C % cm == 0, f"implicit conv needs channels % {cm} == 0"
     # the kernel's fp32-reciprocal index division is exact below 2^24
     assert g.N * g.P * g.Q < (1 << 24) and g.N * g.H * g.W < (1 << 24), "conv too large for one launch"
     assert op.x.numel() < (1 << 31), "implicit conv uses 32-bit element offsets"
@@ -144,21 +150,27 @@ def choose_splits(M: int, N: int, K: int, groups: int = 1, tile: int = 0) -> tup
 
 def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
          groups: int = 1, c_gstride: int = 0, bias: torch.Tensor | None = None, relu: bool = False,
-         splits: int | None = None, gate: torch.Tensor | None = None) -> None:
+         splits: int | None = None, gate: torch.Tensor | None = None,
+         deq: tuple[torch.Tensor, torch.Tensor] | None = None) -> None:
     """Run one (possibly grouped, split-K) GEMM.  ``epi``: EPI_BF16 (store bf16 with
     bias/ReLU; ``gate``: a bf16 tensor laid out like ``out`` — outputs where gate <= 0
     are zeroed, i.e. a following slope-0 ReLU's backward), EPI_F32 (store), EPI_F32_ACC
     (accumulate into an fp32 output)."""
     if M == 0 or N == 0:
         return
-    sa, a_mc, a_mode = _operand(A)
-    sb, b_mc, b_mode = _operand(B)
-    tile = choose_tile(M, N) if _FORCE_TILE < 0 else _FORCE_TILE
+    fp8 = deq is not None  # e4m3 operands; deq = (1/scale_A, 1/scale_B) device scalars
+    sa, a_mc, a_mode = _operand(A, fp8)
+    sb, b_mc, b_mode = _operand(B, fp8)
+    tile = 0 if fp8 else (choose_tile(M, N) if _FORCE_TILE < 0 else _FORCE_TILE)
+    bk = 128 if fp8 else BK
     if splits is None:
-        splits, kchunk = choose_splits(M, N, K, groups, tile)
+        # the fp8 k-step covers 128 elements in the time a bf16 one covers 64: same model
+        splits, kchunk = choose_splits(M, N, K * BK // bk, groups, tile)
+        kchunk = kchunk * bk // BK
     else:
-        kchunk = -(-(-(-K // splits)) // BK) * BK
-        splits = max(1, -(-K // kchunk))
+        kchunk = -(-(-(-K // splits)) // bk) * bk
+    splits = max(1, -(-K // kchunk))
+    dq = (deq[0].data_ptr(), deq[1].data_ptr()) if fp8 else (0, 0)
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     gp = 0
@@ -166,16 +178,16 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         assert epi == EPI_BF16 and gate.dtype == torch.bfloat16
         gp = gate.data_ptr()
     if splits == 1:
-        args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, BK), a_mc, a_mode, b_mc, b_mode, epi,
+        args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, epi,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
-                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp)
+                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq)
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
         return
     ws = torch.empty((groups, splits, M, N), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
-                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0, tile, 0)
+                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0, tile, 0, int(fp8), *dq)
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
     _lib.call("splitk_reduce", ws, splits, M * N, M, N, N, out, ldc, mode, bias, int(relu),

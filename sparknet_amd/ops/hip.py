@@ -463,3 +463,61 @@ def augment(src_u8, dst, crop, mean=None, mean_mode=0, scale=1.0, rng_state=None
     call("augment", _c(src_u8), dst, N, Cc, Hs, Ws, crop, crop, mean, int(mean_mode), float(scale), rng_state,
          int(train), int(mirror), offs_out)
     return dst
+
+
+# --------------------------------------------------------------------------------------
+# FP8 (e4m3) forward products with per-tensor delayed scaling
+# --------------------------------------------------------------------------------------
+
+FP8_MARGIN = 1.0  # quantisation scale = 448 / (amax * margin)
+
+
+class Fp8Scales:
+    """Device-resident scale slots (csrc/kernels/fp8.hip): [n][scale, amax, 1/scale, -]."""
+
+    def __init__(self, n: int, device):
+        self.slots = torch.zeros((max(n, 1), 4), dtype=torch.float32, device=device)
+        self.slots[:, 0] = 1.0
+        self.slots[:, 2] = 1.0
+        self.n = n
+
+    def slot(self, i: int) -> torch.Tensor:
+        return self.slots[i]
+
+    def deq(self, i: int) -> torch.Tensor:
+        return self.slots[i, 2:3]
+
+    def update(self) -> None:
+        call("fp8_update_scales", self.slots, self.n, float(FP8_MARGIN))
+
+
+def quant_fp8(x: torch.Tensor, slot: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """e4m3 bytes of bf16 ``x`` scaled by slot[0]; folds |x|max into slot[1]."""
+    x = _c(x)
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device) if out is None else out
+    call("quant_fp8", x, q, x.numel(), slot)
+    return q
+
+
+def conv_forward_fp8(xq, wq, b, s: ConvSpec, deq_x, deq_w, relu=False):
+    """Implicit-GEMM convolution on e4m3 operands (v_mfma_scale_f32_16x16x128_f8f6f4),
+    fp32 accumulation, dequantised + bias + ReLU epilogue, bf16 NHWC output."""
+    assert s.Cg % 16 == 0 and s.C % 16 == 0 and xq.dtype == torch.uint8 and wq.dtype == torch.uint8
+    M = s.N * s.P * s.Q
+    kred = s.R * s.S * s.Cg
+    y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=xq.device)
+    A = Im2col(xq, _geom(s), kcontig=True, gstride=s.Cg)
+    B = Dense(wq.view(s.K, kred), kred, True, gstride=s.Kg * kred)
+    gemm(M, s.Kg, kred, A, B, y, s.K, epi=EPI_BF16, groups=s.groups, c_gstride=s.Kg, bias=b, relu=relu,
+         deq=(deq_x, deq_w))
+    return y
+
+
+def linear_forward_fp8(xq, wq, b, deq_x, deq_w, relu=False):
+    M, K = xq.shape
+    N = wq.shape[0]
+    assert K % 16 == 0
+    y = torch.empty((M, N), dtype=BF16, device=xq.device)
+    gemm(M, N, K, Dense(xq, K, True), Dense(wq, K, True), y, N, epi=EPI_BF16, bias=b, relu=relu,
+         deq=(deq_x, deq_w))
+    return y

@@ -88,3 +88,54 @@ def test_linear_dgrad_gate(gpu):
     gate = _bf(256, 384, device=gpu)
     dx = gemm.linear_dgrad(dy, w, gate=gate)
     _close(dx, (dy.float() @ w.float()) * (gate.float() > 0))
+
+
+def _f8(t):
+    """bf16/float tensor -> (e4m3 bytes as uint8, dequantised float) via torch's OCP e4m3."""
+    q = t.float().clamp(-448, 448).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), q.float()
+
+
+def test_quant_fp8_matches_torch(gpu):
+    from sparknet_amd.ops import hip
+    x = (torch.randn(64, 48, device=gpu) * 3).to(torch.bfloat16)
+    sc = hip.Fp8Scales(1, gpu)
+    sc.slots[0, 0] = 20.0
+    q = hip.quant_fp8(x, sc.slot(0))
+    ref, _ = _f8(x.float() * 20.0)
+    mism = (q != ref).float().mean().item()
+    assert mism < 1e-3, mism  # identical rounding (RNE) up to rare ties
+    assert abs(sc.slots[0, 1].item() - x.float().abs().max().item()) < 1e-6
+    sc.update()
+    assert abs(sc.slots[0, 0].item() - 448.0 / x.float().abs().max().item()) < 1e-3
+    assert sc.slots[0, 1].item() == 0.0
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (300, 200, 384), (128, 1000, 4096 + 128)])
+def test_fp8_dense_gemm(gpu, M, N, K):
+    """e4m3 x e4m3 -> fp32 on the scaled MFMA: exact products of representable values."""
+    from sparknet_amd.ops import hip
+    aq, af = _f8(torch.randn(M, K, device=gpu) * 8)
+    bq, bf = _f8(torch.randn(N, K, device=gpu) * 8)
+    da = torch.tensor([0.125], device=gpu)
+    db = torch.tensor([0.25], device=gpu)
+    bias = torch.randn(N, device=gpu)
+    y = hip.linear_forward_fp8(aq, bq, bias, da, db, relu=True)
+    ref = torch.relu(af @ bf.t() * (0.125 * 0.25) + bias)
+    _close(y, ref, 1e-2)
+
+
+@pytest.mark.parametrize("case", [(2, 13, 13, 32, 48, 3, 3, 1, 1, 1), (2, 9, 9, 64, 32, 3, 3, 1, 1, 2),
+                                  (2, 14, 14, 256, 128, 3, 3, 1, 1, 1)])
+def test_fp8_conv_forward(gpu, case):
+    from sparknet_amd.ops import hip
+    from sparknet_amd.ops.spec import ConvSpec
+    import torch.nn.functional as F
+    N, H, W, Cc, K, R, S, st, pd, g = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    xq, xf = _f8(torch.randn(N, H, W, Cc, device=gpu) * 4)
+    wq, wf = _f8(torch.randn(K, R, S, Cc // g, device=gpu) * 4)
+    dx, dw = torch.tensor([0.5], device=gpu), torch.tensor([0.0625], device=gpu)
+    y = hip.conv_forward_fp8(xq, wq, None, s, dx, dw)
+    ref = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), stride=st, padding=pd, groups=g) * (0.5 * 0.0625)
+    _close(y.permute(0, 3, 1, 2), ref, 1e-2)
