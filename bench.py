@@ -33,6 +33,8 @@ def parse():
     p.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the model's train batch)")
     p.add_argument("--tau", type=int, default=50)
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                   help="fp8: e4m3 forward products with per-tensor delayed scaling (bf16 backward)")
     p.add_argument("--overlap-update", action="store_true",
                    help="run large layers' solver updates on a side stream during backward")
     p.add_argument("--profile-steps", type=int, default=0)
@@ -63,7 +65,7 @@ def main():
     from sparknet_amd import models
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.data.prefetch import DeviceFeeder, SyntheticSource
-    from sparknet_amd.engine import LocalSGDTrainer, fuse_input_fold, fuse_relu
+    from sparknet_amd.engine import LocalSGDTrainer, enable_fp8, fuse_input_fold, fuse_relu
     from sparknet_amd.ops import _lib
     from sparknet_amd.parallel import Comm
 
@@ -82,6 +84,7 @@ def main():
     feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
                           scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev)
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
+    n_fp8 = enable_fp8(net) if args.dtype == "fp8" else 0
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph,
                               overlap_update=args.overlap_update)
     trainer.broadcast_initial()
@@ -125,7 +128,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / BASELINE_IMG_S, 2) if args.model in HEADLINE else None,
-            "dtype": "bf16",
+            "dtype": "fp8" if n_fp8 else "bf16",
             "data": "synthetic (uint8 256x256 -> on-device random crop/mirror/mean), random-init weights",
             "config": {
                 "model": f"{args.model} (bvlc_reference_caffenet / AlexNet)" if args.model == "caffenet"
@@ -135,7 +138,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
-                "hipgraph": not args.no_graph, "fused_input_fold": fused_fold,
+                "hipgraph": not args.no_graph, "fused_input_fold": fused_fold, "fp8_layers": n_fp8,
                 "final_loss": round(final_loss, 4),
             },
         }

@@ -33,6 +33,8 @@ def base_parser(desc: str, **defaults) -> argparse.ArgumentParser:
     p.add_argument("--sync-sgd", action="store_true", help="all-reduce gradients every step (tau=1 semantics)")
     p.add_argument("--log-dir", default=None)
     p.add_argument("--fail-at-round", type=int, default=-1, help="fault injection: rank 0 exits at round r")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                   help="GPU compute: bf16, or fp8 (e4m3 forward products, bf16 backward, fp32 masters)")
     p.add_argument("--native-loader", action=argparse.BooleanOptionalAction, default=True,
                    help="file-backed datasets go through the C++ loader (csrc/runtime/loader.cpp)")
     return p

@@ -90,6 +90,11 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
         fuse_relu(solver.net)
         for tn in solver.test_nets:
             fuse_relu(tn)
+        if getattr(args, "dtype", "bf16") == "fp8":
+            from ..engine import enable_fp8
+            log_fp8 = enable_fp8(solver.net)
+        else:
+            log_fp8 = 0
     if args.weights:
         solver.net.copy_trained_layers_from(args.weights)
     start_round = 0
@@ -126,7 +131,8 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
         trainer.broadcast_initial()
     trainer.round = start_round
     stop = StopFlag()
-    log.log(f"{model}: {world} worker(s), batch {args.batch}, tau {args.tau}, device {dev}")
+    log.log(f"{model}: {world} worker(s), batch {args.batch}, tau {args.tau}, device {dev}"
+            + (f", fp8 forward in {log_fp8} layers" if dev.type == "cuda" and log_fp8 else ""))
     for r in range(start_round, args.rounds):
         if args.test_every and r % args.test_every == 0:
             scores, names, total = evaluate(solver, tfeeder, n_test, comm)

@@ -43,6 +43,8 @@ class NetContext:
     # flat offsets of params whose gradient buffer was NOT cleared (lazy clear): the first
     # backward contribution overwrites instead of accumulating (Layer.grad_overwrite)
     stale_diffs: set = field(default_factory=set)
+    # fp8 forward products (engine.enable_fp8): ops.hip.Fp8Scales shared by the net's layers
+    fp8: object = None
 
     def next_stream_id(self) -> int:
         self.layer_counter += 1

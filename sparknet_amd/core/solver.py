@@ -252,6 +252,8 @@ class Solver:
             from .. import ops
             ops.advance_rng(net.ctx.rng_state)
         net.finish_param_diffs()
+        if getattr(net.ctx, "fp8", None) is not None:
+            net.ctx.fp8.update()
         if self.param.iter_size > 1:
             loss = loss / self.param.iter_size
         for cb in self.callbacks:

@@ -114,6 +114,35 @@ def fuse_input_fold(net, feeder) -> bool:
     return True
 
 
+def enable_fp8(net) -> int:
+    """Run the forward products of eligible Convolution / InnerProduct layers in OCP e4m3
+    (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation) with per-tensor delayed
+    scaling: each layer quantises its input and weights with the scale derived from the
+    previous iteration's amax (ops.hip.Fp8Scales; updated once per iteration by
+    :func:`fp8_step`).  Gradients, masters and checkpoints stay bf16 / fp32.  Layers whose
+    channels are not multiples of 16 (e.g. an RGB input conv) stay bf16.  GPU only;
+    returns the number of fp8 layers."""
+    if net.device.type != "cuda":
+        return 0
+    from .ops import hip
+    chosen = []
+    for li, layer in enumerate(net.layers):
+        if layer.type_name in ("Convolution", "InnerProduct") and len(net.bottom_vecs[li]) == 1:
+            if layer.fp8_eligible(net.bottom_vecs[li][0]):
+                chosen.append(layer)
+    sc = hip.Fp8Scales(2 * len(chosen), net.device)
+    for i, layer in enumerate(chosen):
+        layer.fp8_slots = (2 * i, 2 * i + 1)
+    net.ctx.fp8 = sc if chosen else None
+    return len(chosen)
+
+
+def fp8_step(net) -> None:
+    """Per-iteration amax -> scale update of an fp8-enabled net (one small launch)."""
+    if getattr(net.ctx, "fp8", None) is not None:
+        net.ctx.fp8.update()
+
+
 class OverlappedUpdate:
     """Runs each layer's fused solver update on a side stream as soon as backward has
     produced that layer's final gradients, so the bandwidth-bound update (CaffeNet: 61 M
@@ -176,6 +205,7 @@ class GraphStep:
             self.overlap.begin()
         loss = net.forward_backward()
         net.finish_param_diffs()
+        fp8_step(net)
         ops.advance_rng(net.ctx.rng_state)
         if self.overlap is not None:
             self.overlap.end()

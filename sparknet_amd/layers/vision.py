@@ -95,8 +95,27 @@ class ConvolutionLayer(Layer):
         self._ws = [{} for _ in bottoms]  # forward -> backward scratch (e.g. folded input)
         for i, (b, t) in enumerate(zip(bottoms, tops)):
             s = self.spec(b)
+            if self.fp8_slots is not None and b.data.is_cuda:
+                t.data = self._forward_fp8(b.data, w, bias, s)
+                continue
             folded = self.folded_input if i == 0 else None
             t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i], folded=folded)
+
+    fp8_slots = None  # (x slot, w slot) in ctx.fp8 when the forward product runs in e4m3
+
+    def fp8_eligible(self, b) -> bool:
+        s = self.spec(b)
+        return s.C % 16 == 0 and s.Cg % 16 == 0 and s.dh == 1 and s.dw == 1
+
+    def _forward_fp8(self, x, w, bias, s):
+        """e4m3 forward product (delayed per-tensor scales); backward stays bf16 on the
+        bf16 activations and weights (fp32 masters are untouched)."""
+        from ..ops import hip
+        sc = self.ctx.fp8
+        ix, iw = self.fp8_slots
+        xq = hip.quant_fp8(x, sc.slot(ix))
+        wq = hip.quant_fp8(w, sc.slot(iw))
+        return hip.conv_forward_fp8(xq, wq, bias, s, sc.deq(ix), sc.deq(iw), relu=self.fuse_relu)
 
     supports_grad_overwrite = True
 
@@ -324,8 +343,21 @@ class InnerProductLayer(Layer):
         M = b.count_range(0, self.axis)
         x2 = b.data.reshape(M, self.Kdim)
         bias = self.bias.data if self.bias is not None else None
-        y = ops.linear_forward(x2, self.weight.compute, bias, self.fuse_relu)
+        if self.fp8_slots is not None and x2.is_cuda:
+            from ..ops import hip
+            sc = self.ctx.fp8
+            ix, iw = self.fp8_slots
+            xq = hip.quant_fp8(x2, sc.slot(ix))
+            wq = hip.quant_fp8(self.weight.compute, sc.slot(iw))
+            y = hip.linear_forward_fp8(xq, wq, bias, sc.deq(ix), sc.deq(iw), relu=self.fuse_relu)
+        else:
+            y = ops.linear_forward(x2, self.weight.compute, bias, self.fuse_relu)
         tops[0].data = y.reshape(tops[0].data.shape)
+
+    fp8_slots = None
+
+    def fp8_eligible(self, b) -> bool:
+        return self.Kdim % 16 == 0
 
     def backward(self, tops, propagate_down, bottoms):
         b = bottoms[0]

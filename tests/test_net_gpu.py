@@ -2,6 +2,8 @@
 the fp32 CPU engine on the same weights and inputs, and fused-vs-unfused graph passes.
 Reference analogue: Caffe's layer tests run every layer on CPU and GPU with the CPU as
 oracle (caffe/src/caffe/test/test_*_layer.cpp); here the whole net is compared."""
+import math
+
 import pytest
 import torch
 
@@ -100,3 +102,32 @@ def test_training_is_bitwise_deterministic(gpu):
     b, _ = _graph_solver(False)
     assert torch.equal(a.net.flat_data, b.net.flat_data)
     assert torch.equal(a.history[0], b.history[0])
+
+
+def test_fp8_forward_training(gpu):
+    """enable_fp8: e4m3 forward products with delayed scaling track the bf16 net and train."""
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.engine import GraphStep, enable_fp8, fuse_relu
+    net_p = models.vgg16(train_batch=4, test_batch=4, crop=32, classes=10)
+    losses = {}
+    for mode in ("bf16", "fp8"):
+        sp = models.zoo.vgg16_solver(net_p)
+        sp.base_lr = 0.002
+        solver = Solver(sp, device=torch.device("cuda:0"), seed=5, build_test_nets=False)
+        fuse_relu(solver.net)
+        if mode == "fp8":
+            assert enable_fp8(solver.net) >= 14  # 12 of 13 convs (not the RGB input) + 3 IPs
+        g = torch.Generator().manual_seed(2)
+        x = torch.randn(4, 3, 32, 32, generator=g) * 0.5
+        y = torch.tensor([[1.0], [3.0], [5.0], [7.0]])
+
+        def pre():
+            solver.net.blob_by_name("data").set_nchw(x)
+            solver.net.blob_by_name("label").set_nchw(y)
+        st = GraphStep(solver, warmup=2, pre=pre, overlap=False)
+        seq = [float(st.step()) for _ in range(12)]
+        losses[mode] = seq
+        assert all(math.isfinite(v) for v in seq), seq
+    # same data every step: both must fit it; fp8 stays close to bf16
+    assert losses["fp8"][-1] < losses["fp8"][0]
+    assert abs(losses["fp8"][0] - losses["bf16"][0]) < 0.05 * abs(losses["bf16"][0]) + 0.05
