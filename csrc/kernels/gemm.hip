@@ -73,6 +73,7 @@ struct SnGemmArgs {
   int fp8;            // operands are e4m3 bytes (K-contiguous only); k counts fp8 elements
   const float* deq_a; // fp8: dequantisation factors (1 / quantisation scale) of A and B, device scalars
   const float* deq_b;
+  int raster_n;       // N-fastest tile order (see gemm_kernel)
 };
 
 }  // extern "C"
@@ -333,7 +334,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
     int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
     bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   }
-  const int tm = bid % tiles_m, tn = bid / tiles_m;
+  // raster: M-fastest by default; N-fastest (args.raster_n) when a few N tiles share a tall A
+  // panel (conv fwd / dgrad: pixels x channels) so its N tiles run together and the panel
+  // is read from HBM once and from L2 for the others.
+  const int tiles_n = (args.N + BN - 1) / BN;
+  const int tm = args.raster_n ? bid / tiles_n : bid % tiles_m;
+  const int tn = args.raster_n ? bid % tiles_n : bid / tiles_m;
   const int m_blk = tm * BM, n_blk = tn * BN;
   const int split = blockIdx.y, grp = blockIdx.z;
   const int k0 = split * args.kchunk;

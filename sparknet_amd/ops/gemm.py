@@ -106,6 +106,7 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256)}
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
+_RASTER_N = int(os.environ.get("SN_GEMM_RASTER_N", "-1"))  # -1: heuristic
 
 
 def choose_tile(M: int, N: int) -> int:
@@ -171,6 +172,9 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         kchunk = -(-(-(-K // splits)) // bk) * bk
     splits = max(1, -(-K // kchunk))
     dq = (deq[0].data_ptr(), deq[1].data_ptr()) if fp8 else (0, 0)
+    bm, bn = TILES[tile]
+    tm_, tn_ = -(-M // bm), -(-N // bn)
+    raster = int(_RASTER_N if _RASTER_N >= 0 else (1 < tn_ <= 8 and tm_ >= 8 * tn_))
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     gp = 0
@@ -180,14 +184,14 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
     if splits == 1:
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, epi,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
-                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq)
+                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster)
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
         return
     ws = torch.empty((groups, splits, M, N), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
-                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0, tile, 0, int(fp8), *dq)
+                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0, tile, 0, int(fp8), *dq, raster)
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
     _lib.call("splitk_reduce", ws, splits, M * N, M, N, N, out, ldc, mode, bias, int(relu),
