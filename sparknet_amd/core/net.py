@@ -609,9 +609,62 @@ class Net:
                     bp.diff.extend(p.to_caffe(p.diff).cpu().reshape(-1).tolist())
         return net
 
+    def to_hdf5(self, path: str, write_diff: bool = False) -> None:
+        """Net::ToHDF5 (net.cpp:926-980): ``data/<layer>/<i>`` for params that own
+        themselves, ``diff/<layer>/<i>`` for every param when ``write_diff``."""
+        from ..utils import hdf5
+        net_pid = {lj: i for i, lj in enumerate(self.param_layer_indices)}
+        data, diff = {}, {}
+        for li, layer in enumerate(self.layers):
+            if layer.type_name == "Split" and layer.lp.name.endswith("_split"):
+                continue
+            ld, lg = {}, {}
+            for j, p in enumerate(layer.params):
+                if self.param_owners[net_pid[(li, j)]] == -1:
+                    ld[str(j)] = p.to_caffe().float().cpu().numpy()
+                if write_diff:
+                    lg[str(j)] = p.to_caffe(p.diff).float().cpu().numpy()
+            data[layer.name] = ld
+            if write_diff:
+                diff[layer.name] = lg
+        tree = {"data": data}
+        if write_diff:
+            tree["diff"] = diff
+        hdf5.write(path, tree)
+
+    def copy_trained_layers_from_hdf5(self, path: str) -> None:
+        """Net::CopyTrainedLayersFromHDF5 (net.cpp:861-908)."""
+        from ..utils import hdf5
+        f = hdf5.File(path)
+        data = f["data"]
+        for lname in data.keys():
+            if lname not in self.layer_names_index:
+                log.info("Ignoring source layer %s", lname)
+                continue
+            li = self.layer_names_index[lname]
+            layer = self.layers[li]
+            src = data[lname]
+            if len(src) > len(layer.params):
+                raise ValueError(f"Incompatible number of blobs for layer {lname!r}")
+            for j, p in enumerate(layer.params):
+                if str(j) not in src:
+                    if p.owner is not None:        # weight-shared in the target: fine
+                        continue
+                    raise ValueError(f"Incompatible number of blobs for layer {lname!r}")
+                t = torch.from_numpy(src[str(j)].read().astype("float32"))
+                if t.numel() != p.caffe_count:
+                    raise ValueError(f"Cannot copy param of layer {lname!r}; shape mismatch. "
+                                     f"Source {tuple(t.shape)}, target {p.caffe_shape}")
+                p.set_caffe(t.reshape(p.caffe_shape))
+        self.sync_compute()
+
     def copy_trained_layers_from(self, src) -> None:
-        """Net::CopyTrainedLayersFrom: match by layer name, fail on shape mismatch."""
+        """Net::CopyTrainedLayersFrom: match by layer name, fail on shape mismatch; a
+        ``.h5`` file name selects the HDF5 reader (net.cpp:842-858)."""
         if isinstance(src, str):
+            if src.endswith(".h5"):
+                self.copy_trained_layers_from_hdf5(src)
+                return
             src = proto.read_net(src)
         for slp in src.layer:
             if slp.name not in self.layer_names_index:

@@ -22,6 +22,7 @@ import os
 import time
 from typing import Callable
 
+import numpy as np
 import torch
 
 from .. import proto
@@ -333,48 +334,69 @@ class Solver:
         return self.param.snapshot_prefix or "snapshot"
 
     def snapshot(self, prefix: str | None = None) -> tuple[str, str]:
+        """Solver::Snapshot (solver.cpp:447-500): binaryproto pair by default, or
+        ``.caffemodel.h5`` / ``.solverstate.h5`` with ``snapshot_format: HDF5``."""
         prefix = prefix or self._prefix()
-        model = f"{prefix}_iter_{self.iter}.caffemodel"
-        state = f"{prefix}_iter_{self.iter}.solverstate"
+        h5 = self.param.HasField("snapshot_format") and self.param.snapshot_format == 0
+        ext = ".h5" if h5 else ""
+        model = f"{prefix}_iter_{self.iter}.caffemodel{ext}"
+        state = f"{prefix}_iter_{self.iter}.solverstate{ext}"
         d = os.path.dirname(model)
         if d:
             os.makedirs(d, exist_ok=True)
-        from ..utils.checkpoint import save_caffemodel
-        if self.param.HasField("snapshot_format") and self.param.snapshot_format == 0:
-            # HDF5 snapshots (sgd_solver.cpp:257-298) need h5py, which this environment
-            # lacks; the binaryproto pair holds the same state
-            log.warning("snapshot_format HDF5 is not available; writing binaryproto snapshots")
-        save_caffemodel(self.net, model, write_diff=self.param.snapshot_diff)
-        proto.write_binary(state, self.solver_state(model))
+        if h5:
+            self.net.to_hdf5(model, write_diff=self.param.snapshot_diff)
+            self._state_to_hdf5(state, model)
+        else:
+            from ..utils.checkpoint import save_caffemodel
+            save_caffemodel(self.net, model, write_diff=self.param.snapshot_diff)
+            proto.write_binary(state, self.solver_state(model))
         log.info("Snapshotting to %s / %s", model, state)
         return model, state
 
-    def solver_state(self, learned_net: str = ""):
-        st = proto.SolverState(iter=self.iter, learned_net=learned_net, current_step=self.current_step)
+    def _history_blobs(self):
+        """history_ in Caffe order and layout: one blob per (history slot, param)."""
         for h in self.history:
             for prm in self.net.learnable_params:
-                seg = h[prm.offset:prm.offset + prm.count].view(prm.shape)
-                bp = st.history.add()
-                bp.shape.dim.extend(prm.caffe_shape)
-                bp.data.extend(prm.to_caffe(seg).cpu().reshape(-1).tolist())
+                yield prm, h[prm.offset:prm.offset + prm.count].view(prm.shape)
+
+    def _state_to_hdf5(self, path: str, learned_net: str) -> None:
+        """SGDSolver::SnapshotSolverStateToHDF5 (sgd_solver.cpp:277-298)."""
+        from ..utils import hdf5
+        hist = {str(i): prm.to_caffe(seg).float().cpu().numpy()
+                for i, (prm, seg) in enumerate(self._history_blobs())}
+        hdf5.write(path, {"iter": np.array([self.iter], np.int32), "learned_net": learned_net,
+                          "current_step": np.array([self.current_step], np.int32), "history": hist})
+
+    def solver_state(self, learned_net: str = ""):
+        st = proto.SolverState(iter=self.iter, learned_net=learned_net, current_step=self.current_step)
+        for prm, seg in self._history_blobs():
+            bp = st.history.add()
+            bp.shape.dim.extend(prm.caffe_shape)
+            bp.data.extend(prm.to_caffe(seg).cpu().reshape(-1).tolist())
         return st
 
     def restore(self, state_file: str) -> None:
-        st = proto.read_binary(state_file, proto.SolverState)
-        self.iter = st.iter
-        self.current_step = st.current_step
-        if st.learned_net:
-            self.net.copy_trained_layers_from(st.learned_net)
-        params = self.net.learnable_params
-        if len(st.history) != len(params) * len(self.history):
+        """Solver::Restore (solver.cpp:509-518): ``.h5`` selects the HDF5 reader."""
+        if state_file.endswith(".h5"):
+            from ..utils import hdf5
+            f = hdf5.File(state_file)
+            self.iter = hdf5.read_int(f["iter"])
+            learned = hdf5.read_string(f["learned_net"]) if "learned_net" in f else ""
+            self.current_step = hdf5.read_int(f["current_step"])
+            hist = f["history"]
+            blobs = [torch.from_numpy(hist[str(i)].read().astype(np.float32)) for i in range(len(hist))]
+        else:
+            st = proto.read_binary(state_file, proto.SolverState)
+            self.iter, self.current_step, learned = st.iter, st.current_step, st.learned_net
+            blobs = [blob_proto_to_tensor(b) for b in st.history]
+        if learned:
+            self.net.copy_trained_layers_from(learned)
+        slots = list(self._history_blobs())
+        if len(blobs) != len(slots):
             raise ValueError("Incorrect length of history blobs.")
-        k = 0
-        for h in self.history:
-            for prm in params:
-                t = blob_proto_to_tensor(st.history[k])
-                h[prm.offset:prm.offset + prm.count].view(prm.shape).copy_(
-                    prm.from_caffe(t).to(h.device))
-                k += 1
+        for (prm, seg), t in zip(slots, blobs):
+            seg.copy_(prm.from_caffe(t).to(seg.device))
         log.info("Restored solver state from %s (iter %d)", state_file, self.iter)
 
     # -- SparkNet-facing helpers --------------------------------------------------------------

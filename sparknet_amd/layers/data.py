@@ -12,6 +12,8 @@
   are not available in this environment) with the DataTransformer semantics
   (crop / mirror / mean / scale).
 * ``ImageData``: image list file decoded with PIL.
+* ``HDF5Data`` / ``HDF5Output``: HDF5 files through the built-in codec
+  (:mod:`sparknet_amd.utils.hdf5`).
 """
 from __future__ import annotations
 
@@ -250,3 +252,112 @@ class ImageDataLayer(ExternalDataLayer):
             labels.append(lab)
         tops[0].set_nchw(torch.stack(imgs))
         tops[1].data.copy_(torch.tensor(labels, dtype=torch.float32))
+
+
+def _resolve_listed(path: str, list_file: str) -> str:
+    """File names in a list file are taken relative to the working directory (as Caffe
+    does); failing that, relative to the list file's directory, then its basename there."""
+    import os
+    if os.path.exists(path):
+        return path
+    base = os.path.dirname(os.path.abspath(list_file))
+    for cand in (os.path.join(base, path), os.path.join(base, os.path.basename(path))):
+        if os.path.exists(cand):
+            return cand
+    raise FileNotFoundError(f"HDF5 file {path!r} listed in {list_file!r} not found")
+
+
+@register("HDF5Data")
+class HDF5DataLayer(Layer):
+    """hdf5_data_layer.cpp:26-160: ``source`` lists HDF5 files; top i is the dataset
+    named like the top; rows are served in order (or shuffled, per file and per pass) and
+    files advance when one is exhausted.  Rows are gathered on the host and copied once
+    per batch."""
+    is_data = True
+    min_tops = 1
+
+    def layer_setup(self, bottoms, tops):
+        if self.lp.HasField("transform_param"):
+            raise ValueError(f"{self.type_name} does not transform data.")
+        p = self.lp.hdf5_data_param
+        with open(p.source) as f:
+            self.files = [_resolve_listed(tok, p.source) for tok in f.read().split()]
+        if not self.files:
+            raise ValueError(f"Must have at least 1 HDF5 filename listed in {p.source}")
+        self.batch = int(p.batch_size)
+        self.shuffle = bool(p.shuffle)
+        self.gen = torch.Generator().manual_seed(int(self.ctx.seed))
+        self.file_perm = self._perm(len(self.files))
+        self.cur_file = 0
+        self._load(self.files[self.file_perm[0]])
+        self.row = 0
+
+    def _perm(self, n):
+        return torch.randperm(n, generator=self.gen).tolist() if self.shuffle else list(range(n))
+
+    def _load(self, path):
+        from ..utils import hdf5
+        f = hdf5.File(path)
+        self.arrays = []
+        for name in self.lp.top:
+            a = f[name].read()
+            if a.ndim < 1:
+                raise ValueError(f"HDF5Data: dataset {name!r} must have at least 1 axis")
+            self.arrays.append(torch.from_numpy(a.astype("float32")))
+        n = self.arrays[0].shape[0]
+        for a in self.arrays[1:]:
+            if a.shape[0] != n:
+                raise ValueError("HDF5Data: all datasets must have the same number of rows")
+        self.data_perm = self._perm(n)
+
+    def reshape(self, bottoms, tops):
+        for t, a in zip(tops, self.arrays):
+            shape = (self.batch,) + tuple(a.shape[1:])
+            t.reshape(shape, self.dtype if len(shape) == 4 else torch.float32)
+
+    def forward(self, bottoms, tops):
+        parts = [[] for _ in tops]
+        for _ in range(self.batch):
+            if self.row == self.arrays[0].shape[0]:
+                if len(self.files) > 1:
+                    self.cur_file += 1
+                    if self.cur_file == len(self.files):
+                        self.cur_file = 0
+                        if self.shuffle:
+                            self.file_perm = self._perm(len(self.files))
+                    self._load(self.files[self.file_perm[self.cur_file]])
+                self.row = 0
+                if self.shuffle:
+                    self.data_perm = self._perm(self.arrays[0].shape[0])
+            r = self.data_perm[self.row]
+            for j in range(len(tops)):
+                parts[j].append(self.arrays[j][r])
+            self.row += 1
+        for t, rows in zip(tops, parts):
+            t.set_nchw(torch.stack(rows))
+
+    def backward(self, tops, propagate_down, bottoms):
+        pass
+
+
+@register("HDF5Output")
+class HDF5OutputLayer(Layer):
+    """hdf5_output_layer.cpp:15-60: writes bottom 0 as ``data`` and bottom 1 as ``label``
+    to ``file_name`` on every forward (the file holds the latest batch)."""
+    exact_bottoms = 2
+    exact_tops = 0
+
+    def layer_setup(self, bottoms, tops):
+        self.file_name = self.lp.hdf5_output_param.file_name
+
+    def reshape(self, bottoms, tops):
+        if bottoms[0].shape[0] != bottoms[1].shape[0]:
+            raise ValueError("data blob and label blob must have the same batch size")
+
+    def forward(self, bottoms, tops):
+        from ..utils import hdf5
+        arrs = [b.nchw().float().cpu().numpy() for b in bottoms]
+        hdf5.write(self.file_name, {"data": arrs[0], "label": arrs[1]})
+
+    def backward(self, tops, propagate_down, bottoms):
+        pass

@@ -36,6 +36,7 @@ def rows_view(blob, axis, diff=False):
 
 class LossLayer(Layer):
     is_loss = True
+    auto_top_blobs = True   # loss_layer.hpp: AutoTopBlobs() -> anonymous loss top
     min_bottoms = 2
     exact_tops = -1
     min_tops = 1

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import torch
 
-from .. import ops
+from .. import ops, proto
 from ..core.layer import Layer, register
 from ..ops.spec import POOL_AVE, POOL_MAX, POOL_STOCHASTIC, ConvSpec, PoolSpec
 
@@ -247,11 +247,17 @@ class PoolingLayer(Layer):
         s = self.spec(bottoms[0])
         x = bottoms[0].data
         if self.method == POOL_STOCHASTIC:
-            # Stochastic pooling: TEST = probability-weighted average (pooling_layer.cu:125-155);
-            # TRAIN sampling is approximated by the same expectation on this engine.
-            xf = x.float().clamp_min(0)
-            y = _stochastic_test(xf, s).to(x.dtype)
-            tops[0].data = y
+            if self.phase == proto.TRAIN:
+                # StoPoolForwardTrain (pooling_layer.cu:88-122): draw u ~ U[0,1) per output,
+                # take the first window element whose running sum reaches u * window sum
+                wins = ops.ref._pool_windows(x.float(), s, 0.0)
+                u = torch.rand(wins.shape[:4], generator=self.ctx.gen).to(wins.device)
+                csum = wins.cumsum(-1)
+                self.aux = (csum >= (u * csum[..., -1])[..., None]).to(torch.uint8).argmax(-1, keepdim=True)
+                tops[0].data = ops.ref.nhwc(wins.gather(-1, self.aux).squeeze(-1)).to(x.dtype)
+            else:
+                # StoPoolForwardTest (pooling_layer.cu:125-155): probability-weighted average
+                tops[0].data = _stochastic_test(x.float().clamp_min(0), s).to(x.dtype)
             return
         y, self.aux = ops.pool_forward_aux(x, s, self.relu_gate)
         tops[0].data = y
@@ -263,6 +269,14 @@ class PoolingLayer(Layer):
         if not propagate_down[0]:
             return
         s = self.spec(bottoms[0])
+        if self.method == POOL_STOCHASTIC:
+            # StoPoolBackward (pooling_layer.cu:270-300): the diff goes to the sampled element
+            xl = bottoms[0].data.float().requires_grad_(True)
+            with torch.enable_grad():
+                y = ops.ref._pool_windows(xl, s, 0.0).gather(-1, self.aux).squeeze(-1)
+                g, = torch.autograd.grad(y, xl, ops.ref.nchw(tops[0].diff.float()))
+            bottoms[0].diff = g.to(bottoms[0].dtype)
+            return
         bottoms[0].diff = ops.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data,
                                             self.relu_gate)
 

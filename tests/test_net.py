@@ -284,3 +284,31 @@ def test_python_layer():
     loss = net.forward_backward()
     assert torch.allclose(net.blob_by_name("y").data, 2.5 * x)
     assert abs(float(loss) - float(((1.5 * x) ** 2).sum() / 2 / 2)) < 1e-5
+
+
+def test_stochastic_pooling_train_samples_proportionally():
+    """StoPoolForwardTrain / StoPoolBackward (pooling_layer.cu:88-122, 270-300): an
+    element is drawn with probability value / window sum; the diff goes to it.  TEST
+    returns sum(x^2) / sum(x) (pooling_layer.cu:125-155)."""
+    n = 4000
+    txt = ('name: "s" force_backward: true layer { name: "in" type: "Input" top: "x" java_data_param { shape { '
+           f'dim: {n} dim: 1 dim: 1 dim: 2 }} }} }} '
+           'layer { name: "p" type: "Pooling" bottom: "x" top: "y" pooling_param { pool: STOCHASTIC '
+           'kernel_h: 1 kernel_w: 2 stride: 1 } }')
+    net = Net(proto.parse_prototxt(txt), phase=proto.TRAIN, seed=5)
+    x = net.blobs[net.blob_names.index("x")]
+    x.set_nchw(torch.tensor([1.0, 3.0]).repeat(n, 1, 1, 1))
+    net.forward()
+    y = net.blobs[net.blob_names.index("y")]
+    vals = y.nchw().reshape(-1)
+    assert set(vals.tolist()) <= {1.0, 3.0}
+    frac = float((vals == 3.0).float().mean())
+    assert abs(frac - 0.75) < 0.03
+    y.set_nchw(torch.ones(n, 1, 1, 1), diff=True)
+    net.backward()
+    g = x.nchw(diff=True).reshape(n, 2)
+    assert torch.equal(g[:, 1], (vals == 3.0).float()) and torch.equal(g.sum(1), torch.ones(n))
+    test = Net(proto.parse_prototxt(txt), phase=proto.TEST)
+    test.blobs[test.blob_names.index("x")].set_nchw(torch.tensor([1.0, 3.0]).repeat(n, 1, 1, 1))
+    test.forward()
+    assert torch.allclose(test.blobs[test.blob_names.index("y")].nchw(), torch.full((n, 1, 1, 1), 2.5))
