@@ -8,6 +8,7 @@
 #include <Python.h>
 #include <dlfcn.h>
 
+#include <cstdarg>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -18,6 +19,7 @@
 namespace {
 
 thread_local std::string g_err;
+sn_error_callback_t g_err_cb = nullptr;
 PyObject* g_mod = nullptr;  // sparknet_amd.capi (owned)
 std::once_flag g_init;
 
@@ -54,6 +56,7 @@ void fetch_error(const char* where) {
   Py_XDECREF(v);
   Py_XDECREF(tb);
   g_err = msg;
+  if (g_err_cb) g_err_cb(g_err.c_str());
 }
 
 std::string package_root() {
@@ -303,5 +306,149 @@ int sn_parse_solver_prototxt(const char* path, char** out, int* len) {
 }
 
 void sn_free(void* p) { std::free(p); }
+
+// -- process-level helpers --------------------------------------------------------------------
+static int module_call(const char* fn, const char* fmt, ...) {
+  ensure_interpreter();
+  Gil g;
+  if (!import_module()) return 1;
+  PyObject* f = PyObject_GetAttrString(g_mod, fn);
+  if (!f) {
+    fetch_error(fn);
+    return 1;
+  }
+  va_list ap;
+  va_start(ap, fmt);
+  PyObject* args = Py_VaBuildValue(fmt, ap);
+  va_end(ap);
+  PyObject* r = args ? PyObject_CallObject(f, args) : nullptr;
+  Py_XDECREF(args);
+  Py_DECREF(f);
+  if (!r) fetch_error(fn);
+  return status(r);
+}
+
+int sn_init_logging(const char* log_filename, int verbosity) {
+  return module_call("init_logging", "(si)", log_filename, verbosity);
+}
+
+int sn_set_basepath(const char* path) { return module_call("set_basepath", "(s)", path); }
+
+int sn_get_int_size(void) { return (int)sizeof(int); }
+int sn_get_dtype_size(void) { return (int)sizeof(float); }
+
+void sn_set_global_error_callback(sn_error_callback_t cb) { g_err_cb = cb; }
+
+int sn_set_mode_cpu(void* s) { return sn_set_device(s, -1); }
+int sn_set_mode_gpu(void* s) { return sn_set_device(s, 0); }
+
+// -- databases ----------------------------------------------------------------------------------
+int sn_create_db(void* s, const char* db_name, const char* db_type) {
+  Gil g;
+  return status(call(s, "create_db", "(ss)", db_name, db_type));
+}
+
+int sn_write_to_db(void* s, const char* image, int label, int channels, int height, int width, const char* key) {
+  Gil g;
+  Py_ssize_t n = (Py_ssize_t)channels * height * width;
+  return status(call(s, "write_to_db", "(y#iiiis)", image, n, label, channels, height, width, key ? key : ""));
+}
+
+int sn_commit_db_txn(void* s) {
+  Gil g;
+  return status(call(s, "commit_db_txn", nullptr));
+}
+
+int sn_close_db(void* s) {
+  Gil g;
+  return status(call(s, "close_db", nullptr));
+}
+
+int sn_save_mean_image(const float* mean, int channels, int height, int width, const char* filename) {
+  return module_call("save_mean_image", "(Kiiis)", (unsigned long long)(uintptr_t)mean, channels, height, width,
+                     filename);
+}
+
+// -- blobs --------------------------------------------------------------------------------------
+static long long int_call(void* s, const char* method, const char* fmt, ...) {
+  if (!s) {
+    g_err = "null state";
+    return -1;
+  }
+  va_list ap;
+  va_start(ap, fmt);
+  PyObject* args = fmt && *fmt ? Py_VaBuildValue(fmt, ap) : PyTuple_New(0);
+  va_end(ap);
+  if (!args) {
+    fetch_error(method);
+    return -1;
+  }
+  PyObject* fn = PyObject_GetAttrString(static_cast<PyObject*>(s), method);
+  PyObject* r = fn ? PyObject_CallObject(fn, args) : nullptr;
+  Py_XDECREF(fn);
+  Py_DECREF(args);
+  if (!r) {
+    fetch_error(method);
+    return -1;
+  }
+  long long v = PyLong_AsLongLong(r);
+  Py_DECREF(r);
+  return v;
+}
+
+int sn_num_layer_weights(void* s, int layer) {
+  Gil g;
+  return (int)int_call(s, "num_layer_weights", "(i)", layer);
+}
+
+int sn_num_data_blobs(void* s) {
+  Gil g;
+  return (int)int_call(s, "num_data_blobs", "()");
+}
+
+int sn_data_blob_name(void* s, int index, char* buf, int buflen) {
+  Gil g;
+  PyObject* r = call(s, "data_blob_name", "(i)", index);
+  if (!r) return 1;
+  const char* c = PyUnicode_AsUTF8(r);
+  int rc = 1;
+  if (c && buflen > 0) {
+    std::strncpy(buf, c, (size_t)buflen - 1);
+    buf[buflen - 1] = 0;
+    rc = 0;
+  }
+  Py_DECREF(r);
+  return rc;
+}
+
+int sn_num_output_blobs(void* s) {
+  Gil g;
+  return (int)int_call(s, "num_output_blobs", "()");
+}
+
+int sn_num_test_scores(void* s) {
+  Gil g;
+  return (int)int_call(s, "num_test_scores", "()");
+}
+
+int sn_blob_num_axes(void* s, int layer, int index) {
+  Gil g;
+  return (int)int_call(s, "blob_num_axes", "(ii)", layer, index);
+}
+
+int sn_blob_axis_shape(void* s, int layer, int index, int axis) {
+  Gil g;
+  return (int)int_call(s, "blob_axis_shape", "(iii)", layer, index, axis);
+}
+
+int sn_blob_get(void* s, int layer, int index, int diff, float* out, long long n) {
+  Gil g;
+  return status(call(s, "blob_get", "(iiiKL)", layer, index, diff, (unsigned long long)(uintptr_t)out, n));
+}
+
+int sn_blob_set(void* s, int layer, int index, int diff, const float* in, long long n) {
+  Gil g;
+  return status(call(s, "blob_set", "(iiiKL)", layer, index, diff, (unsigned long long)(uintptr_t)in, n));
+}
 
 }  // extern "C"

@@ -48,6 +48,38 @@ int sn_parse_net_prototxt(const char* path, char** out, int* len);     // -> ser
 int sn_parse_solver_prototxt(const char* path, char** out, int* len);  // (free with sn_free)
 void sn_free(void* p);
 
+// -- process-level helpers (ccaffe.cpp:33-49, 245-259) ---------------------------------------
+int sn_init_logging(const char* log_filename, int verbosity);  // verbosity: 0 INFO .. 3 FATAL
+int sn_set_basepath(const char* path);                          // chdir, like set_basepath
+int sn_get_int_size(void);
+int sn_get_dtype_size(void);  // size of the host exchange type (fp32)
+typedef void (*sn_error_callback_t)(const char* message);
+void sn_set_global_error_callback(sn_error_callback_t cb);  // called with every error message
+int sn_set_mode_cpu(void* state);
+int sn_set_mode_gpu(void* state);
+
+// -- Datum databases (create_db / write_to_db / commit_db_txn / close_db, ccaffe.cpp:51-81)
+int sn_create_db(void* state, const char* db_name, const char* db_type);  // "leveldb" | "lmdb" | "sndb"
+int sn_write_to_db(void* state, const char* image, int label, int channels, int height, int width,
+                   const char* key);
+int sn_commit_db_txn(void* state);
+int sn_close_db(void* state);
+int sn_save_mean_image(const float* mean, int channels, int height, int width, const char* filename);
+
+// -- blob access (num_layer_weights / get_*_blob / get_data / get_num_axes ..., ccaffe.cpp:142-195)
+// Blobs are addressed as (layer, index): layer >= 0 selects parameter blob `index` of that
+// layer, layer == -1 selects activation blob `index` of the net.  Device-resident
+// blobs are exchanged by copy in logical (Caffe) layout as fp32.
+int sn_num_layer_weights(void* state, int layer);
+int sn_num_data_blobs(void* state);
+int sn_data_blob_name(void* state, int index, char* buf, int buflen);
+int sn_num_output_blobs(void* state);
+int sn_num_test_scores(void* state);
+int sn_blob_num_axes(void* state, int layer, int index);
+int sn_blob_axis_shape(void* state, int layer, int index, int axis);
+int sn_blob_get(void* state, int layer, int index, int diff, float* out, long long n);
+int sn_blob_set(void* state, int layer, int index, int diff, const float* in, long long n);
+
 #ifdef __cplusplus
 }
 #endif

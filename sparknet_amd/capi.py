@@ -13,6 +13,7 @@ then copied to the device.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -136,6 +137,109 @@ class CoreState:
 
     def layer_names(self) -> list[str]:
         return list(self.net.layer_names)
+
+    # -- databases (ccaffe.cpp:51-81) ---------------------------------------------------------
+    def create_db(self, name: str, db_type: str) -> None:
+        import shutil
+        from .data.db import DatumWriter
+        if os.path.isdir(name):
+            shutil.rmtree(name)
+        self._db = DatumWriter(name, commit_every=1 << 62, backend=db_type)
+
+    def write_to_db(self, image: bytes, label: int, c: int, h: int, w: int, key: str) -> None:
+        d = proto.Datum(channels=c, height=h, width=w, data=image, label=label, encoded=False)
+        self._db.put(d, key or None)
+
+    def commit_db_txn(self) -> None:
+        self._db.commit()
+
+    def close_db(self) -> None:
+        self._db.close()
+        self._db = None
+
+    # -- blobs (ccaffe.cpp:142-195) -----------------------------------------------------------
+    def num_layer_weights(self, layer: int) -> int:
+        return len(self.net.layers[layer].params)
+
+    def num_data_blobs(self) -> int:
+        return len(self.net.blobs)
+
+    def data_blob_name(self, index: int) -> str:
+        return self.net.blob_names[index]
+
+    def num_output_blobs(self) -> int:
+        return len(self.net.output_blobs)
+
+    def num_test_scores(self) -> int:
+        return len(self.scores)
+
+    def _blob(self, layer: int, index: int):
+        if layer < 0:
+            return self.net.blobs[index], None
+        return None, self.net.layers[layer].params[index]
+
+    def blob_shape(self, layer: int, index: int) -> tuple:
+        blob, prm = self._blob(layer, index)
+        return tuple(blob.shape) if blob is not None else tuple(prm.caffe_shape)
+
+    def blob_num_axes(self, layer: int, index: int) -> int:
+        return len(self.blob_shape(layer, index))
+
+    def blob_axis_shape(self, layer: int, index: int, axis: int) -> int:
+        return int(self.blob_shape(layer, index)[axis])
+
+    def blob_get(self, layer: int, index: int, diff: int, addr: int, n: int) -> None:
+        blob, prm = self._blob(layer, index)
+        if blob is not None:
+            t = blob.nchw(diff=bool(diff))
+        else:
+            t = prm.to_caffe(prm.diff if diff else None)
+        src = t.detach().float().cpu().reshape(-1).numpy()
+        if n < src.size:
+            raise ValueError(f"buffer holds {n} floats, blob has {src.size}")
+        dst = np.ctypeslib.as_array(C.cast(addr, C.POINTER(C.c_float)), shape=(src.size,))
+        dst[:] = src
+
+    def blob_set(self, layer: int, index: int, diff: int, addr: int, n: int) -> None:
+        blob, prm = self._blob(layer, index)
+        shape = self.blob_shape(layer, index)
+        count = int(np.prod(shape)) if shape else 1
+        if n < count:
+            raise ValueError(f"buffer holds {n} floats, blob has {count}")
+        src = torch.from_numpy(np.ctypeslib.as_array(C.cast(addr, C.POINTER(C.c_float)), shape=(count,)).copy())
+        src = src.reshape(shape)
+        if blob is not None:
+            blob.set_nchw(src, diff=bool(diff))
+        elif diff:
+            prm.diff.copy_(prm.from_caffe(src).to(prm.diff.device))
+        else:
+            prm.set_caffe(src)
+            self.net.sync_compute()
+
+
+def init_logging(log_filename: str, verbosity: int) -> None:
+    """init_logging (ccaffe.cpp:33-37): log records to a file, stderr from ``verbosity``."""
+    import logging
+    root = logging.getLogger("sparknet_amd")
+    root.setLevel(logging.INFO)
+    fh = logging.FileHandler(log_filename)
+    fh.setFormatter(logging.Formatter("%(asctime)s %(levelname)s %(name)s] %(message)s"))
+    root.addHandler(fh)
+    sh = logging.StreamHandler()
+    sh.setLevel([logging.INFO, logging.WARNING, logging.ERROR, logging.CRITICAL][max(0, min(verbosity, 3))])
+    root.addHandler(sh)
+
+
+def set_basepath(path: str) -> None:
+    """set_basepath (ccaffe.cpp:39-41): relative paths in prototxts resolve from here."""
+    os.chdir(path)
+
+
+def save_mean_image(addr: int, c: int, h: int, w: int, filename: str) -> None:
+    """save_mean_image (ccaffe.cpp:83-97)."""
+    from .data.loaders import write_mean_binaryproto
+    mean = np.ctypeslib.as_array(C.cast(addr, C.POINTER(C.c_float)), shape=(c * h * w,)).copy()
+    write_mean_binaryproto(mean.reshape(c, h, w), filename)
 
 
 def parse_net_prototxt(path: str) -> bytes:

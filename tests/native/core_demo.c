@@ -1,7 +1,8 @@
 /* C host program driving the engine through libsn_core (the libccaffe verbs SparkNet's
  * CaffeNet wrapper used: src/main/scala/libs/Net.scala:67-251).  Trains a small net on
  * callback-fed data, tests, round-trips the flat weights and a .caffemodel.
- * usage: core_demo <solver.prototxt> <out.caffemodel> [device]   (prints OK on success) */
+ * Also exercises the per-blob verbs and the Datum database verbs (CreateDB.scala).
+ * usage: core_demo <solver.prototxt> <out.caffemodel> [device] [db_dir]   (prints OK) */
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -79,6 +80,43 @@ int main(int argc, char** argv) {
       fprintf(stderr, "caffemodel round trip mismatch at %lld\n", i);
       return 1;
     }
+  /* per-blob access: parameter blob 0 of layer 2 and activation blob 0 */
+  int nw = sn_num_layer_weights(st, 2);
+  int axes = sn_blob_num_axes(st, 2, 0);
+  long long cnt = 1;
+  for (int a = 0; a < axes; ++a) cnt *= sn_blob_axis_shape(st, 2, 0, a);
+  float* b = (float*)malloc(sizeof(float) * cnt);
+  CHECK(sn_blob_get(st, 2, 0, 0, b, cnt));
+  for (long long i = 0; i < cnt; ++i) b[i] = (float)i * 0.25f;
+  CHECK(sn_blob_set(st, 2, 0, 0, b, cnt));
+  for (long long i = 0; i < cnt; ++i) b[i] = -1.f;
+  CHECK(sn_blob_get(st, 2, 0, 0, b, cnt));
+  for (long long i = 0; i < cnt; ++i)
+    if (b[i] != (float)i * 0.25f) {
+      fprintf(stderr, "blob round trip mismatch at %lld\n", i);
+      return 1;
+    }
+  char bname[64];
+  CHECK(sn_data_blob_name(st, 0, bname, sizeof bname));
+  printf("blobs=%d outputs=%d weights2=%d axes=%d count=%lld blob0=%s\n", sn_num_data_blobs(st),
+         sn_num_output_blobs(st), nw, axes, cnt, bname);
+  free(b);
+  if (argc > 4) { /* CreateDB.makeDBFromPartition through the C verbs */
+    unsigned char img[3 * 4 * 4];
+    char key[16];
+    CHECK(sn_create_db(st, argv[4], "lmdb"));
+    for (int i = 0; i < 5; ++i) {
+      for (int j = 0; j < 48; ++j) img[j] = (unsigned char)(i * 48 + j);
+      snprintf(key, sizeof key, "%d", i);
+      CHECK(sn_write_to_db(st, (const char*)img, i, 3, 4, 4, key));
+      if (i == 2) CHECK(sn_commit_db_txn(st));
+    }
+    CHECK(sn_close_db(st));
+    float mean[3] = {1.f, 2.f, 3.f};
+    char mpath[512];
+    snprintf(mpath, sizeof mpath, "%s.mean.binaryproto", argv[4]);
+    CHECK(sn_save_mean_image(mean, 3, 1, 1, mpath));
+  }
   printf("layers=%d layer2=%s params=%lld loss=%.4f callbacks=%d\n", nl, name, n, loss, calls);
   sn_destroy_state(st);
   free(w);

@@ -35,10 +35,18 @@ def _c_host_program(tmp_path, device):
     env = dict(os.environ)
     if device < 0:
         env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    r = subprocess.run([str(exe), SOLVER, str(tmp_path / "w.caffemodel"), str(device)], capture_output=True,
-                       text=True, timeout=300, env=env)
+    db = tmp_path / "demo_db"
+    r = subprocess.run([str(exe), SOLVER, str(tmp_path / "w.caffemodel"), str(device), str(db)],
+                       capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout, r.stderr[-3000:])
     assert "layers=7 layer2=conv1" in r.stdout and "callbacks=6" in r.stdout
+    assert "weights2=2" in r.stdout and "blob0=data" in r.stdout
+    from sparknet_amd.data.db import DatumReader
+    from sparknet_amd.data.loaders import read_mean_binaryproto
+    rd = DatumReader(str(db))
+    assert len(rd) == 5 and [rd.get(i).label for i in range(5)] == [0, 1, 2, 3, 4]
+    assert list(rd.get(3).data[:2]) == [144, 145]
+    assert read_mean_binaryproto(str(db) + ".mean.binaryproto").reshape(-1).tolist() == [1.0, 2.0, 3.0]
 
 
 def test_c_host_program(core_lib, tmp_path):
