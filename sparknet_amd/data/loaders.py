@@ -79,52 +79,89 @@ def decode_resize(data: bytes, size: tuple[int, int]) -> np.ndarray | None:
 
 
 class ImageNetLoader:
-    """Iterate (planar uint8 image, label) from tar shards or a directory tree."""
+    """Iterate (planar uint8 image, label) from tar shards or a directory tree, local or
+    on S3 (ImageNetLoader.scala:21-96: list the shards under a prefix, read the labels
+    file ``path label`` keyed by file name, stream each tar).  ``root`` / ``labels_file``
+    may be ``s3://bucket/prefix`` URLs (see :mod:`sparknet_amd.data.s3`)."""
 
-    def __init__(self, root: str, labels_file: str | None = None, size=(256, 256)):
+    def __init__(self, root: str, labels_file: str | None = None, size=(256, 256), s3_client=None):
         self.root = root
         self.size = size
         self.labels = {}
+        self._s3 = s3_client
         if labels_file:
-            with open(labels_file) as f:
-                for line in f:
-                    parts = line.split()
-                    if len(parts) >= 2:
-                        self.labels[os.path.basename(parts[0])] = int(parts[1])
+            for line in self._read_text(labels_file).splitlines():
+                parts = line.split()
+                if len(parts) >= 2:
+                    self.labels[os.path.basename(parts[0])] = int(parts[1])
 
-    def _members(self):
+    def _client(self):
+        if self._s3 is None:
+            from .s3 import S3Client
+            self._s3 = S3Client()
+        return self._s3
+
+    def _read_text(self, path: str) -> str:
+        if path.startswith("s3://"):
+            from .s3 import parse_url
+            with self._client().get_object(*parse_url(path)) as r:
+                return r.read().decode()
+        with open(path) as f:
+            return f.read()
+
+    def files(self) -> list[str]:
+        """The shard files (tars / images) in a stable order."""
+        if self.root.startswith("s3://"):
+            from .s3 import parse_url
+            bucket, prefix = parse_url(self.root)
+            return [f"s3://{bucket}/{k}" for k in sorted(self._client().list_objects(bucket, prefix))
+                    if not k.endswith("/")]
         if os.path.isdir(self.root):
+            out = []
             for dirpath, _, files in os.walk(self.root):
-                for fn in sorted(files):
-                    p = os.path.join(dirpath, fn)
-                    if fn.endswith(".tar"):
-                        yield from self._tar(p)
-                    elif fn.lower().endswith((".jpg", ".jpeg", ".png")):
-                        with open(p, "rb") as f:
-                            yield fn, f.read()
-        elif self.root.endswith(".tar"):
-            yield from self._tar(self.root)
+                out += [os.path.join(dirpath, fn) for fn in files
+                        if fn.endswith(".tar") or fn.lower().endswith((".jpg", ".jpeg", ".png"))]
+            return sorted(out)
+        return [self.root]
 
-    @staticmethod
-    def _tar(path):
-        with tarfile.open(path) as tf:
-            for m in tf:
-                if m.isfile():
-                    yield os.path.basename(m.name), tf.extractfile(m).read()
+    def _open(self, path: str):
+        if path.startswith("s3://"):
+            from .s3 import parse_url
+            return self._client().get_object(*parse_url(path))
+        return open(path, "rb")
+
+    def _members(self, files):
+        for p in files:
+            if p.endswith(".tar"):
+                with self._open(p) as fh, tarfile.open(fileobj=fh, mode="r|*") as tf:
+                    for m in tf:
+                        if m.isfile():
+                            yield os.path.basename(m.name), tf.extractfile(m).read()
+            else:
+                with self._open(p) as fh:
+                    yield os.path.basename(p), fh.read()
 
     def __iter__(self):
-        for name, data in self._members():
+        yield from self._decoded(self.files())
+
+    def _decoded(self, files):
+        for name, data in self._members(files):
             img = decode_resize(data, self.size)
             if img is None:
                 continue
             yield img, self.labels.get(name, 0)
 
     def minibatches(self, batch: int, shard: tuple[int, int] = (0, 1)):
-        """Full minibatches only (the remainder is dropped, ScaleAndConvert.scala:45-70)."""
+        """Full minibatches only (the remainder is dropped, ScaleAndConvert.scala:45-70).
+        With at least ``world`` shard files each rank reads only its files (the
+        reference's one-partition-per-file RDD); otherwise images are dealt round-robin."""
         rank, world = shard
+        files = self.files()
+        by_file = len(files) >= world > 1
+        stream = self._decoded(files[rank::world] if by_file else files)
         imgs, labs = [], []
-        for i, (img, lab) in enumerate(self):
-            if i % world != rank:
+        for i, (img, lab) in enumerate(stream):
+            if not by_file and i % world != rank:
                 continue
             imgs.append(img)
             labs.append(lab)
