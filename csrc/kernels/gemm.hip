@@ -68,7 +68,7 @@ struct SnGemmArgs {
   long long ldc, c_gstride, c_split_stride;
   const float* bias;  // per output column n (offset by g*N), EPI_BF16 only
   int relu;
-  int tile;           // 0: 128x128, 1: 256x64 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages)
+  int tile;           // 0: 128x128, 1: 256x64, 4: 128x96 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages)
   const bf16_t* gate; // EPI_BF16: zero outputs where gate (same layout as C) <= 0 (fused ReLU backward)
   int fp8;            // operands are e4m3 bytes (K-contiguous only); k counts fp8 elements
   const float* deq_a; // fp8: dequantisation factors (1 / quantisation scale) of A and B, device scalars
@@ -112,7 +112,8 @@ struct GStager {
   static constexpr int CPL = MC ? TILE / 8 : 8;   // 16-B chunks per LDS row
   static constexpr int RPI = 64 / CPL;            // LDS rows per wave-instruction
   static constexpr int EPC = 16 / ES;             // elements per 16-B chunk (8 bf16, 16 fp8)
-  static_assert(NI >= 1 && (MC || NI % 2 == 0), "KC chunk pattern repeats with period 2 in j");
+  static_assert(NI >= 1 && NI * 8 * NW == TILE, "whole wave-instructions per tile");
+  static_assert(MC || MODE != OP_IM2COL || NI % 2 == 0, "KC im2col: chunk pattern repeats with period 2 in j");
   static_assert(ES == 2 || !MC, "fp8 operands are K-contiguous");
   const char* base;  // element offsets below are scaled by ES
   long long ld;
@@ -309,13 +310,15 @@ SN_DEV i32x8 read_frag8(const char* lds, int x0, int lane) {
   return r;
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, bool FP8 = false>
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, bool FP8 = false,
+          int NFR = 4>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmArgs args) {
   // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
   constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-  constexpr int WN = BN / 64, WM = NW / WN;  // waves along N / M (64x64 per wave)
-  static_assert(WM * 64 == BM && WM * WN == NW, "tile/wave layout mismatch");
+  // waves along N / M; each wave owns 64 rows x (16*NFR) columns (NFR = 4, or 3 for 96-wide tiles)
+  constexpr int WN = BN / (16 * NFR), WM = NW / WN;
+  static_assert(WN * 16 * NFR == BN && WM * 64 == BM && WM * WN == NW, "tile/wave layout mismatch");
   static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
   // Distinct LDS objects (one per stage): the compiler's alias scopes then prove that
   // the ds_reads of one stage do not depend on the DMA in flight into another, so it
@@ -353,26 +356,26 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M);
   sb.init(args.B, grp, wv, lane, n_blk, args.N, n_blk, args.N);
 
-  f32x4 acc[4][4];
+  f32x4 acc[NFR][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NFR; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int wm0 = (wave % WM) * 64, wn0 = (wave / WM) * 64;
+  const int wm0 = (wave % WM) * 64, wn0 = (wave / WM) * (16 * NFR);
   const int nk = k1 > k0 ? (k1 - k0 + BKE - 1) / BKE : 0;
 
   auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
     if constexpr (FP8) {
-      i32x8 fa8[4], fb8[4];
+      i32x8 fa8[4], fb8[NFR];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fb8[i] = read_frag8(lb, wn0 + 16 * i, lane);
+      for (int i = 0; i < NFR; ++i) fb8[i] = read_frag8(lb, wn0 + 16 * i, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa8[i] = read_frag8(la, wm0 + 16 * i, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NFR; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)  // formats 0/0 = e4m3 x e4m3, block scales 2^0 (E8M0 127)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa8[j], acc[i][j], 0, 0, 0, 127, 0,
@@ -380,11 +383,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
       __builtin_amdgcn_s_setprio(0);
       return;
     }
-    bf16x8_t fa[2][4], fb[2][4];
+    bf16x8_t fa[2][4], fb[2][NFR];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fb[s][i] = read_frag<BMC, BN>(lb, wn0 + 16 * i, s, lane);
+      for (int i = 0; i < NFR; ++i) fb[s][i] = read_frag<BMC, BN>(lb, wn0 + 16 * i, s, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[s][i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
     }
@@ -392,7 +395,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NFR; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][i], fa[s][j], acc[i][j], 0, 0, 0);
@@ -447,7 +450,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
     const int m = m_blk + wm0 + 16 * j + mrow_l;
     if (m >= args.M) continue;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NFR; ++i) {
       const int n = n_blk + wn0 + 16 * i + ncol_l;
       if (n >= args.N) continue;
       const bool full = (n + 3 < args.N) && ((args.ldc & 3) == 0);
@@ -516,20 +519,20 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   }
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS>
+template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS, int NFR = 4>
 int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS>), grid, dim3(NW * 64), 0,
-                         st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS, false, NFR>), grid,
+                         dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS>), grid, dim3(NW * 64), 0,
-                         st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS, false, NFR>), grid,
+                         dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32_ACC:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS>), grid, dim3(NW * 64),
-                         0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS, false, NFR>), grid,
+                         dim3(NW * 64), 0, st, a);
       break;
     default:
       return 2;
@@ -553,6 +556,19 @@ int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
   }
   if (a.a_mc == 0 && a.a_mode == OP_IM2COL && a.b_mc == 1 && a.b_mode == OP_FLIPW)  // conv dgrad
     return launch_epi<0, OP_IM2COL, 1, OP_FLIPW, BM, BN, NW, NS>(a, grid, stream);
+  return 4;
+}
+
+// 128x96 tile (waves own 64x48): output widths that are multiples of 96 (AlexNet conv1's
+// 96 filters, conv4's 192 per group) without the 25 % dead columns of a 128-wide tile.
+// The 96-row B image has 12-chunk MC rows, so only K-contiguous (KC) B operands.
+int launch_tile96(const SnGemmArgs& a, hipStream_t stream) {
+  const int tiles = ((a.M + 127) / 128) * ((a.N + 95) / 96);
+  dim3 grid(tiles, a.splits, a.groups);
+  if (a.b_mc || a.b_mode != OP_DENSE) return 4;
+  if (a.a_mc == 0 && a.a_mode == OP_IM2COL) return launch_epi<0, OP_IM2COL, 0, OP_DENSE, 128, 96, 4, 2, 3>(a, grid, stream);
+  if (a.a_mc == 0 && a.a_mode == OP_DENSE) return launch_epi<0, OP_DENSE, 0, OP_DENSE, 128, 96, 4, 2, 3>(a, grid, stream);
+  if (a.a_mc == 1 && a.a_mode == OP_DENSE) return launch_epi<1, OP_DENSE, 0, OP_DENSE, 128, 96, 4, 2, 3>(a, grid, stream);
   return 4;
 }
 
@@ -589,6 +605,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 1: return launch_tile<256, 64, 4, 2>(a, stream);    // skinny N
     case 2: return launch_tile<256, 128, 8, 3>(a, stream);   // 8 waves, 3-stage pipeline
     case 3: return launch_tile<128, 256, 8, 3>(a, stream);
+    case 4: return launch_tile96(a, stream);
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

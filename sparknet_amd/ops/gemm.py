@@ -104,14 +104,20 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
     return s, 0 if op.kcontig else 1, OP_IM2COL
 
 
-TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256)}
+TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96)}
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
 _RASTER_N = int(os.environ.get("SN_GEMM_RASTER_N", "-1"))  # -1: heuristic
 
 
-def choose_tile(M: int, N: int) -> int:
-    """256x64 for skinny N (<= 64 per group, e.g. 48-channel grouped dgrad), else 128x128."""
-    return 1 if N <= 64 and M >= 256 else 0
+def choose_tile(M: int, N: int, b_kcontig: bool = False) -> int:
+    """256x64 for skinny N (<= 64 per group, e.g. 48-channel grouped dgrad); 128x96 when N
+    is a multiple of 96 that 128-wide tiles would pad by a third (AlexNet conv1's 96
+    filters, conv4's 192 per group; K-contiguous B only); else 128x128."""
+    if N <= 64 and M >= 256:
+        return 1
+    if b_kcontig and N % 96 == 0 and N % 128 != 0 and M >= 128:
+        return 4
+    return 0
 
 
 SLOTS = 512          # resident blocks: 2 per CU (64 KB of LDS each) x 256 CUs
@@ -162,7 +168,7 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
     fp8 = deq is not None  # e4m3 operands; deq = (1/scale_A, 1/scale_B) device scalars
     sa, a_mc, a_mode = _operand(A, fp8)
     sb, b_mc, b_mode = _operand(B, fp8)
-    tile = 0 if fp8 else (choose_tile(M, N) if _FORCE_TILE < 0 else _FORCE_TILE)
+    tile = 0 if fp8 else (choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE) if _FORCE_TILE < 0 else _FORCE_TILE)
     bk = 128 if fp8 else BK
     if splits is None:
         # the fp8 k-step covers 128 elements in the time a bf16 one covers 64: same model

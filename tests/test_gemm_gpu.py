@@ -25,10 +25,10 @@ def test_linear_fwd(gpu, M, N, K):
     _close(y, ref)
 
 
-def test_identity_asymmetric(gpu):
-    # A = I with an asymmetric B catches transposed C writes.
+@pytest.mark.parametrize("n", [128, 96, 192])
+def test_identity_asymmetric(gpu, n):
+    # A = I with an asymmetric B catches transposed C writes (96/192: the 128x96 tile).
     from sparknet_amd.ops import gemm
-    n = 128
     eye = torch.eye(n, device=gpu).to(torch.bfloat16)
     w = (torch.arange(n * n, device=gpu).reshape(n, n) % 17).to(torch.bfloat16)
     y = gemm.linear_fwd(eye, w)
@@ -139,3 +139,4 @@ def test_fp8_conv_forward(gpu, case):
     y = hip.conv_forward_fp8(xq, wq, None, s, dx, dw)
     ref = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), stride=st, padding=pd, groups=g) * (0.5 * 0.0625)
     _close(y.permute(0, 3, 1, 2), ref, 1e-2)
+

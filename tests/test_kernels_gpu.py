@@ -34,6 +34,9 @@ CONV_CASES = [
     (2, 15, 15, 16, 16, 3, 3, 2, 1, 1),      # stride 2 dgrad fallback
     (2, 12, 12, 20, 50, 5, 5, 1, 0, 1),      # LeNet conv2 (odd channels)
     (3, 9, 9, 64, 40, 3, 3, 1, 1, 2),
+    (2, 35, 35, 3, 96, 11, 11, 4, 0, 1),     # conv1 with 96 filters: 128x96 tile on the folded input
+    (2, 13, 13, 64, 384, 3, 3, 1, 1, 2),     # conv4-like: 192 filters per group -> 128x96 tile
+    (3, 7, 7, 32, 288, 3, 3, 1, 1, 1),       # 3 x 96-wide N tiles, ragged M
 ]
 
 
