@@ -68,7 +68,7 @@ struct SnGemmArgs {
   long long ldc, c_gstride, c_split_stride;
   const float* bias;  // per output column n (offset by g*N), EPI_BF16 only
   int relu;
-  int tile;           // 0: 128x128, 1: 256x64, 4: 128x96 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages)
+  int tile;           // 0: 128x128, 1: 256x64, 4: 128x96, 5: 256x48 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages)
   const bf16_t* gate; // EPI_BF16: zero outputs where gate (same layout as C) <= 0 (fused ReLU backward)
   int fp8;            // operands are e4m3 bytes (K-contiguous only); k counts fp8 elements
   const float* deq_a; // fp8: dequantisation factors (1 / quantisation scale) of A and B, device scalars
@@ -315,7 +315,10 @@ template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int N
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmArgs args) {
   // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
   constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  // B's LDS image holds BNL >= BN rows: whole wave-instructions per wave (a 48-wide tile
+  // stages 64 rows, the 16 beyond the tile read the zero page)
+  constexpr int BNL = ((BN / 8) % NW == 0) ? BN : (BN + 63) / 64 * 64;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BNL * 128, STAGE = A_BYTES + B_BYTES;
   // waves along N / M; each wave owns 64 rows x (16*NFR) columns (NFR = 4, or 3 for 96-wide tiles)
   constexpr int WN = BN / (16 * NFR), WM = NW / WN;
   static_assert(WN * 16 * NFR == BN && WM * 64 == BM && WM * WN == NW, "tile/wave layout mismatch");
@@ -350,11 +353,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
 
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   using SA = GStager<AMC, AMODE, BM, NW, ES>;
-  using SB = GStager<BMC, BMODE, BN, NW, ES>;
+  using SB = GStager<BMC, BMODE, BNL, NW, ES>;
   SA sa;
   SB sb;
   sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M);
-  sb.init(args.B, grp, wv, lane, n_blk, args.N, n_blk, args.N);
+  const int n_lim = min(args.N, n_blk + BN);
+  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim);
 
   f32x4 acc[NFR][4];
 #pragma unroll
@@ -387,7 +391,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
-      for (int i = 0; i < NFR; ++i) fb[s][i] = read_frag<BMC, BN>(lb, wn0 + 16 * i, s, lane);
+      for (int i = 0; i < NFR; ++i) fb[s][i] = read_frag<BMC, BNL>(lb, wn0 + 16 * i, s, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[s][i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
     }
@@ -403,7 +407,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   };
   auto issue = [&](char* st, int kt) {
     sa.issue(st, wv, k0 + kt * BKE, k1, m_blk, args.M);
-    sb.issue(st + A_BYTES, wv, k0 + kt * BKE, k1, n_blk, args.N);
+    sb.issue(st + A_BYTES, wv, k0 + kt * BKE, k1, n_blk, n_lim);
   };
   if (NS == 2) {
     // One barrier per K-step: retire this wave's DMA of tile kt, barrier (all waves' DMAs
@@ -572,6 +576,27 @@ int launch_tile96(const SnGemmArgs& a, hipStream_t stream) {
   return 4;
 }
 
+// 256x48 tile (4 waves of 64x48; B staged as 64 rows): 48-wide outputs such as AlexNet
+// conv2's dgrad (48 input channels per group) without a quarter of dead MFMA columns.
+template <int NS_ = 2>
+int launch_tile48(const SnGemmArgs& a, hipStream_t stream) {
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 47) / 48);
+  dim3 grid(tiles, a.splits, a.groups);
+  const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  switch (key) {
+    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, 256, 48, 4, NS_, 3>(a, grid, stream);
+    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, 256, 48, 4, NS_, 3>(a, grid, stream);
+    case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE, 256, 48, 4, NS_, 3>(a, grid, stream);
+    case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE, 256, 48, 4, NS_, 3>(a, grid, stream);
+    case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL, 256, 48, 4, NS_, 3>(a, grid, stream);
+    case 0b1000: return launch_epi<1, OP_DENSE, 0, OP_DENSE, 256, 48, 4, NS_, 3>(a, grid, stream);
+    default: break;
+  }
+  if (a.a_mc == 0 && a.a_mode == OP_IM2COL && a.b_mc == 1 && a.b_mode == OP_FLIPW)
+    return launch_epi<0, OP_IM2COL, 1, OP_FLIPW, 256, 48, 4, NS_, 3>(a, grid, stream);
+  return 4;
+}
+
 template <int AMODE>
 int launch_fp8(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
@@ -606,6 +631,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 2: return launch_tile<256, 128, 8, 3>(a, stream);   // 8 waves, 3-stage pipeline
     case 3: return launch_tile<128, 256, 8, 3>(a, stream);
     case 4: return launch_tile96(a, stream);
+    case 5: return launch_tile48(a, stream);
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

@@ -104,17 +104,18 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
     return s, 0 if op.kcontig else 1, OP_IM2COL
 
 
-TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96)}
+TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48)}
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
 _RASTER_N = int(os.environ.get("SN_GEMM_RASTER_N", "-1"))  # -1: heuristic
 
 
 def choose_tile(M: int, N: int, b_kcontig: bool = False) -> int:
-    """256x64 for skinny N (<= 64 per group, e.g. 48-channel grouped dgrad); 128x96 when N
+    """256x64 for skinny N (<= 64 per group; 256x48 when N is 48: AlexNet conv2's dgrad has
+    48 channels per group); 128x96 when N
     is a multiple of 96 that 128-wide tiles would pad by a third (AlexNet conv1's 96
     filters, conv4's 192 per group; K-contiguous B only); else 128x128."""
     if N <= 64 and M >= 256:
-        return 1
+        return 5 if N % 48 == 0 and N % 64 != 0 else 1
     if b_kcontig and N % 96 == 0 and N % 128 != 0 and M >= 128:
         return 4
     return 0

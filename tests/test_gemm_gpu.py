@@ -15,7 +15,8 @@ def _close(a, b, tol=2e-2):
     assert err / scale < tol, f"rel err {err/scale:.3e}"
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 4096, 1024), (100, 70, 200), (77, 96, 363 + 5), (1000, 10, 64)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 4096, 1024), (100, 70, 200), (77, 96, 363 + 5), (1000, 10, 64),
+                                   (600, 48, 200)])
 def test_linear_fwd(gpu, M, N, K):
     from sparknet_amd.ops import gemm
     x, w = _bf(M, K, device=gpu), _bf(N, K, device=gpu)
@@ -35,7 +36,7 @@ def test_identity_asymmetric(gpu, n):
     assert torch.equal(y.float(), w.float().t())
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 4096, 9216), (64, 10, 500), (128, 200, 136), (300, 200, 40)])
+@pytest.mark.parametrize("M,N,K", [(256, 4096, 9216), (64, 10, 500), (128, 200, 136), (300, 200, 40), (700, 64, 48)])
 def test_linear_dgrad(gpu, M, N, K):
     from sparknet_amd.ops import gemm
     dy, w = _bf(M, N, device=gpu), _bf(N, K, device=gpu)

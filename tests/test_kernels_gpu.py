@@ -37,6 +37,7 @@ CONV_CASES = [
     (2, 35, 35, 3, 96, 11, 11, 4, 0, 1),     # conv1 with 96 filters: 128x96 tile on the folded input
     (2, 13, 13, 64, 384, 3, 3, 1, 1, 2),     # conv4-like: 192 filters per group -> 128x96 tile
     (3, 7, 7, 32, 288, 3, 3, 1, 1, 1),       # 3 x 96-wide N tiles, ragged M
+    (2, 27, 27, 96, 64, 5, 5, 1, 2, 2),      # conv2-like: dgrad has 48 channels per group -> 256x48 tile
 ]
 
 
