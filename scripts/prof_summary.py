@@ -3,7 +3,11 @@
 import csv
 import sys
 
+import os
+
 path = sys.argv[1]
+if os.path.isdir(path):
+    path = os.path.join(path, "run_kernel_trace.csv")
 rows = list(csv.DictReader(open(path)))
 idx = [i for i, r in enumerate(rows) if 'solver_update' in r['Kernel_Name']]
 a, b = idx[-2], idx[-1]
@@ -12,7 +16,8 @@ agg = {}
 for r in rows[a + 1:b + 1]:
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     tot += d
-    k = r['Kernel_Name'].split('(')[0][-60:]
+    n = r['Kernel_Name']
+    k = (n.split('(SnGemmArgs')[0] if 'gemm_kernel' in n else n.split('(')[0])[-60:]
     agg[k] = agg.get(k, 0) + d
 print("per-iteration kernel time by kernel (us):")
 for k, v in sorted(agg.items(), key=lambda x: -x[1])[:25]:
@@ -22,5 +27,7 @@ if len(sys.argv) > 2:
     for r in rows[a + 1:b + 1]:
         d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
         n = r['Kernel_Name']
-        if sys.argv[2] in n:
-            print(f"{d:8.1f}us grid=({int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])},{r['Grid_Size_Y']},{r['Grid_Size_Z']}) {n.split('(')[0][-50:]}")
+        if sys.argv[2] == "all" or sys.argv[2] in n:
+            name = n.split('(SnGemmArgs')[0] if 'gemm_kernel' in n else n.split('(')[0]
+            print(f"{d:8.1f}us grid=({int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])},{r['Grid_Size_Y']},"
+                  f"{r['Grid_Size_Z']}) {name[-70:]}")

@@ -11,6 +11,12 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+@pytest.fixture(autouse=True)
+def _log_home(tmp_path, monkeypatch):
+    """Apps write training logs to $SPARKNET_HOME; keep them out of the checkout."""
+    monkeypatch.setenv("SPARKNET_HOME", str(tmp_path / "logs"))
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import torch
