@@ -74,6 +74,14 @@ struct SnGemmArgs {
   const float* deq_a; // fp8: dequantisation factors (1 / quantisation scale) of A and B, device scalars
   const float* deq_b;
   int raster_n;       // N-fastest tile order (see gemm_kernel)
+  // Bias gradient folded into a weight-gradient product (MC B operand only): B column
+  // `ones_col` is a virtual column of ones (for every reduction row < K), so output column
+  // ones_col of C is sum_k A(m, k) = the bias gradient of output channel m.  With
+  // bias_out set (unsplit launch) that column goes to bias_out[grp * M + m] (+= when
+  // bias_acc) instead of C; split-K launches keep it in the fp32 slabs for the reduce.
+  int ones_col;       // -1: none
+  float* bias_out;
+  int bias_acc;
 };
 
 }  // extern "C"
@@ -93,8 +101,10 @@ SN_DEV int swz_mc(int k) {
 template <int TILE>
 SN_DEV int mc_off(int k, int mc) { return k * (TILE * 2) + ((mc << 4) ^ swz_mc<TILE>(k)); }
 
-// Zero source for LDS-DMA lanes that fall outside the matrix (padding, ragged edges).
+// Zero source for LDS-DMA lanes that fall outside the matrix (padding, ragged edges), and
+// the ones page of the bias-gradient column (bf16 1.0 then seven zeros).
 __device__ __attribute__((aligned(16))) uint4 g_zero16[1];
+__device__ __attribute__((aligned(16))) uint32_t g_one16[4] = {0x3F80u, 0u, 0u, 0u};
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -119,18 +129,20 @@ struct GStager {
   long long ld;
   SnConvGeom g;
   int coff;
+  int ones_col;  // MC operands: column index of the virtual ones column (-1: none)
   int rr[NI];  // tile-relative LDS row of this lane in instruction j
   int ch[NI];  // logical 16-B chunk this lane fetches in instruction j
   int rowoff[NI], ph[NI], pw[NI];  // KC+IM2COL: pixel decode (rows fixed across k); rowoff =
   bool pv[NI];                     // element offset of the (h=ph, w=pw) corner, may be < 0
   int cr[NI], cs[NI], cc[NI];  // MC+IM2COL: column decode (cols fixed across k)
-  bool cv[NI];
+  bool cv[NI], co[NI];         //   column valid / column is the ones column
   float invPQ, invQ, invCg, invS, invKg;
 
   SN_DEV void init(const SnOperand& op, int grp, int wave, int lane, int tile_row0, int rows_lim,
-                   int tile_col0, int cols_lim) {
+                   int tile_col0, int cols_lim, int ones = -1) {
     ld = op.ld;
     g = op.g;
+    ones_col = ones;
     if (MODE != OP_IM2COL) {
       base = reinterpret_cast<const char*>(op.ptr) + (long long)grp * op.gstride * ES;
       coff = 0;
@@ -160,7 +172,8 @@ struct GStager {
       }
       if (MODE == OP_IM2COL && MC) {
         int col = tile_col0 + ch[j] * 8;
-        cv[j] = col < cols_lim;
+        co[j] = col == ones_col && col < cols_lim;
+        cv[j] = col < cols_lim && col != ones_col;
         int tap = col / g.Cg;
         cc[j] = col - tap * g.Cg;
         cr[j] = tap / g.S;
@@ -172,8 +185,8 @@ struct GStager {
   // The DMA is issued from inline asm so the compiler's wait-count pass does not see an
   // LDS write it cannot disambiguate (it would drain vmcnt(0) before the next ds_read);
   // every wait on these DMAs is explicit in the K-loop (counted vmcnt + barrier).
-  SN_DEV void dma(const char* src, bool valid, char* lds) {
-    const void* s = valid ? (const void*)src : (const void*)g_zero16;
+  SN_DEV void dma(const char* src, bool valid, char* lds, bool one = false) {
+    const void* s = valid ? (const void*)src : (one ? (const void*)g_one16 : (const void*)g_zero16);
     const uint32_t m0 = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(s) : "memory");
   }
@@ -232,7 +245,9 @@ struct GStager {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           int k = k_tile + rr[j], col = tile_rc0 + ch[j] * 8;
-          dma(base + ((long long)k * ld + col) * 2, k < k_lim && col < rc_lim, dst + j * 1024);
+          const bool one = col == ones_col && col < rc_lim && k < k_lim;
+          dma(base + ((long long)k * ld + col) * 2, k < k_lim && col < rc_lim && col != ones_col, dst + j * 1024,
+              one);
         }
       } else if (MODE == OP_FLIPW) {
         const int RS = g.R * g.S;
@@ -256,7 +271,7 @@ struct GStager {
           int w = q * g.sw - g.pw + cs[j] * g.dw;
           bool v = cv[j] && pix < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
           long long off = ((long long)(n * g.H + h) * g.W + w) * g.C + coff + cc[j];
-          dma(base + off * 2, v, dst + j * 1024);
+          dma(base + off * 2, v, dst + j * 1024, co[j] && pix < k_lim);
         }
       }
     }
@@ -358,7 +373,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   SB sb;
   sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M);
   const int n_lim = min(args.N, n_blk + BN);
-  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim);
+  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1);
 
   f32x4 acc[NFR][4];
 #pragma unroll
@@ -449,6 +464,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   // Epilogue.  acc[i][j] holds D[n][m] with m = lane&15 (+16j), n = 4(lane>>4)+r (+16i):
   // each lane owns 4 consecutive output columns of one output row.
   const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
+  // fp32 outputs: the bias-gradient column (when routed to bias_out) is not part of C
+  const int c_cols = (EPI != EPI_BF16 && args.bias_out) ? args.ones_col : args.N;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int m = m_blk + wm0 + 16 * j + mrow_l;
@@ -457,7 +474,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
     for (int i = 0; i < NFR; ++i) {
       const int n = n_blk + wn0 + 16 * i + ncol_l;
       if (n >= args.N) continue;
-      const bool full = (n + 3 < args.N) && ((args.ldc & 3) == 0);
+      const bool full = (n + 3 < c_cols) && ((args.ldc & 3) == 0);
       f32x4 v = acc[i][j];
       if (FP8) v = v * (args.deq_a[0] * args.deq_b[0]);  // per-tensor fp8 scales
       if (EPI == EPI_BF16) {
@@ -498,6 +515,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
             if (n + r < args.N) C[n + r] = f2bf(o[r]);
         }
       } else {
+        if (args.bias_out && n <= args.ones_col && args.ones_col < n + 4) {
+          const int r = args.ones_col - n;
+          const float bv = r == 0 ? v[0] : (r == 1 ? v[1] : (r == 2 ? v[2] : v[3]));
+          float* bp = args.bias_out + (long long)grp * args.M + m;
+          *bp = args.bias_acc ? *bp + bv : bv;
+        }
+        if (n >= c_cols) continue;
         float* C = reinterpret_cast<float*>(args.C) + split * args.c_split_stride + grp * args.c_gstride +
                    (long long)m * args.ldc;
         if (full) {
@@ -511,7 +535,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (n + r < args.N) {
+            if (n + r < c_cols) {
               if (EPI == EPI_F32_ACC)
                 C[n + r] += v[r];
               else
@@ -617,6 +641,10 @@ int launch_fp8(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
 extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   const SnGemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
+  // the ones column is a whole 16-B chunk of an MC B operand, inside the product's N
+  if (a.ones_col >= 0 && (!a.b_mc || a.b_mode == OP_FLIPW || (a.ones_col & 7) || a.ones_col >= a.N || a.fp8))
+    return 5;
+  if (a.bias_out && (a.ones_col < 0 || a.epi == EPI_BF16)) return 5;
   if (a.fp8) {
     // e4m3 forward products: A (dense or implicit im2col) and B dense, both K-contiguous
     if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || a.a_mc || a.b_mc || a.b_mode != OP_DENSE || !a.deq_a || !a.deq_b)

@@ -10,15 +10,26 @@
 // out (op)= act(sum_s ws[s] + bias)
 //   mode 0: out bf16 = act(sum + bias)     mode 1: out f32 = sum     mode 2: out f32 += sum
 // (gate, mode 0: zero where gate <= 0 — a fused slope-0 ReLU backward)
+// (modes 1/2, a GEMM with a bias-gradient ones column: column extra_col goes to
+//  extra[g * extra_gstride + r], accumulated when extra_acc, instead of out)
 struct ReduceOut {
   void* out;
   long long ldo, out_gstride;
   int cols, mode, relu;
   const float* bias;
   const bf16_t* gate;
+  float* extra;
+  long long extra_gstride;
+  int extra_col, extra_acc;
 };
 
 SN_DEV void reduce_store(const ReduceOut& o, int g, int r, int c, const float* acc) {
+  if (o.extra && c <= o.extra_col && o.extra_col < c + 4) {
+    float* e = o.extra + g * o.extra_gstride + r;
+    const int q = o.extra_col - c;
+    const float v = q == 0 ? acc[0] : (q == 1 ? acc[1] : (q == 2 ? acc[2] : acc[3]));
+    *e = o.extra_acc ? *e + v : v;
+  }
   if (o.mode == 0) {
     const long long base = g * o.out_gstride + (long long)r * o.ldo + c;
     bf16_t* p = reinterpret_cast<bf16_t*>(o.out) + base;
@@ -31,8 +42,9 @@ SN_DEV void reduce_store(const ReduceOut& o, int g, int r, int c, const float* a
     }
   } else {
     float* p = reinterpret_cast<float*>(o.out) + g * o.out_gstride + (long long)r * o.ldo + c;
+    const int cols = o.extra ? o.extra_col : o.cols;
     for (int k = 0; k < 4; ++k) {
-      if (c + k >= o.cols) break;
+      if (c + k >= cols) break;
       p[k] = (o.mode == 2 ? p[k] : 0.f) + acc[k];
     }
   }
@@ -72,7 +84,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_wide(const float* __restric
                                                           long long ws_gstride, ReduceOut o) {
   __shared__ float4 red[16][16];
   const int it = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int cols4 = o.cols >> 2;
+  const int cols4 = (o.cols + 3) >> 2;  // a ragged last float4 reads slab padding (ldw % 4 == 0)
   const long long total = (long long)rows * cols4;
   const long long i = blockIdx.x * 16LL + it;
   const int g = blockIdx.y;
@@ -114,12 +126,15 @@ extern "C" int sn_splitk_reduce(const float* ws, long long splits, long long sst
                                 long long cols, long long ldw, void* out, long long ldo, long long mode,
                                 const float* bias, long long relu, long long groups,
                                 long long ws_gstride, long long out_gstride, const bf16_t* gate,
+                                float* extra, long long extra_col, long long extra_acc, long long extra_gstride,
                                 hipStream_t st) {
   ReduceOut o;
   o.out = out; o.ldo = ldo; o.out_gstride = out_gstride; o.cols = (int)cols; o.mode = (int)mode;
   o.relu = (int)relu; o.bias = bias; o.gate = gate;
+  o.extra = extra; o.extra_col = (int)extra_col; o.extra_acc = (int)extra_acc; o.extra_gstride = extra_gstride;
+  if (extra && (mode == 0 || extra_col != cols - 1)) return 5;
   long long total = rows * ((cols + 3) / 4);
-  if (splits >= 16 && (cols & 3) == 0 && (ldw & 3) == 0) {
+  if (splits >= 16 && ((cols & 3) == 0 || ldw >= ((cols + 3) & ~3LL)) && (ldw & 3) == 0) {
     dim3 grid((unsigned)((total + 15) / 16), (unsigned)groups);
     hipLaunchKernelGGL(splitk_reduce_wide, grid, dim3(256), 0, st, ws, (int)splits, sstride, (int)rows, ldw,
                        ws_gstride, o);

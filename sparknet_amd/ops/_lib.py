@@ -42,7 +42,8 @@ class SnGemmArgs(C.Structure):
                 ("C", C.c_void_p), ("ldc", C.c_longlong), ("c_gstride", C.c_longlong),
                 ("c_split_stride", C.c_longlong),
                 ("bias", C.c_void_p), ("relu", C.c_int), ("tile", C.c_int), ("gate", C.c_void_p),
-                ("fp8", C.c_int), ("deq_a", C.c_void_p), ("deq_b", C.c_void_p), ("raster_n", C.c_int)]
+                ("fp8", C.c_int), ("deq_a", C.c_void_p), ("deq_b", C.c_void_p), ("raster_n", C.c_int),
+                ("ones_col", C.c_int), ("bias_out", C.c_void_p), ("bias_acc", C.c_int)]
 
 
 def lib_path(name: str = "libsn_kernels.so") -> Path:

@@ -159,16 +159,26 @@ def choose_splits(M: int, N: int, K: int, groups: int = 1, tile: int = 0) -> tup
 def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
          groups: int = 1, c_gstride: int = 0, bias: torch.Tensor | None = None, relu: bool = False,
          splits: int | None = None, gate: torch.Tensor | None = None,
-         deq: tuple[torch.Tensor, torch.Tensor] | None = None) -> None:
+         deq: tuple[torch.Tensor, torch.Tensor] | None = None,
+         bias_grad: torch.Tensor | None = None, bias_acc: bool = True) -> None:
     """Run one (possibly grouped, split-K) GEMM.  ``epi``: EPI_BF16 (store bf16 with
     bias/ReLU; ``gate``: a bf16 tensor laid out like ``out`` — outputs where gate <= 0
     are zeroed, i.e. a following slope-0 ReLU's backward), EPI_F32 (store), EPI_F32_ACC
-    (accumulate into an fp32 output)."""
+    (accumulate into an fp32 output).
+
+    ``bias_grad`` (fp32 [groups * M], weight-gradient products with an MC B operand and
+    N % 8 == 0): also compute sum_k A_g(m, k) — the bias gradient — through a virtual
+    ones column N of B, written (``bias_acc``: accumulated) into ``bias_grad[g*M + m]``."""
     if M == 0 or N == 0:
         return
     fp8 = deq is not None  # e4m3 operands; deq = (1/scale_A, 1/scale_B) device scalars
     sa, a_mc, a_mode = _operand(A, fp8)
     sb, b_mc, b_mode = _operand(B, fp8)
+    ones = -1
+    if bias_grad is not None:
+        assert epi in (EPI_F32, EPI_F32_ACC) and b_mc == 1 and b_mode != OP_FLIPW and N % 8 == 0 and not fp8
+        assert bias_grad.dtype == torch.float32 and bias_grad.is_contiguous() and bias_grad.numel() == groups * M
+        ones, N = N, N + 1
     tile = 0 if fp8 else (choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE) if _FORCE_TILE < 0 else _FORCE_TILE)
     bk = 128 if fp8 else BK
     if splits is None:
@@ -188,21 +198,25 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
     if gate is not None:
         assert epi == EPI_BF16 and gate.dtype == torch.bfloat16
         gp = gate.data_ptr()
+    bg = bias_grad.data_ptr() if bias_grad is not None else 0
     if splits == 1:
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, epi,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
-                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster)
+                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster,
+                               ones, bg, int(bias_acc))
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
         return
-    ws = torch.empty((groups, splits, M, N), dtype=torch.float32, device=out.device)
+    ldw = -(-N // 4) * 4  # fp32 slabs keep 16-B rows (the ones column makes N odd)
+    ws = torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
-                           sa, sb, ws.data_ptr(), N, splits * M * N, M * N, 0, 0, tile, 0, int(fp8), *dq, raster)
+                           sa, sb, ws.data_ptr(), ldw, splits * M * ldw, M * ldw, 0, 0, tile, 0, int(fp8), *dq, raster,
+                           ones, 0, 0)
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
-    _lib.call("splitk_reduce", ws, splits, M * N, M, N, N, out, ldc, mode, bias, int(relu),
-              groups, splits * M * N, c_gstride, gate)
+    _lib.call("splitk_reduce", ws, splits, M * ldw, M, N, ldw, out, ldc, mode, bias, int(relu),
+              groups, splits * M * ldw, c_gstride, gate, bias_grad, ones, int(bias_acc), M)
 
 
 # --- dense helpers ---------------------------------------------------------------------
@@ -266,22 +280,27 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = N
     return o
 
 
-def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool = True) -> None:
-    """dw[N,K] (+)= dy[M,N]^T @ x[M,K], fp32 output; both operands read along M."""
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool = True,
+                 db: torch.Tensor | None = None, db_acc: bool = True) -> bool:
+    """dw[N,K] (+)= dy[M,N]^T @ x[M,K], fp32 output; both operands read along M.  With
+    ``db`` the bias gradient db[N] (+)= sum_m dy[m, :] comes out of the same GEMM when the
+    shapes allow it; returns whether db was written."""
     M, N = dy.shape
     K = x.shape[1]
     dyp, xp = _pad8(dy, 1), _pad8(x, 1)
     Np, Kp = dyp.shape[1], xp.shape[1]
     if Np == N and Kp == K and dw.is_contiguous():
+        fuse = db is not None and db.is_contiguous() and db.dtype == torch.float32
         gemm(N, K, M, Dense(dyp, Np, False), Dense(xp, Kp, False), dw, K,
-             epi=EPI_F32_ACC if accumulate else EPI_F32)
-        return
+             epi=EPI_F32_ACC if accumulate else EPI_F32, bias_grad=db if fuse else None, bias_acc=db_acc)
+        return fuse
     tmp = torch.zeros((Np, Kp), dtype=torch.float32, device=dw.device)
     gemm(Np, Kp, M, Dense(dyp, Np, False), Dense(xp, Kp, False), tmp, Kp, epi=EPI_F32)
     if accumulate:
         dw.add_(tmp[:N, :K])
     else:
         dw.copy_(tmp[:N, :K])
+    return False
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = True) -> None:

@@ -139,10 +139,14 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
     x = _c(x)
     M = s.N * s.P * s.Q
     dy2 = dy.view(M, s.K)
-    if db is not None:
-        colsum(dy2, db, accumulate=db_acc)
     kred = s.R * s.S * s.Cg
     plan = _s2d_plan(s) if s.Kg % 8 == 0 else None
+    # the bias gradient rides on the weight-gradient GEMM (ones column) on its implicit
+    # paths; otherwise (no dw, explicit im2col) it is a separate column sum
+    fused_db = db is not None and dw is not None and (
+        plan is not None or (_implicit_ok(s) and s.Kg % 8 == 0))
+    if db is not None and not fused_db:
+        colsum(dy2, db, accumulate=db_acc)
     if dw is not None and plan is not None:
         f, cp, rf, sf, s2 = plan
         cached = ws.get("s2d") if ws is not None else None
@@ -153,7 +157,7 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
         k2 = rf * sf * s2.C
         dw2 = torch.empty((s.K, k2), dtype=torch.float32, device=x.device)
         gemm(s.K, k2, M, Dense(dy2, s.K, kcontig=False), Im2col(x2, _geom(s2), kcontig=False), dw2, k2,
-             epi=EPI_F32)
+             epi=EPI_F32, bias_grad=db if fused_db else None, bias_acc=db_acc)
         call("s2d_weight_grad", dw2, dw, s.K, s.R, s.S, s.C, f, cp, rf, sf, int(dw_acc))
         dw = None
     if dw is not None:
@@ -161,7 +165,7 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
             A = Dense(dy2, s.K, kcontig=False, gstride=s.Kg)
             B = Im2col(x, _geom(s), kcontig=False, gstride=s.Cg)
             gemm(s.Kg, kred, M, A, B, dw, kred, epi=EPI_F32_ACC if dw_acc else EPI_F32, groups=s.groups,
-                 c_gstride=s.Kg * kred)
+                 c_gstride=s.Kg * kred, bias_grad=db if fused_db else None, bias_acc=db_acc)
         else:
             kpad = _round8(kred)
             kgp = _round8(s.Kg)
@@ -225,10 +229,12 @@ def linear_forward(x2, w, b, relu=False):
 
 def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=True, db_acc=True):
     dy2 = _c(dy2)
-    if db is not None:
-        colsum(dy2, db, accumulate=db_acc)
     if dw is not None:
-        linear_wgrad(dy2, _c(x2), dw, accumulate=dw_acc)
+        # the bias gradient comes out of the weight-gradient GEMM when it can (ones column)
+        if not linear_wgrad(dy2, _c(x2), dw, accumulate=dw_acc, db=db, db_acc=db_acc) and db is not None:
+            colsum(dy2, db, accumulate=db_acc)
+    elif db is not None:
+        colsum(dy2, db, accumulate=db_acc)
     if not need_dx:
         return None
     return linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)

@@ -83,6 +83,23 @@ def test_forced_splitk_epilogues(gpu, splits):
     _close(acc, 1 + ref)
 
 
+@pytest.mark.parametrize("splits", [1, 2, 20])
+@pytest.mark.parametrize("acc", [True, False])
+@pytest.mark.parametrize("M,N,K", [(96, 432, 64 * 40), (200, 64, 1000), (48, 1200, 333)])
+def test_wgrad_bias_column(gpu, splits, acc, M, N, K):
+    """Weight-gradient TN product with the virtual ones column: dw = A^T-sum and the bias
+    gradient (row sums of A) from one GEMM, unsplit and through both reduce kernels."""
+    from sparknet_amd.ops import gemm as G
+    a, b = _bf(K, M, device=gpu), _bf(K, N, device=gpu)  # A: [K][M] (MC), B: [K][N] (MC)
+    dw = torch.full((M, N), 3.0, device=gpu)
+    db = torch.full((M,), -2.0, device=gpu)
+    G.gemm(M, N, K, G.Dense(a, M, False), G.Dense(b, N, False), dw, N, epi=G.EPI_F32_ACC if acc else G.EPI_F32,
+           splits=splits, bias_grad=db, bias_acc=acc)
+    base = 3.0 if acc else 0.0
+    _close(dw, base + a.float().t() @ b.float(), 1e-2)
+    _close(db, (-2.0 if acc else 0.0) + a.float().sum(0), 1e-3)
+
+
 def test_linear_dgrad_gate(gpu):
     from sparknet_amd.ops import gemm
     dy, w = _bf(256, 512, device=gpu), _bf(512, 384, device=gpu)

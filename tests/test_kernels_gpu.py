@@ -63,6 +63,25 @@ def test_conv(gpu, case):
     close(db, db_r, 1e-3, what="bias")
 
 
+@pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[2], CONV_CASES[4], CONV_CASES[10]])
+def test_conv_grad_overwrite(gpu, case):
+    """dw_acc / db_acc False (lazily cleared gradients): both are overwritten, including
+    the bias gradient produced by the wgrad GEMM's ones column."""
+    from sparknet_amd.ops import hip
+    N, H, W, Cc, K, R, S, st, pd, g = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    x = rnd(N, H, W, Cc)
+    w = rnd(K, R, S, Cc // g, scale=0.2)
+    dy = rnd(N, s.P, s.Q, K)
+    dw = torch.full((K, R, S, Cc // g), 7.0, device="cuda")
+    db = torch.full((K,), 7.0, device="cuda")
+    hip.conv_backward(dy, x, w, s, False, dw, db, dw_acc=False, db_acc=False)
+    dw_r, db_r = torch.zeros_like(dw), torch.zeros_like(db)
+    ref.conv_backward(dy, x, w, s, False, dw_r, db_r)
+    close(dw, dw_r, what="wgrad")
+    close(db, db_r, 1e-3, what="bias")
+
+
 @pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[8]])
 def test_conv_dgrad_inplace_weights(gpu, case, monkeypatch):
     """dgrad reading W through the FLIPW operand (no flip pass) == the reference."""
