@@ -101,10 +101,14 @@ def main():
 
     t0 = time.perf_counter()
     loss = None
+    averaged = False
     for k in range(args.steps):
         loss = trainer.local_step()
-        if (k + 1) % args.tau == 0:
+        # every tau-th step averages; a timed window shorter than tau still ends with one
+        # average so the collective is always inside the measurement
+        if (k + 1) % args.tau == 0 or (k == args.steps - 1 and not averaged):
             trainer.average()
+            averaged = True
     if comm is not None:
         comm.barrier()
     torch.cuda.synchronize(dev)

@@ -10,8 +10,10 @@
 //  * Sum of bf16 tensors (Split backward / gradient accumulation).
 //  * im2col (explicit, for convs whose per-group channel count is not a multiple of 8 —
 //    i.e. the 3-channel input layer), col2im (stride>1 dgrad), weight flip-transpose
-//    (turns dgrad into a forward implicit-GEMM conv).
+//    (turns dgrad into a forward implicit-GEMM conv), batched over a net's layers.
 #include "common.h"
+
+#include <cstring>
 
 // ---------------- ReLU ----------------
 __global__ void relu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8, float slope) {
@@ -259,6 +261,63 @@ extern "C" int sn_flip_weights(const bf16_t* w, bf16_t* wt, long long G, long lo
   long long total = G * Kg * R * S * Cg;
   hipLaunchKernelGGL(flip_weights, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, w, wt, (int)G, (int)Kg,
                      (int)R, (int)S, (int)Cg);
+  return SN_CHECK_LAUNCH();
+}
+
+// The same flip for every stride-1 convolution of a net in ONE launch (blockIdx.y =
+// layer), run once at the start of backward: the weights are final for the iteration
+// there, and one launch replaces a launch boundary per layer.  32-bit index decode with
+// multiply-high division; one thread per OUTPUT element (coalesced stores, the scattered
+// 2-B reads of a <= 2 MB weight tensor hit L2).
+struct FlipDesc {
+  const bf16_t* w;
+  bf16_t* wt;
+  int total, Kg, R, S;
+  FDiv fKg, fS, fR, fCg;
+};
+
+__global__ void flip_weights_multi(const FlipDesc* __restrict__ descs) {
+  const FlipDesc d = descs[blockIdx.y];
+  const int Cg = (int)d.fCg.d, RS = d.R * d.S;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < d.total; o += gridDim.x * blockDim.x) {
+    // o = (((g*Cg + c)*R + rf)*S + sf)*Kg + k
+    uint32_t t = udiv((uint32_t)o, d.fKg);
+    const int k = o - (int)t * d.Kg;
+    uint32_t t2 = udiv(t, d.fS);
+    const int sf = (int)(t - t2 * d.S);
+    t = udiv(t2, d.fR);
+    const int rf = (int)(t2 - t * d.R);
+    t2 = udiv(t, d.fCg);
+    const int c = (int)(t - t2 * Cg), g = (int)t2;
+    const int i = ((g * d.Kg + k) * RS + (d.R - 1 - rf) * d.S + (d.S - 1 - sf)) * Cg + c;
+    d.wt[o] = d.w[i];
+  }
+}
+
+// descs: device array of n FlipDesc built by sn_flip_desc (host) and uploaded once.
+extern "C" int sn_flip_desc_size() { return (int)sizeof(FlipDesc); }
+
+extern "C" int sn_flip_desc(void* out, const bf16_t* w, bf16_t* wt, long long G, long long Kg, long long R,
+                            long long S, long long Cg) {
+  FlipDesc d;
+  d.w = w;
+  d.wt = wt;
+  d.total = (int)(G * Kg * R * S * Cg);
+  d.Kg = (int)Kg;
+  d.R = (int)R;
+  d.S = (int)S;
+  d.fKg = make_fdiv((uint32_t)Kg);
+  d.fS = make_fdiv((uint32_t)S);
+  d.fR = make_fdiv((uint32_t)R);
+  d.fCg = make_fdiv((uint32_t)Cg);
+  memcpy(out, &d, sizeof d);
+  return 0;
+}
+
+extern "C" int sn_flip_weights_multi(const void* descs, long long n, long long max_total, hipStream_t st) {
+  if (n <= 0) return 0;
+  dim3 grid(sn_blocks(max_total, 256, 4096), (unsigned)n);
+  hipLaunchKernelGGL(flip_weights_multi, grid, dim3(256), 0, st, reinterpret_cast<const FlipDesc*>(descs));
   return SN_CHECK_LAUNCH();
 }
 

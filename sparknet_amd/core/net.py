@@ -214,6 +214,7 @@ class Net:
         self.bottom_vecs: list[list[Blob]] = []
         self.top_vecs: list[list[Blob]] = []
         self.backward_hooks: list = []  # callables(layer_index) run after each layer's backward
+        self.pre_backward_hooks: list = []  # callables() run before the first layer's backward
         self.bottom_ids: list[list[int]] = []
         self.top_ids: list[list[int]] = []
         self.bottom_need_backward: list[list[bool]] = []
@@ -452,6 +453,10 @@ class Net:
             layer.forward(self.bottom_vecs[li], self.top_vecs[li])
             if self.debug_info:
                 self._debug_forward(li)
+        if len(self._loss_tops) == 1 and self._loss_tops[0][1] == 1.0:
+            t = self._loss_tops[0][0].data
+            if t.numel() == 1 and t.dtype == torch.float32:
+                return t.reshape(())  # the usual single unit-weight loss: no extra kernel
         for t, w in self._loss_tops:
             v = t.data.float()
             v = v.sum() * w if v.numel() > 1 else v.reshape(()) * w
@@ -466,11 +471,21 @@ class Net:
         return self.forward_from_to(0, len(self.layers) - 1)
 
     def prefill_loss_diffs(self) -> None:
+        """Top diff of every loss blob = its loss weight (Layer::SetLossWeights).  The fill
+        is skipped while the diff tensor still holds it (same tensor, no in-place write
+        since), so a captured training step carries no fill kernel."""
+        done = self.__dict__.setdefault("_loss_diff_filled", {})
         for t, w in self._loss_tops:
-            t.diff.fill_(w)
+            d = t.diff
+            key = (id(d), d.data_ptr(), d._version, w)
+            if done.get(id(t)) != key:
+                d.fill_(w)
+                done[id(t)] = (id(d), d.data_ptr(), d._version, w)
 
     def backward_from_to(self, start: int, end: int) -> None:
         self.prefill_loss_diffs()
+        for hook in self.pre_backward_hooks:  # e.g. batched dgrad weight flips
+            hook()
         for li in range(start, end - 1, -1):
             if self.layer_need_backward[li]:
                 self.layers[li].backward(self.top_vecs[li], self.bottom_need_backward[li],

@@ -45,7 +45,35 @@ def fuse_relu(net) -> int:
         relu.fused = True
         n += 1
     fuse_relu_backward(net)
+    batch_weight_flips(net)
     return n
+
+
+def batch_weight_flips(net) -> int:
+    """Flip-transpose the dgrad weights of every stride-1 convolution in ONE launch at
+    the start of backward (ops.hip.FlipBatch) instead of one flip launch per layer inside
+    its backward.  GPU only; idempotent; returns the number of layers covered."""
+    if net.device.type != "cuda" or getattr(net, "_flip_batch", None) is not None:
+        return 0
+    from .ops import hip
+    items = []
+    for li, layer in enumerate(net.layers):
+        if layer.type_name != "Convolution" or not net.layer_need_backward[li]:
+            continue
+        if not any(net.bottom_need_backward[li]):
+            continue
+        specs = [layer.spec(b) for b in net.bottom_vecs[li]]
+        if not all(hip.dgrad_uses_flip(s) for s in specs):
+            continue
+        s = specs[0]
+        wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=torch.bfloat16, device=net.device)
+        items.append((layer.weight.compute, wt, s.groups, s.Kg, s.R, s.S, s.Cg))
+        layer.flipped_weights = wt
+    if not items:
+        return 0
+    net._flip_batch = hip.FlipBatch(items, net.device)
+    net.pre_backward_hooks.append(net._flip_batch.run)
+    return len(items)
 
 
 _GATE_CONSUMERS = ("Convolution", "InnerProduct", "Dropout", "Pooling")

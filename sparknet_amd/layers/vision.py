@@ -49,6 +49,7 @@ class ConvolutionLayer(Layer):
     fuse_relu = False  # set by the net's fusion pass when an in-place ReLU follows
     relu_gate = False  # ... and when an in-place ReLU PRODUCES the bottom (backward fused into dgrad)
     folded_input = None  # S2D-folded bottom 0 written by a fused augment (engine.fuse_input_fold)
+    flipped_weights = None  # dgrad weights flipped at the start of backward (engine.batch_weight_flips)
 
     def layer_setup(self, bottoms, tops):
         cp = self.lp.convolution_param
@@ -127,6 +128,9 @@ class ConvolutionLayer(Layer):
             s = self.spec(b)
             gate = b.data if self.relu_gate else None
             ws = self._ws[i] if i < len(getattr(self, "_ws", ())) else None
+            if self.flipped_weights is not None:  # flipped for the whole net (engine.batch_weight_flips)
+                ws = {} if ws is None else ws
+                ws["wt"] = self.flipped_weights
             dw_acc = not (dw is not None and self.grad_overwrite(0))
             db_acc = not (db is not None and self.grad_overwrite(1))
             dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws,

@@ -123,6 +123,48 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None):
     return y
 
 
+def dgrad_uses_flip(s: ConvSpec) -> bool:
+    """Does conv_backward compute this conv's data gradient as a forward conv over
+    flip-transposed weights (the path FlipBatch pre-computes the weights for)?"""
+    return (s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0
+            and not DGRAD_INPLACE_WEIGHTS)
+
+
+class FlipBatch:
+    """Flip-transpose the weights of several convolutions in ONE launch
+    (flip_weights_multi): items are (w, wt, G, Kg, R, S, Cg) with w the bf16 compute
+    weights [K][R][S][Cg] and wt the persistent [G][Cg][R][S][Kg] output.  The device
+    descriptor table holds raw pointers, so run() re-checks them on the host and rebuilds
+    the table if a tensor was re-allocated."""
+
+    def __init__(self, items, device):
+        self.items = list(items)
+        self.device = torch.device(device)
+        self._build()
+
+    def _ptrs(self):
+        return [(w.data_ptr(), wt.data_ptr()) for w, wt, *_ in self.items]
+
+    def _build(self):
+        lib = _lib.kernels()
+        lib.sn_flip_desc_size.restype = C.c_int
+        size = lib.sn_flip_desc_size()
+        buf = (C.c_char * (size * len(self.items)))()
+        for i, (w, wt, G, Kg, R, S, Cg) in enumerate(self.items):
+            assert w.is_contiguous() and wt.is_contiguous() and w.dtype == BF16 and wt.dtype == BF16
+            assert w.numel() == wt.numel() == G * Kg * R * S * Cg < (1 << 31)
+            lib.sn_flip_desc(C.byref(buf, i * size), C.c_void_p(w.data_ptr()), C.c_void_p(wt.data_ptr()),
+                             *(C.c_longlong(v) for v in (G, Kg, R, S, Cg)))
+        self.descs = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(self.device)
+        self.max_total = max(w.numel() for w, *_ in self.items)
+        self.ptrs = self._ptrs()
+
+    def run(self) -> None:
+        if self._ptrs() != self.ptrs:
+            self._build()
+        call("flip_weights_multi", self.descs, len(self.items), self.max_total)
+
+
 def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
     out = torch.zeros((t2.shape[0], n), dtype=t2.dtype, device=t2.device)
     out[:, :t2.shape[1]].copy_(t2)
@@ -192,11 +234,15 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
         g2 = ConvGeom(s.N, s.P, s.Q, s.K, s.H, s.W, s.R, s.S, 1, 1, s.R - 1 - s.ph, s.S - 1 - s.pw, 1, 1, s.Kg)
         kr2 = s.R * s.S * s.Kg
         A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
+        pre = ws.get("wt") if ws is not None else None  # flipped once for the net (FlipBatch)
         if DGRAD_INPLACE_WEIGHTS:
             B = FlipW(_c(w), s.Kg, s.R, s.S, s.Cg)
         else:
-            wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
-            call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
+            if pre is not None:
+                wt = pre
+            else:
+                wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
+                call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
             B = Dense(wt.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
         gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg,
              gate=_c(gate) if gate is not None else None)

@@ -82,6 +82,32 @@ def test_conv_grad_overwrite(gpu, case):
     close(db, db_r, 1e-3, what="bias")
 
 
+def test_flip_batch_matches_single_flips(gpu):
+    """One flip_weights_multi launch == the per-layer flip_weights kernel, incl. after a
+    re-allocation of an input (descriptor table rebuilt)."""
+    from sparknet_amd.ops import _lib, hip
+    shapes = [(2, 128, 5, 5, 48), (1, 384, 3, 3, 256), (2, 192, 3, 3, 192), (1, 24, 1, 1, 32)]
+    items, refs = [], []
+    for G, Kg, R, S, Cg in shapes:
+        w = rnd(G * Kg, R, S, Cg)
+        wt = torch.empty((G, Cg, R, S, Kg), dtype=torch.bfloat16, device="cuda")
+        r = torch.empty_like(wt)
+        _lib.call("flip_weights", w, r, G, Kg, R, S, Cg)
+        items.append((w, wt, G, Kg, R, S, Cg))
+        refs.append(r)
+    fb = hip.FlipBatch(items, "cuda")
+    fb.run()
+    for (_, wt, *_), r in zip(items, refs):
+        assert torch.equal(wt, r)
+    w2 = rnd(*items[0][0].shape)
+    items[0] = (w2,) + items[0][1:]
+    fb.items = items
+    fb.run()
+    r0 = torch.empty_like(refs[0])
+    _lib.call("flip_weights", w2, r0, *shapes[0])
+    assert torch.equal(items[0][1], r0)
+
+
 @pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[8]])
 def test_conv_dgrad_inplace_weights(gpu, case, monkeypatch):
     """dgrad reading W through the FLIPW operand (no flip pass) == the reference."""
