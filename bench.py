@@ -37,6 +37,8 @@ def parse():
                    help="fp8: e4m3 forward products with per-tensor delayed scaling (bf16 backward)")
     p.add_argument("--overlap-update", action="store_true",
                    help="run large layers' solver updates on a side stream during backward")
+    p.add_argument("--no-fuse-fc", action="store_true",
+                   help="store InnerProduct weight gradients and update them in the solver kernel")
     p.add_argument("--profile-steps", type=int, default=0)
     return p.parse_args()
 
@@ -86,7 +88,7 @@ def main():
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
     n_fp8 = enable_fp8(net) if args.dtype == "fp8" else 0
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph,
-                              overlap_update=args.overlap_update)
+                              overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc)
     trainer.broadcast_initial()
 
     # warmup (includes hipGraph capture and one averaging collective to set up RCCL)

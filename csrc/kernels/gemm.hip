@@ -38,7 +38,7 @@ constexpr int BK = 64, NTHR = 256;
 // row k = tap * Kg + kout, col = c  ->  W[g*Kg + kout][R-1-r][S-1-s][c]  (flipped taps,
 // transposed channels) with geometry fields R, S, Cg and C := Kg — no flip pass over W.
 enum { OP_DENSE = 0, OP_IM2COL = 1, OP_FLIPW = 2 };
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_SGD = 3 };
 
 }  // namespace
 
@@ -82,6 +82,17 @@ struct SnGemmArgs {
   int ones_col;       // -1: none
   float* bias_out;
   int bias_acc;
+  // EPI_SGD (InnerProduct weight gradient, unsplit TN product): instead of storing the
+  // gradient, apply the solver update to it in the epilogue — Caffe's ComputeUpdateValue
+  // + Blob::Update (sgd_solver.cpp:207-239, nesterov_solver.cpp:8-69) on the fp32 master
+  // w[m*ldc + n], history h, and the bf16 compute shadow; hyper-parameters are read from
+  // the solver's device tensor (same layout as solver.hip).  sgd_flags: 1 Nesterov, 2 L1.
+  float* sgd_w;
+  float* sgd_h;
+  bf16_t* sgd_shadow;
+  const float* sgd_hyper;
+  float sgd_lr_mult, sgd_decay_mult;
+  int sgd_flags;
 };
 
 }  // extern "C"
@@ -466,6 +477,51 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
   // fp32 outputs: the bias-gradient column (when routed to bias_out) is not part of C
   const int c_cols = (EPI != EPI_BF16 && args.bias_out) ? args.ones_col : args.N;
+  if constexpr (EPI == EPI_SGD) {
+    // Interior tiles: issue every master-weight / history load of the wave's 64x64 sub-tile
+    // first (32 x 16 B per lane in flight), then update and store — a load -> update ->
+    // store chain per fragment would expose the HBM latency 16 times.  Edge tiles and
+    // the bias column take the per-fragment path below.
+    const bool interior = m_blk + BM <= args.M && n_blk + BN <= c_cols && (args.ldc & 3) == 0 &&
+                          ((grp * args.c_gstride) & 3) == 0;
+    if (interior) {
+      const float* hy = args.sgd_hyper;
+      const float rate = hy[0] * args.sgd_lr_mult, mom = hy[1], decay = hy[2] * args.sgd_decay_mult;
+      const float gscale = hy[4];
+      float4 Wv[4][NFR], Av[4][NFR];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) {
+          const long long o = grp * args.c_gstride + (long long)(m_blk + wm0 + 16 * j + mrow_l) * args.ldc +
+                              n_blk + wn0 + 16 * i + ncol_l;
+          Wv[j][i] = *reinterpret_cast<const float4*>(args.sgd_w + o);
+          Av[j][i] = *reinterpret_cast<const float4*>(args.sgd_h + o);
+        }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) {
+          const long long o = grp * args.c_gstride + (long long)(m_blk + wm0 + 16 * j + mrow_l) * args.ldc +
+                              n_blk + wn0 + 16 * i + ncol_l;
+          float W[4] = {Wv[j][i].x, Wv[j][i].y, Wv[j][i].z, Wv[j][i].w};
+          float A[4] = {Av[j][i].x, Av[j][i].y, Av[j][i].z, Av[j][i].w};
+          const f32x4 v = acc[i][j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float gg = v[r] * gscale;
+            gg += decay * ((args.sgd_flags & 2) ? (float)((W[r] > 0.f) - (W[r] < 0.f)) : W[r]);
+            const float prev = A[r];
+            A[r] = mom * A[r] + rate * gg;
+            W[r] -= (args.sgd_flags & 1) ? (1.f + mom) * A[r] - mom * prev : A[r];
+          }
+          *reinterpret_cast<float4*>(args.sgd_w + o) = make_float4(W[0], W[1], W[2], W[3]);
+          *reinterpret_cast<float4*>(args.sgd_h + o) = make_float4(A[0], A[1], A[2], A[3]);
+          *reinterpret_cast<uint2*>(args.sgd_shadow + o) = make_uint2(pack2(W[0], W[1]), pack2(W[2], W[3]));
+        }
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int m = m_blk + wm0 + 16 * j + mrow_l;
@@ -522,6 +578,50 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
           *bp = args.bias_acc ? *bp + bv : bv;
         }
         if (n >= c_cols) continue;
+        if (EPI == EPI_SGD) {
+          // H_LR = 0, H_MOM = 1, H_WD = 2, H_NORM = 4 (solver.hip); same op order as
+          // solver_update_kernel KIND 0 / 1 so both paths give identical weights
+          const float* hy = args.sgd_hyper;
+          const float rate = hy[0] * args.sgd_lr_mult, mom = hy[1], decay = hy[2] * args.sgd_decay_mult;
+          const float gscale = hy[4];
+          const long long o = grp * args.c_gstride + (long long)m * args.ldc + n;
+          const bool vec = (n + 3 < c_cols) && ((args.ldc & 3) == 0) && ((o & 3) == 0);
+          float W[4], A[4];
+          if (vec) {
+            const float4 w4 = *reinterpret_cast<const float4*>(args.sgd_w + o);
+            const float4 a4 = *reinterpret_cast<const float4*>(args.sgd_h + o);
+            W[0] = w4.x; W[1] = w4.y; W[2] = w4.z; W[3] = w4.w;
+            A[0] = a4.x; A[1] = a4.y; A[2] = a4.z; A[3] = a4.w;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              W[r] = n + r < c_cols ? args.sgd_w[o + r] : 0.f;
+              A[r] = n + r < c_cols ? args.sgd_h[o + r] : 0.f;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float gg = v[r] * gscale;
+            gg += decay * ((args.sgd_flags & 2) ? (float)((W[r] > 0.f) - (W[r] < 0.f)) : W[r]);
+            const float prev = A[r];
+            A[r] = mom * A[r] + rate * gg;
+            W[r] -= (args.sgd_flags & 1) ? (1.f + mom) * A[r] - mom * prev : A[r];
+          }
+          if (vec) {
+            *reinterpret_cast<float4*>(args.sgd_w + o) = make_float4(W[0], W[1], W[2], W[3]);
+            *reinterpret_cast<float4*>(args.sgd_h + o) = make_float4(A[0], A[1], A[2], A[3]);
+            *reinterpret_cast<uint2*>(args.sgd_shadow + o) = make_uint2(pack2(W[0], W[1]), pack2(W[2], W[3]));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < c_cols) {
+                args.sgd_w[o + r] = W[r];
+                args.sgd_h[o + r] = A[r];
+                args.sgd_shadow[o + r] = f2bf(W[r]);
+              }
+          }
+          continue;
+        }
         float* C = reinterpret_cast<float*>(args.C) + split * args.c_split_stride + grp * args.c_gstride +
                    (long long)m * args.ldc;
         if (full) {
@@ -573,6 +673,12 @@ int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, a.splits, a.groups);
   const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  if (a.epi == EPI_SGD) {  // fused solver update: InnerProduct weight gradient (TN dense) only
+    if (key != 0b1010 || a.splits != 1 || !a.sgd_w || !a.sgd_h || !a.sgd_shadow || !a.sgd_hyper) return 6;
+    hipLaunchKernelGGL((gemm_kernel<1, OP_DENSE, 1, OP_DENSE, EPI_SGD, BM, BN, NW, NS>), grid, dim3(NW * 64), 0, stream,
+                       a);
+    return SN_CHECK_LAUNCH();
+  }
   switch (key) {
     case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, BM, BN, NW, NS>(a, grid, stream);   // NT dense
     case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, BM, BN, NW, NS>(a, grid, stream);  // conv fwd/dgrad

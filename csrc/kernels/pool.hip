@@ -275,6 +275,76 @@ __global__ void pool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restr
   }
 }
 
+// 3x3 / stride-2 windows (AlexNet / CaffeNet / GoogLeNet pools): in padded coordinates
+// (hp = h + ph) input rows 2b and 2b+1 are covered by windows {b-1, b} and {b}, so ONE
+// thread handles a 2x2 block of input pixels from the same 4 windows — a quarter of the
+// window loads of the per-pixel gather above (which is L2-bandwidth bound: every window
+// is re-read by the ~4 pixels it covers).
+template <bool MAX>
+__global__ void pool_bwd_k3s2(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+                              bf16_t* __restrict__ dx, PoolGeom g, FDiv fBW, FDiv fBH, int BW, int BH) {
+  const int cv = g.C / 8;
+  const long long total = (long long)g.N * BH * BW * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t blk = udiv((uint32_t)i, g.fcv), bh_ = udiv(blk, fBW), n = udiv(bh_, fBH);
+    const int c0 = (int)((uint32_t)i - blk * cv) * 8;
+    const int bw = (int)(blk - bh_ * BW), bh = (int)(bh_ - n * BH);
+    uint4 dv[4];
+    uint2 mv[4];
+    bool ok[4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int p = bh - 1 + a, q = bw - 1 + b, t = a * 2 + b;
+        ok[t] = p >= 0 && p < g.P && q >= 0 && q < g.Q;
+        const int pc = min(max(p, 0), g.P - 1), qc = min(max(q, 0), g.Q - 1);
+        const long long o = (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0;
+        dv[t] = *reinterpret_cast<const uint4*>(dy + o);
+        if (MAX) mv[t] = *reinterpret_cast<const uint2*>(mask + o);
+      }
+    float f[4][8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) unpack8(dv[t], f[t]);
+    float scale[4] = {1.f, 1.f, 1.f, 1.f};
+    if (!MAX) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int p = bh - 1 + (t >> 1), q = bw - 1 + (t & 1);
+        const int hs = 2 * p - g.ph, ws = 2 * q - g.pw;
+        const int he = min(hs + 3, g.H + g.ph), we = min(ws + 3, g.W + g.pw);
+        scale[t] = ok[t] ? 1.f / (float)((he - hs) * (we - ws)) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int h = 2 * bh + a - g.ph, w = 2 * bw + b - g.pw;
+        if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int wa = t >> 1, wb = t & 1;  // window p = bh-1+wa covers row a iff wa == 1 or a == 0
+          if ((wa == 0 && a == 1) || (wb == 0 && b == 1)) continue;
+          if (MAX) {
+            // window-relative offset of this pixel: row (2bh+a) - 2p = a + 2(1-wa)
+            const int widx = (a + 2 * (1 - wa)) * 3 + (b + 2 * (1 - wb));
+            const uint32_t mw[2] = {mv[t].x, mv[t].y};
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (ok[t] && (int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == widx) acc[k] += f[t][k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += f[t][k] * scale[t];
+          }
+        }
+        *reinterpret_cast<uint4*>(dx + (((long long)n * g.H + h) * g.W + w) * g.C + c0) = pack8(acc);
+      }
+  }
+}
+
 static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long long P, long long Q, long long kh,
                        long long kw, long long sh, long long sw, long long ph, long long pw) {
   PoolGeom g;
@@ -319,7 +389,18 @@ extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, lo
   long long total = N * H * W * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
   const long long nh = (kh + sh - 1) / sh, nw = (kw + sw - 1) / sw;
-  if (vec && nh == nw && nh >= 1 && nh <= 3) {
+  if (vec && kh == 3 && kw == 3 && sh == 2 && sw == 2) {
+    // 2x2 input pixels per thread over the padded extent [0, H + ph) x [0, W + pw)
+    const int BH = (int)((H + ph + 1) / 2), BW = (int)((W + pw + 1) / 2);
+    const long long nt = N * BH * BW * (C / 8);
+    dim3 g2(sn_blocks(nt, 256, 16384));
+    if (method == 0)
+      hipLaunchKernelGGL((pool_bwd_k3s2<true>), g2, dim3(256), 0, st, dy, mask, dx, g, make_fdiv((uint32_t)BW),
+                         make_fdiv((uint32_t)BH), BW, BH);
+    else
+      hipLaunchKernelGGL((pool_bwd_k3s2<false>), g2, dim3(256), 0, st, dy, mask, dx, g, make_fdiv((uint32_t)BW),
+                         make_fdiv((uint32_t)BH), BW, BH);
+  } else if (vec && nh == nw && nh >= 1 && nh <= 3) {
 #define SN_POOL_BWD_K(NN)                                                                             \
   do {                                                                                                \
     if (method == 0) hipLaunchKernelGGL((pool_bwd_k<NN, NN, true>), grid, dim3(256), 0, st, dy, mask, dx, g);  \

@@ -128,11 +128,21 @@ class Solver:
         self._build_tables()
 
     def _build_tables(self) -> None:
-        """Chunk table for the fused update kernel: (start, count, lr_mult, decay_mult)."""
+        """Chunk table for the fused update kernel: (start, count, lr_mult, decay_mult).
+        Params updated inside their layer's backward (set_fused_update) are left out."""
         from .. import ops
         segs = self.net.param_segments()
         self.segments = segs
-        self._tables = ops.solver_tables(segs, self.net.num_param_elems, self.device)
+        fused = getattr(self, "fused_offsets", set())
+        self._tables = ops.solver_tables([s for s in segs if s[0] not in fused], self.net.num_param_elems,
+                                         self.device)
+
+    def set_fused_update(self, offsets) -> None:
+        """Declare params whose solver update runs in their layer's weight-gradient GEMM
+        epilogue (engine.fuse_fc_updates); hyper-parameters are then staged before the
+        forward pass, since that update reads them during backward."""
+        self.fused_offsets = set(offsets)
+        self._build_tables()
 
     # -- learning rate (SGDSolver::GetLearningRate) ------------------------------------
     def get_learning_rate(self) -> float:
@@ -243,6 +253,8 @@ class Solver:
     def iteration(self):
         """One training iteration minus bookkeeping: returns the device loss."""
         net = self.net
+        if getattr(self, "fused_offsets", None):
+            self.stage_hyper()  # the in-backward (fused) updates read this iteration's rate
         net.clear_param_diffs(lazy=True)
         for cb in self.callbacks:
             getattr(cb, "on_start", lambda: None)()

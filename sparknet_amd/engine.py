@@ -113,6 +113,53 @@ def fuse_relu_backward(net) -> int:
     return n
 
 
+class _FusedFCUpdate:
+    """The solver state an InnerProduct layer needs to apply its weight update in the
+    wgrad GEMM epilogue (resolved at call time, so re-allocated buffers are followed)."""
+
+    def __init__(self, solver, param, flags: int):
+        self.solver, self.p, self.flags = solver, param, flags
+
+    def sgd(self) -> dict:
+        p = self.p
+        h = self.solver.history[0][p.offset:p.offset + p.count].view(p.data.shape)
+        return {"w": p.data, "h": h, "shadow": p.compute, "hyper": self.solver.hyper, "lr_mult": p.lr_mult,
+                "decay_mult": p.decay_mult, "flags": self.flags}
+
+
+def fuse_fc_updates(solver) -> int:
+    """Apply the SGD / Nesterov update of InnerProduct weights inside their weight-gradient
+    GEMM (EPI_SGD epilogue): the gradient is consumed where it is produced instead of
+    being written to the flat gradient buffer and read back by the solver kernel
+    (CaffeNet: 58.6 M of 61 M parameters, 8 B/param of HBM traffic saved).  Caffe applies
+    the update after the whole backward pass (solver.cpp:237-240); per parameter the
+    arithmetic is identical.  Requires what OverlappedUpdate requires (no clipping, no
+    iter_size accumulation, no gradient callbacks) plus unshared weights with channel
+    counts % 8 == 0.  Returns the number of fused layers."""
+    net = solver.net
+    if net.device.type != "cuda" or not solver.overlap_eligible() or solver.type not in ("SGD", "Nesterov"):
+        return 0
+    if net.flat_compute is net.flat_data or solver.param.regularization_type not in ("L1", "L2"):
+        return 0
+    users: dict = {}
+    for layer in net.layers:
+        for p in layer.params:
+            users[p.offset] = users.get(p.offset, 0) + 1
+    flags = (1 if solver.type == "Nesterov" else 0) | (2 if solver.param.regularization_type == "L1" else 0)
+    offsets = []
+    for li, layer in enumerate(net.layers):
+        if layer.type_name != "InnerProduct" or not net.layer_need_backward[li] or not layer.param_grads_needed(0):
+            continue
+        p = layer.weight
+        if p.owner is not None or users.get(p.offset, 0) != 1 or layer.N % 8 or layer.Kdim % 8:
+            continue
+        layer.fused_update = _FusedFCUpdate(solver, p, flags)
+        offsets.append(p.offset)
+    if offsets:
+        solver.set_fused_update(offsets)
+    return len(offsets)
+
+
 def fuse_input_fold(net, feeder) -> bool:
     """If the feeder's data blob is consumed only by a strided low-channel convolution on
     the space-to-depth path (AlexNet/CaffeNet conv1), make the feeder write the folded
@@ -214,7 +261,7 @@ class OverlappedUpdate:
 class GraphStep:
     """One captured solver iteration (iter_size = 1)."""
 
-    def __init__(self, solver: Solver, warmup: int = 2, pre=None, overlap: bool = True):
+    def __init__(self, solver: Solver, warmup: int = 2, pre=None, overlap: bool = True, fuse_fc: bool = True):
         self.solver = solver
         self.pre = pre  # callable run (eagerly) before each replay, e.g. feeder.stage
         self.graph = None
@@ -224,6 +271,8 @@ class GraphStep:
         if overlap and solver.overlap_eligible():
             self.overlap = OverlappedUpdate(solver)
             solver.net.backward_hooks.append(self.overlap.hook)
+        elif fuse_fc:
+            fuse_fc_updates(solver)
 
     def _body(self):
         s = self.solver
@@ -282,14 +331,15 @@ class LocalSGDTrainer:
     """tau local steps + weight averaging per round (SparkNet's model averaging)."""
 
     def __init__(self, solver: Solver, comm=None, tau: int = 50, feeder=None, use_graph: bool = True,
-                 log_every: int = 0, overlap_update: bool = False):
+                 log_every: int = 0, overlap_update: bool = False, fuse_fc: bool = True):
         self.solver = solver
         self.comm = comm
         self.tau = tau
         self.feeder = feeder
         self.round = 0
         self.use_graph = use_graph and solver.device.type == "cuda"
-        self.step_fn = GraphStep(solver, pre=self._pre, overlap=overlap_update) if self.use_graph else None
+        self.step_fn = (GraphStep(solver, pre=self._pre, overlap=overlap_update, fuse_fc=fuse_fc)
+                        if self.use_graph else None)
         self.log_every = log_every
         self.times = {"compute": 0.0, "allreduce": 0.0}
 

@@ -373,6 +373,7 @@ class InnerProductLayer(Layer):
         tops[0].data = y.reshape(tops[0].data.shape)
 
     fp8_slots = None
+    fused_update = None  # solver update applied in the wgrad epilogue (engine.fuse_fc_updates)
 
     def fp8_eligible(self, b) -> bool:
         return self.Kdim % 16 == 0
@@ -387,8 +388,15 @@ class InnerProductLayer(Layer):
         gate = b.data if self.relu_gate else None
         dw_acc = not (dw is not None and self.grad_overwrite(0))
         db_acc = not (db is not None and self.grad_overwrite(1))
-        dx = ops.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db, gate,
-                                 dw_acc=dw_acc, db_acc=db_acc)
+        if self.fused_update is not None and dw is not None and x2.is_cuda:
+            # the weight gradient goes straight into the solver update (engine.fuse_fc_updates
+            # admits only unshared weights with iter_size 1: this is its one and only write)
+            from ..ops import hip
+            dx = hip.linear_backward_sgd(dy2, x2, self.weight.compute, bool(propagate_down[0]),
+                                         self.fused_update.sgd(), db, gate, db_acc=db_acc)
+        else:
+            dx = ops.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db, gate,
+                                     dw_acc=dw_acc, db_acc=db_acc)
         if propagate_down[0]:
             b.diff = dx.reshape(b.data.shape)
 

@@ -22,7 +22,7 @@ import torch
 from . import _lib
 
 OP_DENSE, OP_IM2COL, OP_FLIPW = 0, 1, 2
-EPI_BF16, EPI_F32, EPI_F32_ACC = 0, 1, 2
+EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_SGD = 0, 1, 2, 3
 BM = BN = 128
 BK = 64
 
@@ -160,7 +160,7 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
          groups: int = 1, c_gstride: int = 0, bias: torch.Tensor | None = None, relu: bool = False,
          splits: int | None = None, gate: torch.Tensor | None = None,
          deq: tuple[torch.Tensor, torch.Tensor] | None = None,
-         bias_grad: torch.Tensor | None = None, bias_acc: bool = True) -> None:
+         bias_grad: torch.Tensor | None = None, bias_acc: bool = True, sgd: dict | None = None) -> None:
     """Run one (possibly grouped, split-K) GEMM.  ``epi``: EPI_BF16 (store bf16 with
     bias/ReLU; ``gate``: a bf16 tensor laid out like ``out`` — outputs where gate <= 0
     are zeroed, i.e. a following slope-0 ReLU's backward), EPI_F32 (store), EPI_F32_ACC
@@ -168,18 +168,30 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
 
     ``bias_grad`` (fp32 [groups * M], weight-gradient products with an MC B operand and
     N % 8 == 0): also compute sum_k A_g(m, k) — the bias gradient — through a virtual
-    ones column N of B, written (``bias_acc``: accumulated) into ``bias_grad[g*M + m]``."""
+    ones column N of B, written (``bias_acc``: accumulated) into ``bias_grad[g*M + m]``.
+
+    ``epi=EPI_SGD`` with ``sgd`` = {w, h, shadow, hyper, lr_mult, decay_mult, flags}:
+    the product is the gradient of the fp32 master ``w`` (laid out like ``out``), and the
+    epilogue applies the solver update to w / h / shadow instead of storing it."""
     if M == 0 or N == 0:
         return
+    sg = (0, 0, 0, 0, 0.0, 0.0, 0)
+    if epi == EPI_SGD:
+        assert sgd is not None and groups == 1 and deq is None
+        splits = 1
+        sg = (sgd["w"].data_ptr(), sgd["h"].data_ptr(), sgd["shadow"].data_ptr(), sgd["hyper"].data_ptr(),
+              float(sgd["lr_mult"]), float(sgd["decay_mult"]), int(sgd["flags"]))
     fp8 = deq is not None  # e4m3 operands; deq = (1/scale_A, 1/scale_B) device scalars
     sa, a_mc, a_mode = _operand(A, fp8)
     sb, b_mc, b_mode = _operand(B, fp8)
     ones = -1
     if bias_grad is not None:
-        assert epi in (EPI_F32, EPI_F32_ACC) and b_mc == 1 and b_mode != OP_FLIPW and N % 8 == 0 and not fp8
+        assert epi in (EPI_F32, EPI_F32_ACC, EPI_SGD) and b_mc == 1 and b_mode != OP_FLIPW and N % 8 == 0 and not fp8
         assert bias_grad.dtype == torch.float32 and bias_grad.is_contiguous() and bias_grad.numel() == groups * M
         ones, N = N, N + 1
     tile = 0 if fp8 else (choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE) if _FORCE_TILE < 0 else _FORCE_TILE)
+    if epi == EPI_SGD and tile not in (0, 1, 2, 3):
+        tile = 0  # the fused-update epilogue is instantiated for the generic tiles only
     bk = 128 if fp8 else BK
     if splits is None:
         # the fp8 k-step covers 128 elements in the time a bf16 one covers 64: same model
@@ -203,7 +215,7 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, epi,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
                                bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster,
-                               ones, bg, int(bias_acc))
+                               ones, bg, int(bias_acc), *sg)
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
@@ -212,7 +224,7 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
     ws = torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
                            sa, sb, ws.data_ptr(), ldw, splits * M * ldw, M * ldw, 0, 0, tile, 0, int(fp8), *dq, raster,
-                           ones, 0, 0)
+                           ones, 0, 0, *sg)
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
     _lib.call("splitk_reduce", ws, splits, M * ldw, M, N, ldw, out, ldc, mode, bias, int(relu),
@@ -301,6 +313,21 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate
     else:
         dw.copy_(tmp[:N, :K])
     return False
+
+
+def linear_wgrad_sgd(dy: torch.Tensor, x: torch.Tensor, sgd: dict, db: torch.Tensor | None = None,
+                     db_acc: bool = True) -> bool:
+    """The InnerProduct weight gradient dy^T @ x consumed in the GEMM epilogue by the
+    solver update of sgd["w"] / ["h"] / ["shadow"] (EPI_SGD; the gradient is never
+    stored).  Needs N, K % 8 == 0.  Returns whether db (the bias gradient) was written."""
+    M, N = dy.shape
+    K = x.shape[1]
+    assert N % 8 == 0 and K % 8 == 0 and dy.is_contiguous() and x.is_contiguous()
+    fuse = db is not None and db.is_contiguous() and db.dtype == torch.float32
+    w = sgd["w"]
+    gemm(N, K, M, Dense(dy, N, False), Dense(x, K, False), w, K, epi=EPI_SGD, sgd=sgd,
+         bias_grad=db if fuse else None, bias_acc=db_acc)
+    return fuse
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = True) -> None:

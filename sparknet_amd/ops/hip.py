@@ -286,6 +286,20 @@ def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=Tru
     return linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)
 
 
+def linear_backward_sgd(dy2, x2, w, need_dx, sgd, db=None, gate=None, db_acc=True):
+    """InnerProduct backward whose weight gradient is consumed by the solver update in the
+    GEMM epilogue (gemm.linear_wgrad_sgd).  The data gradient runs FIRST: it reads the
+    bf16 compute weights ``w`` that the fused update then overwrites."""
+    dy2, x2 = _c(dy2), _c(x2)
+    dx = None
+    if need_dx:
+        dx = linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)
+    from .gemm import linear_wgrad_sgd
+    if not linear_wgrad_sgd(dy2, x2, sgd, db, db_acc) and db is not None:
+        colsum(dy2, db, accumulate=db_acc)
+    return dx
+
+
 # --------------------------------------------------------------------------------------
 # Pooling / LRN
 # --------------------------------------------------------------------------------------

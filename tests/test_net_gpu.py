@@ -58,7 +58,7 @@ def test_caffenet_gpu_matches_cpu_engine(gpu):
     assert err < 5e-2, err
 
 
-def _graph_solver(overlap):
+def _graph_solver(overlap, fuse_fc=False):
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.engine import GraphStep, fuse_relu
     sp = models.zoo.caffenet_solver(_tiny_caffenet(0.5))
@@ -72,7 +72,7 @@ def _graph_solver(overlap):
         x, y = next(it)
         solver.net.blob_by_name("data").set_nchw(x)
         solver.net.blob_by_name("label").set_nchw(y)
-    step = GraphStep(solver, warmup=1, pre=pre, overlap=overlap)
+    step = GraphStep(solver, warmup=1, pre=pre, overlap=overlap, fuse_fc=fuse_fc)
     if step.overlap is not None:  # the tiny net's layers are below the production threshold
         from sparknet_amd.engine import OverlappedUpdate
         solver.net.backward_hooks.clear()
@@ -95,11 +95,25 @@ def test_overlapped_update_matches_serial(gpu):
     assert torch.equal(s0.history[0], s1.history[0])
 
 
+def test_fused_fc_update_matches_solver_kernel(gpu):
+    """InnerProduct weight updates applied in the wgrad GEMM epilogue == the same
+    iterations with gradients stored and updated by the solver kernel."""
+    s0, _ = _graph_solver(False, fuse_fc=False)
+    s1, st1 = _graph_solver(False, fuse_fc=True)
+    fused = [l for l in s1.net.layers if getattr(l, "fused_update", None) is not None]
+    assert len(fused) == 2  # fc6, fc7 (fc8 has 7 outputs: not a multiple of 8)
+    assert s0.iter == s1.iter
+    for a, b in ((s0.net.flat_data, s1.net.flat_data), (s0.history[0], s1.history[0])):
+        err = (a - b).abs().max().item() / (a.abs().max().item() + 1e-12)
+        assert err < 1e-5, err
+    assert torch.equal(s1.net.flat_compute, s1.net.flat_data.to(torch.bfloat16))
+
+
 def test_training_is_bitwise_deterministic(gpu):
     """Fixed Philox seeds + atomics-free reductions (split-K slabs, colsum, solver): two
     identical graph-captured runs end with bitwise-identical weights and momentum."""
-    a, _ = _graph_solver(False)
-    b, _ = _graph_solver(False)
+    a, _ = _graph_solver(False, fuse_fc=True)
+    b, _ = _graph_solver(False, fuse_fc=True)
     assert torch.equal(a.net.flat_data, b.net.flat_data)
     assert torch.equal(a.history[0], b.history[0])
 
