@@ -44,6 +44,10 @@ class LossLayer(Layer):
     def reshape(self, bottoms, tops):
         tops[0].reshape((), torch.float32)
 
+    def allow_force_backward(self, bottom_id: int) -> bool:
+        """Labels / targets never get a forced gradient (loss_layer.hpp AllowForceBackward)."""
+        return bottom_id != 1
+
 
 @register("SoftmaxWithLoss")
 class SoftmaxWithLossLayer(LossLayer):

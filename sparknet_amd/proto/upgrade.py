@@ -59,6 +59,32 @@ def upgrade_v1_layer(v1, layer) -> None:
             getattr(layer, f).CopyFrom(getattr(v1, f))
 
 
+_SOLVER_TYPE_NAMES = {0: "SGD", 1: "Nesterov", 2: "AdaGrad", 3: "RMSProp", 4: "AdaDelta", 5: "Adam"}
+
+
+def solver_needs_upgrade(sp) -> bool:
+    return sp.HasField("solver_type")
+
+
+def upgrade_solver(sp):
+    """UpgradeSolverType (caffe/src/caffe/util/upgrade_proto.cpp:948-980): the legacy
+    ``solver_type`` enum becomes the ``type`` string."""
+    if sp.HasField("solver_type"):
+        if sp.HasField("type"):
+            raise ValueError("Failed to upgrade solver: old solver_type field (enum) and new type field "
+                             "(string) cannot be both specified")
+        t = int(sp.solver_type)
+        if t not in _SOLVER_TYPE_NAMES:
+            raise ValueError(f"Unknown SolverParameter solver_type: {t}")
+        sp.type = _SOLVER_TYPE_NAMES[t]
+        sp.ClearField("solver_type")
+    return sp
+
+
+def net_needs_upgrade(net) -> bool:
+    return len(net.layers) > 0
+
+
 def upgrade_net(net):
     if len(net.layers) == 0:
         return net
