@@ -189,27 +189,40 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         assert epi in (EPI_F32, EPI_F32_ACC, EPI_SGD) and b_mc == 1 and b_mode != OP_FLIPW and N % 8 == 0 and not fp8
         assert bias_grad.dtype == torch.float32 and bias_grad.is_contiguous() and bias_grad.numel() == groups * M
         ones, N = N, N + 1
-    tile = 0 if fp8 else (choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE) if _FORCE_TILE < 0 else _FORCE_TILE)
-    if epi == EPI_SGD and tile not in (0, 1, 2, 3):
-        tile = 0  # the fused-update epilogue is instantiated for the generic tiles only
     bk = 128 if fp8 else BK
-    if splits is None:
-        # the fp8 k-step covers 128 elements in the time a bf16 one covers 64: same model
-        splits, kchunk = choose_splits(M, N, K * BK // bk, groups, tile)
-        kchunk = kchunk * bk // BK
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous()
+    if gate is not None:
+        assert epi == EPI_BF16 and gate.dtype == torch.bfloat16
+    ops = (sa, a_mc, a_mode, sb, b_mc, b_mode)
+    if splits is not None or fp8 or _FORCE_TILE >= 0:
+        tile = 0 if fp8 else (_FORCE_TILE if _FORCE_TILE >= 0 else choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE))
+        if epi == EPI_SGD and tile not in (0, 1, 2, 3):
+            tile = 0
+        if splits is None:
+            splits, kchunk = choose_splits(M, N, K * BK // bk, groups, tile)
+            kchunk = kchunk * bk // BK
+        else:
+            kchunk = -(-(-(-K // splits)) // bk) * bk
     else:
-        kchunk = -(-(-(-K // splits)) // bk) * bk
+        tile, splits, kchunk = _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate,
+                                             bias_grad, bias_acc, ones, sg)
+    _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc, ones, sg,
+            tile, splits, kchunk, deq)
+
+
+def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc, ones, sg,
+            tile, splits, kchunk, deq=None):
+    """One GEMM launch (+ the split-K reduce) with an explicit tile / split choice."""
+    sa, a_mc, a_mode, sb, b_mc, b_mode = ops
+    fp8 = deq is not None
+    bk = 128 if fp8 else BK
     splits = max(1, -(-K // kchunk))
     dq = (deq[0].data_ptr(), deq[1].data_ptr()) if fp8 else (0, 0)
     bm, bn = TILES[tile]
     tm_, tn_ = -(-M // bm), -(-N // bn)
     raster = int(_RASTER_N if _RASTER_N >= 0 else (1 < tn_ <= 8 and tm_ >= 8 * tn_))
-    if bias is not None:
-        assert bias.dtype == torch.float32 and bias.is_contiguous()
-    gp = 0
-    if gate is not None:
-        assert epi == EPI_BF16 and gate.dtype == torch.bfloat16
-        gp = gate.data_ptr()
+    gp = gate.data_ptr() if gate is not None else 0
     bg = bias_grad.data_ptr() if bias_grad is not None else 0
     if splits == 1:
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, epi,
@@ -229,6 +242,88 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
     _lib.call("splitk_reduce", ws, splits, M * ldw, M, N, ldw, out, ldc, mode, bias, int(relu),
               groups, splits * M * ldw, c_gstride, gate, bias_grad, ones, int(bias_acc), M)
+
+
+# --- per-shape autotuning ----------------------------------------------------------------
+# The cost model picks a tile and split-K factor from the shape alone; the first eager
+# call of every distinct GEMM (shape, operand kinds and geometry, epilogue) instead times
+# the candidate tiles x split factors on scratch outputs and caches the fastest.  Graph
+# captures replay the cached choice.  SN_GEMM_AUTOTUNE=0 keeps the model's choice (fully
+# reproducible tile selection across processes).
+_AUTOTUNE = os.environ.get("SN_GEMM_AUTOTUNE", "1") != "0"
+_TUNED: dict = {}
+
+
+def _geom_key(s) -> tuple:
+    return (s.ld, s.gstride) + tuple(getattr(s.g, f) for f, _ in s.g._fields_)
+
+
+def _candidates(M, N, K, groups, b_kc_dense, epi):
+    tiles = [0, 1, 2]
+    if N >= 256:
+        tiles.append(3)
+    if epi != EPI_SGD:
+        if b_kc_dense and N % 96 == 0:
+            tiles.append(4)
+        if N % 48 == 0 and N <= 96 and M >= 256:
+            tiles.append(5)
+    out = []
+    for t in tiles:
+        s, kc = choose_splits(M, N, K, groups, t)
+        out.append((t, s, kc))
+        if epi == EPI_SGD:
+            continue
+        for s2 in {1, 2 * s} - {s}:
+            kc2 = -(-(-(-K // s2)) // BK) * BK
+            s2 = max(1, -(-K // kc2))
+            if s2 * M * N * groups * 4 <= (256 << 20):
+                out.append((t, s2, kc2))
+    return list(dict.fromkeys(out))
+
+
+def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
+                  ones, sg):
+    sa, a_mc, a_mode, sb, b_mc, b_mode = ops
+    b_kc_dense = b_mc == 0 and b_mode == OP_DENSE
+    key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None,
+           _geom_key(sa), _geom_key(sb), out.dtype)
+    hit = _TUNED.get(key)
+    if hit is not None:
+        return hit
+    tile = choose_tile(M, N, b_kc_dense)
+    if epi == EPI_SGD and tile not in (0, 1, 2, 3):
+        tile = 0
+    splits, kchunk = choose_splits(M, N, K, groups, tile)
+    default = (tile, splits, kchunk)
+    extent = (groups - 1) * c_gstride + (M - 1) * ldc + (N - (1 if ones >= 0 else 0))
+    if (not _AUTOTUNE or epi == EPI_SGD or not out.is_cuda or not out.is_contiguous() or extent > out.numel()
+            or torch.cuda.is_current_stream_capturing()):
+        return default
+    scratch = torch.empty_like(out)
+    bscratch = torch.zeros_like(bias_grad) if bias_grad is not None else None
+    best, best_t = default, float("inf")
+    for cand in _candidates(M, N, K, groups, b_kc_dense, epi):
+        t, s, kc = cand
+
+        def run():
+            _launch(M, N, K, groups, ops, epi, scratch, ldc, c_gstride, bias, relu, gate, bscratch, bias_acc,
+                    ones, sg, t, s, kc)
+        try:
+            run()
+        except RuntimeError:  # a tile this operand combination has no instance for
+            continue
+        times = []
+        for _ in range(2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            run()
+            e1.record()
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1))
+        if min(times) < best_t:
+            best, best_t = cand, min(times)
+    _TUNED[key] = best
+    return best
 
 
 # --- dense helpers ---------------------------------------------------------------------
