@@ -254,6 +254,149 @@ class ImageDataLayer(ExternalDataLayer):
         tops[1].data.copy_(torch.tensor(labels, dtype=torch.float32))
 
 
+@register("WindowData")
+class WindowDataLayer(ExternalDataLayer):
+    """R-CNN window sampler (caffe/src/caffe/layers/window_data_layer.cpp:33-468), PIL
+    instead of OpenCV. The window file repeats ``# idx / path / C H W / n / n x (label
+    overlap x1 y1 x2 y2)``; windows with overlap >= fg_threshold are foreground, those
+    below bg_threshold background (label forced to 0). Each batch draws
+    ``batch - int(batch * fg_fraction)`` background windows and then the foreground ones,
+    crops them with optional context padding (``warp`` or ``square`` mode), resizes
+    bilinearly to crop_size, mirrors, and writes (pixel - mean) * scale into a zeroed
+    batch — the padded border stays 0, as in the reference."""
+    exact_tops = 2
+
+    def layer_setup(self, bottoms, tops):
+        super().layer_setup(bottoms, tops)
+        import numpy as np
+        p = self.lp.window_data_param
+        tp = self.lp.transform_param
+        self.p, self.crop, self.mirror = p, int(tp.crop_size), bool(tp.mirror)
+        if self.crop <= 0:
+            raise ValueError(f"WindowData layer {self.name!r} needs transform_param.crop_size > 0")
+        self.images, self.fg, self.bg = [], [], []
+        with open(p.source) as f:
+            tok = f.read().split()
+        i = 0
+        while i < len(tok):
+            if tok[i] != "#":
+                raise ValueError(f"window file {p.source!r}: expected '#' at token {i}")
+            idx, path = int(tok[i + 1]), p.root_folder + tok[i + 2]
+            c, h, w, n = (int(t) for t in tok[i + 3:i + 7])
+            i += 7
+            while len(self.images) <= idx:
+                self.images.append(None)
+            self.images[idx] = (path, (c, h, w))
+            for _ in range(n):
+                lab, ov = int(tok[i]), float(tok[i + 1])
+                x1, y1, x2, y2 = (int(t) for t in tok[i + 2:i + 6])
+                i += 6
+                if ov >= p.fg_threshold:
+                    if lab <= 0:
+                        raise ValueError("foreground windows need a positive label")
+                    self.fg.append((idx, lab, ov, x1, y1, x2, y2))
+                elif ov < p.bg_threshold:
+                    self.bg.append((idx, 0, 0.0, x1, y1, x2, y2))
+        if not self.images:
+            raise ValueError(f"window file {p.source!r} is empty")
+        self.channels = self.images[0][1][0]
+        self.mean = self.mean_values = None
+        if tp.mean_file:
+            if len(tp.mean_value):
+                raise ValueError("Cannot specify mean_file and mean_value at the same time")
+            from ..data.loaders import read_mean_binaryproto
+            self.mean = np.asarray(read_mean_binaryproto(tp.mean_file), np.float32)
+        elif len(tp.mean_value):
+            mv = list(tp.mean_value)
+            self.mean_values = np.asarray(mv if len(mv) > 1 else mv * self.channels, np.float32)
+        self.rng = np.random.default_rng(self.ctx.seed)
+        self.cache = {}
+
+    def reshape(self, bottoms, tops):
+        super().reshape(bottoms, tops)
+        b = int(self.p.batch_size)
+        tops[0].reshape((b, self.channels, self.crop, self.crop), self.dtype)
+        tops[1].reshape((b,), torch.float32)
+
+    def _image(self, idx):
+        import numpy as np
+        from PIL import Image
+        if idx in self.cache:
+            return self.cache[idx]
+        a = np.asarray(Image.open(self.images[idx][0]).convert("RGB"), np.uint8)[:, :, ::-1]  # BGR
+        if self.p.cache_images:
+            self.cache[idx] = a
+        return a
+
+    def _window(self, win, mirror):
+        """One cropped window: (HWC uint8 patch, pad_h, pad_w)."""
+        import numpy as np
+        from PIL import Image
+        img = self._image(win[0])
+        rows, cols = img.shape[:2]
+        crop, ctx_pad = self.crop, int(self.p.context_pad)
+        x1, y1, x2, y2 = win[3:]
+        out_w = out_h = crop
+        pad_h = pad_w = 0
+        if ctx_pad > 0 or self.p.crop_mode == "square":
+            cscale = crop / (crop - 2 * ctx_pad)
+            hh, hw = (y2 - y1 + 1) / 2.0, (x2 - x1 + 1) / 2.0
+            cx, cy = x1 + hw, y1 + hh
+            if self.p.crop_mode == "square":
+                hh = hw = max(hh, hw)
+            x1, x2 = int(round(cx - hw * cscale)), int(round(cx + hw * cscale))
+            y1, y2 = int(round(cy - hh * cscale)), int(round(cy + hh * cscale))
+            uh, uw = y2 - y1 + 1, x2 - x1 + 1
+            px1, py1 = max(0, -x1), max(0, -y1)
+            px2, py2 = max(0, x2 - cols + 1), max(0, y2 - rows + 1)
+            x1, x2, y1, y2 = x1 + px1, x2 - px2, y1 + py1, y2 - py2
+            sx, sy = crop / uw, crop / uh
+            out_w = int(round((x2 - x1 + 1) * sx))
+            out_h = int(round((y2 - y1 + 1) * sy))
+            px1, px2 = int(round(px1 * sx)), int(round(px2 * sx))
+            py1 = int(round(py1 * sy))
+            pad_h, pad_w = py1, (px2 if mirror else px1)
+            out_h, out_w = min(out_h, crop - pad_h), min(out_w, crop - pad_w)
+        roi = np.ascontiguousarray(img[y1:y2 + 1, x1:x2 + 1])
+        patch = np.asarray(Image.fromarray(roi).resize((out_w, out_h), Image.BILINEAR), np.uint8)
+        if mirror:
+            patch = patch[:, ::-1]
+        return patch, pad_h, pad_w
+
+    def next_batch(self):
+        """Host batch: (N x C x crop x crop float32, N labels)."""
+        import numpy as np
+        b, crop = int(self.p.batch_size), self.crop
+        data = np.zeros((b, self.channels, crop, crop), np.float32)
+        labels = np.zeros((b,), np.float32)
+        n_fg = int(b * self.p.fg_fraction)
+        item = 0
+        for pool, count in ((self.bg, b - n_fg), (self.fg, n_fg)):
+            for _ in range(count):
+                win = pool[int(self.rng.integers(len(pool)))]
+                mirror = self.mirror and bool(self.rng.integers(2))
+                patch, ph, pw = self._window(win, mirror)
+                h, w = patch.shape[:2]
+                px = patch.transpose(2, 0, 1).astype(np.float32)
+                if self.mean is not None:
+                    off = (self.mean.shape[2] - crop) // 2
+                    px = px - self.mean[:, off + ph:off + ph + h, off + pw:off + pw + w]
+                elif self.mean_values is not None:
+                    px = px - self.mean_values[:, None, None]
+                data[item, :, ph:ph + h, pw:pw + w] = px * self.p.scale
+                labels[item] = win[1]
+                item += 1
+        return data, labels
+
+    def forward(self, bottoms, tops):
+        if self.source is not None:
+            self.source(self, tops)
+            return
+        data, labels = self.next_batch()
+        tops[0].set_nchw(torch.from_numpy(data).to(self.dtype))
+        tops[1].data.copy_(torch.from_numpy(labels))
+
+
 def _resolve_listed(path: str, list_file: str) -> str:
     """File names in a list file are taken relative to the working directory (as Caffe
     does); failing that, relative to the list file's directory, then its basename there."""

@@ -20,6 +20,7 @@ from __future__ import annotations
 from .. import proto as _proto
 from . import draw, io  # noqa: F401
 from .classifier import Classifier  # noqa: F401
+from .detector import Detector  # noqa: F401
 from .net import (AdaDeltaSolver, AdaGradSolver, AdamSolver, Net, NesterovSolver, RMSPropSolver,  # noqa: F401
                   SGDSolver, get_solver, set_device, set_mode_cpu, set_mode_gpu)
 from .net_spec import NetSpec, layers, params, to_proto  # noqa: F401

@@ -229,3 +229,31 @@ def test_solver_types(tmp_path, cls):
     s = getattr(caffe, cls)(str(sf))
     s.step(3)
     assert s.iter == 3 and s._s.type == cls[:-len("Solver")]
+
+
+def test_detector_windows_and_context_crop(tmp_path):
+    """detector.py: detect_windows warps every window through the net; context padding
+    grows the box and fills the out-of-image part with the raw-space mean."""
+    from PIL import Image
+    deploy = tmp_path / "det.prototxt"
+    deploy.write_text("""name: 'det' input: 'data' input_shape { dim: 4 dim: 3 dim: 8 dim: 8 }
+      layer { name: 'ip' type: 'InnerProduct' bottom: 'data' top: 'ip'
+        inner_product_param { num_output: 5 weight_filler { type: 'gaussian' std: 0.1 } } }
+      layer { name: 'prob' type: 'Softmax' bottom: 'ip' top: 'prob' }""")
+    net = caffe.Net(str(deploy), caffe.TEST)
+    w = str(tmp_path / "det.caffemodel")
+    net.save(w)
+    img = tmp_path / "im.png"
+    Image.fromarray(np.random.default_rng(0).integers(0, 256, (20, 24, 3), dtype=np.uint8)).save(img)
+    det = caffe.Detector(str(deploy), w, raw_scale=255.0)
+    wins = [np.array([0, 0, 10, 12]), np.array([5, 6, 19, 23]), np.array([2, 2, 8, 8])]
+    out = det.detect_windows([(str(img), wins)])
+    assert len(out) == 3 and out[1]["filename"] == str(img)
+    assert all(d["prediction"].shape == (5,) and abs(d["prediction"].sum() - 1) < 1e-4 for d in out)
+    mean = np.array([10.0, 20.0, 30.0])
+    det = caffe.Detector(str(deploy), w, mean=mean, raw_scale=255.0, context_pad=2)
+    im = caffe.io.load_image(str(img))
+    c = det.crop(im, np.array([0, 0, 19, 23]))  # whole image: the border is context
+    assert c.shape == (8, 8, 3)
+    assert np.allclose(c[0, 0], mean / 255.0) and np.allclose(c[-1, -1], mean / 255.0)
+    assert 0.0 <= c[4, 4].min() and c[4, 4].max() <= 1.0

@@ -107,3 +107,42 @@ I1016 10:00:12.500000  1 sgd_solver.cpp:5] Iteration 100, lr = 0.01
     assert test[0]["accuracy"] == 0.1
     tr, te = tools.write_parsed_log(str(log), str(tmp_path))
     assert open(tr).readline().startswith("NumIters")
+
+
+def test_window_data_layer(tmp_path):
+    """WindowData (window_data_layer.cpp): bg windows first, fg after; constant images make
+    the warped crops exact; context padding past the image edge leaves a zero border."""
+    from PIL import Image
+    from sparknet_amd.core.net import Net
+    for i, v in enumerate((40, 200)):
+        Image.fromarray(np.full((20, 30, 3), v, np.uint8)).save(tmp_path / f"w{i}.png")
+    wf = tmp_path / "windows.txt"
+    wf.write_text("# 0\nw0.png\n3 20 30\n2\n1 0.9 2 3 12 15\n0 0.1 0 0 29 19\n"
+                  "# 1\nw1.png\n3 20 30\n1\n2 0.7 5 5 25 15\n")
+
+    def net(pad, mean_value=10.0):
+        txt = f"""name: 'w'
+          layer {{ name: 'd' type: 'WindowData' top: 'data' top: 'label'
+            transform_param {{ crop_size: 8 mirror: true mean_value: {mean_value} }}
+            window_data_param {{ source: '{wf}' root_folder: '{tmp_path}/' batch_size: 8
+              fg_fraction: 0.5 scale: 0.5 context_pad: {pad} }} }}"""
+        return Net(proto.parse_prototxt(txt), phase=proto.TRAIN, seed=3)
+
+    n = net(0)
+    n.forward()
+    data = n.blob_by_name("data").nchw().float().numpy()
+    lab = n.blob_by_name("label").data.float().numpy()
+    assert data.shape == (8, 3, 8, 8)
+    assert (lab[:4] == 0).all() and set(lab[4:].tolist()) <= {1.0, 2.0}
+    for k in range(8):
+        v = {0: 40, 1: 40, 2: 200}[int(lab[k])] if lab[k] else 40
+        assert np.allclose(data[k], (v - 10.0) * 0.5)
+    n = net(2)
+    n.forward()
+    data = n.blob_by_name("data").nchw().float().numpy()
+    lab = n.blob_by_name("label").data.float().numpy()
+    bg = data[:4]  # full-image background window grown by the context: zero border
+    # window grows to x -15..45, y -10..30: a 4x4 patch at offset (2, 2) either way
+    assert np.allclose(bg[:, :, 2:6, 2:6], (40 - 10.0) * 0.5)
+    assert (bg[:, :, :2] == 0).all() and (bg[:, :, 6:] == 0).all()
+    assert (bg[:, :, :, :2] == 0).all() and (bg[:, :, :, 6:] == 0).all()
