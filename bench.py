@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--no-fuse-fc", action="store_true",
                    help="store InnerProduct weight gradients and update them in the solver kernel")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--host-profile", action="store_true",
+                   help="after the timed run, report the host time per step part (stderr)")
     return p.parse_args()
 
 
@@ -149,8 +151,59 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+    if args.host_profile and trainer.step_fn is not None:
+        host_profile(trainer, dev)
     if comm is not None:
         comm.close()
+
+
+def host_profile(trainer, dev, n=200):
+    """Host-side cost of each part of a graph step (feeder, hyper staging, replay) against
+    the GPU time of the same steps: tells whether a small model is launch-bound."""
+    import torch
+    g, s = trainer.step_fn, trainer.solver
+    parts = {"feeder": 0.0, "hyper": 0.0, "replay": 0.0}
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        a = time.perf_counter()
+        g.pre()
+        b = time.perf_counter()
+        s.stage_hyper()
+        c = time.perf_counter()
+        g.graph.replay()
+        d = time.perf_counter()
+        s.iter += 1
+        parts["feeder"] += b - a
+        parts["hyper"] += c - b
+        parts["replay"] += d - c
+    host = time.perf_counter() - t0
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    print("host us/step: " + " ".join(f"{k}={1e6 * v / n:.1f}" for k, v in parts.items()) +
+          f" total={1e6 * host / n:.1f}; wall us/step={1e6 * wall / n:.1f}", file=sys.stderr, flush=True)
+    f = trainer.feeder
+    if f is None:
+        return
+    sub = {"stage": 0.0, "prefetch": 0.0}
+    for _ in range(n):
+        a = time.perf_counter()
+        f.stage()
+        b = time.perf_counter()
+        f.prefetch()
+        sub["stage"] += b - a
+        sub["prefetch"] += time.perf_counter() - b
+    torch.cuda.synchronize(dev)
+    x, _ = f.source.next_batch()
+    dx = f.slots[0][0]
+    a = time.perf_counter()
+    for _ in range(n):
+        with torch.cuda.stream(f.copy_stream):
+            dx.copy_(x, non_blocking=True)
+    sub["h2d_copy_only"] = time.perf_counter() - a
+    torch.cuda.synchronize(dev)
+    print("feeder us/step: " + " ".join(f"{k}={1e6 * v / n:.1f}" for k, v in sub.items()) +
+          f" pinned={x.is_pinned()}", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":

@@ -123,8 +123,7 @@ class Solver:
         self.history = [torch.zeros(max(n, 1), dtype=torch.float32, device=self.device)
                         for _ in range(N_HISTORY[self.type])]
         self.hyper = torch.zeros(N_HYPER, dtype=torch.float32, device=self.device)
-        self._hyper_host = torch.zeros(N_HYPER, dtype=torch.float32,
-                                       pin_memory=self.device.type == "cuda")
+        self._hyper_staged: list | None = None
         self._build_tables()
 
     def _build_tables(self) -> None:
@@ -188,8 +187,16 @@ class Solver:
     def stage_hyper(self, rate: float | None = None) -> float:
         """Write this iteration's hyper-parameters into the device tensor (async H2D)."""
         rate = self.get_learning_rate() if rate is None else rate
-        self._hyper_host.copy_(torch.tensor(self.hyper_values(rate)))
-        self.hyper.copy_(self._hyper_host, non_blocking=True)
+        vals = self.hyper_values(rate)
+        vals[H_T] = 0.0  # host-side only (Adam's correction is folded into H_CORR)
+        if vals == self._hyper_staged:  # unchanged (fixed / step policies): no copy at all
+            return rate
+        self._hyper_staged = vals
+        # a fresh pinned buffer per change: a host write never races an H2D still queued
+        host = torch.tensor(vals, dtype=torch.float32)
+        if self.device.type == "cuda":
+            host = host.pin_memory()
+        self.hyper.copy_(host, non_blocking=True)
         return rate
 
     # -- update (ApplyUpdate) -------------------------------------------------------------
