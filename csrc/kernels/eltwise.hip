@@ -8,6 +8,7 @@
 //  * fp32 -> bf16 cast of the flat parameter buffer (compute shadow refresh).
 //  * Philox counter advance (device side, so captured graphs get fresh masks per replay).
 //  * Sum of bf16 tensors (Split backward / gradient accumulation).
+//  * Channel concat fwd / bwd of NHWC blobs (+ fused ReLU-backward mask).
 //  * im2col (explicit, for convs whose per-group channel count is not a multiple of 8 —
 //    i.e. the 3-channel input layer), col2im (stride>1 dgrad), weight flip-transpose
 //    (turns dgrad into a forward implicit-GEMM conv), batched over a net's layers.
@@ -149,6 +150,78 @@ extern "C" int sn_sum_bf16(const bf16_t* const* ptrs, long long k, bf16_t* out, 
     SN_SUM_CASE(5) SN_SUM_CASE(6) SN_SUM_CASE(7) SN_SUM_CASE(8)
 #undef SN_SUM_CASE
   }
+  return SN_CHECK_LAUNCH();
+}
+
+// ---------------- Channel concat (NHWC) ----------------
+// Concat on the channel axis of NHWC bf16 blobs (concat_layer.cu:6-71) as one launch per
+// direction; blockIdx.y = part.  Forward copies part i into channels [off_i, off_i + c_i)
+// of every pixel; backward slices the top gradient back out and, for parts produced by
+// an in-place slope-0 ReLU, applies its mask (gate = the part's own ReLU output), which
+// replaces that ReLU's separate backward pass.  Channel counts are multiples of 8.
+struct ConcatDesc {
+  const bf16_t* part[8];  // forward: part data; backward: part diff (written)
+  const bf16_t* gate[8];  // backward only: ReLU output of the part, or null
+  int c8[8], off8[8];     // channels / offset in 16-B chunks
+  int ct8;                // top channels in chunks
+  long long pix;          // N*H*W
+};
+
+template <bool BWD>
+__global__ void concat_nhwc(ConcatDesc d, bf16_t* __restrict__ top) {
+  const int part = blockIdx.y;
+  if (!d.part[part]) return;  // backward: a part that needs no gradient
+  const int ci8 = d.c8[part];
+  const long long total = d.pix * ci8;
+  const uint4* g = reinterpret_cast<const uint4*>(d.gate[part]);
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < total; j += (long long)gridDim.x * blockDim.x) {
+    const long long p = j / ci8;
+    const long long t = p * d.ct8 + d.off8[part] + (j - p * ci8);
+    if (!BWD) {
+      reinterpret_cast<uint4*>(top)[t] = reinterpret_cast<const uint4*>(d.part[part])[j];
+    } else {
+      uint4 v = reinterpret_cast<const uint4*>(top)[t];
+      if (g) {
+        const uint4 m = g[j];
+        // bf16 > 0  <=>  sign clear and magnitude in (0, +inf]  (zero and NaN fail, as in relu_bwd)
+        auto keep = [](unsigned int w, unsigned int x) {
+          const unsigned int a = w & 0x7fffu, b = (w >> 16) & 0x7fffu;
+          const unsigned int lo = ((w & 0x8000u) == 0 && a != 0 && a <= 0x7f80u) ? 0xffffu : 0u;
+          const unsigned int hi = ((w & 0x80000000u) == 0 && b != 0 && b <= 0x7f80u) ? 0xffff0000u : 0u;
+          return x & (lo | hi);
+        };
+        v.x = keep(m.x, v.x);
+        v.y = keep(m.y, v.y);
+        v.z = keep(m.z, v.z);
+        v.w = keep(m.w, v.w);
+      }
+      reinterpret_cast<uint4*>(const_cast<bf16_t*>(d.part[part]))[j] = v;
+    }
+  }
+}
+
+extern "C" int sn_concat_nhwc(const bf16_t* const* parts, const bf16_t* const* gates, const long long* chans,
+                              long long nparts, bf16_t* top, long long pix, long long bwd, hipStream_t st) {
+  if (nparts < 1 || nparts > 8) return 7;
+  ConcatDesc d;
+  memset(&d, 0, sizeof(d));
+  long long off = 0, maxc = 0;
+  for (int i = 0; i < nparts; ++i) {
+    if (chans[i] % 8 || chans[i] <= 0) return 7;
+    d.part[i] = parts[i];
+    d.gate[i] = gates ? gates[i] : nullptr;
+    d.c8[i] = (int)(chans[i] / 8);
+    d.off8[i] = (int)(off / 8);
+    off += chans[i];
+    if (chans[i] > maxc) maxc = chans[i];
+  }
+  d.ct8 = (int)(off / 8);
+  d.pix = pix;
+  const dim3 grid(sn_blocks(pix * (maxc / 8), 256, 8192), (unsigned)nparts);
+  if (bwd)
+    hipLaunchKernelGGL(concat_nhwc<true>, grid, dim3(256), 0, st, d, top);
+  else
+    hipLaunchKernelGGL(concat_nhwc<false>, grid, dim3(256), 0, st, d, top);
   return SN_CHECK_LAUNCH();
 }
 

@@ -83,8 +83,9 @@ def fuse_relu_backward(net) -> int:
     """Fold the backward of every in-place slope-0 ReLU into the backward of the single
     layer that consumes its output (Caffe's ReLU backward is a separate pass over the
     gradient, relu_layer.cu:24-41): conv / inner-product dgrad epilogues, the dropout
-    kernel and the max-pool argmax mask then zero the gradient where the ReLU output is
-    not positive, and the ReLU layer's own backward becomes a no-op.  Returns the count."""
+    kernel, the max-pool argmax mask and the channel-concat backward (Inception outputs)
+    then zero the gradient where the ReLU output is not positive, and the ReLU layer's
+    own backward becomes a no-op.  Returns the count."""
     n = 0
     for li, relu in enumerate(net.layers):
         if relu.type_name != "ReLU" or getattr(relu, "slope", 1.0) != 0.0:
@@ -101,6 +102,14 @@ def fuse_relu_backward(net) -> int:
         if len(consumers) > 1 and blob not in net.top_ids[lc]:
             continue
         cons = net.layers[lc]
+        if cons.type_name == "Concat" and len(net.bottom_ids[lc]) > 1 and blob not in net.top_ids[lc] \
+                and blob not in getattr(net, "output_blob_ids", ()):
+            # concat backward slices the gradient per bottom: the mask is applied while slicing
+            pos = {i for i, b in enumerate(net.bottom_ids[lc]) if b == blob}
+            cons.relu_gate_parts = frozenset(cons.relu_gate_parts | pos)
+            relu.bwd_fused = True
+            n += 1
+            continue
         if cons.type_name not in _GATE_CONSUMERS or len(net.bottom_ids[lc]) != 1:
             continue
         if cons.type_name == "Pooling" and (cons.method != 0 or len(net.top_ids[lc]) != 1):

@@ -75,20 +75,47 @@ class ConcatLayer(Layer):
             shape[self.axis] += b.shape[self.axis]
         tops[0].reshape(tuple(shape), bottoms[0].dtype)
 
+    relu_gate_parts: frozenset = frozenset()  # bottoms whose in-place ReLU backward runs here
+
+    def _hip_ok(self, bottoms, ax) -> bool:
+        """One-launch HIP path: channel concat of NHWC bf16 device blobs, <= 8 parts."""
+        b0 = bottoms[0].data
+        return (b0.is_cuda and b0.dtype == torch.bfloat16 and ax == b0.dim() - 1 and len(bottoms) <= 8
+                and all(b.data.shape[-1] % 8 == 0 for b in bottoms))
+
     def forward(self, bottoms, tops):
         if len(bottoms) == 1:
             tops[0].data = bottoms[0].data
             return
         ax = _phys_axis(bottoms[0], self.axis)
+        if self._hip_ok(bottoms, ax):
+            from ..ops import hip
+            shape = list(bottoms[0].data.shape)
+            shape[-1] = sum(b.data.shape[-1] for b in bottoms)
+            out = torch.empty(shape, dtype=torch.bfloat16, device=bottoms[0].data.device)
+            tops[0].data = hip.concat_channels([b.data for b in bottoms], out)
+            return
         tops[0].data = torch.cat([b.data for b in bottoms], dim=ax)
 
     def backward(self, tops, propagate_down, bottoms):
         ax = _phys_axis(bottoms[0], self.axis)
+        gates = [i in self.relu_gate_parts for i in range(len(bottoms))]
+        if len(bottoms) > 1 and self._hip_ok(bottoms, ax):
+            from ..ops import hip
+            diffs = [torch.empty_like(b.data) if propagate_down[i] else None for i, b in enumerate(bottoms)]
+            hip.concat_channels_bwd(tops[0].diff, diffs, [b.data if g and d is not None else None
+                                                         for b, g, d in zip(bottoms, gates, diffs)],
+                                    [b.data.shape[-1] for b in bottoms])
+            for b, d in zip(bottoms, diffs):
+                if d is not None:
+                    b.diff = d
+            return
         off = 0
         for i, b in enumerate(bottoms):
             n = b.shape[self.axis]
             if propagate_down[i]:
-                b.diff = tops[0].diff.narrow(ax, off, n).contiguous()
+                d = tops[0].diff.narrow(ax, off, n)
+                b.diff = (d * (b.data > 0).to(d.dtype)) if gates[i] else d.contiguous()
             off += n
 
 

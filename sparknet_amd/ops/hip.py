@@ -405,6 +405,40 @@ def advance_rng(rng_state):
     call("advance_rng", rng_state)
 
 
+def concat_channels(parts, out):
+    """NHWC channel concat of bf16 ``parts`` into ``out`` (one launch, <= 8 parts)."""
+    pix = out.numel() // out.shape[-1]
+    parts = [_c(t) for t in parts]
+    assert sum(t.shape[-1] for t in parts) == out.shape[-1] and all(t.numel() // t.shape[-1] == pix for t in parts)
+    _concat(parts, None, [t.shape[-1] for t in parts], out, pix, 0)
+    return out
+
+
+def concat_channels_bwd(dy, diffs, gates, chans):
+    """Backward of concat_channels: ``diffs[i]`` (pre-allocated, or None to skip the part)
+    get channels [sum(chans[:i]), +chans[i]) of ``dy``, masked by ``gates[i] > 0`` when a
+    gate is given."""
+    dy = _c(dy)
+    pix = dy.numel() // dy.shape[-1]
+    assert sum(chans) == dy.shape[-1]
+    for d, g, c in zip(diffs, gates, chans):
+        assert d is None or (d.is_contiguous() and d.shape[-1] == c and d.numel() // c == pix)
+        assert g is None or (g.is_contiguous() and d is not None and g.shape == d.shape)
+    _concat(diffs, gates, chans, dy, pix, 1)
+
+
+def _concat(parts, gates, chans, top, pix, bwd):
+    n = len(parts)
+    P = (C.c_void_p * 8)(*[(t.data_ptr() if t is not None else 0) for t in parts] + [0] * (8 - n))
+    G = (C.c_void_p * 8)(*[(g.data_ptr() if g is not None else 0) for g in (gates or [None] * n)] + [0] * (8 - n))
+    Ch = (C.c_longlong * 8)(*list(chans) + [0] * (8 - n))
+    _lib.check(_lib.kernels().sn_concat_nhwc(P, G, Ch, C.c_longlong(n), C.c_void_p(top.data_ptr()),
+                                             C.c_longlong(pix), C.c_longlong(bwd), C.c_void_p(_lib.stream_ptr())),
+               "concat_nhwc")
+    if _lib.DEBUG_SYNC:
+        _lib.debug_sync("concat_nhwc")
+
+
 def sum_bf16(tensors, out=None):
     out = torch.empty_like(tensors[0]) if out is None else out
     n = out.numel()

@@ -302,3 +302,28 @@ def test_sum_bf16(gpu, k):
     from sparknet_amd.ops import hip
     xs = [rnd(3, 5, 8) for _ in range(k)]
     close(hip.sum_bf16(xs), sum(x.float() for x in xs), 1e-2)
+
+
+def test_concat_channels_fwd_bwd_gate(gpu):
+    """NHWC channel concat (one launch) and its backward with per-part ReLU masks and a
+    skipped part, against torch.cat / narrow."""
+    from sparknet_amd.ops import hip
+    chans = [64, 24, 128, 8]
+    parts = [rnd(3, 7, 9, c) for c in chans]
+    out = torch.empty(3, 7, 9, sum(chans), dtype=torch.bfloat16, device=gpu)
+    hip.concat_channels(parts, out)
+    assert torch.equal(out, torch.cat(parts, dim=-1))
+    dy = rnd(3, 7, 9, sum(chans))
+    parts[1][0, 0, 0, :4] = 0.0  # exact zeros: masked like relu_bwd (x > 0 fails)
+    diffs = [torch.empty_like(p) for p in parts]
+    diffs[2] = None
+    gates = [parts[0], parts[1], None, parts[3]]
+    hip.concat_channels_bwd(dy, diffs, gates, chans)
+    off = 0
+    for i, c in enumerate(chans):
+        want = dy[..., off:off + c]
+        if gates[i] is not None:
+            want = want * (parts[i] > 0).to(want.dtype)
+        if diffs[i] is not None:
+            assert torch.equal(diffs[i], want), i
+        off += c

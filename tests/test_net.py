@@ -222,6 +222,29 @@ def test_relu_forward_backward_fusion_matches_unfused():
     assert torch.allclose(g0, g1, rtol=1e-5, atol=1e-6 * float(g0.abs().max()))
 
 
+def _googlenet_tiny():
+    n = models.googlenet(train_batch=2, test_batch=2, crop=67, classes=7, aux=False)
+    for l in n.layer:
+        if l.type == "Dropout":
+            l.dropout_param.dropout_ratio = 0.0
+        if l.name == "pool5/7x7_s1":
+            for f in ("kernel_h", "kernel_w", "stride_h", "stride_w", "kernel_size", "stride"):
+                l.pooling_param.ClearField(f)
+            l.pooling_param.global_pooling = True
+    return n
+
+
+def test_concat_relu_backward_fusion_matches_unfused():
+    """Inception branch ReLUs feeding a Concat: their backward masks are applied by the
+    concat backward (relu_gate_parts) and the result equals the unfused gradients."""
+    n = _googlenet_tiny()
+    l0, g0, _ = _grads_with_fusion(n, False)
+    l1, g1, counts = _grads_with_fusion(n, True)
+    assert counts[1] >= 9 * 4, counts  # at least the four branch outputs of each inception module
+    assert abs(l0 - l1) < 1e-5 * max(1.0, abs(l0))
+    assert torch.allclose(g0, g1, rtol=1e-5, atol=1e-6 * float(g0.abs().max()))
+
+
 def test_lazy_gradient_clear_matches_memset():
     """clear_param_diffs(lazy=True) + first-write overwrite == memset + accumulate, with
     garbage left in the buffer, two accumulated passes (iter_size), a frozen layer and a

@@ -49,6 +49,30 @@ def test_relu_gate_fusion_on_gpu(gpu):
     assert err < 1e-2, err
 
 
+def test_googlenet_concat_gate_on_gpu(gpu):
+    """GoogLeNet: HIP channel concat and the Inception ReLU masks applied in the concat
+    backward, fused vs unfused on the GPU, and the fused GPU pass vs the fp32 CPU engine."""
+    n = models.googlenet(train_batch=2, test_batch=2, crop=67, classes=7, aux=False)
+    for l in n.layer:
+        if l.type == "Dropout":
+            l.dropout_param.dropout_ratio = 0.0
+        if l.name == "pool5/7x7_s1":
+            for f in ("kernel_h", "kernel_w", "stride_h", "stride_w", "kernel_size", "stride"):
+                l.pooling_param.ClearField(f)
+            l.pooling_param.global_pooling = True
+    l0, g0, net0 = _run(n, gpu, False)
+    l1, g1, net = _run(n, gpu, True, weights=net0.flat_data.detach().float().cpu())
+    gated = sum(len(getattr(l, "relu_gate_parts", ())) for l in net.layers if l.type_name == "Concat")
+    assert gated == 9 * 4, gated
+    assert abs(l0 - l1) <= 1e-3 * max(1.0, abs(l0))
+    err = (g0 - g1).abs().max().item() / (g0.abs().max().item() + 1e-12)
+    assert err < 1e-2, err
+    lc, gc, _ = _run(n, "cpu", False, weights=net0.flat_data.detach().float().cpu())
+    assert abs(lc - l1) <= 3e-2 * max(1.0, abs(lc))
+    cos = torch.nn.functional.cosine_similarity(gc, g1, dim=0).item()
+    assert cos > 0.99, cos
+
+
 def test_caffenet_gpu_matches_cpu_engine(gpu):
     n = _tiny_caffenet(0.0)
     lc, gc, netc = _run(n, "cpu", False)
