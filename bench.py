@@ -39,6 +39,8 @@ def parse():
                    help="run large layers' solver updates on a side stream during backward")
     p.add_argument("--no-fuse-fc", action="store_true",
                    help="store InnerProduct weight gradients and update them in the solver kernel")
+    p.add_argument("--streams", type=int, default=4,
+                   help="HIP streams for parallel branches (Inception towers) inside the graph; 1 = sequential")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--host-profile", action="store_true",
                    help="after the timed run, report the host time per step part (stderr)")
@@ -90,7 +92,8 @@ def main():
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
     n_fp8 = enable_fp8(net) if args.dtype == "fp8" else 0
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph,
-                              overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc)
+                              overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc,
+                              streams=args.streams)
     trainer.broadcast_initial()
 
     # warmup (includes hipGraph capture and one averaging collective to set up RCCL)
@@ -146,7 +149,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
-                "hipgraph": not args.no_graph, "fused_input_fold": fused_fold, "fp8_layers": n_fp8,
+                "hipgraph": not args.no_graph, "streams": args.streams, "fused_input_fold": fused_fold, "fp8_layers": n_fp8,
                 "final_loss": round(final_loss, 4),
             },
         }

@@ -453,6 +453,11 @@ class Net:
             layer.forward(self.bottom_vecs[li], self.top_vecs[li])
             if self.debug_info:
                 self._debug_forward(li)
+        return self.loss_value()
+
+    def loss_value(self):
+        """Weighted sum of the loss tops as a device scalar (no host sync)."""
+        loss = None
         if len(self._loss_tops) == 1 and self._loss_tops[0][1] == 1.0:
             t = self._loss_tops[0][0].data
             if t.numel() == 1 and t.dtype == torch.float32:

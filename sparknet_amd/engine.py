@@ -227,6 +227,134 @@ def fp8_step(net) -> None:
         net.ctx.fp8.update()
 
 
+class BranchStreams:
+    """Run independent branches of a DAG net on parallel HIP streams.
+
+    Caffe executes layers strictly in prototxt order on the default stream
+    (net.cpp:565-581, :635-645).  On a 256-CU MI355X the late GoogLeNet Inception stages
+    (7x7 / 14x14 maps, 4 parallel towers) launch GEMMs of 50-150 tiles each, so a
+    sequential schedule leaves most CUs idle.  This scheduler derives the dependency DAG
+    from blob reads / writes (forward: bottoms -> tops; backward: top diffs + blob data ->
+    bottom diffs + param diffs; read-after-write, write-after-read and write-after-write
+    hazards), assigns every layer to one of ``n_streams`` streams (a layer continues the
+    stream of a producer it directly follows, otherwise takes the least recently used
+    stream) and joins streams with events.  Inside a hipGraph capture the events become
+    graph edges, so the towers of one Inception module run concurrently with no host
+    involvement.  Every blob and gradient keeps its single producer, so results are
+    bitwise identical to the sequential order.  Nets with backward hooks keep a
+    sequential backward."""
+
+    def __init__(self, net, n_streams: int = 4):
+        self.net = net
+        self.n = max(1, n_streams)
+        self.side = None  # created on first run (the plan itself is device-independent)
+        L = len(net.layers)
+        fwd = [(li, {("v", b) for b in net.bottom_ids[li]}, {("v", b) for b in net.top_ids[li]})
+               for li in range(L)]
+        bwd = []
+        for li in range(L - 1, -1, -1):
+            if not net.layer_need_backward[li]:
+                continue
+            reads = {("v", b) for b in list(net.bottom_ids[li]) + list(net.top_ids[li])}
+            reads |= {("d", b) for b in net.top_ids[li]}
+            writes = {("d", b) for b, need in zip(net.bottom_ids[li], net.bottom_need_backward[li]) if need}
+            writes |= {("p", p.offset) for p in net.layers[li].params}
+            bwd.append((li, reads, writes))
+        self.fwd_plan = self._plan(fwd)
+        self.bwd_plan = self._plan(bwd)
+
+    def _plan(self, nodes):
+        last_w, readers = {}, {}
+        tail = [-1] * self.n                           # last position placed on each stream
+        seen = [[-1] * self.n for _ in range(self.n)]  # seen[s][x]: last pos of stream x that s waited on
+        stream_of, plan = [], []
+        for pos, (li, reads, writes) in enumerate(nodes):
+            deps = {last_w[r] for r in reads if r in last_w}
+            for w in writes:
+                if w in last_w:
+                    deps.add(last_w[w])
+                deps |= readers.get(w, set())
+            deps.discard(pos)
+            follow = [stream_of[d] for d in sorted(deps, reverse=True) if tail[stream_of[d]] == d]
+            if follow:
+                sid = follow[0]
+            elif not deps:
+                sid = 0
+            else:
+                sid = min(range(self.n), key=lambda s: tail[s])
+            waits = [d for d in sorted(deps) if stream_of[d] != sid and d > seen[sid][stream_of[d]]]
+            for d in waits:
+                seen[sid][stream_of[d]] = max(seen[sid][stream_of[d]], d)
+            stream_of.append(sid)
+            tail[sid] = pos
+            plan.append([li, sid, waits, False])
+            for r in reads:
+                readers.setdefault(r, set()).add(pos)
+            for w in writes:
+                last_w[w] = pos
+                readers[w] = set()
+        for _, _, waits, _ in list(plan):
+            for d in waits:
+                plan[d][3] = True
+        return plan
+
+    def streams_used(self, backward: bool = False) -> int:
+        return len({sid for _, sid, _, _ in (self.bwd_plan if backward else self.fwd_plan)})
+
+    def _run(self, plan, fn) -> None:
+        if self.side is None:
+            self.side = [torch.cuda.Stream(self.net.device) for _ in range(self.n - 1)]
+        main = torch.cuda.current_stream(self.net.device)
+        streams = [main] + self.side
+        for s in self.side:
+            s.wait_stream(main)
+        events = {}
+        for pos, (li, sid, waits, record) in enumerate(plan):
+            st = streams[sid]
+            for d in waits:
+                st.wait_event(events[d])
+            with torch.cuda.stream(st):
+                fn(li)
+            if record:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                events[pos] = ev
+        for s in self.side:
+            main.wait_stream(s)
+
+    def forward(self):
+        net = self.net
+        self._run(self.fwd_plan, lambda li: net.layers[li].forward(net.bottom_vecs[li], net.top_vecs[li]))
+        return net.loss_value()
+
+    def backward(self) -> None:
+        net = self.net
+        if net.backward_hooks:
+            net.backward()
+            return
+        net.prefill_loss_diffs()
+        for hook in net.pre_backward_hooks:
+            hook()
+        self._run(self.bwd_plan, lambda li: net.layers[li].backward(
+            net.top_vecs[li], net.bottom_need_backward[li], net.bottom_vecs[li]))
+
+    def forward_backward(self):
+        loss = self.forward()
+        self.backward()
+        return loss
+
+
+def branch_streams(net, n_streams: int = 4):
+    """A :class:`BranchStreams` executor for ``net`` when its layer DAG has parallel
+    branches (the plan puts work on more than one stream), else None."""
+    if net.device.type != "cuda" or n_streams <= 1:
+        return None
+    bs = BranchStreams(net, n_streams)
+    if bs.streams_used() <= 1 and bs.streams_used(backward=True) <= 1:
+        return None
+    return bs
+
+
 class OverlappedUpdate:
     """Runs each layer's fused solver update on a side stream as soon as backward has
     produced that layer's final gradients, so the bandwidth-bound update (CaffeNet: 61 M
@@ -270,7 +398,8 @@ class OverlappedUpdate:
 class GraphStep:
     """One captured solver iteration (iter_size = 1)."""
 
-    def __init__(self, solver: Solver, warmup: int = 2, pre=None, overlap: bool = True, fuse_fc: bool = True):
+    def __init__(self, solver: Solver, warmup: int = 2, pre=None, overlap: bool = True, fuse_fc: bool = True,
+                 streams: int = 4):
         self.solver = solver
         self.pre = pre  # callable run (eagerly) before each replay, e.g. feeder.stage
         self.graph = None
@@ -282,6 +411,11 @@ class GraphStep:
             solver.net.backward_hooks.append(self.overlap.hook)
         elif fuse_fc:
             fuse_fc_updates(solver)
+        # parallel Inception towers etc.; built lazily, used from the 2nd warmup iteration
+        # on (the first one autotunes GEMMs, timed on an otherwise idle GPU)
+        self.n_streams = streams if not solver.net.debug_info else 1
+        self.branches = None
+        self._use_branches = False
 
     def _body(self):
         s = self.solver
@@ -289,7 +423,10 @@ class GraphStep:
         net.clear_param_diffs(lazy=True)
         if self.overlap is not None:
             self.overlap.begin()
-        loss = net.forward_backward()
+        if self._use_branches and self.branches is None:
+            self.branches = branch_streams(net, self.n_streams) or False
+        loss = (self.branches.forward_backward() if self._use_branches and self.branches
+                else net.forward_backward())
         net.finish_param_diffs()
         fp8_step(net)
         ops.advance_rng(net.ctx.rng_state)
@@ -305,7 +442,8 @@ class GraphStep:
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            for _ in range(self.warmup):
+            for w in range(self.warmup):
+                self._use_branches = w > 0
                 if self.pre:
                     self.pre()
                 s.stage_hyper()
@@ -314,6 +452,7 @@ class GraphStep:
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
+        self._use_branches = True
         if self.pre:
             self.pre()
         s.stage_hyper()
@@ -340,14 +479,14 @@ class LocalSGDTrainer:
     """tau local steps + weight averaging per round (SparkNet's model averaging)."""
 
     def __init__(self, solver: Solver, comm=None, tau: int = 50, feeder=None, use_graph: bool = True,
-                 log_every: int = 0, overlap_update: bool = False, fuse_fc: bool = True):
+                 log_every: int = 0, overlap_update: bool = False, fuse_fc: bool = True, streams: int = 4):
         self.solver = solver
         self.comm = comm
         self.tau = tau
         self.feeder = feeder
         self.round = 0
         self.use_graph = use_graph and solver.device.type == "cuda"
-        self.step_fn = (GraphStep(solver, pre=self._pre, overlap=overlap_update, fuse_fc=fuse_fc)
+        self.step_fn = (GraphStep(solver, pre=self._pre, overlap=overlap_update, fuse_fc=fuse_fc, streams=streams)
                         if self.use_graph else None)
         self.log_every = log_every
         self.times = {"compute": 0.0, "allreduce": 0.0}

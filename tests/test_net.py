@@ -335,3 +335,46 @@ def test_stochastic_pooling_train_samples_proportionally():
     test.blobs[test.blob_names.index("x")].set_nchw(torch.tensor([1.0, 3.0]).repeat(n, 1, 1, 1))
     test.forward()
     assert torch.allclose(test.blobs[test.blob_names.index("y")].nchw(), torch.full((n, 1, 1, 1), 2.5))
+
+
+def test_branch_stream_plan_respects_dependencies():
+    """engine.BranchStreams: GoogLeNet's Inception towers are spread over several streams,
+    and replaying the plan in stream order (each stream serial, cross-stream waits
+    honoured) never runs a layer before the producers of what it reads or before the
+    readers / writers of what it overwrites."""
+    from sparknet_amd import models, proto
+    from sparknet_amd.core.net import Net
+    from sparknet_amd.engine import BranchStreams
+    n = models.googlenet(train_batch=1, test_batch=1, crop=67, classes=7, aux=False)
+    for l in n.layer:
+        if l.name == "pool5/7x7_s1":
+            for f in ("kernel_h", "kernel_w", "stride_h", "stride_w", "kernel_size", "stride"):
+                l.pooling_param.ClearField(f)
+            l.pooling_param.global_pooling = True
+    net = Net(n, phase=proto.TRAIN, seed=1, device="cpu")
+    bs = BranchStreams(net, 4)
+    assert bs.streams_used() == 4 and bs.streams_used(backward=True) == 4
+    for plan in (bs.fwd_plan, bs.bwd_plan):
+        # the earliest time each node may run when streams proceed in parallel (unit cost)
+        finish, stream_t = {}, [0] * 4
+        for pos, (li, sid, waits, _) in enumerate(plan):
+            start = max([stream_t[sid]] + [finish[d] for d in waits])
+            finish[pos] = start + 1
+            stream_t[sid] = finish[pos]
+        # a node's start >= finish of every earlier node it conflicts with
+        order = [li for li, _, _, _ in plan]
+        fwd = plan is bs.fwd_plan
+        def rw(li):
+            if fwd:
+                return set(net.bottom_ids[li]), set(net.top_ids[li])
+            r = {("v", b) for b in list(net.bottom_ids[li]) + list(net.top_ids[li])} | \
+                {("d", b) for b in net.top_ids[li]}
+            w = {("d", b) for b, need in zip(net.bottom_ids[li], net.bottom_need_backward[li]) if need}
+            return r, w | {("p", p.offset) for p in net.layers[li].params}
+        for j in range(len(order)):
+            rj, wj = rw(order[j])
+            for i in range(j):
+                ri, wi = rw(order[i])
+                if (wi & rj) or (wi & wj) or (ri & wj):
+                    assert finish[j] - 1 >= finish[i], (order[i], order[j])
+        assert max(finish.values()) < len(plan)  # some layers really overlap

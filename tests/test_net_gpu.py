@@ -169,3 +169,49 @@ def test_fp8_forward_training(gpu):
     # same data every step: both must fit it; fp8 stays close to bf16
     assert losses["fp8"][-1] < losses["fp8"][0]
     assert abs(losses["fp8"][0] - losses["bf16"][0]) < 0.05 * abs(losses["bf16"][0]) + 0.05
+
+
+def test_googlenet_branch_streams_bitwise(gpu):
+    """engine.BranchStreams runs the Inception towers on 4 HIP streams (eager and inside a
+    captured hipGraph); loss and every parameter gradient are bitwise equal to the
+    sequential schedule."""
+    from sparknet_amd.engine import BranchStreams, fuse_relu
+    n = models.googlenet(train_batch=4, test_batch=4, crop=67, classes=7, aux=True)
+    for l in n.layer:
+        if l.type == "Dropout":
+            l.dropout_param.dropout_ratio = 0.0
+        if l.name in ("pool5/7x7_s1", "loss1/ave_pool", "loss2/ave_pool"):
+            for f in ("kernel_h", "kernel_w", "stride_h", "stride_w", "kernel_size", "stride"):
+                l.pooling_param.ClearField(f)
+            l.pooling_param.global_pooling = True
+    net = Net(n, phase=proto.TRAIN, seed=3, device=gpu)
+    fuse_relu(net)
+    g = torch.Generator().manual_seed(5)
+    net.blob_by_name("data").set_nchw(torch.randn(4, 3, 67, 67, generator=g) * 20)
+    net.blob_by_name("label").set_nchw(torch.tensor([[1.0], [5.0], [0.0], [6.0]]))
+
+    def once(fn):
+        net.clear_param_diffs()
+        loss = fn()
+        torch.cuda.synchronize()
+        return float(loss), net.flat_diff.detach().clone()
+
+    l0, g0 = once(net.forward_backward)
+    bs = BranchStreams(net, 4)
+    assert bs.streams_used() == 4
+    l1, g1 = once(bs.forward_backward)
+    assert l0 == l1 and torch.equal(g0, g1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        once(bs.forward_backward)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    net.clear_param_diffs()
+    with torch.cuda.graph(graph):
+        loss = bs.forward_backward()
+    for _ in range(2):
+        net.flat_diff.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert float(loss) == l0 and torch.equal(net.flat_diff, g0)
