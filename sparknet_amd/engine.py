@@ -242,7 +242,9 @@ class BranchStreams:
     graph edges, so the towers of one Inception module run concurrently with no host
     involvement.  Every blob and gradient keeps its single producer, so results are
     bitwise identical to the sequential order.  Nets with backward hooks keep a
-    sequential backward."""
+    sequential backward.  Status: eager multi-stream runs are verified bitwise on the
+    MI355X; the captured variant segfaults in hipStreamEndCapture (under
+    investigation), so GraphStep keeps ``streams=1`` by default."""
 
     def __init__(self, net, n_streams: int = 4):
         self.net = net
@@ -304,23 +306,31 @@ class BranchStreams:
     def _run(self, plan, fn) -> None:
         if self.side is None:
             self.side = [torch.cuda.Stream(self.net.device) for _ in range(self.n - 1)]
+            self._events = {}
+            self._fork_join = (torch.cuda.Event(), [torch.cuda.Event() for _ in self.side])
         main = torch.cuda.current_stream(self.net.device)
         streams = [main] + self.side
+        # Events live as long as the executor: a captured hipGraph references the event
+        # objects of its record / wait nodes, and HIP crashes at capture end if an event
+        # recorded during the capture was destroyed before it.
+        evs = self._events.setdefault(id(plan), {})
+        fork, join = self._fork_join
+        fork.record(main)
         for s in self.side:
-            s.wait_stream(main)
-        events = {}
+            s.wait_event(fork)
         for pos, (li, sid, waits, record) in enumerate(plan):
             st = streams[sid]
             for d in waits:
-                st.wait_event(events[d])
+                st.wait_event(evs[d])
             with torch.cuda.stream(st):
                 fn(li)
             if record:
-                ev = torch.cuda.Event()
-                ev.record(st)
-                events[pos] = ev
-        for s in self.side:
-            main.wait_stream(s)
+                if pos not in evs:
+                    evs[pos] = torch.cuda.Event()
+                evs[pos].record(st)
+        for s, ev in zip(self.side, join):
+            ev.record(s)
+            main.wait_event(ev)
 
     def forward(self):
         net = self.net
@@ -399,7 +409,7 @@ class GraphStep:
     """One captured solver iteration (iter_size = 1)."""
 
     def __init__(self, solver: Solver, warmup: int = 2, pre=None, overlap: bool = True, fuse_fc: bool = True,
-                 streams: int = 4):
+                 streams: int = 1):
         self.solver = solver
         self.pre = pre  # callable run (eagerly) before each replay, e.g. feeder.stage
         self.graph = None
@@ -412,7 +422,10 @@ class GraphStep:
         elif fuse_fc:
             fuse_fc_updates(solver)
         # parallel Inception towers etc.; built lazily, used from the 2nd warmup iteration
-        # on (the first one autotunes GEMMs, timed on an otherwise idle GPU)
+        # on (the first one autotunes GEMMs, timed on an otherwise idle GPU).  Off by
+        # default: eager multi-stream execution is verified bitwise, but capturing the
+        # multi-stream schedule into a hipGraph currently crashes inside
+        # hipStreamEndCapture on ROCm 7 (docs/PERF_NOTES.md)
         self.n_streams = streams if not solver.net.debug_info else 1
         self.branches = None
         self._use_branches = False
@@ -479,7 +492,7 @@ class LocalSGDTrainer:
     """tau local steps + weight averaging per round (SparkNet's model averaging)."""
 
     def __init__(self, solver: Solver, comm=None, tau: int = 50, feeder=None, use_graph: bool = True,
-                 log_every: int = 0, overlap_update: bool = False, fuse_fc: bool = True, streams: int = 4):
+                 log_every: int = 0, overlap_update: bool = False, fuse_fc: bool = True, streams: int = 1):
         self.solver = solver
         self.comm = comm
         self.tau = tau
