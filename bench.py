@@ -39,9 +39,9 @@ def parse():
                    help="run large layers' solver updates on a side stream during backward")
     p.add_argument("--no-fuse-fc", action="store_true",
                    help="store InnerProduct weight gradients and update them in the solver kernel")
-    p.add_argument("--streams", type=int, default=1,
+    p.add_argument("--streams", type=int, default=2,
                    help="HIP streams for parallel branches (Inception towers) inside the graph; 1 = sequential "
-                        "(experimental: >1 crashes at graph capture on ROCm 7)")
+                        "(>= 3 crashes at graph capture on ROCm 7)")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--host-profile", action="store_true",
                    help="after the timed run, report the host time per step part (stderr)")

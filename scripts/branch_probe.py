@@ -42,13 +42,23 @@ torch.cuda.synchronize()
 print("side-stream eager ok", flush=True)
 g = torch.cuda.CUDAGraph()
 which = sys.argv[3] if len(sys.argv) > 3 else "both"
-with torch.cuda.graph(g):
-    if which == "fwd":
-        bs.forward()
-    elif which == "bwd":
-        net.backward_from_to(len(net.layers) - 1, 0) if False else bs.backward()
-    else:
-        bs.forward_backward()
+import traceback  # noqa: E402
+cs = torch.cuda.Stream()
+cs.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(cs):
+    g.capture_begin()
+    try:
+        if which == "fwd":
+            bs.forward()
+        else:
+            bs.forward_backward()
+        print("body ok", flush=True)
+    except BaseException:
+        traceback.print_exc()
+        sys.stdout.flush(); sys.stderr.flush()
+        os._exit(3)
+    g.capture_end()
+torch.cuda.current_stream().wait_stream(cs)
 print("capture ok", flush=True)
 g.replay()
 torch.cuda.synchronize()

@@ -242,9 +242,11 @@ class BranchStreams:
     graph edges, so the towers of one Inception module run concurrently with no host
     involvement.  Every blob and gradient keeps its single producer, so results are
     bitwise identical to the sequential order.  Nets with backward hooks keep a
-    sequential backward.  Status: eager multi-stream runs are verified bitwise on the
-    MI355X; the captured variant segfaults in hipStreamEndCapture (under
-    investigation), so GraphStep keeps ``streams=1`` by default."""
+    sequential backward.  Status on the MI355X: eager runs with 4 streams and hipGraph
+    captures with 2 streams are verified bitwise (GoogLeNet 17.1k -> 19.4k img/s);
+    captures with >= 3 streams segfault in hipStreamEndCapture even though plain
+    PyTorch 4-stream captures work (scripts/capture_probe*.py), so GraphStep uses
+    ``streams=2``."""
 
     def __init__(self, net, n_streams: int = 4):
         self.net = net
@@ -409,7 +411,7 @@ class GraphStep:
     """One captured solver iteration (iter_size = 1)."""
 
     def __init__(self, solver: Solver, warmup: int = 2, pre=None, overlap: bool = True, fuse_fc: bool = True,
-                 streams: int = 1):
+                 streams: int = 2):
         self.solver = solver
         self.pre = pre  # callable run (eagerly) before each replay, e.g. feeder.stage
         self.graph = None
@@ -422,10 +424,9 @@ class GraphStep:
         elif fuse_fc:
             fuse_fc_updates(solver)
         # parallel Inception towers etc.; built lazily, used from the 2nd warmup iteration
-        # on (the first one autotunes GEMMs, timed on an otherwise idle GPU).  Off by
-        # default: eager multi-stream execution is verified bitwise, but capturing the
-        # multi-stream schedule into a hipGraph currently crashes inside
-        # hipStreamEndCapture on ROCm 7 (docs/PERF_NOTES.md)
+        # on (the first one autotunes GEMMs, timed on an otherwise idle GPU).  Two
+        # streams by default: captures with >= 3 streams crash inside hipStreamEndCapture
+        # on ROCm 7 (docs/PERF_NOTES.md)
         self.n_streams = streams if not solver.net.debug_info else 1
         self.branches = None
         self._use_branches = False
@@ -492,7 +493,7 @@ class LocalSGDTrainer:
     """tau local steps + weight averaging per round (SparkNet's model averaging)."""
 
     def __init__(self, solver: Solver, comm=None, tau: int = 50, feeder=None, use_graph: bool = True,
-                 log_every: int = 0, overlap_update: bool = False, fuse_fc: bool = True, streams: int = 1):
+                 log_every: int = 0, overlap_update: bool = False, fuse_fc: bool = True, streams: int = 2):
         self.solver = solver
         self.comm = comm
         self.tau = tau
