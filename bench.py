@@ -41,7 +41,7 @@ def parse():
                    help="store InnerProduct weight gradients and update them in the solver kernel")
     p.add_argument("--streams", type=int, default=2,
                    help="HIP streams for parallel branches (Inception towers) inside the graph; 1 = sequential "
-                        "(>= 3 crashes at graph capture on ROCm 7)")
+                        "(>= 3 uses the star topology, see engine.BranchStreams)")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--host-profile", action="store_true",
                    help="after the timed run, report the host time per step part (stderr)")

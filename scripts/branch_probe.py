@@ -24,7 +24,8 @@ net = Net(n, phase=proto.TRAIN, seed=3, device="cuda")
 fuse_relu(net)
 net.blob_by_name("data").set_nchw(torch.randn(4, 3, 67, 67) * 20)
 net.blob_by_name("label").set_nchw(torch.tensor([[1.0], [5.0], [0.0], [6.0]]))
-bs = BranchStreams(net, nstreams)
+bs = BranchStreams(net, nstreams, star=os.environ.get('SN_STAR') == '1')
+print('streams used', bs.streams_used(), bs.streams_used(True), flush=True)
 for plan in (bs.fwd_plan, bs.bwd_plan):  # nodes past `limit` go to stream 0 with full waits
     pass
 net.clear_param_diffs()

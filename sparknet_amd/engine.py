@@ -243,14 +243,16 @@ class BranchStreams:
     involvement.  Every blob and gradient keeps its single producer, so results are
     bitwise identical to the sequential order.  Nets with backward hooks keep a
     sequential backward.  Status on the MI355X: eager runs with 4 streams and hipGraph
-    captures with 2 streams are verified bitwise (GoogLeNet 17.1k -> 19.4k img/s);
-    captures with >= 3 streams segfault in hipStreamEndCapture even though plain
-    PyTorch 4-stream captures work (scripts/capture_probe*.py), so GraphStep uses
-    ``streams=2``."""
+    captures with 2 streams or with 4 streams in the ``star`` topology are verified
+    bitwise (GoogLeNet 17.1k -> 19.4k / 19.5k img/s).  A capture in which one side stream
+    waits on an event of another side stream segfaults in hipStreamEndCapture on ROCm 7,
+    so ``star`` (side streams wait only on the main stream; a layer with inputs from
+    several side streams runs on the main stream) is used whenever n_streams > 2."""
 
-    def __init__(self, net, n_streams: int = 4):
+    def __init__(self, net, n_streams: int = 4, star: bool = False):
         self.net = net
         self.n = max(1, n_streams)
+        self.star = star
         self.side = None  # created on first run (the plan itself is device-independent)
         L = len(net.layers)
         fwd = [(li, {("v", b) for b in net.bottom_ids[li]}, {("v", b) for b in net.top_ids[li]})
@@ -286,6 +288,8 @@ class BranchStreams:
                 sid = 0
             else:
                 sid = min(range(self.n), key=lambda s: tail[s])
+            if self.star and sid != 0 and any(stream_of[d] not in (0, sid) for d in deps):
+                sid = 0  # star topology: side streams only ever wait on the main stream
             waits = [d for d in sorted(deps) if stream_of[d] != sid and d > seen[sid][stream_of[d]]]
             for d in waits:
                 seen[sid][stream_of[d]] = max(seen[sid][stream_of[d]], d)
@@ -361,7 +365,7 @@ def branch_streams(net, n_streams: int = 4):
     branches (the plan puts work on more than one stream), else None."""
     if net.device.type != "cuda" or n_streams <= 1:
         return None
-    bs = BranchStreams(net, n_streams)
+    bs = BranchStreams(net, n_streams, star=n_streams > 2)
     if bs.streams_used() <= 1 and bs.streams_used(backward=True) <= 1:
         return None
     return bs
@@ -425,8 +429,7 @@ class GraphStep:
             fuse_fc_updates(solver)
         # parallel Inception towers etc.; built lazily, used from the 2nd warmup iteration
         # on (the first one autotunes GEMMs, timed on an otherwise idle GPU).  Two
-        # streams by default: captures with >= 3 streams crash inside hipStreamEndCapture
-        # on ROCm 7 (docs/PERF_NOTES.md)
+        # streams by default; more use the star topology (see BranchStreams)
         self.n_streams = streams if not solver.net.debug_info else 1
         self.branches = None
         self._use_branches = False

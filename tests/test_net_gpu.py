@@ -174,8 +174,9 @@ def test_fp8_forward_training(gpu):
 def test_googlenet_branch_streams_bitwise(gpu):
     """engine.BranchStreams runs the Inception towers on 4 HIP streams (eager); loss and
     every parameter gradient are bitwise equal to the sequential schedule; the same holds
-    for the 2-stream schedule captured into a hipGraph and replayed.  (Captures with >= 3
-    streams crash in hipStreamEndCapture, see engine.BranchStreams.)"""
+    for the 2-stream and the 4-stream star schedules captured into hipGraphs and replayed.
+    (Captures with side-stream -> side-stream waits crash in hipStreamEndCapture, see
+    engine.BranchStreams.)"""
     from sparknet_amd.engine import BranchStreams, fuse_relu
     n = models.googlenet(train_batch=4, test_batch=4, crop=67, classes=7, aux=True)
     for l in n.layer:
@@ -208,17 +209,20 @@ def test_googlenet_branch_streams_bitwise(gpu):
         l2, g2 = once(bs.forward_backward)
     torch.cuda.current_stream().wait_stream(s)
     assert l0 == l2 and torch.equal(g0, g2)
-    # captured into a hipGraph with 2 streams (the GraphStep default)
-    b2 = BranchStreams(net, 2)
-    with torch.cuda.stream(s):
-        once(b2.forward_backward)
-    torch.cuda.current_stream().wait_stream(s)
-    graph = torch.cuda.CUDAGraph()
-    net.clear_param_diffs()
-    with torch.cuda.graph(graph):
-        loss = b2.forward_backward()
-    for _ in range(2):
-        net.flat_diff.zero_()
-        graph.replay()
-        torch.cuda.synchronize()
-        assert float(loss) == l0 and torch.equal(net.flat_diff, g0)
+    # captured into hipGraphs: 2 streams (the GraphStep default) and 4 streams in the star
+    # topology (side streams wait only on the main stream)
+    graphs = []
+    for b2 in (BranchStreams(net, 2), BranchStreams(net, 4, star=True)):
+        with torch.cuda.stream(s):
+            once(b2.forward_backward)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        net.clear_param_diffs()
+        with torch.cuda.graph(graph):
+            loss = b2.forward_backward()
+        graphs.append(graph)
+        for _ in range(2):
+            net.flat_diff.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            assert float(loss) == l0 and torch.equal(net.flat_diff, g0)
