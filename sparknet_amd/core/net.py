@@ -447,7 +447,6 @@ class Net:
 
     # -- execution ---------------------------------------------------------------------
     def forward_from_to(self, start: int, end: int):
-        loss = None
         for li in range(start, end + 1):
             layer = self.layers[li]
             layer.forward(self.bottom_vecs[li], self.top_vecs[li])
