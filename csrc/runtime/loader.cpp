@@ -270,28 +270,31 @@ class Loader {
     return files_.empty() ? 20 : 0;
   }
 
-  const std::vector<long long>& perm(long long epoch) {
+  // Shared ownership: a worker keeps its epoch's permutation alive while it reads it,
+  // even if other workers have since evicted that epoch from the small cache.
+  std::shared_ptr<const std::vector<long long>> perm(long long epoch) {
     std::lock_guard<std::mutex> lk(perm_mu_);
     auto it = perms_.find(epoch);
     if (it != perms_.end()) return it->second;
-    std::vector<long long> p(shard_n_);
-    for (long long i = 0; i < shard_n_; ++i) p[i] = i;
+    auto p = std::make_shared<std::vector<long long>>(shard_n_);
+    for (long long i = 0; i < shard_n_; ++i) (*p)[i] = i;
     std::mt19937_64 g(splitmix(cfg_.seed ^ splitmix((uint64_t)epoch + 1)));
     for (long long i = shard_n_ - 1; i > 0; --i) {
       long long j = (long long)(g() % (uint64_t)(i + 1));
-      std::swap(p[i], p[j]);
+      std::swap((*p)[i], (*p)[j]);
     }
     if (perms_.size() > 3) perms_.erase(perms_.begin());
-    return perms_.emplace(epoch, std::move(p)).first->second;
+    perms_.emplace(epoch, p);
+    return p;
   }
 
   void indices(long long b, std::vector<long long>& out) {
     out.resize(cfg_.batch);
     const long long P = batches_per_epoch_;
     if (cfg_.sampler == 0) {
-      const auto& p = perm(b / P);
+      const auto p = perm(b / P);
       const long long k = b % P;
-      for (int i = 0; i < cfg_.batch; ++i) out[i] = p[k * cfg_.batch + i];
+      for (int i = 0; i < cfg_.batch; ++i) out[i] = (*p)[k * cfg_.batch + i];
     } else if (cfg_.sampler == 1) {
       for (int i = 0; i < cfg_.batch; ++i) out[i] = (b * cfg_.batch + i) % shard_n_;
     } else {
@@ -374,7 +377,7 @@ class Loader {
   std::atomic<long long> next_fill_{0};
   long long next_consume_ = 0;
   bool stop_ = false;
-  std::map<long long, std::vector<long long>> perms_;
+  std::map<long long, std::shared_ptr<const std::vector<long long>>> perms_;
   long long filled_ = 0, consumed_ = 0;
   double fill_s_ = 0.0, wait_s_ = 0.0;
 };

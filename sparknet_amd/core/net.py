@@ -671,7 +671,7 @@ class Net:
                         continue
                     raise ValueError(f"Incompatible number of blobs for layer {lname!r}")
                 t = torch.from_numpy(src[str(j)].read().astype("float32"))
-                if t.numel() != p.caffe_count:
+                if tuple(t.shape) != tuple(p.caffe_shape):
                     raise ValueError(f"Cannot copy param of layer {lname!r}; shape mismatch. "
                                      f"Source {tuple(t.shape)}, target {p.caffe_shape}")
                 p.set_caffe(t.reshape(p.caffe_shape))
@@ -693,7 +693,7 @@ class Net:
                 raise ValueError(f"Incompatible number of blobs for layer {slp.name!r}")
             for p, bp in zip(layer.params, slp.blobs):
                 t = blob_proto_to_tensor(bp)
-                if t.numel() != p.caffe_count:
+                if not blob_shape_equals(bp, p.caffe_shape):
                     raise ValueError(f"Cannot copy param of layer {slp.name!r}; shape mismatch. "
                                      f"Source {tuple(t.shape)}, target {p.caffe_shape}")
                 p.set_caffe(t.reshape(p.caffe_shape))
@@ -738,6 +738,19 @@ class Net:
 
     def __repr__(self):
         return f"Net({self.name!r}, {len(self.layers)} layers, {self.num_param_elems if self.flat_data is not None else '?'} param elems)"
+
+
+def blob_shape_equals(bp, shape) -> bool:
+    """Blob::ShapeEquals (blob.cpp:474-490): a legacy (num, channels, height, width) proto
+    matches a target of <= 4 axes padded with leading 1s; otherwise shapes match exactly."""
+    shape = tuple(int(s) for s in shape)
+    if not bp.HasField("shape") and (bp.num or bp.channels or bp.height or bp.width):
+        if len(shape) > 4:
+            return False
+        return (1,) * (4 - len(shape)) + shape == (bp.num, bp.channels, bp.height, bp.width)
+    if bp.HasField("shape"):
+        return tuple(bp.shape.dim) == shape
+    return (len(bp.data) or len(bp.double_data)) == (shape[0] if len(shape) == 1 else -1)
 
 
 def blob_proto_to_tensor(bp) -> torch.Tensor:

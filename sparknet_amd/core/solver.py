@@ -58,6 +58,7 @@ class Solver:
         self.current_step = 0
         self.callbacks: list = []
         self.action_request: Callable[[], str] | None = None
+        self.requested_early_exit = False
         self.losses: list[torch.Tensor] = []
         self.smoothed_loss = 0.0
         self.net = train_net if train_net is not None else self._init_train_net(dtype)
@@ -301,6 +302,7 @@ class Solver:
             if req == "snapshot":
                 self.snapshot()
             elif req == "stop":
+                self.requested_early_exit = True
                 break
         del start_iter
 
@@ -309,7 +311,8 @@ class Solver:
         if resume_file:
             self.restore(resume_file)
         p = self.param
-        while self.iter < p.max_iter:
+        self.requested_early_exit = False
+        while self.iter < p.max_iter and not self.requested_early_exit:
             if p.test_interval and self.iter % p.test_interval == 0 and (self.iter > 0 or p.test_initialization):
                 self.test_all()
             n = p.max_iter - self.iter
@@ -318,7 +321,14 @@ class Solver:
             self.step(n)
         if p.snapshot_after_train and (not p.snapshot or self.iter % p.snapshot != 0):
             self.snapshot()
+        if self.requested_early_exit:  # solver.cpp:300-310: no final pass after a stop request
+            log.info("Optimization stopped early.")
+            return
+        # solver.cpp:317-324: final forward-only loss display, then test on test_interval
         if p.display and self.iter % p.display == 0:
+            loss = self.net.forward()
+            log.info("Iteration %d, loss = %g", self.iter, float(loss))
+        if p.test_interval and self.iter % p.test_interval == 0:
             self.test_all()
 
     # -- testing ------------------------------------------------------------------------------

@@ -73,6 +73,37 @@ int main() {
       sn_loader_destroy(h);  // workers still blocked on slots must be joined cleanly
     }
   }
+  // Many epochs in flight at once (1 batch per epoch, 8 slots, 8 threads): workers read
+  // permutations that other workers evict from the loader's epoch cache.
+  {
+    SnLoaderConfig c;
+    std::memset(&c, 0, sizeof(c));
+    c.source = 1;
+    c.mem_images = imgs.data();
+    c.mem_labels = labs.data();
+    c.mem_count = B;
+    c.image_bytes = ib;
+    c.batch = B;
+    c.sampler = 0;
+    c.world = 1;
+    c.seed = 3;
+    c.slots = 8;
+    c.threads = 8;
+    int err = 0;
+    void* h = sn_loader_create(&c, &err);
+    if (!h) { std::printf("create failed %d\n", err); return 2; }
+    std::vector<long long> idx(B);
+    for (int it = 0; it < 400; ++it) {
+      uint8_t* im;
+      int32_t* lb;
+      long long seq = sn_loader_acquire(h, &im, &lb);
+      sn_loader_batch_indices(h, seq, idx.data());
+      for (int i = 0; i < B; ++i)
+        if (lb[i] != labs[idx[i]] || std::memcmp(im + (size_t)i * ib, &imgs[(size_t)idx[i] * ib], ib)) ++bad;
+      sn_loader_release(h, seq);
+    }
+    sn_loader_destroy(h);
+  }
   std::printf("bad=%d\n", bad);
   return bad ? 1 : 0;
 }

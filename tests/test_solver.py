@@ -162,3 +162,41 @@ def test_snapshot_restore_equivalence(tmp_path):
     b.step(3)
     assert torch.allclose(a.net.flat_data, b.net.flat_data, atol=1e-6)
     assert torch.allclose(a.history[0], b.history[0], atol=1e-6)
+
+
+def test_stop_request_ends_solve():
+    """A 'stop' action request ends Solve() (solver.cpp:300-310): iter stops advancing
+    and no final display / test pass runs."""
+    s = lsq_solver(max_iter=100, display=1, test_interval=0)
+    calls = []
+
+    def req():
+        calls.append(s.iter)
+        return "stop" if s.iter >= 5 else "none"
+
+    s.action_request = req
+    s.solve()
+    assert s.iter == 5
+    assert s.requested_early_exit
+
+
+def test_copy_trained_layers_rejects_same_count_other_shape():
+    """Net::CopyTrainedLayersFrom compares shapes (Blob::ShapeEquals), not element counts:
+    an InnerProduct weight of the same count but transposed shape must be refused, while
+    a legacy 4-D blob with leading 1s is accepted."""
+    a = lsq_solver()
+    src = a.net.to_proto()
+    w = a.net.layer_by_name("ip").params[0].to_caffe()   # [1, D]
+    lp = [l for l in src.layer if l.name == "ip"][0]
+    del lp.blobs[0].shape.dim[:]
+    lp.blobs[0].shape.dim.extend([D, 1])                  # same count, transposed
+    with pytest.raises(ValueError, match="shape mismatch"):
+        lsq_solver().net.copy_trained_layers_from(src)
+    src2 = a.net.to_proto()
+    lp2 = [l for l in src2.layer if l.name == "ip"][0]
+    del lp2.blobs[0].shape.dim[:]
+    lp2.blobs[0].ClearField("shape")
+    lp2.blobs[0].num, lp2.blobs[0].channels, lp2.blobs[0].height, lp2.blobs[0].width = 1, 1, 1, D
+    b = lsq_solver()
+    b.net.copy_trained_layers_from(src2)
+    assert torch.equal(b.net.layer_by_name("ip").params[0].to_caffe(), w)
