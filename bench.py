@@ -9,8 +9,12 @@ backward, fused SGD/momentum/weight-decay update (bf16 compute, fp32 masters), a
 tau-th step the cross-GPU weight average.  Random-init weights, synthetic data.
 
 Single GPU:  python bench.py --steps 50 --warmup 10
-N GPUs:      python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+N GPUs:      python bench.py --gpus N ...   (starts N ranks itself: parallel/launch.py), or
+             python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
                  --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+Every rank runs on its own GPU; the JSON line (rank 0) reports the whole-job img/s from the
+slowest rank's time, the per-rank ms/step, the measured all-reduce time per averaging and
+an RCCL bus-bandwidth probe of the 244 MB averaging payload at three bucket sizes.
 """
 from __future__ import annotations
 
@@ -43,6 +47,8 @@ def parse():
                    help="HIP streams for parallel branches (Inception towers) inside the graph; 1 = sequential "
                         "(>= 3 uses the star topology, see engine.BranchStreams)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--cpu", action="store_true",
+                   help="fp32 reference engine on the CPU with gloo (tests the launcher / JSON path; not a benchmark)")
     p.add_argument("--host-profile", action="store_true",
                    help="after the timed run, report the host time per step part (stderr)")
     return p.parse_args()
@@ -62,12 +68,32 @@ HEADLINE = ("caffenet", "alexnet")
 
 def main():
     args = parse()
+    from sparknet_amd.parallel.launch import launched_world, spawn_local
+    world_env = launched_world()
+    if world_env is None and args.gpus > 1:
+        # `python bench.py --gpus N`: start N ranks (one per GPU) before any GPU call here
+        return spawn_local(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:])
+    world = world_env or 1
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s); launch with "
+              f"torch.distributed.run --nproc-per-node {args.gpus} or run `python bench.py --gpus {args.gpus}`",
+              file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     import torch
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    if args.cpu:
+        dev = torch.device("cpu")
+        numa = -1
+    else:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        from sparknet_amd.parallel.topology import bind_to_gpu_numa
+        numa = bind_to_gpu_numa(local_rank) if world > 1 else -1
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
 
     from sparknet_amd import models
     from sparknet_amd.core.solver import Solver
@@ -76,8 +102,11 @@ def main():
     from sparknet_amd.ops import _lib
     from sparknet_amd.parallel import Comm
 
-    _lib.kernels()
-    comm = Comm(device=dev) if world > 1 else None
+    if dev.type == "cuda":
+        _lib.kernels()
+    comm = Comm(device=dev if dev.type == "cuda" else None, watchdog=True, timeout_s=600.0) if world > 1 else None
+    if comm is not None:
+        assert comm.world_size == world == args.gpus, (comm.world_size, world, args.gpus)
     B, C, HW, crop, classes, mean, in_scale = DEFAULTS[args.model]
     B = args.batch or B
     kw = dict(train_batch=B, test_batch=max(1, min(B, 50)))
@@ -86,13 +115,14 @@ def main():
     solver_param = models.solver_for(args.model, **kw)
     solver = Solver(solver_param, device=dev, seed=1701 + rank, build_test_nets=False)
     net = solver.net
-    fuse_relu(net)
+    if dev.type == "cuda":
+        fuse_relu(net)
     src = SyntheticSource(B, C, HW, HW, classes=classes, pool=3, seed=rank)
     feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
                           scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev)
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
     n_fp8 = enable_fp8(net) if args.dtype == "fp8" else 0
-    trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph,
+    trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph and not args.cpu,
                               overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc,
                               streams=args.streams)
     trainer.broadcast_initial()
@@ -102,11 +132,12 @@ def main():
         trainer.local_step()
     if comm is not None:
         trainer.average()
-    torch.cuda.synchronize(dev)
+    sync()
     if comm is not None:
         comm.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
 
+    avg_events = []
     t0 = time.perf_counter()
     loss = None
     averaged = False
@@ -115,14 +146,28 @@ def main():
         # every tau-th step averages; a timed window shorter than tau still ends with one
         # average so the collective is always inside the measurement
         if (k + 1) % args.tau == 0 or (k == args.steps - 1 and not averaged):
-            trainer.average()
+            if comm is not None and dev.type == "cuda":
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+                trainer.average()
+                ev[1].record()
+                avg_events.append(ev)
+            elif comm is not None:
+                trainer.average()
+                avg_events.append(None)
             averaged = True
     if comm is not None:
         comm.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    sync()
+    elapsed_rank = time.perf_counter() - t0
+    elapsed = elapsed_rank
+    per_rank_ms = [round(1000.0 * elapsed_rank / args.steps, 3)]
+    avg_ms = [e[0].elapsed_time(e[1]) for e in avg_events if e is not None]
+    comm_info = None
     if comm is not None:
-        elapsed = comm.max_over_ranks(elapsed)
+        elapsed = comm.max_over_ranks(elapsed_rank)
+        per_rank_ms = [round(1000.0 * v / args.steps, 3) for v in comm.allgather_float(elapsed_rank)]
+        comm_info = comm_bench(comm, net.flat_data, dev, sync)
     final_loss = float(loss) if loss is not None else float("nan")
 
     ms = 1000.0 * elapsed / args.steps
@@ -140,8 +185,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / BASELINE_IMG_S, 2) if args.model in HEADLINE else None,
-            "dtype": "fp8" if n_fp8 else "bf16",
-            "data": "synthetic (uint8 256x256 -> on-device random crop/mirror/mean), random-init weights",
+            "dtype": "fp8" if n_fp8 else ("fp32-cpu" if dev.type == "cpu" else "bf16"),
+            "data": f"synthetic (uint8 {HW}x{HW} -> on-device random crop/mirror/mean), random-init weights",
             "config": {
                 "model": f"{args.model} (bvlc_reference_caffenet / AlexNet)" if args.model == "caffenet"
                 else args.model,
@@ -150,15 +195,49 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
-                "hipgraph": not args.no_graph, "streams": args.streams, "fused_input_fold": fused_fold, "fp8_layers": n_fp8,
+                "hipgraph": trainer.use_graph, "streams": args.streams, "fused_input_fold": fused_fold, "fp8_layers": n_fp8,
                 "final_loss": round(final_loss, 4),
             },
+            "rccl_world": comm.world_size if comm is not None else 1,
+            "per_rank_ms_per_step": per_rank_ms,
+            "averages_in_window": len(avg_events) if comm is not None else 0,
+            "allreduce_ms_per_average": round(sum(avg_ms) / len(avg_ms), 3) if avg_ms else None,
+            "avg_payload_mb": round(net.flat_data.numel() * 4 / 1e6, 1),
+            "numa_node_rank0": numa,
         }
+        if comm_info is not None:
+            out["comm_bench"] = comm_info
         print(json.dumps(out), flush=True)
     if args.host_profile and trainer.step_fn is not None:
         host_profile(trainer, dev)
     if comm is not None:
         comm.close()
+    return 0
+
+
+def comm_bench(comm, flat, dev, sync, bucket_mb=(256, 64, 16), iters=4):
+    """After the timed window: all-reduce a scratch copy of the flat fp32 weight buffer at
+    several bucket sizes and report the RCCL bus bandwidth (2(n-1)/n * bytes / time), so a
+    multi-GPU run records how well the averaging collective uses the xGMI links."""
+    scratch = flat.detach().clone()
+    n = comm.world_size
+    out = {}
+    saved = comm.bucket_bytes
+    for mb in bucket_mb:
+        comm.bucket_bytes = mb << 20
+        comm.allreduce_sum(scratch)
+        sync()
+        comm.barrier()
+        t = time.perf_counter()
+        for _ in range(iters):
+            comm.allreduce_sum(scratch)
+        sync()
+        dt = comm.max_over_ranks((time.perf_counter() - t) / iters)
+        nbytes = scratch.numel() * 4
+        out[f"bucket_{mb}MB"] = {"ms": round(1000 * dt, 3), "busbw_GBps": round(2 * (n - 1) / n * nbytes / dt / 1e9, 1)}
+    comm.bucket_bytes = saved
+    del scratch
+    return out
 
 
 def host_profile(trainer, dev, n=200):

@@ -10,17 +10,21 @@ cifar10_full with JavaData inputs, mean-subtracted planar float input.
 from __future__ import annotations
 
 import os
+import sys
 
 from ..data.loaders import CifarLoader
 from ..data.sampler import shard_range
 from . import runner
-from .common import base_parser
+from .common import base_parser, maybe_launch
 
 
 def main(argv=None):
     p = base_parser("SparkNet CifarApp on MI355X", model="cifar10_full", tau=10, rounds=100, test_every=10,
                     batch=100, test_batch=100)
     args = p.parse_args(argv)
+    rc = maybe_launch(args, "sparknet_amd.apps.cifar_app", argv)
+    if rc is not None:
+        return rc
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     train = test = None
@@ -52,4 +56,5 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    _r = main()
+    sys.exit(_r if isinstance(_r, int) else 0)

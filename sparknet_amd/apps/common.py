@@ -32,7 +32,13 @@ def base_parser(desc: str, **defaults) -> argparse.ArgumentParser:
     p.add_argument("--cpu", action="store_true", help="run the fp32 reference path on the CPU")
     p.add_argument("--sync-sgd", action="store_true", help="all-reduce gradients every step (tau=1 semantics)")
     p.add_argument("--log-dir", default=None)
-    p.add_argument("--fail-at-round", type=int, default=-1, help="fault injection: rank 0 exits at round r")
+    p.add_argument("--fail-at-round", type=int, default=-1, help="fault injection: a rank exits at round r")
+    p.add_argument("--fail-rank", type=int, default=0, help="fault injection: the rank that exits")
+    p.add_argument("--nproc", type=int, default=1,
+                   help="start this many ranks on this node (one per GPU) unless already launched "
+                        "by torch.distributed.run")
+    p.add_argument("--pg-timeout", type=float, default=300.0,
+                   help="collective timeout in seconds (a dead peer is detected sooner by the watchdog)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                    help="GPU compute: bf16, or fp8 (e4m3 forward products, bf16 backward, fp32 masters)")
     p.add_argument("--native-loader", action=argparse.BooleanOptionalAction, default=True,
@@ -52,8 +58,21 @@ def setup(args):
         from ..ops import _lib
         _lib.kernels()
     from ..parallel import Comm
-    comm = Comm(device=dev if dev.type == "cuda" else None) if world > 1 else None
+    comm = (Comm(device=dev if dev.type == "cuda" else None, timeout_s=getattr(args, "pg_timeout", 300.0),
+                 watchdog=True) if world > 1 else None)
     return rank, world, dev, comm
+
+
+def maybe_launch(args, module: str, argv=None):
+    """``--nproc N`` outside a launcher: start N ranks of ``python -m module argv`` on this
+    node (parallel.launch.spawn_local, before any GPU call) and return the job's exit code;
+    otherwise None (this process is a rank, or the job is single-process)."""
+    from ..parallel.launch import launched_world, spawn_local
+    if args.nproc <= 1 or launched_world() is not None:
+        return None
+    import sys
+    rest = list(sys.argv[1:] if argv is None else argv)
+    return spawn_local(args.nproc, ["-m", module] + rest)
 
 
 class StopFlag:

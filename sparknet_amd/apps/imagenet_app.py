@@ -11,13 +11,14 @@ mean subtraction is actually applied (the reference's loop was a no-op).
 from __future__ import annotations
 
 import os
+import sys
 
 import numpy as np
 import torch
 
 from ..data.loaders import ImageNetLoader
 from . import runner
-from .common import base_parser
+from .common import base_parser, maybe_launch
 
 
 def main(argv=None):
@@ -28,6 +29,9 @@ def main(argv=None):
     p.add_argument("--val-labels", default=None)
     p.add_argument("--max-images", type=int, default=0)
     args = p.parse_args(argv)
+    rc = maybe_launch(args, "sparknet_amd.apps.imagenet_app", argv)
+    if rc is not None:
+        return rc
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     train = test = None
@@ -52,4 +56,5 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    _r = main()
+    sys.exit(_r if isinstance(_r, int) else 0)

@@ -133,6 +133,19 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
     stop = StopFlag()
     log.log(f"{model}: {world} worker(s), batch {args.batch}, tau {args.tau}, device {dev}"
             + (f", fp8 forward in {log_fp8} layers" if dev.type == "cuda" and log_fp8 else ""))
+    try:
+        _rounds(args, solver, trainer, tfeeder, n_test, comm, log, stop, start_round, rank, world, dev)
+    except BaseException:
+        if comm is not None:
+            comm.abort()  # peers exit now instead of waiting in the next collective
+        raise
+    log.close()
+    if comm is not None:
+        comm.close()
+    return solver
+
+
+def _rounds(args, solver, trainer, tfeeder, n_test, comm, log, stop, start_round, rank, world, dev):
     for r in range(start_round, args.rounds):
         if args.test_every and r % args.test_every == 0:
             scores, names, total = evaluate(solver, tfeeder, n_test, comm)
@@ -140,8 +153,8 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
                 if "accuracy" in name or "top" in name:
                     log.log(f"{100.0 * v / max(total, 1):.2f}% accuracy ({name})", i=r)
             log.metric(event="test", round=r, **{n: v / max(total, 1) for n, v in zip(names, scores)})
-        if r == args.fail_at_round and rank == 0:
-            log.log(f"fault injection: rank 0 exits at round {r}")
+        if r == args.fail_at_round and rank == getattr(args, "fail_rank", 0):
+            log.log(f"fault injection: rank {rank} exits at round {r}")
             os._exit(3)
         t0 = time.perf_counter()
         log.log("training", i=r)
@@ -159,10 +172,6 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
         if req == "stop":
             log.log("stop requested")
             break
-    log.close()
-    if comm is not None:
-        comm.close()
-    return solver
 
 
 def checkpoint(solver, prefix: str, round_: int, rank: int, comm=None) -> None:

@@ -19,19 +19,96 @@ only to bound transient memory and let the sync-SGD mode overlap with backward.
 """
 from __future__ import annotations
 
+import atexit
 import datetime
 import os
+import sys
+import threading
 
 import torch
 import torch.distributed as dist
 
 DEFAULT_BUCKET_BYTES = 256 << 20
+WATCHDOG_EXIT_CODE = 75
+
+
+class Watchdog:
+    """Fail-fast rank monitor (the reference fails the whole Spark job on the
+    first task failure, spark.task.maxFailures=1, src/main/scala/apps/CifarApp.scala:30).
+
+    Every rank runs a daemon thread on its own client connection to the job's TCP store:
+    it bumps its heartbeat counter every ``interval`` seconds and reads the peers'.  A
+    peer whose counter has not moved for ``timeout`` seconds (process died: os._exit,
+    segfault, OOM kill), a set ``abort`` key (a peer caught an exception and called
+    :meth:`abort`) or a lost store connection ends this process with exit code 75
+    within seconds — instead of blocking in the next all-reduce until the process-group
+    timeout.  A rank that finishes normally marks itself done first (close / atexit), so
+    peers never mistake a clean exit for a failure."""
+
+    def __init__(self, rank: int, world: int, interval: float = 1.0, timeout: float | None = None,
+                 prefix: str = "sn_watchdog"):
+        self.rank, self.world, self.interval = rank, world, interval
+        self.timeout = timeout if timeout is not None else float(os.environ.get("SN_WATCHDOG_TIMEOUT", "20"))
+        host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ["MASTER_PORT"])
+        base = dist.TCPStore(host, port, world, False, timeout=datetime.timedelta(seconds=30),
+                             wait_for_workers=False)
+        self.store = dist.PrefixStore(prefix, base)
+        self._stop = threading.Event()
+        self._done = False
+        self.thread = threading.Thread(target=self._loop, name="sn-watchdog", daemon=True)
+        self.thread.start()
+        atexit.register(self.stop)
+
+    def _fail(self, why: str) -> None:
+        if self._stop.is_set():
+            return
+        print(f"[watchdog rank {self.rank}] {why}: exiting", file=sys.stderr, flush=True)
+        os._exit(WATCHDOG_EXIT_CODE)
+
+    def _loop(self) -> None:
+        import time
+        peers = [r for r in range(self.world) if r != self.rank]
+        last = {r: (-1, time.monotonic()) for r in peers}
+        while not self._stop.wait(self.interval):
+            try:
+                self.store.add(f"hb/{self.rank}", 1)
+                if self.store.add("abort", 0) > 0:
+                    self._fail("a peer requested an abort")
+                now = time.monotonic()
+                for r in peers:
+                    v = self.store.add(f"hb/{r}", 0)
+                    if v != last[r][0]:
+                        last[r] = (v, now)
+                    elif now - last[r][1] > self.timeout and self.store.add(f"done/{r}", 0) == 0:
+                        self._fail(f"rank {r} stopped responding ({self.timeout:.0f} s without a heartbeat)")
+            except Exception as e:  # store host gone: the job is failing
+                if not self._stop.is_set():
+                    self._fail(f"lost the job store ({type(e).__name__}: {e})")
+
+    def abort(self) -> None:
+        try:
+            self.store.add("abort", 1)
+        except Exception:
+            pass
+
+    def stop(self) -> None:
+        if self._done:
+            return
+        self._done = True
+        self._stop.set()
+        try:
+            self.store.add(f"done/{self.rank}", 1)
+        except Exception:
+            pass
+        self.thread.join(timeout=5)
 
 
 class Comm:
     def __init__(self, backend: str | None = None, device=None, timeout_s: float = 1800.0,
-                 bucket_bytes: int = DEFAULT_BUCKET_BYTES):
+                 bucket_bytes: int = DEFAULT_BUCKET_BYTES, watchdog: bool = False):
         self.bucket_bytes = bucket_bytes
+        self.watchdog = None
         if dist.is_available() and dist.is_initialized():
             self.owns = False
         elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -46,6 +123,8 @@ class Comm:
             self.owns = False
         self.world_size = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
+        if watchdog and self.world_size > 1 and "MASTER_PORT" in os.environ:
+            self.watchdog = Watchdog(self.rank, self.world_size)
 
     # -- helpers ------------------------------------------------------------------------
     def _buckets(self, flat: torch.Tensor):
@@ -111,6 +190,15 @@ class Comm:
         dist.all_gather(out, t)
         return [int(x.item()) for x in out]
 
+    def allgather_float(self, v: float) -> list[float]:
+        if self.world_size == 1:
+            return [v]
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        out = [torch.zeros_like(t) for _ in range(self.world_size)]
+        dist.all_gather(out, t)
+        return [float(x.item()) for x in out]
+
     def max_over_ranks(self, v: float) -> float:
         if self.world_size == 1:
             return v
@@ -119,7 +207,17 @@ class Comm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def abort(self) -> None:
+        """Tell every peer to exit now (called when this rank hits an error)."""
+        if self.watchdog is not None:
+            self.watchdog.abort()
+
     def close(self) -> None:
+        if self.watchdog is not None:
+            # every rank marks itself done before any rank (possibly the store host) exits
+            self.watchdog.stop()
+            self.barrier()
+            self.watchdog = None
         if self.owns and dist.is_initialized():
             dist.destroy_process_group()
 

@@ -1,0 +1,41 @@
+"""bench.py contract on the CPU: `--gpus N` outside a launcher starts N ranks through
+parallel.launch.spawn_local (the path the 8-GPU run takes with `python bench.py --gpus 8`),
+every rank joins one process group, and rank 0 prints ONE JSON line for the whole job."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--cpu", "--model", "cifar10_quick", "--batch", "4", "--steps", "3", "--warmup", "1", "--tau", "2"]
+
+
+def _clean_env():
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "2"
+    return env
+
+
+def test_bench_spawns_n_ranks_and_reports_job_json():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, env=_clean_env(),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rccl_world"] == 2
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 8
+    assert len(out["per_rank_ms_per_step"]) == 2
+    assert out["steps"] == 3 and out["averages_in_window"] >= 1
+    assert out["ms_per_step"] >= max(out["per_rank_ms_per_step"]) - 1e-3  # slowest rank's clock
+    assert set(out["comm_bench"]) == {"bucket_256MB", "bucket_64MB", "bucket_16MB"}
+
+
+def test_bench_refuses_world_mismatch():
+    env = _clean_env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "--gpus 2" in r.stderr
