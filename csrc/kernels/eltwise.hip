@@ -17,7 +17,9 @@
 #include <cstring>
 
 // ---------------- ReLU ----------------
-__global__ void relu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8, float slope) {
+// n % 8 != 0: the vector loop covers n / 8 chunks, block 0 finishes the tail scalar.
+__global__ void relu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n, float slope) {
+  const long long n8 = n / 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     float f[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], f);
@@ -25,10 +27,16 @@ __global__ void relu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, l
     for (int k = 0; k < 8; ++k) f[k] = f[k] > 0.f ? f[k] : f[k] * slope;
     reinterpret_cast<uint4*>(y)[i] = pack8(f);
   }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
+    const long long e = n8 * 8 + threadIdx.x;
+    const float f = bf2f(x[e]);
+    y[e] = f2bf(f > 0.f ? f : f * slope);
+  }
 }
 
 __global__ void relu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, bf16_t* __restrict__ dx,
-                         long long n8, float slope) {
+                         long long n, float slope) {
+  const long long n8 = n / 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     float g[8], v[8];
     unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
@@ -37,17 +45,21 @@ __global__ void relu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict
     for (int k = 0; k < 8; ++k) g[k] = v[k] > 0.f ? g[k] : g[k] * slope;
     reinterpret_cast<uint4*>(dx)[i] = pack8(g);
   }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
+    const long long e = n8 * 8 + threadIdx.x;
+    const float g = bf2f(dy[e]);
+    dx[e] = f2bf(bf2f(x[e]) > 0.f ? g : g * slope);
+  }
 }
 
 extern "C" int sn_relu_fwd(const bf16_t* x, bf16_t* y, long long n, float slope, hipStream_t st) {
-  if (n % 8) return 7;
-  hipLaunchKernelGGL(relu_fwd, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, x, y, n / 8, slope);
+  hipLaunchKernelGGL(relu_fwd, dim3(sn_blocks(n / 8 > 0 ? n / 8 : 1, 256, 16384)), dim3(256), 0, st, x, y, n, slope);
   return SN_CHECK_LAUNCH();
 }
 
 extern "C" int sn_relu_bwd(const bf16_t* dy, const bf16_t* x, bf16_t* dx, long long n, float slope, hipStream_t st) {
-  if (n % 8) return 7;
-  hipLaunchKernelGGL(relu_bwd, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, dy, x, dx, n / 8, slope);
+  hipLaunchKernelGGL(relu_bwd, dim3(sn_blocks(n / 8 > 0 ? n / 8 : 1, 256, 16384)), dim3(256), 0, st, dy, x, dx, n,
+                     slope);
   return SN_CHECK_LAUNCH();
 }
 
@@ -55,23 +67,23 @@ extern "C" int sn_relu_bwd(const bf16_t* dy, const bf16_t* x, bf16_t* dx, long l
 // keep(i) = philox(key=seed, ctr=(i_lo, i_hi | stream<<16, counter_lo, counter_hi)).x > thr
 // gate (optional, backward only): the in-place ReLU output feeding this dropout — its
 // slope-0 backward mask (gate > 0) is applied here instead of in a separate pass.
-__global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8,
+__global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n,
                                const long long* __restrict__ rng, int stream, uint32_t thr, float scale,
                                const bf16_t* __restrict__ gate) {
   const unsigned long long seed = (unsigned long long)rng[0];
   const unsigned long long counter = (unsigned long long)rng[1];
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  auto keep = [&](unsigned long long e) {
+    uint4 ctr = make_uint4((uint32_t)e, (uint32_t)(e >> 32) | ((uint32_t)(stream & 0xffff) << 16),
+                           (uint32_t)counter, (uint32_t)(counter >> 32));
+    return philox4x32(key, ctr).x > thr;
+  };
+  const long long n8 = n / 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     float f[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], f);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      unsigned long long e = (unsigned long long)(i * 8 + k);
-      uint4 ctr = make_uint4((uint32_t)e, (uint32_t)(e >> 32) | ((uint32_t)(stream & 0xffff) << 16),
-                             (uint32_t)counter, (uint32_t)(counter >> 32));
-      uint32_t u = philox4x32(key, ctr).x;
-      f[k] = (u > thr) ? f[k] * scale : 0.f;
-    }
+    for (int k = 0; k < 8; ++k) f[k] = keep((unsigned long long)(i * 8 + k)) ? f[k] * scale : 0.f;
     if (gate) {
       float gv[8];
       unpack8(reinterpret_cast<const uint4*>(gate)[i], gv);
@@ -80,15 +92,21 @@ __global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
     }
     reinterpret_cast<uint4*>(y)[i] = pack8(f);
   }
+  // element counts that are not a multiple of 8: the last n % 8 elements, scalar
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
+    const long long e = n8 * 8 + threadIdx.x;
+    float f = keep((unsigned long long)e) ? bf2f(x[e]) * scale : 0.f;
+    if (gate && !(bf2f(gate[e]) > 0.f)) f = 0.f;
+    y[e] = f2bf(f);
+  }
 }
 
 extern "C" int sn_dropout(const bf16_t* x, bf16_t* y, long long n, const long long* rng, long long stream,
                           float ratio, const bf16_t* gate, hipStream_t st) {
-  if (n % 8) return 7;
   uint32_t thr = (uint32_t)((double)4294967295u * (double)ratio);
   float scale = 1.f / (1.f - ratio);
-  hipLaunchKernelGGL(dropout_kernel, dim3(sn_blocks(n / 8, 256, 16384)), dim3(256), 0, st, x, y, n / 8, rng,
-                     (int)stream, thr, scale, gate);
+  hipLaunchKernelGGL(dropout_kernel, dim3(sn_blocks(n / 8 > 0 ? n / 8 : 1, 256, 16384)), dim3(256), 0, st, x, y, n,
+                     rng, (int)stream, thr, scale, gate);
   return SN_CHECK_LAUNCH();
 }
 

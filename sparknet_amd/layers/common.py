@@ -7,6 +7,10 @@ tile,reduction,argmax,batch_reindex,filter,embed,mvn,batch_norm,spp}_layer.*.
 Channel-axis operations on 4-D blobs (Concat/Slice along axis 1) act on the physical
 last axis of the NHWC storage.  Flatten/Reshape keep Caffe's logical (C, H, W) order by
 converting through the NCHW view.
+
+On the GPU every layer here runs HIP kernels (csrc/kernels/eltwise.hip for the hot Split /
+channel Concat, csrc/kernels/layers.hip for the rest, wrapped by ops.layers_hip); the
+tensor-math bodies are the fp32 CPU reference path.
 """
 from __future__ import annotations
 
@@ -21,6 +25,38 @@ def _phys_axis(blob, axis):
     if blob.is_image:
         return {0: 0, 1: 3, 2: 1, 3: 2}[axis]
     return axis
+
+
+def _oai(t: torch.Tensor, ax: int):
+    """(outer, A, inner) of a contiguous tensor around physical axis ``ax``."""
+    outer = 1
+    for d in t.shape[:ax]:
+        outer *= d
+    inner = 1
+    for d in t.shape[ax + 1:]:
+        inner *= d
+    return outer, t.shape[ax], inner
+
+
+def _lh():
+    from ..ops import layers_hip
+    return layers_hip
+
+
+def _to_logical(blob, diff=False):
+    """Contiguous logical-order (NCHW for images) copy / view of a GPU blob."""
+    t = blob.diff if diff else blob.data
+    if blob.is_image:
+        return _lh().nhwc_to_nchw(t)
+    return t
+
+
+def _from_logical(t, blob):
+    """Physical-layout tensor for ``blob`` from a logical-order tensor of the same count."""
+    if blob.is_image:
+        N, C_, H, W = blob.shape
+        return _lh().nchw_to_nhwc(t.reshape(N, C_, H * W), N, C_, H, W)
+    return t.reshape(blob.data.shape)
 
 
 @register("Split")
@@ -48,10 +84,27 @@ class SplitLayer(Layer):
             # one fused fp32-accumulating pass over all top diffs (HIP sum_bf16)
             bottoms[0].diff = ops.sum_bf16(diffs)
             return
+        if d0.is_cuda:
+            bottoms[0].diff = _eltwise_sum_gpu(diffs)
+            return
         acc = d0.float() if d0.dtype != torch.float32 else d0.clone()
         for d in diffs[1:]:
             acc = acc + d.float()
         bottoms[0].diff = acc.to(bottoms[0].dtype)
+
+
+def _eltwise_sum_gpu(ts, coeffs=None):
+    """Sum (with coefficients) of same-shape GPU tensors with the HIP eltwise kernel; more
+    than 16 inputs are folded in chunks (the running sum is input 0 of the next chunk)."""
+    lh = _lh()
+    coeffs = list(coeffs) if coeffs is not None else [1.0] * len(ts)
+    acc, _ = lh.eltwise_fwd(1, ts[:16], coeffs[:16])
+    i = 16
+    while i < len(ts):
+        chunk = ts[i:i + 15]
+        acc, _ = lh.eltwise_fwd(1, [acc] + chunk, [1.0] + coeffs[i:i + 15])
+        i += 15
+    return acc
 
 
 @register("Concat")
@@ -95,6 +148,18 @@ class ConcatLayer(Layer):
             out = torch.empty(shape, dtype=torch.bfloat16, device=bottoms[0].data.device)
             tops[0].data = hip.concat_channels([b.data for b in bottoms], out)
             return
+        if bottoms[0].data.is_cuda:
+            lh = _lh()
+            shape = list(bottoms[0].data.shape)
+            shape[ax] = sum(b.data.shape[ax] for b in bottoms)
+            out = torch.empty(shape, dtype=tops[0].dtype, device=bottoms[0].data.device)
+            off = 0
+            for b in bottoms:
+                o, A, i = _oai(b.data, ax)
+                lh.axis_copy(b.data, out, o, A, shape[ax], i, 0, off, A)
+                off += A
+            tops[0].data = out
+            return
         tops[0].data = torch.cat([b.data for b in bottoms], dim=ax)
 
     def backward(self, tops, propagate_down, bottoms):
@@ -111,11 +176,18 @@ class ConcatLayer(Layer):
                     b.diff = d
             return
         off = 0
+        top_d = tops[0].diff
         for i, b in enumerate(bottoms):
             n = b.shape[self.axis]
             if propagate_down[i]:
-                d = tops[0].diff.narrow(ax, off, n)
-                b.diff = (d * (b.data > 0).to(d.dtype)) if gates[i] else d.contiguous()
+                if top_d.is_cuda:
+                    o, A, inner = _oai(top_d, ax)
+                    d = torch.empty_like(b.data)
+                    _lh().axis_copy(top_d, d, o, A, n, inner, off, 0, n)
+                    b.diff = ops.relu_backward(d, b.data) if gates[i] else d
+                else:
+                    d = top_d.narrow(ax, off, n)
+                    b.diff = (d * (b.data > 0).to(d.dtype)) if gates[i] else d.contiguous()
             off += n
 
 
@@ -150,15 +222,32 @@ class SliceLayer(Layer):
 
     def forward(self, bottoms, tops):
         ax = _phys_axis(bottoms[0], self.axis)
+        x = bottoms[0].data
         off = 0
         for t, s in zip(tops, self.sizes):
-            t.data = bottoms[0].data.narrow(ax, off, s).contiguous()
+            if x.is_cuda:
+                o, A, i = _oai(x, ax)
+                y = torch.empty(t.data.shape, dtype=x.dtype, device=x.device)
+                _lh().axis_copy(x, y, o, A, s, i, off, 0, s)
+                t.data = y
+            else:
+                t.data = x.narrow(ax, off, s).contiguous()
             off += s
 
     def backward(self, tops, propagate_down, bottoms):
-        if propagate_down[0]:
-            ax = _phys_axis(bottoms[0], self.axis)
-            bottoms[0].diff = torch.cat([t.diff for t in tops], dim=ax)
+        if not propagate_down[0]:
+            return
+        ax = _phys_axis(bottoms[0], self.axis)
+        if tops[0].diff.is_cuda:
+            g = torch.empty_like(bottoms[0].data)
+            o, A, i = _oai(g, ax)
+            off = 0
+            for t, s in zip(tops, self.sizes):
+                _lh().axis_copy(t.diff, g, o, s, A, i, 0, off, s)
+                off += s
+            bottoms[0].diff = g
+            return
+        bottoms[0].diff = torch.cat([t.diff for t in tops], dim=ax)
 
 
 @register("Eltwise")
@@ -182,7 +271,22 @@ class EltwiseLayer(Layer):
                 raise ValueError("Eltwise: bottoms must have the same shape")
         tops[0].reshape(bottoms[0].shape, bottoms[0].dtype)
 
+    def _gpu_inputs(self, bottoms):
+        # an in-place top aliases bottom 0: keep the inputs the backward needs
+        return [b.data for b in bottoms]
+
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            lh = _lh()
+            xs = [b.data for b in bottoms]
+            if len(xs) > 16:
+                raise ValueError("Eltwise on the GPU supports at most 16 bottoms")
+            if tops[0] is bottoms[0] and self.op == 0:
+                xs = [x.clone() for x in xs]
+            y, self.mask = lh.eltwise_fwd(self.op, xs, self.coeff)
+            self._xs = xs
+            tops[0].data = y
+            return
         xs = [b.data.float() for b in bottoms]
         if self.op == 0:
             y = xs[0]
@@ -199,6 +303,15 @@ class EltwiseLayer(Layer):
         tops[0].data = y.to(tops[0].dtype)
 
     def backward(self, tops, propagate_down, bottoms):
+        if tops[0].diff.is_cuda:
+            lh = _lh()
+            dy, y = tops[0].diff, tops[0].data
+            grads = [lh.eltwise_bwd(self.op, self._xs, self.coeff, i, self.stable, y, dy, self.mask)
+                     if propagate_down[i] else None for i in range(len(bottoms))]
+            for b, g in zip(bottoms, grads):
+                if g is not None:
+                    b.diff = g
+            return
         dy = tops[0].diff.float()
         y = tops[0].data.float()
         for i, b in enumerate(bottoms):
@@ -242,11 +355,23 @@ class FlattenLayer(Layer):
 
 
 def _logical_copy(b, t):
+    if b.data.is_cuda:
+        if not b.is_image and not t.is_image:
+            t.data = b.data.view(t.data.shape)  # Caffe ShareData: no copy
+        else:
+            t.data = _from_logical(_to_logical(b), t)
+        return
     logical = b.nchw().contiguous().reshape(t.shape)
     t.data = logical.permute(0, 2, 3, 1).contiguous() if t.is_image else logical
 
 
 def _logical_copy_diff(t, b):
+    if t.diff.is_cuda:
+        if not b.is_image and not t.is_image:
+            b.diff = t.diff.view(b.data.shape)  # Caffe ShareDiff
+        else:
+            b.diff = _from_logical(_to_logical(t, diff=True), b)
+        return
     logical = t.nchw(diff=True).contiguous().reshape(b.shape)
     b.diff = logical.permute(0, 2, 3, 1).contiguous() if b.is_image else logical
 
@@ -282,15 +407,11 @@ class ReshapeLayer(Layer):
         tops[0].reshape(tuple(shape), b.dtype)
 
     def forward(self, bottoms, tops):
-        b, t = bottoms[0], tops[0]
-        logical = b.nchw().contiguous().reshape(t.shape)
-        t.data = logical.permute(0, 2, 3, 1).contiguous() if t.is_image else logical
+        _logical_copy(bottoms[0], tops[0])
 
     def backward(self, tops, propagate_down, bottoms):
         if propagate_down[0]:
-            b, t = bottoms[0], tops[0]
-            logical = t.nchw(diff=True).contiguous().reshape(b.shape)
-            b.diff = logical.permute(0, 2, 3, 1).contiguous() if b.is_image else logical
+            _logical_copy_diff(tops[0], bottoms[0])
 
 
 @register("Silence")
@@ -325,6 +446,16 @@ class TileLayer(Layer):
         tops[0].reshape(tuple(shape), b.dtype)
 
     def forward(self, bottoms, tops):
+        b, t = bottoms[0], tops[0]
+        if b.data.is_cuda:
+            ax = _phys_axis(b, self.axis)
+            x = b.data
+            o, A, i = _oai(x, ax)
+            y = torch.empty(t.data.shape, dtype=x.dtype, device=x.device)
+            for k in range(self.tiles):
+                _lh().axis_copy(x, y, o, A, A * self.tiles, i, 0, k * A, A)
+            t.data = y
+            return
         x = bottoms[0].nchw()
         reps = [1] * x.dim()
         reps[self.axis] = self.tiles
@@ -333,6 +464,12 @@ class TileLayer(Layer):
         t.data = y.permute(0, 2, 3, 1).contiguous() if t.is_image else y
 
     def backward(self, tops, propagate_down, bottoms):
+        if propagate_down[0] and tops[0].diff.is_cuda:
+            b = bottoms[0]
+            ax = _phys_axis(b, self.axis)
+            o, A, i = _oai(b.data, ax)
+            b.diff = _lh().tile_bwd(tops[0].diff, o, A, i, self.tiles, b.data.shape)
+            return
         if propagate_down[0]:
             b = bottoms[0]
             d = tops[0].nchw(diff=True).float()
@@ -353,7 +490,26 @@ class ReductionLayer(Layer):
         self.op, self.coeff = int(p.operation), float(p.coeff)
         tops[0].reshape(b.shape[:self.axis], torch.float32)
 
+    def _gpu_segments(self, b, diff=False):
+        """(logical-order tensor or physical, segs, L): image blobs reduced over axes >= 2
+        are converted to NCHW first (their segments are not contiguous in NHWC)."""
+        segs = b.count_range(0, self.axis)
+        L = b.count // max(segs, 1)
+        t = b.diff if diff else b.data
+        if b.is_image and self.axis >= 2:
+            return _to_logical(b, diff), segs, L, True
+        return t, segs, L, False
+
     def forward(self, bottoms, tops):
+        b = bottoms[0]
+        if b.data.is_cuda:
+            lh = _lh()
+            x, segs, L, _ = self._gpu_segments(b)
+            mode = {1: lh.RED_SUM, 2: lh.RED_ABS, 3: lh.RED_SQ, 4: lh.RED_SUM}[self.op]
+            scale = self.coeff / L if self.op == 4 else self.coeff
+            out = lh.axis_reduce(mode, x, None, 1, 1, segs, L, scale=scale)
+            tops[0].data = out.reshape(tops[0].data.shape)
+            return
         x = bottoms[0].nchw().float()
         x = x.reshape(x.shape[:self.axis] + (-1,)) if self.axis < x.dim() else x
         if self.op == 1:
@@ -370,6 +526,12 @@ class ReductionLayer(Layer):
         if not propagate_down[0]:
             return
         b = bottoms[0]
+        if b.data.is_cuda:
+            lh = _lh()
+            x, segs, L, logical = self._gpu_segments(b)
+            g = lh.reduction_bwd(x, tops[0].diff.reshape(-1), segs, L, self.op, self.coeff)
+            b.diff = _from_logical(g, b) if logical else g.reshape(b.data.shape)
+            return
         x = b.nchw().float().reshape(b.shape[:self.axis] + (-1,))
         dy = tops[0].diff.float().reshape(b.shape[:self.axis] + (1,)) * self.coeff
         if self.op == 1:
@@ -405,6 +567,22 @@ class ArgMaxLayer(Layer):
         tops[0].reshape(shape, torch.float32)
 
     def forward(self, bottoms, tops):
+        b, t = bottoms[0], tops[0]
+        if b.data.is_cuda:
+            lh = _lh()
+            x = _to_logical(b)  # indices refer to Caffe's logical (C, H, W) order
+            if self.axis is None:
+                out = lh.topk(x, b.shape[0], b.count // b.shape[0], 1, self.top_k, self.out_max_val, 0,
+                              t.data.shape)
+            else:
+                outer = b.count_range(0, self.axis)
+                inner = b.count_range(self.axis + 1)
+                lshape = list(b.shape)
+                lshape[self.axis] = self.top_k
+                out = lh.topk(x, outer, b.shape[self.axis], inner, self.top_k, self.out_max_val, 1, lshape)
+                out = _from_logical(out, t)
+            t.data = out
+            return
         x = bottoms[0].nchw().float()
         if self.axis is None:
             x2 = x.reshape(x.shape[0], -1)
@@ -426,10 +604,22 @@ class BatchReindexLayer(Layer):
         tops[0].reshape((bottoms[1].count,) + bottoms[0].shape[1:], bottoms[0].dtype)
 
     def forward(self, bottoms, tops):
+        x = bottoms[0].data
+        if x.is_cuda:
+            self.idx = bottoms[1].data.reshape(-1).float()
+            row = x.numel() // max(x.shape[0], 1)
+            tops[0].data = _lh().gather_rows(x, self.idx, self.idx.numel(), row, tops[0].data.shape)
+            return
         self.idx = bottoms[1].data.reshape(-1).long()
         tops[0].data = bottoms[0].data.index_select(0, self.idx)
 
     def backward(self, tops, propagate_down, bottoms):
+        if propagate_down[0] and tops[0].diff.is_cuda:
+            x = bottoms[0].data
+            g = torch.empty_like(x)
+            row = x.numel() // max(x.shape[0], 1)
+            bottoms[0].diff = _lh().index_add_rows(tops[0].diff, self.idx, x.shape[0], row, g, acc=False)
+            return
         if propagate_down[0]:
             g = torch.zeros(bottoms[0].data.shape, dtype=torch.float32, device=self.device)
             g.index_add_(0, self.idx, tops[0].diff.float())
@@ -441,21 +631,38 @@ class FilterLayer(Layer):
     min_bottoms = 2
     min_tops = 1
 
+    def _host_index(self, bottoms):
+        """Selected row indices, read on the host like Caffe's FilterLayer::Reshape
+        (filter_layer.cpp:42-62 reads the selector blob's cpu_data)."""
+        sel = bottoms[-1].data.reshape(-1).detach().float().cpu()
+        return [i for i, v in enumerate(sel.tolist()) if v != 0]
+
     def reshape(self, bottoms, tops):
-        sel = bottoms[-1].data.reshape(-1)
-        n = int((sel != 0).sum()) if sel.numel() else 0
+        n = len(self._host_index(bottoms)) if bottoms[-1].count else 0
         for b, t in zip(bottoms[:-1], tops):
             t.reshape((n,) + b.shape[1:], b.dtype)
 
     def forward(self, bottoms, tops):
-        self.idx = torch.nonzero(bottoms[-1].data.reshape(-1) != 0)[:, 0]
+        host = self._host_index(bottoms)
+        if bottoms[0].data.is_cuda:
+            self.idx = torch.tensor(host, dtype=torch.int32).to(bottoms[0].data.device, non_blocking=True)
+            for b, t in zip(bottoms[:-1], tops):
+                t.reshape((len(host),) + b.shape[1:], b.dtype)
+                row = b.data.numel() // max(b.data.shape[0], 1)
+                t.data = _lh().gather_rows(b.data, self.idx, len(host), row, t.data.shape)
+            return
+        self.idx = torch.tensor(host, dtype=torch.long)
         for b, t in zip(bottoms[:-1], tops):
             t.reshape((len(self.idx),) + b.shape[1:], b.dtype)
             t.data = b.data.index_select(0, self.idx)
 
     def backward(self, tops, propagate_down, bottoms):
         for i, (b, t) in enumerate(zip(bottoms[:-1], tops)):
-            if propagate_down[i]:
+            if propagate_down[i] and t.diff.is_cuda:
+                row = b.data.numel() // max(b.data.shape[0], 1)
+                b.diff = _lh().index_add_rows(t.diff, self.idx, b.data.shape[0], row, torch.empty_like(b.data),
+                                              acc=False)
+            elif propagate_down[i]:
                 g = torch.zeros_like(b.data)
                 g.index_copy_(0, self.idx, t.diff)
                 b.diff = g
@@ -478,6 +685,12 @@ class EmbedLayer(Layer):
         tops[0].reshape(bottoms[0].shape + (self.N,), self.dtype)
 
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            self.idx = bottoms[0].data.reshape(-1).float()
+            tops[0].data = _lh().gather_rows(self.weight.data, self.idx, self.idx.numel(), self.N, tops[0].data.shape,
+                                             bias=self.bias.data if self.bias is not None else None,
+                                             out_dtype=self.dtype)
+            return
         self.idx = bottoms[0].data.reshape(-1).long()
         y = self.weight.data.index_select(0, self.idx)
         if self.bias is not None:
@@ -485,6 +698,14 @@ class EmbedLayer(Layer):
         tops[0].data = y.reshape(tops[0].data.shape).to(self.dtype)
 
     def backward(self, tops, propagate_down, bottoms):
+        if tops[0].diff.is_cuda:
+            lh = _lh()
+            dy = tops[0].diff
+            if self.param_grads_needed(0):
+                lh.index_add_rows(dy, self.idx, self.K, self.N, self.weight.diff, acc=True)
+            if self.bias is not None and self.param_grads_needed(1):
+                lh.axis_reduce(lh.RED_SUM, dy, None, 1, self.idx.numel(), self.N, 1, out=self.bias.diff, acc=True)
+            return
         dy = tops[0].diff.float().reshape(-1, self.N)
         if self.param_grads_needed(0):
             self.weight.diff.index_add_(0, self.idx, dy)
@@ -504,8 +725,33 @@ class MVNLayer(Layer):
         p = self.lp.mvn_param
         return (1, 2, 3) if p.across_channels else (1, 2)  # NHWC: spatial dims 1,2 (+channel 3)
 
+    def _gpu_geom(self, x):
+        """[B][outer][A][inner] of the per-statistic groups: (n, c) over (h, w) in NHWC, or
+        n over everything when across_channels (2-D blobs: n over c)."""
+        p = self.lp.mvn_param
+        N = x.shape[0]
+        if x.dim() == 4 and not p.across_channels:
+            return N, x.shape[1] * x.shape[2], x.shape[3], 1
+        if x.dim() != 4 and not p.across_channels and x.dim() > 2:
+            inner = x.numel() // (N * x.shape[1])
+            return N, 1, x.shape[1], inner
+        return N, 1, 1, x.numel() // N
+
     def forward(self, bottoms, tops):
         p = self.lp.mvn_param
+        if bottoms[0].data.is_cuda:
+            lh = _lh()
+            x = bottoms[0].data
+            B, outer, A, inner = self._gpu_geom(x)
+            self.geom = (B, outer, A, inner)
+            s1 = lh.axis_reduce(lh.RED_SUM, x, None, B, outer, A, inner)
+            s2 = lh.axis_reduce(lh.RED_SQ, x, None, B, outer, A, inner) if p.normalize_variance else None
+            mean, _, inv = lh.stats_finalize(s1, s2, outer * inner, p.eps, 1 if p.normalize_variance else 2)
+            self.inv = inv if p.normalize_variance else None
+            y = lh.chan_affine(x, mean, self.inv, outer, A, inner)
+            self.y = y
+            tops[0].data = y
+            return
         x = bottoms[0].data.float()
         dims = self._dims(x)
         xm = x - x.mean(dim=dims, keepdim=True)
@@ -521,6 +767,17 @@ class MVNLayer(Layer):
         if not propagate_down[0]:
             return
         p = self.lp.mvn_param
+        if tops[0].diff.is_cuda:
+            lh = _lh()
+            B, outer, A, inner = self.geom
+            dy = tops[0].diff
+            cnt = outer * inner
+            m1 = lh.axis_reduce(lh.RED_SUM, dy, None, B, outer, A, inner, scale=1.0 / cnt)
+            m2 = (lh.axis_reduce(lh.RED_DOT, dy, self.y, B, outer, A, inner, scale=1.0 / cnt)
+                  if p.normalize_variance else None)
+            bottoms[0].diff = lh.norm_bwd(dy, self.y if p.normalize_variance else None, m1, m2, self.inv,
+                                          outer, A, inner)
+            return
         dy = tops[0].diff.float()
         dims = self._dims(dy)
         if p.normalize_variance:
@@ -561,7 +818,31 @@ class BatchNormLayer(Layer):
     def _bc(self, v, x):
         return v.reshape(1, 1, 1, -1) if x.dim() == 4 else v.reshape([1, -1] + [1] * (x.dim() - 2))
 
+    def _gpu_geom(self, x):
+        if x.dim() == 4:
+            return x.numel() // x.shape[3], x.shape[3], 1
+        inner = x.numel() // (x.shape[0] * x.shape[1]) if x.dim() > 1 else 1
+        return x.shape[0], x.shape[1] if x.dim() > 1 else 1, inner
+
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            lh = _lh()
+            x = bottoms[0].data
+            outer, C_, inner = self._gpu_geom(x)
+            self.geom = (outer, C_, inner)
+            if self.use_global:
+                mean, self.inv_std = lh.bn_global(self.mean.data, self.var.data, self.factor.data, self.eps)
+            else:
+                s1 = lh.axis_reduce(lh.RED_SUM, x, None, 1, outer, C_, inner)
+                s2 = lh.axis_reduce(lh.RED_SQ, x, None, 1, outer, C_, inner)
+                mean, var, self.inv_std = lh.stats_finalize(s1, s2, outer * inner, self.eps, 0)
+                m = outer * inner
+                lh.bn_running(self.mean.data, self.var.data, self.factor.data, mean, var, self.frac,
+                              m / max(m - 1, 1))
+            y = lh.chan_affine(x, mean, self.inv_std, outer, C_, inner)
+            self.xhat = y
+            tops[0].data = y
+            return
         x = bottoms[0].data.float()
         if self.use_global:
             f = self.factor.data.reshape(())
@@ -582,6 +863,18 @@ class BatchNormLayer(Layer):
 
     def backward(self, tops, propagate_down, bottoms):
         if not propagate_down[0]:
+            return
+        if tops[0].diff.is_cuda:
+            lh = _lh()
+            outer, C_, inner = self.geom
+            dy = tops[0].diff
+            if self.use_global:
+                bottoms[0].diff = lh.norm_bwd(dy, None, None, None, self.inv_std, outer, C_, inner)
+                return
+            cnt = outer * inner
+            m1 = lh.axis_reduce(lh.RED_SUM, dy, None, 1, outer, C_, inner, scale=1.0 / cnt)
+            m2 = lh.axis_reduce(lh.RED_DOT, dy, self.xhat, 1, outer, C_, inner, scale=1.0 / cnt)
+            bottoms[0].diff = lh.norm_bwd(dy, self.xhat, m1, m2, self.inv_std, outer, C_, inner)
             return
         dy = tops[0].diff.float()
         if self.use_global:
@@ -626,6 +919,24 @@ class SPPLayer(Layer):
     def forward(self, bottoms, tops):
         from .. import ops
         b = bottoms[0]
+        if b.data.is_cuda:
+            # each level: HIP pooling (NHWC), then its NCHW-flattened bins copied into the
+            # level's column range of the top
+            lh = _lh()
+            N = b.shape[0]
+            total = tops[0].shape[1]
+            y = torch.empty((N, total), dtype=tops[0].dtype, device=b.data.device)
+            self.aux = []
+            off = 0
+            for s in self._specs(b):
+                p, aux = ops.pool_forward_aux(b.data, s)
+                self.aux.append(aux)
+                n = s.C * s.P * s.Q
+                flat = lh.nhwc_to_nchw(p).reshape(N, n)
+                lh.axis_copy(flat, y, N, n, total, 1, 0, off, n)
+                off += n
+            tops[0].data = y
+            return
         outs = []
         for s in self._specs(b):
             y = ops.ref.pool_forward(b.data.float(), s)  # NHWC
@@ -637,6 +948,21 @@ class SPPLayer(Layer):
             return
         from .. import ops
         b = bottoms[0]
+        if b.data.is_cuda:
+            lh = _lh()
+            N = b.shape[0]
+            total = tops[0].shape[1]
+            grads = []
+            off = 0
+            for s, aux in zip(self._specs(b), self.aux):
+                n = s.C * s.P * s.Q
+                d = torch.empty((N, n), dtype=b.data.dtype, device=b.data.device)
+                lh.axis_copy(tops[0].diff, d, N, total, n, 1, off, 0, n)
+                dy = lh.nchw_to_nhwc(d.reshape(N, s.C, s.P * s.Q), N, s.C, s.P, s.Q)
+                grads.append(ops.pool_backward(dy, b.data, s, aux))
+                off += n
+            b.diff = grads[0] if len(grads) == 1 else _eltwise_sum_gpu(grads)
+            return
         g = torch.zeros(b.data.shape, dtype=torch.float32, device=self.device)
         off = 0
         for s in self._specs(b):

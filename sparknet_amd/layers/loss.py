@@ -29,9 +29,64 @@ def rows_view(blob, axis, diff=False):
         return t.reshape(-1, blob.shape[1])
     if axis == len(blob.shape) - 1 or blob.count_range(axis + 1) == 1:
         return t.reshape(-1, blob.shape[axis])
-    # generic: move axis last
+    # generic: move axis last ([outer][A][inner] -> [outer][inner][A])
+    if t.is_cuda:
+        outer, A, inner = blob.count_range(0, axis), blob.shape[axis], blob.count_range(axis + 1)
+        return _lh().transpose(t, outer, A, inner).reshape(-1, A)
     perm = [d for d in range(t.dim()) if d != axis] + [axis]
     return t.permute(*perm).reshape(-1, blob.shape[axis])
+
+
+def rows_view_back(rows, blob, axis):
+    """Inverse of :func:`rows_view` for a result in the [rows, A] layout."""
+    axis = blob.canonical_axis(axis)
+    if blob.is_image or axis == len(blob.shape) - 1 or blob.count_range(axis + 1) == 1:
+        return rows.reshape(blob.data.shape)
+    outer, A, inner = blob.count_range(0, axis), blob.shape[axis], blob.count_range(axis + 1)
+    return _lh().transpose(rows.reshape(outer, inner, A), outer, inner, A).reshape(blob.data.shape)
+
+
+def _lh():
+    from ..ops import layers_hip
+    return layers_hip
+
+
+def _sample_rows(blob, diff=False):
+    """[N, count / N] in Caffe's logical per-sample order (NHWC images are transposed)."""
+    t = blob.diff if diff else blob.data
+    N = blob.shape[0] if blob.shape else 1
+    if blob.is_image and blob.shape[2] * blob.shape[3] > 1:
+        t = _lh().nhwc_to_nchw(t)
+    return t.reshape(N, -1)
+
+
+def _sample_rows_back(g, blob):
+    """Inverse of :func:`_sample_rows` for a gradient."""
+    if blob.is_image and blob.shape[2] * blob.shape[3] > 1:
+        N, C_, H, W = blob.shape
+        return _lh().nchw_to_nhwc(g.reshape(N, C_, H * W), N, C_, H, W)
+    return g.reshape(blob.data.shape)
+
+
+class _RowLossGPU:
+    """Shared GPU path of the row-structured losses: per-row terms in one HIP kernel, a
+    deterministic device sum (no host sync), gradients in one HIP kernel."""
+
+    kind = ""
+
+    def _gpu_label(self, bottoms):
+        return bottoms[1].data.reshape(-1).float() if len(bottoms) > 1 else None
+
+    def gpu_forward(self, x, t, label, H=None, margin=0.0, legacy=False):
+        lh = _lh()
+        M = x.shape[0]
+        self._ws = lh.loss_rows_fwd(self.kind, x, t, label, H, M, x.shape[1], margin, legacy)
+        return lh.loss_sum(self._ws, M, 1.0 / M)
+
+    def gpu_backward(self, x, t, label, lw, H=None, margin=0.0, legacy=False):
+        M = x.shape[0]
+        return _lh().loss_rows_bwd(self.kind, x, t, label, H, M, x.shape[1], lw, 1.0 / M, 1.0, self._ws, margin,
+                                   legacy)
 
 
 class LossLayer(Layer):
@@ -102,6 +157,9 @@ class SoftmaxLayer(Layer):
 
     def forward(self, bottoms, tops):
         b = bottoms[0]
+        if b.data.is_cuda:
+            tops[0].data = rows_view_back(ops.softmax_forward(rows_view(b, self.axis)), b, self.axis)
+            return
         y = ops.softmax_forward(rows_view(b, self.axis))
         if b.is_image or self.axis == len(b.shape) - 1 or b.count_range(self.axis + 1) == 1:
             tops[0].data = y.reshape(tops[0].data.shape)
@@ -112,6 +170,10 @@ class SoftmaxLayer(Layer):
         if not propagate_down[0]:
             return
         t, b = tops[0], bottoms[0]
+        if t.diff.is_cuda:
+            g = ops.softmax_backward(rows_view(t, self.axis, diff=True), rows_view(t, self.axis))
+            b.diff = rows_view_back(g, b, self.axis)
+            return
         if b.is_image or self.axis == len(b.shape) - 1 or b.count_range(self.axis + 1) == 1:
             g = ops.softmax_backward(rows_view(t, self.axis, diff=True), rows_view(t, self.axis))
             b.diff = g.reshape(b.data.shape)
@@ -144,16 +206,28 @@ class AccuracyLayer(Layer):
 
 
 @register("EuclideanLoss")
-class EuclideanLossLayer(LossLayer):
+class EuclideanLossLayer(LossLayer, _RowLossGPU):
     exact_bottoms = 2
+    kind = "Euclidean"
 
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            a, b = bottoms[0].data.reshape(bottoms[0].shape[0], -1), bottoms[1].data.reshape(bottoms[0].shape[0], -1)
+            tops[0].data = self.gpu_forward(a, b, None).reshape(())
+            return
         self.d = bottoms[0].data.float() - bottoms[1].data.float()
         n = bottoms[0].shape[0]
         tops[0].data = ((self.d * self.d).sum() / n / 2.0).reshape(())
 
     def backward(self, tops, propagate_down, bottoms):
         n = bottoms[0].shape[0]
+        if tops[0].diff.is_cuda:
+            rows = [bottoms[i].data.reshape(n, -1) for i in range(2)]
+            for i in range(2):
+                if propagate_down[i]:  # d/dx_i of |x_0 - x_1|^2 / 2N = (x_i - x_other) / N
+                    g = self.gpu_backward(rows[i], rows[1 - i], None, tops[0].diff)
+                    bottoms[i].diff = g.reshape(bottoms[i].data.shape)
+            return
         lw = tops[0].diff.float()
         for i in range(2):
             if propagate_down[i]:
@@ -162,10 +236,15 @@ class EuclideanLossLayer(LossLayer):
 
 
 @register("SigmoidCrossEntropyLoss")
-class SigmoidCrossEntropyLossLayer(LossLayer):
+class SigmoidCrossEntropyLossLayer(LossLayer, _RowLossGPU):
     exact_bottoms = 2
+    kind = "SigmoidXent"
 
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            x, t = _sample_rows(bottoms[0]), _sample_rows(bottoms[1])
+            tops[0].data = self.gpu_forward(x, t.reshape(x.shape), None).reshape(())
+            return
         x = bottoms[0].data.float()
         t = bottoms[1].data.float().reshape(x.shape)
         self.sig = torch.sigmoid(x)
@@ -175,6 +254,11 @@ class SigmoidCrossEntropyLossLayer(LossLayer):
     def backward(self, tops, propagate_down, bottoms):
         if len(propagate_down) > 1 and propagate_down[1]:
             raise ValueError("SigmoidCrossEntropyLoss cannot backpropagate to label inputs")
+        if propagate_down[0] and tops[0].diff.is_cuda:
+            x, t = _sample_rows(bottoms[0]), _sample_rows(bottoms[1])
+            g = self.gpu_backward(x, t.reshape(x.shape), None, tops[0].diff)
+            bottoms[0].diff = _sample_rows_back(g, bottoms[0])
+            return
         if propagate_down[0]:
             t = bottoms[1].data.float().reshape(self.sig.shape)
             g = (self.sig - t) * (tops[0].diff.float() / bottoms[0].shape[0])
@@ -182,10 +266,14 @@ class SigmoidCrossEntropyLossLayer(LossLayer):
 
 
 @register("HingeLoss")
-class HingeLossLayer(LossLayer):
+class HingeLossLayer(LossLayer, _RowLossGPU):
     exact_bottoms = 2
 
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            self.kind = "HingeL2" if int(self.lp.hinge_loss_param.norm) == 2 else "HingeL1"
+            tops[0].data = self.gpu_forward(_sample_rows(bottoms[0]), None, self._gpu_label(bottoms)).reshape(())
+            return
         x = rows_view(bottoms[0], 1).float()
         lab = bottoms[1].data.reshape(-1).long()
         sign = -torch.ones_like(x)
@@ -198,6 +286,10 @@ class HingeLossLayer(LossLayer):
         tops[0].data = (v / x.shape[0]).reshape(())
 
     def backward(self, tops, propagate_down, bottoms):
+        if propagate_down[0] and tops[0].diff.is_cuda:
+            g = self.gpu_backward(_sample_rows(bottoms[0]), None, self._gpu_label(bottoms), tops[0].diff)
+            bottoms[0].diff = _sample_rows_back(g, bottoms[0])
+            return
         if propagate_down[0]:
             n = self.m.shape[0]
             g = -self.sign * ((2 * self.m) if self.l2 else (self.m > 0).float())
@@ -206,16 +298,24 @@ class HingeLossLayer(LossLayer):
 
 
 @register("MultinomialLogisticLoss")
-class MultinomialLogisticLossLayer(LossLayer):
+class MultinomialLogisticLossLayer(LossLayer, _RowLossGPU):
     exact_bottoms = 2
+    kind = "Multinomial"
 
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            tops[0].data = self.gpu_forward(_sample_rows(bottoms[0]), None, self._gpu_label(bottoms)).reshape(())
+            return
         p = rows_view(bottoms[0], 1).float()
         lab = bottoms[1].data.reshape(-1).long()
         self.pl = p.gather(1, lab[:, None]).clamp_min(1e-20)
         tops[0].data = (-torch.log(self.pl).sum() / p.shape[0]).reshape(())
 
     def backward(self, tops, propagate_down, bottoms):
+        if propagate_down[0] and tops[0].diff.is_cuda:
+            g = self.gpu_backward(_sample_rows(bottoms[0]), None, self._gpu_label(bottoms), tops[0].diff)
+            bottoms[0].diff = _sample_rows_back(g, bottoms[0])
+            return
         if propagate_down[0]:
             p = rows_view(bottoms[0], 1).float()
             lab = bottoms[1].data.reshape(-1).long()
@@ -226,9 +326,14 @@ class MultinomialLogisticLossLayer(LossLayer):
 
 
 @register("InfogainLoss")
-class InfogainLossLayer(LossLayer):
+class InfogainLossLayer(LossLayer, _RowLossGPU):
     min_bottoms = 2
     max_bottoms = 3
+    kind = "Infogain"
+
+    def _gpu_H(self, bottoms, dim):
+        H = self.H if self.H is not None else bottoms[2].data
+        return H.reshape(dim, -1).float().contiguous()
 
     def layer_setup(self, bottoms, tops):
         self.H = None
@@ -240,6 +345,11 @@ class InfogainLossLayer(LossLayer):
                 bottoms[0].shape[1], -1).to(self.device)
 
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            x = _sample_rows(bottoms[0])
+            self._Hg = self._gpu_H(bottoms, x.shape[1])
+            tops[0].data = self.gpu_forward(x, None, self._gpu_label(bottoms), self._Hg).reshape(())
+            return
         p = rows_view(bottoms[0], 1).float()
         H = self.H if self.H is not None else bottoms[2].data.float().reshape(p.shape[1], -1)
         lab = bottoms[1].data.reshape(-1).long()
@@ -248,17 +358,28 @@ class InfogainLossLayer(LossLayer):
         tops[0].data = (-(self.Hl * torch.log(self.p)).sum() / p.shape[0]).reshape(())
 
     def backward(self, tops, propagate_down, bottoms):
+        if propagate_down[0] and tops[0].diff.is_cuda:
+            g = self.gpu_backward(_sample_rows(bottoms[0]), None, self._gpu_label(bottoms), tops[0].diff, self._Hg)
+            bottoms[0].diff = _sample_rows_back(g, bottoms[0])
+            return
         if propagate_down[0]:
             g = -self.Hl / self.p * (tops[0].diff.float() / self.p.shape[0])
             bottoms[0].diff = g.reshape(bottoms[0].data.shape).to(bottoms[0].dtype)
 
 
 @register("ContrastiveLoss")
-class ContrastiveLossLayer(LossLayer):
+class ContrastiveLossLayer(LossLayer, _RowLossGPU):
     exact_bottoms = 3
+    kind = "Contrastive"
 
     def forward(self, bottoms, tops):
         p = self.lp.contrastive_loss_param
+        if bottoms[0].data.is_cuda:
+            n = bottoms[0].shape[0]
+            a, b = bottoms[0].data.reshape(n, -1), bottoms[1].data.reshape(n, -1)
+            self._y = bottoms[2].data.reshape(-1).float()
+            tops[0].data = self.gpu_forward(a, b, self._y, None, p.margin, p.legacy_version).reshape(())
+            return
         a = bottoms[0].data.float().reshape(bottoms[0].shape[0], -1)
         b = bottoms[1].data.float().reshape(a.shape)
         y = bottoms[2].data.float().reshape(-1)
@@ -274,6 +395,16 @@ class ContrastiveLossLayer(LossLayer):
         tops[0].data = loss.reshape(())
 
     def backward(self, tops, propagate_down, bottoms):
+        if tops[0].diff.is_cuda:
+            p = self.lp.contrastive_loss_param
+            n = bottoms[0].shape[0]
+            rows = [bottoms[i].data.reshape(n, -1) for i in range(2)]
+            for i in range(2):
+                if propagate_down[i]:  # gradient of bottom i: coef * (x_i - x_other) * lw / N
+                    g = self.gpu_backward(rows[i], rows[1 - i], self._y, tops[0].diff, None, p.margin,
+                                          p.legacy_version)
+                    bottoms[i].diff = g.reshape(bottoms[i].data.shape)
+            return
         n = self.diff.shape[0]
         lw = tops[0].diff.float() / n
         if self.legacy:

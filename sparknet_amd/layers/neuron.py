@@ -5,7 +5,9 @@ References: caffe/src/caffe/layers/{relu,dropout,sigmoid,tanh,absval,bnll,exp,lo
 threshold,prelu}_layer.{cpp,cu}.  ReLU and Dropout are on the hot path and run HIP
 kernels (ReLU forward is usually fused into the producing conv/IP epilogue by the net);
 Dropout regenerates its Philox mask in backward instead of storing it.  The remaining
-neurons are expressed as tensor math (used by the sigmoid cifar variants and tests).
+neurons run one templated HIP elementwise kernel per direction on the GPU
+(csrc/kernels/layers.hip ``neuron_fwd_k`` / ``neuron_bwd_k``, fp32 math, 8-wide bf16
+vectors) and fp32 tensor math on the CPU reference path.
 """
 from __future__ import annotations
 
@@ -73,7 +75,15 @@ class DropoutLayer(NeuronLayer):
 
 
 class _Elementwise(NeuronLayer):
-    """y = f(x), dx = dy * f'(x, y), computed in fp32 and stored in the compute dtype."""
+    """y = f(x), dx = dy * f'(x, y), computed in fp32 and stored in the compute dtype.
+    ``kind`` names the HIP kernel (ops.layers_hip.NEURON); ``needs_x`` says whether the
+    derivative reads the input (an in-place layer then keeps a copy of it)."""
+
+    kind: str = ""
+    needs_x = True
+
+    def hip_params(self):
+        return (0.0, 0.0, 0.0)
 
     def f(self, x):
         raise NotImplementedError
@@ -83,11 +93,22 @@ class _Elementwise(NeuronLayer):
 
     def forward(self, bottoms, tops):
         x = bottoms[0].data
+        if x.is_cuda:
+            from ..ops import layers_hip as lh
+            self._x = x.clone() if (tops[0] is bottoms[0] and self.needs_x) else None
+            tops[0].data = lh.neuron_fwd(self.kind, x, None, *self.hip_params())
+            return
         self._x = x.float() if tops[0] is bottoms[0] else None
         tops[0].data = self.f(x.float()).to(x.dtype)
 
     def backward(self, tops, propagate_down, bottoms):
         if not propagate_down[0]:
+            return
+        dy = tops[0].diff
+        if dy.is_cuda:
+            from ..ops import layers_hip as lh
+            x = (self._x if self._x is not None else bottoms[0].data) if self.needs_x else None
+            bottoms[0].diff = lh.neuron_bwd(self.kind, x, tops[0].data, dy, *self.hip_params())
             return
         x = self._x if self._x is not None else bottoms[0].data.float()
         y = tops[0].data.float()
@@ -96,6 +117,8 @@ class _Elementwise(NeuronLayer):
 
 @register("Sigmoid")
 class SigmoidLayer(_Elementwise):
+    kind, needs_x = "Sigmoid", False
+
     def f(self, x):
         return torch.sigmoid(x)
 
@@ -105,6 +128,8 @@ class SigmoidLayer(_Elementwise):
 
 @register("TanH")
 class TanHLayer(_Elementwise):
+    kind, needs_x = "TanH", False
+
     def f(self, x):
         return torch.tanh(x)
 
@@ -114,6 +139,8 @@ class TanHLayer(_Elementwise):
 
 @register("AbsVal")
 class AbsValLayer(_Elementwise):
+    kind = "AbsVal"
+
     def f(self, x):
         return x.abs()
 
@@ -123,6 +150,8 @@ class AbsValLayer(_Elementwise):
 
 @register("BNLL")
 class BNLLLayer(_Elementwise):
+    kind = "BNLL"
+
     def f(self, x):
         return torch.where(x > 0, x + torch.log1p(torch.exp(-x)), torch.log1p(torch.exp(x)))
 
@@ -133,6 +162,11 @@ class BNLLLayer(_Elementwise):
 
 @register("Exp")
 class ExpLayer(_Elementwise):
+    kind, needs_x = "Exp", False
+
+    def hip_params(self):
+        return (self.log_base * self.scale, self.log_base * self.shift, 0.0)
+
     def layer_setup(self, bottoms, tops):
         p = self.lp.exp_param
         base, self.scale, self.shift = float(p.base), float(p.scale), float(p.shift)
@@ -149,6 +183,11 @@ class ExpLayer(_Elementwise):
 
 @register("Log")
 class LogLayer(_Elementwise):
+    kind = "Log"
+
+    def hip_params(self):
+        return (self.scale, self.shift, self.inv_log_base)
+
     def layer_setup(self, bottoms, tops):
         p = self.lp.log_param
         base, self.scale, self.shift = float(p.base), float(p.scale), float(p.shift)
@@ -163,6 +202,11 @@ class LogLayer(_Elementwise):
 
 @register("Power")
 class PowerLayer(_Elementwise):
+    kind = "Power"
+
+    def hip_params(self):
+        return (self.power, self.scale, self.shift)
+
     def layer_setup(self, bottoms, tops):
         p = self.lp.power_param
         self.power, self.scale, self.shift = float(p.power), float(p.scale), float(p.shift)
@@ -182,7 +226,12 @@ class ThresholdLayer(NeuronLayer):
         self.t = float(self.lp.threshold_param.threshold)
 
     def forward(self, bottoms, tops):
-        tops[0].data = (bottoms[0].data.float() > self.t).to(self.dtype)
+        x = bottoms[0].data
+        if x.is_cuda:
+            from ..ops import layers_hip as lh
+            tops[0].data = lh.neuron_fwd("Threshold", x, self.dtype, self.t)
+            return
+        tops[0].data = (x.float() > self.t).to(self.dtype)
 
     def backward(self, tops, propagate_down, bottoms):
         if propagate_down[0]:
@@ -212,13 +261,41 @@ class PReLULayer(NeuronLayer):
             return a.reshape(1, 1, 1, -1)
         return a.reshape([1, -1] + [1] * (x.dim() - 2))
 
+    def _geom(self, x):
+        """(C, inner, outer) of the channel axis in the physical layout (NHWC: inner 1)."""
+        if self.shared:
+            return 1, 1, x.numel()
+        if x.dim() == 4:
+            return x.shape[-1], 1, x.numel() // x.shape[-1]
+        inner = 1
+        for d in x.shape[2:]:
+            inner *= d
+        return x.shape[1], inner, x.shape[0]
+
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            from ..ops import layers_hip as lh
+            x = bottoms[0].data
+            self._x = x.clone() if tops[0] is bottoms[0] else x
+            C_, inner, _ = self._geom(x)
+            tops[0].data = lh.prelu_fwd(x, self.slope.data, C_, inner)
+            return
         x = bottoms[0].data.float()
         self._x = x
         a = self._bcast(self.slope.data.float(), x)
         tops[0].data = torch.where(x > 0, x, x * a).to(self.dtype)
 
     def backward(self, tops, propagate_down, bottoms):
+        if tops[0].diff.is_cuda:
+            from ..ops import layers_hip as lh
+            x, dy = self._x, tops[0].diff
+            C_, inner, outer = self._geom(x)
+            if self.param_grads_needed(0):
+                # slope gradient: sum over everything but the channel of dy * x * [x <= 0]
+                lh.axis_reduce(lh.RED_PRELU, dy, x, 1, outer, C_, inner, out=self.slope.diff.view(-1), acc=True)
+            if propagate_down[0]:
+                bottoms[0].diff = lh.prelu_bwd(x, dy, self.slope.data, C_, inner)
+            return
         x = self._x
         dy = tops[0].diff.float()
         a = self._bcast(self.slope.data.float(), x)

@@ -250,6 +250,13 @@ class PoolingLayer(Layer):
     def forward(self, bottoms, tops):
         s = self.spec(bottoms[0])
         x = bottoms[0].data
+        if self.method == POOL_STOCHASTIC and x.is_cuda:
+            from ..ops import layers_hip
+            if getattr(self, "stream", None) is None:
+                self.stream = self.ctx.next_stream_id()
+            train = self.phase == proto.TRAIN
+            tops[0].data, self.aux = layers_hip.stopool(x, s, self.ctx.rng_state, self.stream, train)
+            return
         if self.method == POOL_STOCHASTIC:
             if self.phase == proto.TRAIN:
                 # StoPoolForwardTrain (pooling_layer.cu:88-122): draw u ~ U[0,1) per output,
@@ -273,6 +280,12 @@ class PoolingLayer(Layer):
         if not propagate_down[0]:
             return
         s = self.spec(bottoms[0])
+        if self.method == POOL_STOCHASTIC and tops[0].diff.is_cuda:
+            # the sampled window offsets are a max-pool style mask: gather backward
+            import dataclasses
+            sm = dataclasses.replace(s, method=0)
+            bottoms[0].diff = ops.pool_backward(tops[0].diff, bottoms[0].data, sm, self.aux)
+            return
         if self.method == POOL_STOCHASTIC:
             # StoPoolBackward (pooling_layer.cu:270-300): the diff goes to the sampled element
             xl = bottoms[0].data.float().requires_grad_(True)
@@ -416,7 +429,16 @@ class Im2colLayer(Layer):
         Q = (W + 2 * self.pw - self.S) // self.sw + 1
         tops[0].reshape((N, C * self.R * self.S, P, Q), self.dtype)
 
+    def _geom(self, b, t):
+        N, C_, H, W = b.shape
+        return (N, H, W, C_, t.shape[2], t.shape[3], self.R, self.S, self.sh, self.sw, self.ph, self.pw, 1, 1)
+
     def forward(self, bottoms, tops):
+        if bottoms[0].data.is_cuda:
+            from ..ops import layers_hip
+            b, t = bottoms[0], tops[0]
+            t.data = layers_hip.im2col_caffe(b.data, self._geom(b, t), t.data.shape)
+            return
         xn = bottoms[0].nchw().float()
         cols = torch.nn.functional.unfold(xn, (self.R, self.S), padding=(self.ph, self.pw),
                                           stride=(self.sh, self.sw))
@@ -428,6 +450,10 @@ class Im2colLayer(Layer):
         if not propagate_down[0]:
             return
         t, b = tops[0], bottoms[0]
+        if t.diff.is_cuda:
+            from ..ops import layers_hip
+            b.diff = layers_hip.col2im_caffe(t.diff, self._geom(b, t), b.data.shape)
+            return
         d = t.nchw(diff=True).float().reshape(t.shape[0], t.shape[1], -1)
         x = torch.nn.functional.fold(d, b.shape[2:], (self.R, self.S), padding=(self.ph, self.pw),
                                      stride=(self.sh, self.sw))

@@ -362,9 +362,8 @@ def lrn_backward(dy, x, size, alpha, beta, k, within=False, y=None):
 
 def relu_forward(x, slope=0.0):
     x = _c(x)
-    if x.numel() % 8:
-        xf = x.float()
-        return torch.where(xf > 0, xf, xf * slope).to(x.dtype)
+    if x.dtype != BF16:
+        raise TypeError(f"relu_forward: GPU activations are bf16, got {x.dtype}")
     y = torch.empty_like(x)
     call("relu_fwd", x, y, x.numel(), float(slope))
     return y
@@ -372,9 +371,6 @@ def relu_forward(x, slope=0.0):
 
 def relu_backward(dy, x, slope=0.0):
     dy, x = _c(dy), _c(x)
-    if x.numel() % 8:
-        xf = x.float()
-        return (dy.float() * torch.where(xf > 0, 1.0, slope)).to(dy.dtype)
     dx = torch.empty_like(dy)
     call("relu_bwd", dy, x, dx, x.numel(), float(slope))
     return dx
@@ -382,8 +378,6 @@ def relu_backward(dy, x, slope=0.0):
 
 def _dropout(x, ratio, rng_state, stream, gate=None):
     x = _c(x)
-    if x.numel() % 8:
-        raise NotImplementedError("dropout on GPU needs element count % 8 == 0")
     y = torch.empty_like(x)
     call("dropout", x, y, x.numel(), rng_state, int(stream), float(ratio), _c(gate) if gate is not None else None)
     return y
