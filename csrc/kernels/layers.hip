@@ -150,11 +150,13 @@ __global__ void __launch_bounds__(256) neuron_bwd_k(const void* __restrict__ x, 
 }
 
 // PReLU over [outer][C][inner] (inner = 1 for NHWC images / [N, C] blobs); shared: C = 1
+// x may be fp32 (a 2-D blob from an Input layer) while y / dy / dx are the compute dtype.
 __global__ void __launch_bounds__(256) prelu_fwd_k(const void* __restrict__ x, const float* __restrict__ slope,
-                                                   void* __restrict__ y, long long n, int C, long long inner, int dt) {
+                                                   void* __restrict__ y, long long n, int C, long long inner, int dtx,
+                                                   int dt) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float v = ldv(x, i, dt);
+    const float v = ldv(x, i, dtx);
     const int c = C == 1 ? 0 : (int)((i / inner) % C);
     stv(y, i, dt, v > 0.f ? v : v * slope[c]);
   }
@@ -162,10 +164,10 @@ __global__ void __launch_bounds__(256) prelu_fwd_k(const void* __restrict__ x, c
 
 __global__ void __launch_bounds__(256) prelu_bwd_k(const void* __restrict__ x, const void* __restrict__ dy,
                                                    const float* __restrict__ slope, void* __restrict__ dx, long long n,
-                                                   int C, long long inner, int dt) {
+                                                   int C, long long inner, int dtx, int dt) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float v = ldv(x, i, dt), d = ldv(dy, i, dt);
+    const float v = ldv(x, i, dtx), d = ldv(dy, i, dt);
     const int c = C == 1 ? 0 : (int)((i / inner) % C);
     stv(dx, i, dt, v > 0.f ? d : d * slope[c]);
   }
@@ -781,15 +783,16 @@ int sn_neuron_bwd(long long kind, const void* x, const void* y, const void* dy, 
   return SN_CHECK_LAUNCH();
 }
 
-int sn_prelu_fwd(const void* x, const float* slope, void* y, long long n, long long C, long long inner, long long dt,
-                 hipStream_t st) {
-  hipLaunchKernelGGL(prelu_fwd_k, dim3(grid_for(n)), dim3(256), 0, st, x, slope, y, n, (int)C, inner, (int)dt);
+int sn_prelu_fwd(const void* x, const float* slope, void* y, long long n, long long C, long long inner, long long dtx,
+                 long long dt, hipStream_t st) {
+  hipLaunchKernelGGL(prelu_fwd_k, dim3(grid_for(n)), dim3(256), 0, st, x, slope, y, n, (int)C, inner, (int)dtx, (int)dt);
   return SN_CHECK_LAUNCH();
 }
 
 int sn_prelu_bwd(const void* x, const void* dy, const float* slope, void* dx, long long n, long long C,
-                 long long inner, long long dt, hipStream_t st) {
-  hipLaunchKernelGGL(prelu_bwd_k, dim3(grid_for(n)), dim3(256), 0, st, x, dy, slope, dx, n, (int)C, inner, (int)dt);
+                 long long inner, long long dtx, long long dt, hipStream_t st) {
+  hipLaunchKernelGGL(prelu_bwd_k, dim3(grid_for(n)), dim3(256), 0, st, x, dy, slope, dx, n, (int)C, inner, (int)dtx,
+                     (int)dt);
   return SN_CHECK_LAUNCH();
 }
 

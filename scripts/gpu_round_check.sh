@@ -1,13 +1,12 @@
-# Round-end style GPU check: gpu tests, smoke, CaffeNet + GoogLeNet benches, kernel profile.
-# Every GPU step has its own time limit; the chain stops at the first failure.
+#!/bin/bash
+# One GPU pass: gpu tests, smoke, 1-GPU bench, rocprofv3 kernel stats of the bench.
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-    > gpurun_out/gpu_tests.log 2>&1 && tail -2 gpurun_out/gpu_tests.log && \
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 240 python -u bench.py > gpurun_out/c.json 2> gpurun_out/c.err && cat gpurun_out/c.json && \
-timeout -k 10 240 python -u bench.py --model googlenet --steps 30 --warmup 5 > gpurun_out/g.json 2> gpurun_out/g.err && \
-cat gpurun_out/g.json && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 \
-    > gpurun_out/prof.log 2>&1 && echo PROF_OK
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -3 gpurun_out/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench failed; tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json

@@ -278,7 +278,7 @@ class PReLULayer(NeuronLayer):
             x = bottoms[0].data
             self._x = x.clone() if tops[0] is bottoms[0] else x
             C_, inner, _ = self._geom(x)
-            tops[0].data = lh.prelu_fwd(x, self.slope.data, C_, inner)
+            tops[0].data = lh.prelu_fwd(x, self.slope.data, C_, inner, out_dtype=tops[0].dtype)
             return
         x = bottoms[0].data.float()
         self._x = x

@@ -25,6 +25,22 @@ def _c(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous() else t.contiguous()
 
 
+def as_bf16(t: torch.Tensor | None) -> torch.Tensor | None:
+    """Contiguous bf16 view of a GPU activation.  Non-image blobs fed by Input / data
+    layers stay fp32 (labels, 2-D features); the bf16-only kernels below get a bf16 copy
+    made by the native cast kernel instead of reading fp32 bytes as bf16."""
+    if t is None:
+        return None
+    t = _c(t)
+    if t.dtype == BF16:
+        return t
+    if t.dtype != torch.float32:
+        raise TypeError(f"GPU activations are bf16 or fp32, got {t.dtype}")
+    out = torch.empty(t.shape, dtype=BF16, device=t.device)
+    call("cast_f32_bf16", t, out, t.numel())
+    return out
+
+
 def _round8(n: int) -> int:
     return -(-n // 8) * 8
 
@@ -361,25 +377,23 @@ def lrn_backward(dy, x, size, alpha, beta, k, within=False, y=None):
 # --------------------------------------------------------------------------------------
 
 def relu_forward(x, slope=0.0):
-    x = _c(x)
-    if x.dtype != BF16:
-        raise TypeError(f"relu_forward: GPU activations are bf16, got {x.dtype}")
+    x = as_bf16(x)
     y = torch.empty_like(x)
     call("relu_fwd", x, y, x.numel(), float(slope))
     return y
 
 
 def relu_backward(dy, x, slope=0.0):
-    dy, x = _c(dy), _c(x)
+    dy, x = as_bf16(dy), as_bf16(x)
     dx = torch.empty_like(dy)
     call("relu_bwd", dy, x, dx, x.numel(), float(slope))
     return dx
 
 
 def _dropout(x, ratio, rng_state, stream, gate=None):
-    x = _c(x)
+    x = as_bf16(x)
     y = torch.empty_like(x)
-    call("dropout", x, y, x.numel(), rng_state, int(stream), float(ratio), _c(gate) if gate is not None else None)
+    call("dropout", x, y, x.numel(), rng_state, int(stream), float(ratio), as_bf16(gate))
     return y
 
 
@@ -474,15 +488,16 @@ def softmax_loss_backward(prob, labels, loss_weight, norm, ignore_label=None, dt
 
 
 def softmax_forward(x2):
-    x2 = _c(x2)
+    x2 = as_bf16(x2)
     y = torch.empty_like(x2)
     call("softmax_fwd", x2, y, x2.shape[0], x2.shape[1])
     return y
 
 
 def softmax_backward(dy2, y2):
+    dy2, y2 = as_bf16(dy2), as_bf16(y2)
     dx = torch.empty_like(y2)
-    call("softmax_bwd", _c(dy2), _c(y2), dx, y2.shape[0], y2.shape[1])
+    call("softmax_bwd", dy2, y2, dx, y2.shape[0], y2.shape[1])
     return dx
 
 

@@ -52,17 +52,18 @@ def neuron_bwd(kind: str, x, y, dy, a=0.0, b=0.0, c=0.0):
     return dx
 
 
-def prelu_fwd(x, slope, C_, inner):
+def prelu_fwd(x, slope, C_, inner, out_dtype=None):
     x = _c(x)
-    y = torch.empty_like(x)
-    call("prelu_fwd", x, _c(slope), y, x.numel(), C_, inner, dt(x))
+    y = torch.empty(x.shape, dtype=out_dtype or x.dtype, device=x.device)
+    call("prelu_fwd", x, _c(slope), y, x.numel(), C_, inner, dt(x), dt(y))
     return y
 
 
 def prelu_bwd(x, dy, slope, C_, inner):
+    """dx in dy's dtype; x may be in another dtype (an fp32 2-D Input blob)."""
     dy = _c(dy)
     dx = torch.empty_like(dy)
-    call("prelu_bwd", _c(x), dy, _c(slope), dx, dy.numel(), C_, inner, dt(dy))
+    call("prelu_bwd", _c(x), dy, _c(slope), dx, dy.numel(), C_, inner, dt(x), dt(dy))
     return dx
 
 
