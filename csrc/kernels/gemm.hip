@@ -68,7 +68,8 @@ struct SnGemmArgs {
   long long ldc, c_gstride, c_split_stride;
   const float* bias;  // per output column n (offset by g*N), EPI_BF16 only
   int relu;
-  int tile;           // 0: 128x128, 1: 256x64, 4: 128x96, 5: 256x48 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages)
+  int tile;           // 0: 128x128, 1: 256x64, 4: 128x96, 5: 256x48 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages);
+                      // 6: 256x256, 7: 256x128 (gemm256_kernel: 8 waves, half-tile phased pipeline)
   const bf16_t* gate; // EPI_BF16: zero outputs where gate (same layout as C) <= 0 (fused ReLU backward)
   int fp8;            // operands are e4m3 bytes (K-contiguous only); k counts fp8 elements
   const float* deq_a; // fp8: dequantisation factors (1 / quantisation scale) of A and B, device scalars
@@ -118,6 +119,7 @@ __device__ __attribute__((aligned(16))) uint4 g_zero16[1];
 __device__ __attribute__((aligned(16))) uint32_t g_one16[4] = {0x3F80u, 0u, 0u, 0u};
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // Global->LDS staging of one operand tile with global_load_lds_dwordx4 (LDS-DMA, no VGPR
 // round trip and no ds_write pass).  One wave-instruction writes 1 KB of LDS linearly
@@ -148,12 +150,32 @@ struct GStager {
   int cr[NI], cs[NI], cc[NI];  // MC+IM2COL: column decode (cols fixed across k)
   bool cv[NI], co[NI];         //   column valid / column is the ones column
   float invPQ, invQ, invCg, invS, invKg;
+  // KC+IM2COL: (tap row, tap col, channel) of the NEXT tile to issue — tiles are issued in
+  // order, so the decode advances by one K-step per issue (wave-uniform, scalar) instead
+  // of dividing k_tile by Cg and S every time; and a raw buffer resource over the input
+  // tensor, so the DMA takes a 32-bit byte offset and a lane outside the image reads
+  // offset 0xffffffff, which the buffer range check turns into zeros (no zero-page select,
+  // no 64-bit address arithmetic per lane).
+  int nr, ns, nc;
+  i32x4 rsrc;
 
   SN_DEV void init(const SnOperand& op, int grp, int wave, int lane, int tile_row0, int rows_lim,
-                   int tile_col0, int cols_lim, int ones = -1) {
+                   int tile_col0, int cols_lim, int ones = -1, int k_start = 0) {
     ld = op.ld;
     g = op.g;
     ones_col = ones;
+    if (MODE == OP_IM2COL && !MC) {
+      const int tap = k_start / g.Cg;
+      nc = k_start - tap * g.Cg;
+      nr = tap / g.S;
+      ns = tap - nr * g.S;
+      const unsigned long long a = reinterpret_cast<unsigned long long>(op.ptr);
+      const unsigned nbytes = (unsigned)((unsigned long long)g.N * g.H * g.W * g.C * ES);
+      rsrc[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
+      rsrc[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffffu));
+      rsrc[2] = __builtin_amdgcn_readfirstlane((int)nbytes);
+      rsrc[3] = 0x00020000;
+    }
     if (MODE != OP_IM2COL) {
       base = reinterpret_cast<const char*>(op.ptr) + (long long)grp * op.gstride * ES;
       coff = 0;
@@ -201,6 +223,13 @@ struct GStager {
     const uint32_t m0 = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(s) : "memory");
   }
+  // LDS-DMA through the buffer resource: byte offset off (0xffffffff: out of range -> 0)
+  SN_DEV void dma_buf(unsigned off, char* lds) {
+    const uint32_t m0 = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off),
+                 "s"(rsrc)
+                 : "memory");
+  }
 
   // Issue the LDS-DMA of the tile whose first reduction index is k_tile into `lds`.
   SN_DEV void issue(char* lds, int wave, int k_tile, int k_lim, int tile_rc0, int rc_lim) {
@@ -213,11 +242,18 @@ struct GStager {
           dma(base + ((long long)row * ld + k) * ES, row < rc_lim && k < k_lim, dst + j * 1024);
         }
       } else {
-        // k = (tap, c), c innermost.  k_tile is wave-uniform: decode it once on the scalar
-        // unit, then each lane adds its chunk (< 8*EPC channels), which crosses at most one
-        // tap boundary when Cg >= 8*EPC — no per-lane division on the fast path.
-        const int tap0 = k_tile / g.Cg, c0 = k_tile - tap0 * g.Cg;
-        const int r0 = tap0 / g.S, s0 = tap0 - r0 * g.S;
+        // k = (tap, c), c innermost.  (r0, s0, c0) is the running scalar decode of k_tile;
+        // each lane adds its chunk (< 8*EPC channels), which crosses at most one tap
+        // boundary when Cg >= 8*EPC — no per-lane division on the fast path.
+        const int c0 = nc, r0 = nr, s0 = ns;
+        nc += 8 * EPC;
+        while (nc >= g.Cg) {
+          nc -= g.Cg;
+          if (++ns == g.S) {
+            ns = 0;
+            ++nr;
+          }
+        }
         int kv[2], dh[2], dw[2], toff[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -248,7 +284,7 @@ struct GStager {
           const int e = j & 1;
           const int h = ph[j] + dh[e], w = pw[j] + dw[e];
           const bool v = kv[e] && pv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          dma(base + (long long)(rowoff[j] + toff[e]) * ES, v, dst + j * 1024);
+          dma_buf(v ? (unsigned)(rowoff[j] + toff[e]) * (unsigned)ES : 0xffffffffu, dst + j * 1024);
         }
       }
     } else {
@@ -336,6 +372,125 @@ SN_DEV i32x8 read_frag8(const char* lds, int x0, int lane) {
   return r;
 }
 
+// Store one 4-column output fragment v = C[m][n..n+3] (the caller checked m < M, n < N):
+// bias / ReLU / ReLU-backward gate for bf16 outputs, fp32 store / accumulate (+ the
+// bias-gradient column routed to bias_out), or the fused solver update (EPI_SGD).
+template <int EPI, bool FP8>
+SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, f32x4 v, int c_cols) {
+  const bool full = (n + 3 < c_cols) && ((args.ldc & 3) == 0);
+  if (FP8) v = v * (args.deq_a[0] * args.deq_b[0]);  // per-tensor fp8 scales
+  if (EPI == EPI_BF16) {
+    bf16_t* C = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride + (long long)m * args.ldc;
+    float o[4] = {v[0], v[1], v[2], v[3]};
+    if (args.bias) {
+      const float* bz = args.bias + (long long)grp * args.N;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] += (n + r < args.N) ? bz[n + r] : 0.f;
+    }
+    if (args.relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
+    }
+    if (args.gate) {
+      const bf16_t* gp = args.gate + grp * args.c_gstride + (long long)m * args.ldc + n;
+      float gv[4];
+      if (full && (args.c_gstride & 3) == 0) {
+        const uint2 u = *reinterpret_cast<const uint2*>(gp);
+        gv[0] = __uint_as_float(u.x << 16);
+        gv[1] = __uint_as_float(u.x & 0xffff0000u);
+        gv[2] = __uint_as_float(u.y << 16);
+        gv[3] = __uint_as_float(u.y & 0xffff0000u);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gv[r] = (n + r < args.N) ? bf2f(gp[r]) : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!(gv[r] > 0.f)) o[r] = 0.f;
+    }
+    if (full) {
+      uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      *reinterpret_cast<uint2*>(C + n) = pk;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < args.N) C[n + r] = f2bf(o[r]);
+    }
+  } else {
+    if (args.bias_out && n <= args.ones_col && args.ones_col < n + 4) {
+      const int r = args.ones_col - n;
+      const float bv = r == 0 ? v[0] : (r == 1 ? v[1] : (r == 2 ? v[2] : v[3]));
+      float* bp = args.bias_out + (long long)grp * args.M + m;
+      *bp = args.bias_acc ? *bp + bv : bv;
+    }
+    if (n >= c_cols) return;
+    if (EPI == EPI_SGD) {
+      // H_LR = 0, H_MOM = 1, H_WD = 2, H_NORM = 4 (solver.hip); same op order as
+      // solver_update_kernel KIND 0 / 1 so both paths give identical weights
+      const float* hy = args.sgd_hyper;
+      const float rate = hy[0] * args.sgd_lr_mult, mom = hy[1], decay = hy[2] * args.sgd_decay_mult;
+      const float gscale = hy[4];
+      const long long o = grp * args.c_gstride + (long long)m * args.ldc + n;
+      const bool vec = (n + 3 < c_cols) && ((args.ldc & 3) == 0) && ((o & 3) == 0);
+      float W[4], A[4];
+      if (vec) {
+        const float4 w4 = *reinterpret_cast<const float4*>(args.sgd_w + o);
+        const float4 a4 = *reinterpret_cast<const float4*>(args.sgd_h + o);
+        W[0] = w4.x; W[1] = w4.y; W[2] = w4.z; W[3] = w4.w;
+        A[0] = a4.x; A[1] = a4.y; A[2] = a4.z; A[3] = a4.w;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          W[r] = n + r < c_cols ? args.sgd_w[o + r] : 0.f;
+          A[r] = n + r < c_cols ? args.sgd_h[o + r] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float gg = v[r] * gscale;
+        gg += decay * ((args.sgd_flags & 2) ? (float)((W[r] > 0.f) - (W[r] < 0.f)) : W[r]);
+        const float prev = A[r];
+        A[r] = mom * A[r] + rate * gg;
+        W[r] -= (args.sgd_flags & 1) ? (1.f + mom) * A[r] - mom * prev : A[r];
+      }
+      if (vec) {
+        *reinterpret_cast<float4*>(args.sgd_w + o) = make_float4(W[0], W[1], W[2], W[3]);
+        *reinterpret_cast<float4*>(args.sgd_h + o) = make_float4(A[0], A[1], A[2], A[3]);
+        *reinterpret_cast<uint2*>(args.sgd_shadow + o) = make_uint2(pack2(W[0], W[1]), pack2(W[2], W[3]));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < c_cols) {
+            args.sgd_w[o + r] = W[r];
+            args.sgd_h[o + r] = A[r];
+            args.sgd_shadow[o + r] = f2bf(W[r]);
+          }
+      }
+      return;
+    }
+    float* C = reinterpret_cast<float*>(args.C) + split * args.c_split_stride + grp * args.c_gstride +
+               (long long)m * args.ldc;
+    if (full) {
+      float4* p = reinterpret_cast<float4*>(C + n);
+      if (EPI == EPI_F32_ACC) {
+        float4 o = *p;
+        *p = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+      } else {
+        *p = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < c_cols) {
+          if (EPI == EPI_F32_ACC)
+            C[n + r] += v[r];
+          else
+            C[n + r] = v[r];
+        }
+    }
+  }
+}
+
 template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, bool FP8 = false,
           int NFR = 4>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmArgs args) {
@@ -382,7 +537,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   using SB = GStager<BMC, BMODE, BNL, NW, ES>;
   SA sa;
   SB sb;
-  sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M);
+  sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, split * args.kchunk);
   const int n_lim = min(args.N, n_blk + BN);
   sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1);
 
@@ -530,121 +685,238 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
     for (int i = 0; i < NFR; ++i) {
       const int n = n_blk + wn0 + 16 * i + ncol_l;
       if (n >= args.N) continue;
-      const bool full = (n + 3 < c_cols) && ((args.ldc & 3) == 0);
-      f32x4 v = acc[i][j];
-      if (FP8) v = v * (args.deq_a[0] * args.deq_b[0]);  // per-tensor fp8 scales
-      if (EPI == EPI_BF16) {
-        bf16_t* C = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride + (long long)m * args.ldc;
-        float o[4] = {v[0], v[1], v[2], v[3]};
-        if (args.bias) {
-          const float* bz = args.bias + (long long)grp * args.N;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] += (n + r < args.N) ? bz[n + r] : 0.f;
-        }
-        if (args.relu) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
-        }
-        if (args.gate) {
-          const bf16_t* gp = args.gate + grp * args.c_gstride + (long long)m * args.ldc + n;
-          float gv[4];
-          if (full && (args.c_gstride & 3) == 0) {
-            const uint2 u = *reinterpret_cast<const uint2*>(gp);
-            gv[0] = __uint_as_float(u.x << 16);
-            gv[1] = __uint_as_float(u.x & 0xffff0000u);
-            gv[2] = __uint_as_float(u.y << 16);
-            gv[3] = __uint_as_float(u.y & 0xffff0000u);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) gv[r] = (n + r < args.N) ? bf2f(gp[r]) : 0.f;
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (!(gv[r] > 0.f)) o[r] = 0.f;
-        }
-        if (full) {
-          uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-          *reinterpret_cast<uint2*>(C + n) = pk;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < args.N) C[n + r] = f2bf(o[r]);
-        }
-      } else {
-        if (args.bias_out && n <= args.ones_col && args.ones_col < n + 4) {
-          const int r = args.ones_col - n;
-          const float bv = r == 0 ? v[0] : (r == 1 ? v[1] : (r == 2 ? v[2] : v[3]));
-          float* bp = args.bias_out + (long long)grp * args.M + m;
-          *bp = args.bias_acc ? *bp + bv : bv;
-        }
-        if (n >= c_cols) continue;
-        if (EPI == EPI_SGD) {
-          // H_LR = 0, H_MOM = 1, H_WD = 2, H_NORM = 4 (solver.hip); same op order as
-          // solver_update_kernel KIND 0 / 1 so both paths give identical weights
-          const float* hy = args.sgd_hyper;
-          const float rate = hy[0] * args.sgd_lr_mult, mom = hy[1], decay = hy[2] * args.sgd_decay_mult;
-          const float gscale = hy[4];
-          const long long o = grp * args.c_gstride + (long long)m * args.ldc + n;
-          const bool vec = (n + 3 < c_cols) && ((args.ldc & 3) == 0) && ((o & 3) == 0);
-          float W[4], A[4];
-          if (vec) {
-            const float4 w4 = *reinterpret_cast<const float4*>(args.sgd_w + o);
-            const float4 a4 = *reinterpret_cast<const float4*>(args.sgd_h + o);
-            W[0] = w4.x; W[1] = w4.y; W[2] = w4.z; W[3] = w4.w;
-            A[0] = a4.x; A[1] = a4.y; A[2] = a4.z; A[3] = a4.w;
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              W[r] = n + r < c_cols ? args.sgd_w[o + r] : 0.f;
-              A[r] = n + r < c_cols ? args.sgd_h[o + r] : 0.f;
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float gg = v[r] * gscale;
-            gg += decay * ((args.sgd_flags & 2) ? (float)((W[r] > 0.f) - (W[r] < 0.f)) : W[r]);
-            const float prev = A[r];
-            A[r] = mom * A[r] + rate * gg;
-            W[r] -= (args.sgd_flags & 1) ? (1.f + mom) * A[r] - mom * prev : A[r];
-          }
-          if (vec) {
-            *reinterpret_cast<float4*>(args.sgd_w + o) = make_float4(W[0], W[1], W[2], W[3]);
-            *reinterpret_cast<float4*>(args.sgd_h + o) = make_float4(A[0], A[1], A[2], A[3]);
-            *reinterpret_cast<uint2*>(args.sgd_shadow + o) = make_uint2(pack2(W[0], W[1]), pack2(W[2], W[3]));
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (n + r < c_cols) {
-                args.sgd_w[o + r] = W[r];
-                args.sgd_h[o + r] = A[r];
-                args.sgd_shadow[o + r] = f2bf(W[r]);
-              }
-          }
-          continue;
-        }
-        float* C = reinterpret_cast<float*>(args.C) + split * args.c_split_stride + grp * args.c_gstride +
-                   (long long)m * args.ldc;
-        if (full) {
-          float4* p = reinterpret_cast<float4*>(C + n);
-          if (EPI == EPI_F32_ACC) {
-            float4 o = *p;
-            *p = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
-          } else {
-            *p = make_float4(v[0], v[1], v[2], v[3]);
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < c_cols) {
-              if (EPI == EPI_F32_ACC)
-                C[n + r] += v[r];
-              else
-                C[n + r] = v[r];
-            }
-        }
-      }
+      epi_store<EPI, FP8>(args, grp, split, m, n, acc[i][j], c_cols);
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// gemm256_kernel: 256 x BN block tile (BN = 256 or 128), 8 waves (512 threads), one
+// block per CU, phased LDS-DMA pipeline with loads in flight ACROSS barriers.
+//
+// Each operand tile of a K-step (BK = 64) is staged as two halves (A: rows 0-127 /
+// 128-255, B: rows or columns 0..BN/2-1 / BN/2..BN-1), each its own swizzled LDS image
+// (same images and reads as gemm_kernel, at TILE = the half size).  A wave owns a
+// (2 x MF frags) x (2 x NF frags) sub-tile whose row / column halves come from the two
+// LDS halves, so one K-step is four phases over the quadrants (lo,lo) (lo,hi) (hi,hi)
+// (hi,lo): the A_lo / B_lo halves are read only in phase 1, B_hi only in phase 2 and
+// A_hi only in phase 3, and each half is re-filled (for the K-step two ahead) as soon as
+// every wave is past its last read.  The DMA issue stream is one half per phase:
+//      P1(t): A_hi(t+1)   P2(t): A_lo(t+2)   P3(t): B_lo(t+2)   P4(t): B_hi(t+2)
+// so every half is issued ~6 phases (1.5 K-steps of MFMA) before it is read, and each
+// phase waits with a COUNTED vmcnt for exactly the halves it reads (raw s_barrier, no
+// vmcnt(0) in the loop: cdna_hip_programming.md §5 "Pipelining across barriers", the
+// 256² template of §5).  Phase 4 reads nothing new and needs no barrier.  DMAs past the
+// last K-step read the zero page, which keeps the vmcnt arithmetic uniform.
+// ---------------------------------------------------------------------------------------
+// PH = 2 merges the phases pairwise: X = (lo,lo)+(lo,hi) reading A_lo, B_lo, B_hi and
+// Y = (hi,hi)+(hi,lo) reading A_hi; DMA stream X(t): A_hi(t+1), Y(t): A_lo, B_lo, B_hi of
+// t+2 — two barriers per K-step and twice the MFMAs behind each read burst.
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BN, int PH = 2>
+__global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
+  constexpr int BM = 256, HA = 128, HB = BN / 2, NW = 8;
+  constexpr int WM = BN == 256 ? 2 : 4, WN = NW / WM;
+  constexpr int MF = HA / (16 * WM), NF = HB / (16 * WN);  // 16-row frags per half
+  constexpr int A_HALF = HA * 128, B_HALF = HB * 128;     // bytes (KC and MC images alike)
+  constexpr int STAGE = 2 * A_HALF + 2 * B_HALF;
+  using SA = GStager<AMC, AMODE, HA, NW>;
+  using SB = GStager<BMC, BMODE, HB, NW>;
+  constexpr int H_A = SA::NI, H_B = SB::NI;  // DMA instructions per wave per half
+  constexpr int VM1 = 2 * H_A + 3 * H_B, VM23 = 3 * H_A + 2 * H_B;
+  static_assert(MF >= 1 && NF >= 1 && MF * 16 * WM == HA && NF * 16 * WN == HB, "wave layout");
+  static_assert(2 * STAGE <= 160 * 1024, "LDS");
+
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int wr = wv % WM, wc = wv / WM;
+
+  int bid = blockIdx.x;
+  const int nwg = gridDim.x;
+  if (nwg >= 16) {
+    int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  }
+  const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
+  const int tm = args.raster_n ? bid / tiles_n : bid % tiles_m;
+  const int tn = args.raster_n ? bid % tiles_n : bid / tiles_m;
+  const int m_blk = tm * BM, n_blk = tn * BN;
+  const int split = blockIdx.y, grp = blockIdx.z;
+  const int k0 = split * args.kchunk, k1 = min(args.K, k0 + args.kchunk);
+  const int nk = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
+  const int n_lim = min(args.N, n_blk + BN);
+  const int ones = BMC ? args.ones_col : -1;
+
+  SA sa_lo, sa_hi;
+  SB sb_lo, sb_hi;
+  sa_lo.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, k0);
+  sa_hi.init(args.A, grp, wv, lane, m_blk + HA, args.M, m_blk + HA, args.M, -1, k0);
+  sb_lo.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, ones);
+  sb_hi.init(args.B, grp, wv, lane, n_blk + HB, n_lim, n_blk + HB, n_lim, ones);
+
+  auto A_lo = [&](int b) { return smem + b * STAGE; };
+  auto A_hi = [&](int b) { return smem + b * STAGE + A_HALF; };
+  auto B_lo = [&](int b) { return smem + b * STAGE + 2 * A_HALF; };
+  auto B_hi = [&](int b) { return smem + b * STAGE + 2 * A_HALF + B_HALF; };
+  auto kt = [&](int t) { return k0 + t * BK; };
+  auto dma_a_lo = [&](int t) { sa_lo.issue(A_lo(t & 1), wv, kt(t), k1, m_blk, args.M); };
+  auto dma_a_hi = [&](int t) { sa_hi.issue(A_hi(t & 1), wv, kt(t), k1, m_blk + HA, args.M); };
+  auto dma_b_lo = [&](int t) { sb_lo.issue(B_lo(t & 1), wv, kt(t), k1, n_blk, n_lim); };
+  auto dma_b_hi = [&](int t) { sb_hi.issue(B_hi(t & 1), wv, kt(t), k1, n_blk + HB, n_lim); };
+
+  f32x4 acc[2][2][NF][MF];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < NF; ++i)
+#pragma unroll
+        for (int j = 0; j < MF; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t fa[2][MF], fbl[2][NF], fbh[2][NF];
+  auto read_a = [&](const char* base) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < MF; ++j) fa[s][j] = read_frag<AMC, HA>(base, wr * (MF * 16) + 16 * j, s, lane);
+  };
+  auto read_b = [&](bf16x8_t (&fb)[2][NF], const char* base) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < NF; ++i) fb[s][i] = read_frag<BMC, HB>(base, wc * (NF * 16) + 16 * i, s, lane);
+  };
+  auto mma = [&](f32x4 (&c)[NF][MF], const bf16x8_t (&fb)[2][NF]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < NF; ++i)
+#pragma unroll
+        for (int j = 0; j < MF; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][i], fa[s][j], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if (nk > 0) {
+    // prologue: K-step 0 whole, K-step 1 without A_hi (issued in P1(0))
+    dma_a_lo(0);
+    dma_b_lo(0);
+    dma_b_hi(0);
+    dma_a_hi(0);
+    dma_a_lo(1);
+    dma_b_lo(1);
+    dma_b_hi(1);
+    if constexpr (PH == 2) {
+      constexpr int VMX = 2 * H_A + 2 * H_B;
+      // prologue above also issued B_hi(1) and A_hi(0): the stream matches X/Y's
+      for (int t = 0; t < nk; ++t) {
+        const int b = t & 1;
+        // X: needs A_lo(t), B_lo(t), B_hi(t)
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(VMX));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        dma_a_hi(t + 1);
+        read_a(A_lo(b));
+        read_b(fbl, B_lo(b));
+        read_b(fbh, B_hi(b));
+        mma(acc[0][0], fbl);
+        mma(acc[0][1], fbh);
+        // Y: needs A_hi(t); A_lo / B_lo / B_hi of buffer b are free after this barrier
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(VMX));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        dma_a_lo(t + 2);
+        dma_b_lo(t + 2);
+        dma_b_hi(t + 2);
+        read_a(A_hi(b));
+        mma(acc[1][1], fbh);
+        mma(acc[1][0], fbl);
+      }
+    } else
+    for (int t = 0; t < nk; ++t) {
+      const int b = t & 1;
+      // P1: needs A_lo(t), B_lo(t)
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM1));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      dma_a_hi(t + 1);
+      read_a(A_lo(b));
+      read_b(fbl, B_lo(b));
+      mma(acc[0][0], fbl);
+      // P2: needs B_hi(t)
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM23));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      dma_a_lo(t + 2);
+      read_b(fbh, B_hi(b));
+      mma(acc[0][1], fbh);
+      // P3: needs A_hi(t)
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM23));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      dma_b_lo(t + 2);
+      read_a(A_hi(b));
+      mma(acc[1][1], fbh);
+      // P4: B_hi(b) was last read in P2, every wave is past P3's barrier
+      dma_b_hi(t + 2);
+      mma(acc[1][0], fbl);
+    }
+    // no LDS-DMA may still be landing when the workgroup retires
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+
+  const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
+  const int c_cols = (EPI != EPI_BF16 && args.bias_out) ? args.ones_col : args.N;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int j = 0; j < MF; ++j) {
+      const int m = m_blk + mh * HA + wr * (MF * 16) + 16 * j + mrow_l;
+      if (m >= args.M) continue;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+          const int n = n_blk + nh * HB + wc * (NF * 16) + 16 * i + ncol_l;
+          if (n >= args.N) continue;
+          epi_store<EPI, false>(args, grp, split, m, n, acc[mh][nh][i][j], c_cols);
+        }
+    }
+}
+
+template <int AMC, int AMODE, int BMC, int BMODE, int BN, int PH>
+int launch256_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
+  switch (a.epi) {
+    case EPI_BF16:
+      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BN, PH>), grid, dim3(512), 0, st, a);
+      break;
+    case EPI_F32:
+      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BN, PH>), grid, dim3(512), 0, st, a);
+      break;
+    case EPI_F32_ACC:
+      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BN, PH>), grid, dim3(512), 0, st, a);
+      break;
+    default:
+      return 2;
+  }
+  return SN_CHECK_LAUNCH();
+}
+
+template <int BN, int PH = 2>
+int launch256(const SnGemmArgs& a, hipStream_t stream) {
+  const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, a.splits, a.groups);
+  const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  switch (key) {
+    case 0b0000: return launch256_epi<0, OP_DENSE, 0, OP_DENSE, BN, PH>(a, grid, stream);   // NT dense
+    case 0b0100: return launch256_epi<0, OP_IM2COL, 0, OP_DENSE, BN, PH>(a, grid, stream);  // conv fwd / dgrad
+    case 0b0010: return launch256_epi<0, OP_DENSE, 1, OP_DENSE, BN, PH>(a, grid, stream);   // NN dense
+    case 0b1010: return launch256_epi<1, OP_DENSE, 1, OP_DENSE, BN, PH>(a, grid, stream);   // TN dense
+    case 0b1011: return launch256_epi<1, OP_DENSE, 1, OP_IM2COL, BN, PH>(a, grid, stream);  // conv wgrad
+    default: break;
+  }
+  return 4;
 }
 
 template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS, int NFR = 4>
@@ -766,6 +1038,10 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 3: return launch_tile<128, 256, 8, 3>(a, stream);
     case 4: return launch_tile96(a, stream);
     case 5: return launch_tile48(a, stream);
+    case 6: return a.epi == EPI_SGD ? 4 : launch256<256>(a, stream);  // 8 waves, phased DMA pipeline
+    case 7: return a.epi == EPI_SGD ? 4 : launch256<128>(a, stream);
+    case 8: return a.epi == EPI_SGD ? 4 : launch256<256, 4>(a, stream);  // 4-phase variant (A/B probes)
+    case 9: return a.epi == EPI_SGD ? 4 : launch256<128, 4>(a, stream);
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

@@ -15,6 +15,7 @@
 from __future__ import annotations
 
 import logging
+import os
 import time
 
 import torch
@@ -433,6 +434,11 @@ class GraphStep:
         self.n_streams = streams if not solver.net.debug_info else 1
         self.branches = None
         self._use_branches = False
+        # weight gradients (+ fused FC updates) on a side stream during backward
+        # (ops.hip.WgradStream); like the branch streams, not in the autotuning iteration
+        self.wgrad_stream = None
+        self.use_wgrad_stream = (os.environ.get("SN_WGRAD_STREAM", "0") == "1" and solver.device.type == "cuda"
+                                 and not solver.net.debug_info)
 
     def _body(self):
         s = self.solver
@@ -442,8 +448,18 @@ class GraphStep:
             self.overlap.begin()
         if self._use_branches and self.branches is None:
             self.branches = branch_streams(net, self.n_streams) or False
-        loss = (self.branches.forward_backward() if self._use_branches and self.branches
-                else net.forward_backward())
+        side_wgrad = self.use_wgrad_stream and self._use_branches
+        if side_wgrad:
+            from .ops import hip
+            if self.wgrad_stream is None:
+                self.wgrad_stream = torch.cuda.Stream(s.device)
+            hip.WgradStream.begin(self.wgrad_stream)
+        try:
+            loss = (self.branches.forward_backward() if self._use_branches and self.branches
+                    else net.forward_backward())
+        finally:
+            if side_wgrad:
+                hip.WgradStream.join()
         net.finish_param_diffs()
         fp8_step(net)
         ops.advance_rng(net.ctx.rng_state)

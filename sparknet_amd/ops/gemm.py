@@ -104,9 +104,14 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
     return s, 0 if op.kcontig else 1, OP_IM2COL
 
 
-TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48)}
+TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
+         6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128)}
+# gemm256_kernel tiles (6, 7) run one 512-thread block per CU
+_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256}
+_KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1}
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
 _RASTER_N = int(os.environ.get("SN_GEMM_RASTER_N", "-1"))  # -1: heuristic
+_TILE256 = os.environ.get("SN_GEMM_TILE256", "1") != "0"  # autotune candidates 6 / 7 (gemm256_kernel)
 
 
 def choose_tile(M: int, N: int, b_kcontig: bool = False) -> int:
@@ -127,11 +132,11 @@ BLOCK_OVERHEAD = 4   # prologue + epilogue of a block, in k-steps
 REDUCE_BW = 5e12     # split-K slab read+write, bytes/s effective (+ one launch)
 
 
-def _cost(tiles: int, ktiles: int, s: int, out_elems: int) -> float:
+def _cost(tiles: int, ktiles: int, s: int, out_elems: int, tile: int = 0) -> float:
     """Modelled microseconds of a GEMM split s ways: whole waves of SLOTS blocks (a wave
     that is 1 % full costs a full block time) plus the slab reduction."""
     kt = -(-ktiles // s)
-    t = -(-tiles * s // SLOTS) * (kt + BLOCK_OVERHEAD) * KTILE_US
+    t = -(-tiles * s // _SLOTS.get(tile, SLOTS)) * (kt + BLOCK_OVERHEAD) * _KTILE_US.get(tile, KTILE_US)
     if s > 1:
         t += (out_elems * 4.0 * (s + 1)) / REDUCE_BW * 1e6 + 3.0
     return t
@@ -145,9 +150,9 @@ def choose_splits(M: int, N: int, K: int, groups: int = 1, tile: int = 0) -> tup
     ktiles = -(-K // BK)
     ws_cap = max(1, (256 << 20) // max(1, 4 * M * N * groups))  # fp32 partial slabs <= 256 MB
     smax = max(1, min(256, ktiles // 4, ws_cap))
-    best, best_t = 1, _cost(tiles, ktiles, 1, M * N * groups)
+    best, best_t = 1, _cost(tiles, ktiles, 1, M * N * groups, tile)
     for s in range(2, smax + 1):
-        t = _cost(tiles, ktiles, s, M * N * groups)
+        t = _cost(tiles, ktiles, s, M * N * groups, tile)
         if t < best_t * 0.98:
             best, best_t = s, t
     kchunk = -(-K // best)
@@ -263,6 +268,10 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
     tiles = [0, 1, 2]
     if N >= 256:
         tiles.append(3)
+    if epi != EPI_SGD and _TILE256 and M >= 256:
+        tiles.append(7)
+        if N > 128:
+            tiles.append(6)
     if epi != EPI_SGD:
         if b_kc_dense and N % 96 == 0:
             tiles.append(4)

@@ -7,7 +7,9 @@ channel counts are not multiples of 8).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import os
 
 import torch
 
@@ -23,6 +25,48 @@ DGRAD_INPLACE_WEIGHTS = False  # conv dgrad: read W via the FLIPW operand instea
 
 def _c(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous() else t.contiguous()
+
+
+class WgradStream:
+    """Weight gradients on a side stream.  A weight gradient (and, for fused InnerProduct
+    layers, the solver update in its epilogue) feeds nothing later in backward, so while
+    it is enabled conv / InnerProduct backward issue it on ``stream`` — forked from the
+    main stream at that point — and the data gradient (the critical path) continues on
+    the main stream concurrently: tail waves of one GEMM fill with the other, and the
+    bandwidth-bound fused FC update overlaps compute-bound conv backward.  ``join()``
+    (before the param-diff finish / solver update) makes the main stream wait for it.
+    Star topology only (the side stream waits on the main stream alone): layers already
+    running on a BranchStreams side stream keep their wgrad inline.  Tensors the side
+    work reads (activations, top diffs) stay referenced by their blobs until the join."""
+    stream = None
+    main = None
+    used = False
+
+    @classmethod
+    def begin(cls, stream) -> None:
+        cls.stream, cls.main, cls.used = stream, torch.cuda.current_stream(stream.device), False
+
+    @classmethod
+    def join(cls) -> None:
+        if cls.stream is not None and cls.used:
+            cls.main.wait_stream(cls.stream)
+        cls.stream = cls.main = None
+        cls.used = False
+
+
+_WGRAD_KINDS = os.environ.get("SN_WGRAD_KINDS", "conv,fc,fcsgd").split(",")
+
+
+@contextlib.contextmanager
+def wgrad_side(kind: str = "conv"):
+    ss = WgradStream.stream
+    if ss is None or kind not in _WGRAD_KINDS or torch.cuda.current_stream(ss.device) != WgradStream.main:
+        yield
+        return
+    ss.wait_stream(WgradStream.main)
+    WgradStream.used = True
+    with torch.cuda.stream(ss):
+        yield
 
 
 def as_bf16(t: torch.Tensor | None) -> torch.Tensor | None:
@@ -203,6 +247,14 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
     # paths; otherwise (no dw, explicit im2col) it is a separate column sum
     fused_db = db is not None and dw is not None and (
         plan is not None or (_implicit_ok(s) and s.Kg % 8 == 0))
+    with wgrad_side():
+        _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc)
+    if not need_dx:
+        return None
+    return _conv_dgrad(dy, x, w, s, M, gate, ws)
+
+
+def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc):
     if db is not None and not fused_db:
         colsum(dy2, db, accumulate=db_acc)
     if dw is not None and plan is not None:
@@ -239,8 +291,10 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
                     dw2[g * s.Kg:(g + 1) * s.Kg].add_(tmp[:s.Kg, :kred])
                 else:
                     dw2[g * s.Kg:(g + 1) * s.Kg].copy_(tmp[:s.Kg, :kred])
-    if not need_dx:
-        return None
+
+
+def _conv_dgrad(dy, x, w, s, M, gate, ws):
+    dy2 = dy.view(M, s.K)
     dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
     if s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0:
         # dgrad == forward conv of dy with flipped / transposed weights, pad' = R-1-pad.
@@ -291,12 +345,13 @@ def linear_forward(x2, w, b, relu=False):
 
 def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=True, db_acc=True):
     dy2 = _c(dy2)
-    if dw is not None:
-        # the bias gradient comes out of the weight-gradient GEMM when it can (ones column)
-        if not linear_wgrad(dy2, _c(x2), dw, accumulate=dw_acc, db=db, db_acc=db_acc) and db is not None:
+    with wgrad_side("fc"):
+        if dw is not None:
+            # the bias gradient comes out of the weight-gradient GEMM when it can (ones column)
+            if not linear_wgrad(dy2, _c(x2), dw, accumulate=dw_acc, db=db, db_acc=db_acc) and db is not None:
+                colsum(dy2, db, accumulate=db_acc)
+        elif db is not None:
             colsum(dy2, db, accumulate=db_acc)
-    elif db is not None:
-        colsum(dy2, db, accumulate=db_acc)
     if not need_dx:
         return None
     return linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)
@@ -311,8 +366,9 @@ def linear_backward_sgd(dy2, x2, w, need_dx, sgd, db=None, gate=None, db_acc=Tru
     if need_dx:
         dx = linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)
     from .gemm import linear_wgrad_sgd
-    if not linear_wgrad_sgd(dy2, x2, sgd, db, db_acc) and db is not None:
-        colsum(dy2, db, accumulate=db_acc)
+    with wgrad_side("fcsgd"):  # forked after the dgrad: the update overwrites w
+        if not linear_wgrad_sgd(dy2, x2, sgd, db, db_acc) and db is not None:
+            colsum(dy2, db, accumulate=db_acc)
     return dx
 
 

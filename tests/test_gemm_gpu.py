@@ -158,3 +158,72 @@ def test_fp8_conv_forward(gpu, case):
     ref = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), stride=st, padding=pd, groups=g) * (0.5 * 0.0625)
     _close(y.permute(0, 3, 1, 2), ref, 1e-2)
 
+
+
+# --- gemm256_kernel (tiles 6 = 256x256, 7 = 256x128): every operand layout, ragged edges,
+# short and long K (the phased DMA pipeline issues zero-page DMAs past the last K-step),
+# split-K, the bias-gradient column and the implicit-GEMM convolutions
+@pytest.mark.parametrize("tile", [6, 7])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 200, 136), (1000, 384, 2304), (513, 129, 1000), (64, 48, 40)])
+def test_gemm256_layouts(gpu, tile, M, N, K, monkeypatch):
+    from sparknet_amd.ops import gemm as G
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    x, w = _bf(M, K, device=gpu), _bf(N, K, device=gpu)
+    b = torch.randn(N, device=gpu)
+    _close(G.linear_fwd(x, w, b, relu=True), torch.relu(x.float() @ w.float().t() + b))
+    dy = _bf(M, N, device=gpu)
+    w2 = _bf(N, K, device=gpu)
+    _close(G.linear_dgrad(dy, w2), dy.float() @ w2.float())
+    dw = torch.ones(N, K, device=gpu)
+    G.linear_wgrad(dy, x, dw, accumulate=True)
+    _close(dw, 1 + dy.float().t() @ x.float())
+
+
+@pytest.mark.parametrize("tile", [6, 7])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm256_bias_column_and_splitk(gpu, tile, splits, monkeypatch):
+    from sparknet_amd.ops import gemm as G
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    M, N, K = 96, 432, 64 * 40 + 17
+    a, bm = _bf(K, M, device=gpu), _bf(K, N, device=gpu)
+    dw = torch.full((M, N), 3.0, device=gpu)
+    db = torch.full((M,), -2.0, device=gpu)
+    G.gemm(M, N, K, G.Dense(a, M, False), G.Dense(bm, N, False), dw, N, epi=G.EPI_F32_ACC, splits=splits,
+           bias_grad=db, bias_acc=True)
+    _close(dw, 3.0 + a.float().t() @ bm.float(), 1e-2)
+    _close(db, -2.0 + a.float().sum(0), 1e-3)
+    x, w = _bf(M * 3, K, device=gpu), _bf(N, K, device=gpu)
+    y = torch.empty(M * 3, N, device=gpu, dtype=torch.bfloat16)
+    gate = _bf(M * 3, N, device=gpu)
+    G.gemm(M * 3, N, K, G.Dense(_pad(x), 64 * 41, True), G.Dense(_pad(w), 64 * 41, True), y, N, epi=G.EPI_BF16,
+           splits=splits, gate=gate)
+    _close(y, (x.float() @ w.float().t()) * (gate.float() > 0))
+
+
+def _pad(t):
+    out = torch.zeros(t.shape[0], 64 * 41, dtype=t.dtype, device=t.device)
+    out[:, :t.shape[1]] = t
+    return out
+
+
+@pytest.mark.parametrize("tile", [6, 7])
+@pytest.mark.parametrize("case", [(2, 13, 13, 64, 384, 3, 3, 1, 1, 1), (2, 27, 27, 96, 256, 5, 5, 1, 2, 2),
+                                  (4, 14, 14, 32, 128, 1, 1, 1, 0, 1), (3, 9, 9, 64, 40, 3, 3, 1, 1, 2)])
+def test_gemm256_conv(gpu, tile, case, monkeypatch):
+    from sparknet_amd.ops import gemm as G, hip, ref
+    from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    N, H, W, Cc, K, R, S, st, pd, g = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    x = _bf(N, H, W, Cc, device=gpu)
+    w = (torch.randn(K, R, S, Cc // g, device=gpu) * 0.1).to(torch.bfloat16)
+    bias = torch.randn(K, device=gpu)
+    _close(hip.conv_forward(x, w, bias, s, relu=True), ref.conv_forward(x, w, bias, s, relu=True))
+    dy = _bf(N, s.P, s.Q, K, device=gpu)
+    dw, db = torch.zeros(K, R, S, Cc // g, device=gpu), torch.zeros(K, device=gpu)
+    dw_r, db_r = torch.zeros_like(dw), torch.zeros_like(db)
+    dx = hip.conv_backward(dy, x, w, s, True, dw, db)
+    dx_r = ref.conv_backward(dy, x, w, s, True, dw_r, db_r)
+    _close(dx, dx_r)
+    _close(dw, dw_r)
+    _close(db, db_r, 1e-3)
