@@ -158,23 +158,32 @@ struct GStager {
   // no 64-bit address arithmetic per lane).
   int nr, ns, nc;
   i32x4 rsrc;
+  // MC+IM2COL: decode (n, p, q) of this lane's instruction-0 row pixel for the NEXT tile
+  // (advanced by BK pixels per issue; rows of instruction j are RPI pixels further on),
+  // per-instruction column terms, and whether this wave holds a ones-column lane (then it
+  // stages through global loads and the ones page; otherwise through the buffer resource)
+  int sn_, sp_, sq_;
+  int cdh[MC ? NI : 1], cdw[MC ? NI : 1], colo[MC ? NI : 1];
+  bool wave_has_one;
 
   SN_DEV void init(const SnOperand& op, int grp, int wave, int lane, int tile_row0, int rows_lim,
                    int tile_col0, int cols_lim, int ones = -1, int k_start = 0) {
     ld = op.ld;
     g = op.g;
     ones_col = ones;
-    if (MODE == OP_IM2COL && !MC) {
-      const int tap = k_start / g.Cg;
-      nc = k_start - tap * g.Cg;
-      nr = tap / g.S;
-      ns = tap - nr * g.S;
+    if (MODE == OP_IM2COL) {
       const unsigned long long a = reinterpret_cast<unsigned long long>(op.ptr);
       const unsigned nbytes = (unsigned)((unsigned long long)g.N * g.H * g.W * g.C * ES);
       rsrc[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
       rsrc[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffffu));
       rsrc[2] = __builtin_amdgcn_readfirstlane((int)nbytes);
       rsrc[3] = 0x00020000;
+    }
+    if (MODE == OP_IM2COL && !MC) {
+      const int tap = k_start / g.Cg;
+      nc = k_start - tap * g.Cg;
+      nr = tap / g.S;
+      ns = tap - nr * g.S;
     }
     if (MODE != OP_IM2COL) {
       base = reinterpret_cast<const char*>(op.ptr) + (long long)grp * op.gstride * ES;
@@ -211,7 +220,21 @@ struct GStager {
         cc[j] = col - tap * g.Cg;
         cr[j] = tap / g.S;
         cs[j] = tap - cr[j] * g.S;
+        cdh[j] = cr[j] * g.dh;
+        cdw[j] = cs[j] * g.dw;
+        colo[j] = (cdh[j] * g.W + cdw[j]) * g.C + coff + cc[j];
       }
+    }
+    if (MODE == OP_IM2COL && MC) {
+      const int PQ = g.P * g.Q, pix = k_start + rr[0];
+      sn_ = fdiv(pix, PQ, invPQ);
+      const int pq = pix - sn_ * PQ;
+      sp_ = fdiv(pq, g.Q, invQ);
+      sq_ = pq - sp_ * g.Q;
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) any = any || co[j];
+      wave_has_one = __ballot(any) != 0ull;
     }
   }
 
@@ -308,17 +331,45 @@ struct GStager {
           dma(base + off * 2, v, dst + j * 1024);
         }
       } else {
-        const int PQ = g.P * g.Q;
+        // rows = pixels: walk the lane's pixel (n, p, q) by RPI per instruction instead of
+        // two divisions per instruction; offsets are 32-bit (host: < 2^31 elements)
+        int n = sn_, p = sp_, q = sq_;
+        int off[NI];
+        bool val[NI];
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          int pix = k_tile + rr[j];
-          int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
-          int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
-          int h = p * g.sh - g.ph + cr[j] * g.dh;
-          int w = q * g.sw - g.pw + cs[j] * g.dw;
-          bool v = cv[j] && pix < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          long long off = ((long long)(n * g.H + h) * g.W + w) * g.C + coff + cc[j];
-          dma(base + off * 2, v, dst + j * 1024, co[j] && pix < k_lim);
+          if (j > 0) {
+            q += RPI;
+            while (q >= g.Q) {
+              q -= g.Q;
+              ++p;
+            }
+            while (p >= g.P) {
+              p -= g.P;
+              ++n;
+            }
+          }
+          const int hrow = p * g.sh - g.ph, wrow = q * g.sw - g.pw;
+          val[j] = cv[j] && k_tile + rr[j] < k_lim && (unsigned)(hrow + cdh[j]) < (unsigned)g.H &&
+                   (unsigned)(wrow + cdw[j]) < (unsigned)g.W;
+          off[j] = ((n * g.H + hrow) * g.W + wrow) * g.C + colo[j];
+        }
+        if (!wave_has_one) {
+#pragma unroll
+          for (int j = 0; j < NI; ++j) dma_buf(val[j] ? (unsigned)off[j] * 2u : 0xffffffffu, dst + j * 1024);
+        } else {
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            dma(base + (long long)off[j] * 2, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
+        }
+        // next tile: BK pixels on
+        sq_ += BK;
+        const int dp = fdiv(sq_, g.Q, invQ);
+        sq_ -= dp * g.Q;
+        sp_ += dp;
+        while (sp_ >= g.P) {
+          sp_ -= g.P;
+          ++sn_;
         }
       }
     }
@@ -539,7 +590,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   SB sb;
   sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, split * args.kchunk);
   const int n_lim = min(args.N, n_blk + BN);
-  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1);
+  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1, split * args.kchunk);
 
   f32x4 acc[NFR][4];
 #pragma unroll
@@ -751,8 +802,8 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
   SB sb_lo, sb_hi;
   sa_lo.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, k0);
   sa_hi.init(args.A, grp, wv, lane, m_blk + HA, args.M, m_blk + HA, args.M, -1, k0);
-  sb_lo.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, ones);
-  sb_hi.init(args.B, grp, wv, lane, n_blk + HB, n_lim, n_blk + HB, n_lim, ones);
+  sb_lo.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, ones, k0);
+  sb_hi.init(args.B, grp, wv, lane, n_blk + HB, n_lim, n_blk + HB, n_lim, ones, k0);
 
   auto A_lo = [&](int b) { return smem + b * STAGE; };
   auto A_hi = [&](int b) { return smem + b * STAGE + A_HALF; };
