@@ -575,11 +575,16 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   // raster: M-fastest by default; N-fastest (args.raster_n) when a few N tiles share a tall A
   // panel (conv fwd / dgrad: pixels x channels) so its N tiles run together and the panel
   // is read from HBM once and from L2 for the others.
+  // The grid is 1-D over (tile, split, group), tile fastest: after the remap the tiles of
+  // one split / group (which share the A panel of that K range, e.g. a weight gradient's
+  // dy chunk read by every N tile) are contiguous and so run on one XCD and its L2.
   const int tiles_n = (args.N + BN - 1) / BN;
-  const int tm = args.raster_n ? bid / tiles_n : bid % tiles_m;
-  const int tn = args.raster_n ? bid % tiles_n : bid / tiles_m;
+  const int tiles = tiles_m * tiles_n;
+  const int tile = bid % tiles, rest = bid / tiles;
+  const int split = rest % args.splits, grp = rest / args.splits;
+  const int tm = args.raster_n ? tile / tiles_n : tile % tiles_m;
+  const int tn = args.raster_n ? tile % tiles_n : tile / tiles_m;
   const int m_blk = tm * BM, n_blk = tn * BN;
-  const int split = blockIdx.y, grp = blockIdx.z;
   const int k0 = split * args.kchunk;
   const int k1 = min(args.K, k0 + args.kchunk);
 
@@ -789,10 +794,12 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
     bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   }
   const int tiles_m = (args.M + BM - 1) / BM, tiles_n = (args.N + BN - 1) / BN;
-  const int tm = args.raster_n ? bid / tiles_n : bid % tiles_m;
-  const int tn = args.raster_n ? bid % tiles_n : bid / tiles_m;
+  const int tiles = tiles_m * tiles_n;  // 1-D grid over (tile, split, group), as gemm_kernel
+  const int tile = bid % tiles, rest = bid / tiles;
+  const int split = rest % args.splits, grp = rest / args.splits;
+  const int tm = args.raster_n ? tile / tiles_n : tile % tiles_m;
+  const int tn = args.raster_n ? tile % tiles_n : tile / tiles_m;
   const int m_blk = tm * BM, n_blk = tn * BN;
-  const int split = blockIdx.y, grp = blockIdx.z;
   const int k0 = split * args.kchunk, k1 = min(args.K, k0 + args.kchunk);
   const int nk = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
   const int n_lim = min(args.N, n_blk + BN);
@@ -957,7 +964,7 @@ int launch256_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
 template <int BN, int PH = 2>
 int launch256(const SnGemmArgs& a, hipStream_t stream) {
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles, a.splits, a.groups);
+  dim3 grid(tiles * a.splits * a.groups);
   const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
   switch (key) {
     case 0b0000: return launch256_epi<0, OP_DENSE, 0, OP_DENSE, BN, PH>(a, grid, stream);   // NT dense
@@ -994,7 +1001,7 @@ int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
 template <int BM, int BN, int NW, int NS>
 int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles, a.splits, a.groups);
+  dim3 grid(tiles * a.splits * a.groups);
   const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
   if (a.epi == EPI_SGD) {  // fused solver update: InnerProduct weight gradient (TN dense) only
     if (key != 0b1010 || a.splits != 1 || !a.sgd_w || !a.sgd_h || !a.sgd_shadow || !a.sgd_hyper) return 6;
@@ -1021,7 +1028,7 @@ int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
 // The 96-row B image has 12-chunk MC rows, so only K-contiguous (KC) B operands.
 int launch_tile96(const SnGemmArgs& a, hipStream_t stream) {
   const int tiles = ((a.M + 127) / 128) * ((a.N + 95) / 96);
-  dim3 grid(tiles, a.splits, a.groups);
+  dim3 grid(tiles * a.splits * a.groups);
   if (a.b_mc || a.b_mode != OP_DENSE) return 4;
   if (a.a_mc == 0 && a.a_mode == OP_IM2COL) return launch_epi<0, OP_IM2COL, 0, OP_DENSE, 128, 96, 4, 2, 3>(a, grid, stream);
   if (a.a_mc == 0 && a.a_mode == OP_DENSE) return launch_epi<0, OP_DENSE, 0, OP_DENSE, 128, 96, 4, 2, 3>(a, grid, stream);
@@ -1034,7 +1041,7 @@ int launch_tile96(const SnGemmArgs& a, hipStream_t stream) {
 template <int NS_ = 2>
 int launch_tile48(const SnGemmArgs& a, hipStream_t stream) {
   const int tiles = ((a.M + 255) / 256) * ((a.N + 47) / 48);
-  dim3 grid(tiles, a.splits, a.groups);
+  dim3 grid(tiles * a.splits * a.groups);
   const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
   switch (key) {
     case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, 256, 48, 4, NS_, 3>(a, grid, stream);
@@ -1079,7 +1086,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || a.a_mc || a.b_mc || a.b_mode != OP_DENSE || !a.deq_a || !a.deq_b)
       return 3;
     const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    dim3 grid(tiles, a.splits, a.groups);
+    dim3 grid(tiles * a.splits * a.groups);
     return a.a_mode == OP_IM2COL ? launch_fp8<OP_IM2COL>(a, grid, stream) : launch_fp8<OP_DENSE>(a, grid, stream);
   }
   if (a.kchunk <= 0 || (a.kchunk % BK) != 0) return 3;
