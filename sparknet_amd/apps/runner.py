@@ -78,6 +78,8 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
     """``train_data`` / ``test_data``: (uint8 NCHW tensor, int labels) for THIS rank, or
     None for synthetic batches of ``data_shape`` (C, H, W)."""
     rank, world, dev, comm = setup(args)
+    if callable(mean):  # e.g. a streamed, all-reduced mean image (ImageNetApp)
+        mean = mean(comm)
     log = TrainingLog(args.log_dir, rank, name=log_name)
     C, H, W = data_shape
     kw = dict(train_batch=args.batch, test_batch=args.test_batch)
@@ -105,8 +107,8 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
         log.log(f"resumed from {args.resume} at round {start_round}")
 
     from ..data.native import NativeLoader
-    if isinstance(train_data, NativeLoader):
-        src = train_data
+    if isinstance(train_data, (NativeLoader, HostBatchSource)):
+        src = train_data  # native loader / streaming JPEG ring (data.stream)
     elif train_data is not None:
         src = WindowedSource(train_data[0], train_data[1], args.batch, args.tau, seed=args.seed * 101 + rank)
     else:
@@ -115,7 +117,10 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
     feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
                           scale=scale, mirror=mirror, train=True, rng_state=net.ctx.rng_state, device=dev)
     tn = solver.test_nets[0]
-    if test_data is not None:
+    if isinstance(test_data, HostBatchSource):
+        tsrc = test_data
+        n_test = max(1, int(getattr(args, "test_batches", 0) or 10))
+    elif test_data is not None:
         tsrc = ListSource(test_data[0], test_data[1], args.test_batch)
         n_test = tsrc.n
     else:

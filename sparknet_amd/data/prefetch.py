@@ -161,8 +161,12 @@ class DeviceFeeder:
                 ev.record(self.copy_stream)
             self.events[slot] = ev
         else:
+            ev = None
             dx.copy_(x)
             dy.copy_(y)
+        done = getattr(self.source, "submitted", None)  # ring sources recycle x after the copy
+        if done is not None:
+            done(x, ev)
         self._pending = slot
         self.k += 1
 
