@@ -108,6 +108,23 @@ SN_DEV uint4 philox4x32(uint2 key, uint4 ctr) {
   return ctr;
 }
 
+// Dropout keep decisions (Philox4x32-10 keyed by the net's seed; counter = (e / 4, layer
+// stream, per-iteration counter); element e uses output word e % 4, so one Philox call
+// covers 4 consecutive elements.  dropout_layer.cu draws one curand uniform per element
+// instead.)  Shared by dropout_kernel and the fused GEMM / split-K epilogues, which must
+// draw identical masks.
+SN_DEV uint4 dropout_bits4(const long long* rng, int stream, unsigned long long e4) {
+  const unsigned long long seed = (unsigned long long)rng[0], counter = (unsigned long long)rng[1];
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint4 ctr = make_uint4((uint32_t)e4, (uint32_t)(e4 >> 32) | ((uint32_t)(stream & 0xffff) << 16),
+                               (uint32_t)counter, (uint32_t)(counter >> 32));
+  return philox4x32(key, ctr);
+}
+SN_DEV uint32_t pick4(uint4 u, int k) { return k == 0 ? u.x : (k == 1 ? u.y : (k == 2 ? u.z : u.w)); }
+SN_DEV bool dropout_keep(const long long* rng, int stream, unsigned thr, unsigned long long e) {
+  return pick4(dropout_bits4(rng, stream, e >> 2), (int)(e & 3)) > thr;
+}
+
 #define SN_CHECK_LAUNCH() (hipGetLastError() == hipSuccess ? 0 : 1)
 
 static inline int sn_blocks(long long n, int per_block, int cap = 65535 * 8) {

@@ -64,26 +64,21 @@ extern "C" int sn_relu_bwd(const bf16_t* dy, const bf16_t* x, bf16_t* dx, long l
 }
 
 // ---------------- Dropout ----------------
-// keep(i) = philox(key=seed, ctr=(i_lo, i_hi | stream<<16, counter_lo, counter_hi)).x > thr
+// keep(i) = word i%4 of philox(key=seed, ctr=(i/4 lo, i/4 hi | stream<<16, counter lo, hi)) > thr
 // gate (optional, backward only): the in-place ReLU output feeding this dropout — its
 // slope-0 backward mask (gate > 0) is applied here instead of in a separate pass.
 __global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n,
                                const long long* __restrict__ rng, int stream, uint32_t thr, float scale,
                                const bf16_t* __restrict__ gate) {
-  const unsigned long long seed = (unsigned long long)rng[0];
-  const unsigned long long counter = (unsigned long long)rng[1];
-  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-  auto keep = [&](unsigned long long e) {
-    uint4 ctr = make_uint4((uint32_t)e, (uint32_t)(e >> 32) | ((uint32_t)(stream & 0xffff) << 16),
-                           (uint32_t)counter, (uint32_t)(counter >> 32));
-    return philox4x32(key, ctr).x > thr;
-  };
+  auto keep = [&](unsigned long long e) { return dropout_keep(rng, stream, thr, e); };
   const long long n8 = n / 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     float f[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+    const uint4 u0 = dropout_bits4(rng, stream, (unsigned long long)i * 2), u1 = dropout_bits4(rng, stream, (unsigned long long)i * 2 + 1);
+    const uint32_t b[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) f[k] = keep((unsigned long long)(i * 8 + k)) ? f[k] * scale : 0.f;
+    for (int k = 0; k < 8; ++k) f[k] = b[k] > thr ? f[k] * scale : 0.f;
     if (gate) {
       float gv[8];
       unpack8(reinterpret_cast<const uint4*>(gate)[i], gv);

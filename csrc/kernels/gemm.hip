@@ -38,7 +38,11 @@ constexpr int BK = 64, NTHR = 256;
 // row k = tap * Kg + kout, col = c  ->  W[g*Kg + kout][R-1-r][S-1-s][c]  (flipped taps,
 // transposed channels) with geometry fields R, S, Cg and C := Kg — no flip pass over W.
 enum { OP_DENSE = 0, OP_IM2COL = 1, OP_FLIPW = 2 };
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_SGD = 3 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_SGD = 3, EPI_BF16_DROP = 4 };
+// EPI_BF16_DROP: EPI_BF16 + the fused Dropout forward (its own instantiations, so the
+// Philox code does not weigh on every bf16 epilogue)
+template <int EPI>
+constexpr bool epi_bf16() { return EPI == EPI_BF16 || EPI == EPI_BF16_DROP; }
 
 }  // namespace
 
@@ -94,6 +98,16 @@ struct SnGemmArgs {
   const float* sgd_hyper;
   float sgd_lr_mult, sgd_decay_mult;
   int sgd_flags;
+  // EPI_BF16 extras: fused Dropout forward (Philox keep mask of element index
+  // grp * c_gstride + m * ldc + n — the same mask dropout_kernel draws for that blob, so the
+  // standalone backward could regenerate it) applied after bias / ReLU, and a scale on the
+  // gated values (a fused Dropout backward: gate = the dropout output, > 0 exactly where
+  // the ReLU passed and the element was kept, times 1 / (1 - ratio)).
+  const long long* drop_rng;  // null: no dropout
+  int drop_stream;
+  unsigned drop_thr;
+  float drop_scale;
+  float gate_scale;
 };
 
 }  // extern "C"
@@ -430,7 +444,7 @@ template <int EPI, bool FP8>
 SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, f32x4 v, int c_cols) {
   const bool full = (n + 3 < c_cols) && ((args.ldc & 3) == 0);
   if (FP8) v = v * (args.deq_a[0] * args.deq_b[0]);  // per-tensor fp8 scales
-  if (EPI == EPI_BF16) {
+  if (epi_bf16<EPI>()) {
     bf16_t* C = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride + (long long)m * args.ldc;
     float o[4] = {v[0], v[1], v[2], v[3]};
     if (args.bias) {
@@ -456,8 +470,21 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
         for (int r = 0; r < 4; ++r) gv[r] = (n + r < args.N) ? bf2f(gp[r]) : 0.f;
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (!(gv[r] > 0.f)) o[r] = 0.f;
+      for (int r = 0; r < 4; ++r) o[r] = gv[r] > 0.f ? o[r] * args.gate_scale : 0.f;
+    }
+    if (EPI == EPI_BF16_DROP) {
+      const long long e0 = grp * args.c_gstride + (long long)m * args.ldc + n;
+      if ((e0 & 3) == 0) {  // the usual case: the 4 columns are one Philox draw
+        const uint4 u = dropout_bits4(args.drop_rng, args.drop_stream, (unsigned long long)e0 >> 2);
+        o[0] = u.x > args.drop_thr ? o[0] * args.drop_scale : 0.f;
+        o[1] = u.y > args.drop_thr ? o[1] * args.drop_scale : 0.f;
+        o[2] = u.z > args.drop_thr ? o[2] * args.drop_scale : 0.f;
+        o[3] = u.w > args.drop_thr ? o[3] * args.drop_scale : 0.f;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          o[r] = dropout_keep(args.drop_rng, args.drop_stream, args.drop_thr, e0 + r) ? o[r] * args.drop_scale : 0.f;
+      }
     }
     if (full) {
       uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
@@ -687,7 +714,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   // each lane owns 4 consecutive output columns of one output row.
   const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
   // fp32 outputs: the bias-gradient column (when routed to bias_out) is not part of C
-  const int c_cols = (EPI != EPI_BF16 && args.bias_out) ? args.ones_col : args.N;
+  const int c_cols = (!epi_bf16<EPI>() && args.bias_out) ? args.ones_col : args.N;
   if constexpr (EPI == EPI_SGD) {
     // Interior tiles: issue every master-weight / history load of the wave's 64x64 sub-tile
     // first (32 x 16 B per lane in flight), then update and store — a load -> update ->
@@ -925,7 +952,7 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
   }
 
   const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
-  const int c_cols = (EPI != EPI_BF16 && args.bias_out) ? args.ones_col : args.N;
+  const int c_cols = (!epi_bf16<EPI>() && args.bias_out) ? args.ones_col : args.N;
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
@@ -982,6 +1009,11 @@ int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
       hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS, false, NFR>), grid,
+                         dim3(NW * 64), 0, st, a);
+      break;
+    case EPI_BF16_DROP:  // InnerProduct forward only (dense NT)
+      if (AMC || AMODE != OP_DENSE || BMC || BMODE != OP_DENSE) return 4;
+      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, NW, NS, false, NFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32:
@@ -1063,6 +1095,11 @@ int launch_fp8(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
     case EPI_BF16:
       hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_BF16, 128, 128, 4, 2, true>), grid, dim3(256), 0, st, a);
       break;
+    case EPI_BF16_DROP:
+      if (AMODE != OP_DENSE) return 4;
+      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, 128, 128, 4, 2, true>), grid, dim3(256), 0,
+                         st, a);
+      break;
     case EPI_F32:
       hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_F32, 128, 128, 4, 2, true>), grid, dim3(256), 0, st, a);
       break;
@@ -1080,7 +1117,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   // the ones column is a whole 16-B chunk of an MC B operand, inside the product's N
   if (a.ones_col >= 0 && (!a.b_mc || a.b_mode == OP_FLIPW || (a.ones_col & 7) || a.ones_col >= a.N || a.fp8))
     return 5;
-  if (a.bias_out && (a.ones_col < 0 || a.epi == EPI_BF16)) return 5;
+  if (a.bias_out && (a.ones_col < 0 || a.epi == EPI_BF16 || a.epi == EPI_BF16_DROP)) return 5;
   if (a.fp8) {
     // e4m3 forward products: A (dense or implicit im2col) and B dense, both K-contiguous
     if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || a.a_mc || a.b_mc || a.b_mode != OP_DENSE || !a.deq_a || !a.deq_b)

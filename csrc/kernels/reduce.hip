@@ -21,6 +21,10 @@ struct ReduceOut {
   float* extra;
   long long extra_gstride;
   int extra_col, extra_acc;
+  const long long* drop_rng;  // mode 0: fused dropout / gate scale, as the GEMM epilogue
+  int drop_stream;
+  unsigned drop_thr;
+  float drop_scale, gate_scale;
 };
 
 SN_DEV void reduce_store(const ReduceOut& o, int g, int r, int c, const float* acc) {
@@ -37,7 +41,8 @@ SN_DEV void reduce_store(const ReduceOut& o, int g, int r, int c, const float* a
       if (c + k >= o.cols) break;
       float v = acc[k] + (o.bias ? o.bias[(long long)g * o.cols + c + k] : 0.f);
       if (o.relu) v = fmaxf(v, 0.f);
-      if (o.gate && !(bf2f(o.gate[base + k]) > 0.f)) v = 0.f;
+      if (o.gate) v = bf2f(o.gate[base + k]) > 0.f ? v * o.gate_scale : 0.f;
+      if (o.drop_rng) v = dropout_keep(o.drop_rng, o.drop_stream, o.drop_thr, base + k) ? v * o.drop_scale : 0.f;
       p[k] = f2bf(v);
     }
   } else {
@@ -127,8 +132,14 @@ extern "C" int sn_splitk_reduce(const float* ws, long long splits, long long sst
                                 const float* bias, long long relu, long long groups,
                                 long long ws_gstride, long long out_gstride, const bf16_t* gate,
                                 float* extra, long long extra_col, long long extra_acc, long long extra_gstride,
-                                hipStream_t st) {
+                                const long long* drop_rng, long long drop_stream, float drop_ratio,
+                                float gate_scale, hipStream_t st) {
   ReduceOut o;
+  o.drop_rng = drop_rng;
+  o.drop_stream = (int)drop_stream;
+  o.drop_thr = (uint32_t)((double)4294967295u * (double)drop_ratio);
+  o.drop_scale = 1.f / (1.f - drop_ratio);
+  o.gate_scale = gate_scale;
   o.out = out; o.ldo = ldo; o.out_gstride = out_gstride; o.cols = (int)cols; o.mode = (int)mode;
   o.relu = (int)relu; o.bias = bias; o.gate = gate;
   o.extra = extra; o.extra_col = (int)extra_col; o.extra_acc = (int)extra_acc; o.extra_gstride = extra_gstride;

@@ -46,7 +46,52 @@ def fuse_relu(net) -> int:
         relu.fused = True
         n += 1
     fuse_relu_backward(net)
+    fuse_dropout(net)
     batch_weight_flips(net)
+    return n
+
+
+def fuse_dropout(net) -> int:
+    """Apply an in-place TRAIN-phase Dropout inside the producing InnerProduct's epilogue
+    (after its fused bias + ReLU: CaffeNet fc6 -> relu6 -> drop6, fc7 -> relu7 -> drop7),
+    and its backward inside the consumer InnerProduct's dgrad epilogue: with the ReLU
+    backward already folded into the dropout (fuse_relu_backward), d(pre-activation) =
+    dy / (1-p) where the dropout output is > 0, else 0 — exactly Caffe's ReLU-after-in-place-
+    dropout gate (relu_layer.cu reads the overwritten bottom) times dropout_layer.cu's
+    mask * scale.  Both standalone dropout passes disappear.  GPU only; returns the count."""
+    if net.device.type != "cuda" or os.environ.get("SN_FUSE_DROPOUT", "1") == "0":
+        return 0
+    n = 0
+    for li in range(1, len(net.layers)):
+        d = net.layers[li]
+        if d.type_name != "Dropout" or d.phase != 0 or not (d.ratio > 0) or d.fused_into is not None:
+            continue
+        if net.bottom_ids[li] != net.top_ids[li] or not getattr(d, "relu_gate", False):
+            continue
+        blob = net.top_ids[li][0]
+        # the producer: the InnerProduct whose fused-ReLU output this is (the ReLU in between is fused)
+        prods = [lj for lj in range(li) if blob in net.top_ids[lj]]
+        lp = next((lj for lj in reversed(prods) if net.layers[lj].type_name == "InnerProduct"), None)
+        if lp is None or not getattr(net.layers[lp], "fuse_relu", False):
+            continue
+        between = [net.layers[lj] for lj in prods if lj > lp]
+        if any(not (l.type_name == "ReLU" and getattr(l, "fused", False)) for l in between):
+            continue
+        consumers = [lj for lj in range(li + 1, len(net.layers)) if blob in net.bottom_ids[lj]]
+        if len(consumers) != 1 or blob in getattr(net, "output_blob_ids", ()):
+            continue
+        lc = consumers[0]
+        cons = net.layers[lc]
+        if cons.type_name != "InnerProduct" or len(net.bottom_ids[lc]) != 1 or blob in net.top_ids[lc]:
+            continue
+        prod = net.layers[lp]
+        if prod.fused_dropout is not None:
+            continue
+        prod.fused_dropout = d
+        d.fused_into = prod
+        cons.relu_gate = True
+        cons.gate_scale = 1.0 / (1.0 - d.ratio)
+        n += 1
     return n
 
 

@@ -56,7 +56,11 @@ class DropoutLayer(NeuronLayer):
             raise ValueError("dropout_ratio must be in [0, 1)")
         self.stream = self.ctx.next_stream_id()
 
+    fused_into = None  # the InnerProduct applying this dropout in its epilogue (engine.fuse_dropout)
+
     def forward(self, bottoms, tops):
+        if self.fused_into is not None and self.phase == 0:
+            return  # in place, already applied by the producer's GEMM epilogue
         if self.phase == 0 and self.ratio > 0:  # TRAIN
             tops[0].data = ops.dropout_forward(bottoms[0].data, self.ratio, self.ctx.rng_state, self.stream)
         elif tops[0] is not bottoms[0]:
@@ -65,6 +69,8 @@ class DropoutLayer(NeuronLayer):
     def backward(self, tops, propagate_down, bottoms):
         if not propagate_down[0]:
             return
+        if self.fused_into is not None and self.phase == 0:
+            return  # mask, scale and ReLU gate applied by the consumer's dgrad epilogue
         if self.phase == 0 and self.ratio > 0:
             gate = bottoms[0].data if self.relu_gate else None
             bottoms[0].diff = ops.dropout_backward(tops[0].diff, self.ratio, self.ctx.rng_state, self.stream, gate)

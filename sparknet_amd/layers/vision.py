@@ -374,19 +374,27 @@ class InnerProductLayer(Layer):
         M = b.count_range(0, self.axis)
         x2 = b.data.reshape(M, self.Kdim)
         bias = self.bias.data if self.bias is not None else None
+        d = self.fused_dropout
+        drop = (d.ctx.rng_state, d.stream, d.ratio) if d is not None and x2.is_cuda and d.phase == 0 else None
         if self.fp8_slots is not None and x2.is_cuda:
             from ..ops import hip
             sc = self.ctx.fp8
             ix, iw = self.fp8_slots
             xq = hip.quant_fp8(x2, sc.slot(ix))
             wq = hip.quant_fp8(self.weight.compute, sc.slot(iw))
-            y = hip.linear_forward_fp8(xq, wq, bias, sc.deq(ix), sc.deq(iw), relu=self.fuse_relu)
+            y = hip.linear_forward_fp8(xq, wq, bias, sc.deq(ix), sc.deq(iw), relu=self.fuse_relu, dropout=drop)
         else:
-            y = ops.linear_forward(x2, self.weight.compute, bias, self.fuse_relu)
+            if drop is not None:  # TRAIN: the in-place dropout applied in the epilogue
+                from ..ops import hip
+                y = hip.linear_forward(x2, self.weight.compute, bias, self.fuse_relu, dropout=drop)
+            else:
+                y = ops.linear_forward(x2, self.weight.compute, bias, self.fuse_relu)
         tops[0].data = y.reshape(tops[0].data.shape)
 
     fp8_slots = None
     fused_update = None  # solver update applied in the wgrad epilogue (engine.fuse_fc_updates)
+    fused_dropout = None  # the in-place Dropout applied in the forward epilogue (engine.fuse_dropout)
+    gate_scale = 1.0      # dgrad gate = a fused dropout's output: scale kept values by 1/(1-p)
 
     def fp8_eligible(self, b) -> bool:
         return self.Kdim % 16 == 0
@@ -406,7 +414,11 @@ class InnerProductLayer(Layer):
             # admits only unshared weights with iter_size 1: this is its one and only write)
             from ..ops import hip
             dx = hip.linear_backward_sgd(dy2, x2, self.weight.compute, bool(propagate_down[0]),
-                                         self.fused_update.sgd(), db, gate, db_acc=db_acc)
+                                         self.fused_update.sgd(), db, gate, db_acc=db_acc, gate_scale=self.gate_scale)
+        elif self.gate_scale != 1.0:
+            from ..ops import hip
+            dx = hip.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db, gate,
+                                     dw_acc=dw_acc, db_acc=db_acc, gate_scale=self.gate_scale)
         else:
             dx = ops.linear_backward(dy2, x2, self.weight.compute, bool(propagate_down[0]), dw, db, gate,
                                      dw_acc=dw_acc, db_acc=db_acc)

@@ -45,7 +45,9 @@ class SnGemmArgs(C.Structure):
                 ("fp8", C.c_int), ("deq_a", C.c_void_p), ("deq_b", C.c_void_p), ("raster_n", C.c_int),
                 ("ones_col", C.c_int), ("bias_out", C.c_void_p), ("bias_acc", C.c_int),
                 ("sgd_w", C.c_void_p), ("sgd_h", C.c_void_p), ("sgd_shadow", C.c_void_p), ("sgd_hyper", C.c_void_p),
-                ("sgd_lr_mult", C.c_float), ("sgd_decay_mult", C.c_float), ("sgd_flags", C.c_int)]
+                ("sgd_lr_mult", C.c_float), ("sgd_decay_mult", C.c_float), ("sgd_flags", C.c_int),
+                ("drop_rng", C.c_void_p), ("drop_stream", C.c_int), ("drop_thr", C.c_uint),
+                ("drop_scale", C.c_float), ("gate_scale", C.c_float)]
 
 
 def lib_path(name: str = "libsn_kernels.so") -> Path:

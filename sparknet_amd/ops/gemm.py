@@ -22,7 +22,7 @@ import torch
 from . import _lib
 
 OP_DENSE, OP_IM2COL, OP_FLIPW = 0, 1, 2
-EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_SGD = 0, 1, 2, 3
+EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_SGD, EPI_BF16_DROP = 0, 1, 2, 3, 4
 BM = BN = 128
 BK = 64
 
@@ -165,7 +165,8 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
          groups: int = 1, c_gstride: int = 0, bias: torch.Tensor | None = None, relu: bool = False,
          splits: int | None = None, gate: torch.Tensor | None = None,
          deq: tuple[torch.Tensor, torch.Tensor] | None = None,
-         bias_grad: torch.Tensor | None = None, bias_acc: bool = True, sgd: dict | None = None) -> None:
+         bias_grad: torch.Tensor | None = None, bias_acc: bool = True, sgd: dict | None = None,
+         dropout: tuple | None = None, gate_scale: float = 1.0) -> None:
     """Run one (possibly grouped, split-K) GEMM.  ``epi``: EPI_BF16 (store bf16 with
     bias/ReLU; ``gate``: a bf16 tensor laid out like ``out`` — outputs where gate <= 0
     are zeroed, i.e. a following slope-0 ReLU's backward), EPI_F32 (store), EPI_F32_ACC
@@ -177,7 +178,12 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
 
     ``epi=EPI_SGD`` with ``sgd`` = {w, h, shadow, hyper, lr_mult, decay_mult, flags}:
     the product is the gradient of the fp32 master ``w`` (laid out like ``out``), and the
-    epilogue applies the solver update to w / h / shadow instead of storing it."""
+    epilogue applies the solver update to w / h / shadow instead of storing it.
+
+    EPI_BF16 only: ``dropout`` = (rng_state, layer stream id, ratio) applies a Dropout
+    forward (Philox keep mask over the output's element index, scaled by 1/(1-ratio))
+    after bias / ReLU; ``gate_scale`` multiplies the values a ``gate`` lets through (a
+    fused Dropout backward: the gate is the dropout output)."""
     if M == 0 or N == 0:
         return
     sg = (0, 0, 0, 0, 0.0, 0.0, 0)
@@ -199,6 +205,11 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     if gate is not None:
         assert epi == EPI_BF16 and gate.dtype == torch.bfloat16
+    xtra = (0, 0, 0.0, float(gate_scale))
+    if dropout is not None:
+        assert epi == EPI_BF16
+        rng, dstream, ratio = dropout
+        xtra = (rng.data_ptr(), int(dstream), float(ratio), float(gate_scale))
     ops = (sa, a_mc, a_mode, sb, b_mc, b_mode)
     if splits is not None or fp8 or _FORCE_TILE >= 0:
         tile = 0 if fp8 else (_FORCE_TILE if _FORCE_TILE >= 0 else choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE))
@@ -211,13 +222,24 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
             kchunk = -(-(-(-K // splits)) // bk) * bk
     else:
         tile, splits, kchunk = _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate,
-                                             bias_grad, bias_acc, ones, sg)
+                                             bias_grad, bias_acc, ones, sg, xtra)
     _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc, ones, sg,
-            tile, splits, kchunk, deq)
+            tile, splits, kchunk, deq, xtra)
+
+
+_NO_XTRA = (0, 0, 0.0, 1.0)
+
+
+def _drop_fields(xtra):
+    """(drop_rng, drop_stream, drop_thr, drop_scale, gate_scale) of SnGemmArgs."""
+    rng, dstream, ratio, gscale = xtra
+    if not rng:
+        return (0, 0, 0, 1.0, gscale)
+    return (rng, dstream, int(4294967295 * ratio) & 0xffffffff, 1.0 / (1.0 - ratio), gscale)
 
 
 def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc, ones, sg,
-            tile, splits, kchunk, deq=None):
+            tile, splits, kchunk, deq=None, xtra=_NO_XTRA):
     """One GEMM launch (+ the split-K reduce) with an explicit tile / split choice."""
     sa, a_mc, a_mode, sb, b_mc, b_mode = ops
     fp8 = deq is not None
@@ -230,10 +252,11 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     gp = gate.data_ptr() if gate is not None else 0
     bg = bias_grad.data_ptr() if bias_grad is not None else 0
     if splits == 1:
-        args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, epi,
+        e = EPI_BF16_DROP if (epi == EPI_BF16 and xtra[0]) else epi
+        args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, e,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
                                bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster,
-                               ones, bg, int(bias_acc), *sg)
+                               ones, bg, int(bias_acc), *sg, *_drop_fields(xtra))
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
@@ -242,11 +265,13 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     ws = torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
                            sa, sb, ws.data_ptr(), ldw, splits * M * ldw, M * ldw, 0, 0, tile, 0, int(fp8), *dq, raster,
-                           ones, 0, 0, *sg)
+                           ones, 0, 0, *sg, *_drop_fields(_NO_XTRA))
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
+    rng, dstream, ratio, gscale = xtra
     _lib.call("splitk_reduce", ws, splits, M * ldw, M, N, ldw, out, ldc, mode, bias, int(relu),
-              groups, splits * M * ldw, c_gstride, gate, bias_grad, ones, int(bias_acc), M)
+              groups, splits * M * ldw, c_gstride, gate, bias_grad, ones, int(bias_acc), M,
+              C.c_void_p(rng), int(dstream), float(ratio), float(gscale))
 
 
 # --- per-shape autotuning ----------------------------------------------------------------
@@ -292,10 +317,10 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
 
 
 def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
-                  ones, sg):
+                  ones, sg, xtra=_NO_XTRA):
     sa, a_mc, a_mode, sb, b_mc, b_mode = ops
     b_kc_dense = b_mc == 0 and b_mode == OP_DENSE
-    key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None,
+    key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None, bool(xtra[0]),
            _geom_key(sa), _geom_key(sb), out.dtype)
     hit = _TUNED.get(key)
     if hit is not None:
@@ -317,7 +342,7 @@ def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, ga
 
         def run(t=t, s=s, kc=kc):
             _launch(M, N, K, groups, ops, epi, scratch, ldc, c_gstride, bias, relu, gate, bscratch, bias_acc,
-                    ones, sg, t, s, kc)
+                    ones, sg, t, s, kc, None, xtra)
         try:
             run()
         except RuntimeError:  # a tile this operand combination has no instance for
@@ -364,21 +389,23 @@ def _pad8(t: torch.Tensor, dim: int) -> torch.Tensor:
 
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
-               relu: bool = False, out: torch.Tensor | None = None) -> torch.Tensor:
-    """y[M,N] = x[M,K] @ w[N,K]^T (+bias, ReLU) in bf16."""
+               relu: bool = False, out: torch.Tensor | None = None, dropout: tuple | None = None) -> torch.Tensor:
+    """y[M,N] = x[M,K] @ w[N,K]^T (+bias, ReLU, fused Dropout forward) in bf16."""
     M, K = x.shape
     N = w.shape[0]
     xp, wp = _pad8(x, 1), _pad8(w, 1)
     Kp = xp.shape[1]
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    if dropout is not None:
+        assert out.is_contiguous()  # the mask is drawn over the blob's element index
     gemm(M, N, Kp, Dense(xp, Kp, True), Dense(wp, Kp, True), out, out.stride(0), epi=EPI_BF16,
-         bias=bias, relu=relu)
+         bias=bias, relu=relu, dropout=dropout)
     return out
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
-                 gate: torch.Tensor | None = None) -> torch.Tensor:
+                 gate: torch.Tensor | None = None, gate_scale: float = 1.0) -> torch.Tensor:
     """dx[M,K] = dy[M,N] @ w[N,K] in bf16 (B operand read transposed from LDS);
     ``gate`` [M,K]: zero dx where gate <= 0 (fused ReLU backward)."""
     M, N = dy.shape
@@ -396,12 +423,13 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = N
         o = out
     if gate is not None and (Kp != K or not gate.is_contiguous()):
         gemm(M, Kp, Np, Dense(dyp, Np, True), Dense(wp, Kp, False), o, o.stride(0), epi=EPI_BF16)
-        o = o[:, :K] * (gate > 0).to(o.dtype)
+        o = o[:, :K] * (gate > 0).to(o.dtype) * gate_scale
         if out is not None:
             out.copy_(o)
             return out
         return o
-    gemm(M, Kp, Np, Dense(dyp, Np, True), Dense(wp, Kp, False), o, o.stride(0), epi=EPI_BF16, gate=gate)
+    gemm(M, Kp, Np, Dense(dyp, Np, True), Dense(wp, Kp, False), o, o.stride(0), epi=EPI_BF16, gate=gate,
+         gate_scale=gate_scale)
     if o is not out:
         o = o[:, :K]
         if out is not None:

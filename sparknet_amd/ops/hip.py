@@ -339,11 +339,13 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws):
 # InnerProduct
 # --------------------------------------------------------------------------------------
 
-def linear_forward(x2, w, b, relu=False):
-    return linear_fwd(_c(x2), _c(w), b, relu)
+def linear_forward(x2, w, b, relu=False, dropout=None):
+    """dropout: (rng_state, stream id, ratio) — a following in-place Dropout applied in
+    the epilogue (engine.fuse_dropout)."""
+    return linear_fwd(_c(x2), _c(w), b, relu, dropout=dropout)
 
 
-def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=True, db_acc=True):
+def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=True, db_acc=True, gate_scale=1.0):
     dy2 = _c(dy2)
     with wgrad_side("fc"):
         if dw is not None:
@@ -354,17 +356,19 @@ def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=Tru
             colsum(dy2, db, accumulate=db_acc)
     if not need_dx:
         return None
-    return linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)
+    return linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None,
+                        gate_scale=gate_scale)
 
 
-def linear_backward_sgd(dy2, x2, w, need_dx, sgd, db=None, gate=None, db_acc=True):
+def linear_backward_sgd(dy2, x2, w, need_dx, sgd, db=None, gate=None, db_acc=True, gate_scale=1.0):
     """InnerProduct backward whose weight gradient is consumed by the solver update in the
     GEMM epilogue (gemm.linear_wgrad_sgd).  The data gradient runs FIRST: it reads the
     bf16 compute weights ``w`` that the fused update then overwrites."""
     dy2, x2 = _c(dy2), _c(x2)
     dx = None
     if need_dx:
-        dx = linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None)
+        dx = linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None,
+                          gate_scale=gate_scale)
     from .gemm import linear_wgrad_sgd
     with wgrad_side("fcsgd"):  # forked after the dgrad: the update overwrites w
         if not linear_wgrad_sgd(dy2, x2, sgd, db, db_acc) and db is not None:
@@ -678,11 +682,11 @@ def conv_forward_fp8(xq, wq, b, s: ConvSpec, deq_x, deq_w, relu=False):
     return y
 
 
-def linear_forward_fp8(xq, wq, b, deq_x, deq_w, relu=False):
+def linear_forward_fp8(xq, wq, b, deq_x, deq_w, relu=False, dropout=None):
     M, K = xq.shape
     N = wq.shape[0]
     assert K % 16 == 0
     y = torch.empty((M, N), dtype=BF16, device=xq.device)
     gemm(M, N, K, Dense(xq, K, True), Dense(wq, K, True), y, N, epi=EPI_BF16, bias=b, relu=relu,
-         deq=(deq_x, deq_w))
+         deq=(deq_x, deq_w), dropout=dropout)
     return y

@@ -198,9 +198,16 @@ _MASK32 = 0xFFFFFFFF
 
 
 def philox_u32(n: int, seed: int, counter: int, stream: int) -> torch.Tensor:
-    """First word of Philox4x32-10 for element indices 0..n-1 — bit-identical to the
-    HIP kernel (csrc/kernels/common.h philox4x32) so CPU and GPU dropout masks agree."""
-    idx = torch.arange(n, dtype=torch.int64)
+    """Dropout words for element indices 0..n-1: element e takes word e % 4 of
+    Philox4x32-10 at counter e // 4 — bit-identical to the HIP kernels
+    (csrc/kernels/common.h dropout_bits4) so CPU and GPU dropout masks agree."""
+    n4 = -(-n // 4)
+    return _philox4(n4, seed, counter, stream).reshape(-1)[:n]
+
+
+def _philox4(n4: int, seed: int, counter: int, stream: int) -> torch.Tensor:
+    """[n4, 4] Philox4x32-10 output words for counters 0..n4-1."""
+    idx = torch.arange(n4, dtype=torch.int64)
     c0 = idx & _MASK32
     c1 = (idx >> 32) & _MASK32
     c1 = c1 | ((stream & 0xFFFF) << 16)
@@ -216,7 +223,7 @@ def philox_u32(n: int, seed: int, counter: int, stream: int) -> torch.Tensor:
         c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
         k0 = (k0 + _W0) & _MASK32
         k1 = (k1 + _W1) & _MASK32
-    return c0
+    return torch.stack([c0, c1, c2, c3], dim=1)
 
 
 def dropout_mask(shape, ratio, seed, counter, stream, device):

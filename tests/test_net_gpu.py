@@ -226,3 +226,20 @@ def test_googlenet_branch_streams_bitwise(gpu):
             graph.replay()
             torch.cuda.synchronize()
             assert float(loss) == l0 and torch.equal(net.flat_diff, g0)
+
+
+def test_fused_dropout_matches_standalone(gpu, monkeypatch):
+    """Dropout applied in the fc6 / fc7 forward epilogues and its backward in the fc7 /
+    fc8 dgrad epilogues (engine.fuse_dropout) == the standalone Philox dropout kernels:
+    same masks (same element index, stream and counter), same loss and gradients."""
+    n = _tiny_caffenet(0.5)
+    l0, g0, net0 = _run(n, gpu, True)  # fused (default)
+    fused = [l.name for l in net0.layers if getattr(l, "fused_dropout", None) is not None]
+    assert fused == ["fc6", "fc7"], fused
+    monkeypatch.setenv("SN_FUSE_DROPOUT", "0")
+    l1, g1, net1 = _run(n, gpu, True, weights=net0.flat_data.detach().float().cpu())
+    assert not any(getattr(l, "fused_dropout", None) for l in net1.layers)
+    assert torch.equal(net0.blob_by_name("fc6").data, net1.blob_by_name("fc6").data)
+    assert abs(l0 - l1) <= 1e-3 * max(1.0, abs(l0))
+    err = (g0 - g1).abs().max().item() / (g0.abs().max().item() + 1e-12)
+    assert err < 2e-2, err
