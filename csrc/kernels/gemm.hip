@@ -722,6 +722,63 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
     // the bias column take the per-fragment path below.
     const bool interior = m_blk + BM <= args.M && n_blk + BN <= c_cols && (args.ldc & 3) == 0 &&
                           ((grp * args.c_gstride) & 3) == 0;
+    if constexpr (BM == 128 && BN == 128 && NW == 4 && NFR == 4 && NS == 2 && !FP8) {
+      // LDS-transposed update (128x128 tiles): the MFMA layout gives each wave-instruction
+      // 16 rows x 64 B, which the HBM streams of w / h / shadow serve at ~3.7 TB/s; the
+      // gradient tile is instead staged through the (now idle) LDS stages as fp32 row-major
+      // (rows 0-63 in smem0, 64-127 in smem1, 16-B chunks XOR-swizzled by row) and every
+      // 32 lanes then update one contiguous 512-B row segment.  The master / history loads
+      // are all issued (32 x 16 B per lane in flight) before the exchange barrier.
+      if (interior) {
+        const float* hy = args.sgd_hyper;
+        const float rate = hy[0] * args.sgd_lr_mult, mom = hy[1], decay = hy[2] * args.sgd_decay_mult;
+        const float gscale = hy[4];
+        const int cq = tid & 31, r0 = tid >> 5;
+        const long long ob = grp * args.c_gstride + (long long)m_blk * args.ldc + n_blk + cq * 4;
+        __builtin_amdgcn_s_barrier();  // every wave is past its last fragment read of the stages
+        char* wbuf = (wave % WM) == 0 ? smem0 : smem1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int lr = 16 * j + mrow_l;
+#pragma unroll
+          for (int i = 0; i < NFR; ++i) {
+            const int ch = (wn0 + 16 * i + ncol_l) >> 2;
+            *reinterpret_cast<f32x4*>(wbuf + lr * 512 + ((ch ^ (lr & 15)) << 4)) = acc[i][j];
+          }
+        }
+        // the accumulators are dead now: issue all 32 master / history loads, then exchange
+        float4 Wv[16], Av[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          const long long o = ob + (long long)(it * 8 + r0) * args.ldc;
+          Wv[it] = *reinterpret_cast<const float4*>(args.sgd_w + o);
+          Av[it] = *reinterpret_cast<const float4*>(args.sgd_h + o);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          const int r = it * 8 + r0, lr = r & 63;
+          const char* rbuf = r < 64 ? smem0 : smem1;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(rbuf + lr * 512 + ((cq ^ (lr & 15)) << 4));
+          float W[4] = {Wv[it].x, Wv[it].y, Wv[it].z, Wv[it].w};
+          float A[4] = {Av[it].x, Av[it].y, Av[it].z, Av[it].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float gg = v[q] * gscale;
+            gg += decay * ((args.sgd_flags & 2) ? (float)((W[q] > 0.f) - (W[q] < 0.f)) : W[q]);
+            const float prev = A[q];
+            A[q] = mom * A[q] + rate * gg;
+            W[q] -= (args.sgd_flags & 1) ? (1.f + mom) * A[q] - mom * prev : A[q];
+          }
+          const long long o = ob + (long long)r * args.ldc;
+          *reinterpret_cast<float4*>(args.sgd_w + o) = make_float4(W[0], W[1], W[2], W[3]);
+          *reinterpret_cast<float4*>(args.sgd_h + o) = make_float4(A[0], A[1], A[2], A[3]);
+          *reinterpret_cast<uint2*>(args.sgd_shadow + o) = make_uint2(pack2(W[0], W[1]), pack2(W[2], W[3]));
+        }
+        return;
+      }
+    }
     if (interior) {
       const float* hy = args.sgd_hyper;
       const float rate = hy[0] * args.sgd_lr_mult, mom = hy[1], decay = hy[2] * args.sgd_decay_mult;
