@@ -138,7 +138,7 @@ def _cost(tiles: int, ktiles: int, s: int, out_elems: int, tile: int = 0) -> flo
     kt = -(-ktiles // s)
     t = -(-tiles * s // _SLOTS.get(tile, SLOTS)) * (kt + BLOCK_OVERHEAD) * _KTILE_US.get(tile, KTILE_US)
     if s > 1:
-        t += (out_elems * 4.0 * (s + 1)) / REDUCE_BW * 1e6 + 3.0
+        t += (out_elems * 4.0 * (s + 1)) / REDUCE_BW * 1e6 + (0.0 if _FIXUP and tile not in _TILE256_IDS else 3.0)
     return t
 
 
@@ -261,6 +261,22 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
         return
+    if _FIXUP and tile not in _TILE256_IDS:
+        # in-kernel split-K: tile-major fp32 slabs + per-tile arrival counters; the last
+        # split of each tile sums the slabs (split order) and runs the real epilogue
+        tiles = tm_ * tn_ * groups
+        ws = torch.empty(tiles * splits * bm * bn, dtype=torch.float32, device=out.device)
+        assert ws.numel() * 4 < (1 << 31), "split-K slabs exceed the 2 GB buffer range"
+        ctr = _counters(out.device, tiles)
+        e = EPI_BF16_DROP if (epi == EPI_BF16 and xtra[0]) else epi
+        args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, e,
+                               sa, sb, out.data_ptr(), ldc, c_gstride, 0,
+                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster,
+                               ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), ws.data_ptr(), ctr)
+        _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
+        if _lib.DEBUG_SYNC:
+            _lib.debug_sync("gemm")
+        return
     ldw = -(-N // 4) * 4  # fp32 slabs keep 16-B rows (the ones column makes N odd)
     ws = torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
@@ -272,6 +288,36 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     _lib.call("splitk_reduce", ws, splits, M * ldw, M, N, ldw, out, ldc, mode, bias, int(relu),
               groups, splits * M * ldw, c_gstride, gate, bias_grad, ones, int(bias_acc), M,
               C.c_void_p(rng), int(dstream), float(ratio), float(gscale))
+
+
+# In-kernel split-K (SnGemmArgs.counters): arrival counters come from a per-device ring of
+# zeroed int32 words; every launch leaves its words at zero again (the last split of a tile
+# re-arms its counter), so a region can be reused by any later launch on the same stream,
+# and launches that may run concurrently (branch streams, graph replays) get distinct
+# regions unless the ring wraps within one in-flight window (4M words).
+# Measured SLOWER than the separate reduce kernel and therefore off by default
+# (SN_SPLITK_FIXUP=1 enables it): CaffeNet 102k -> 86k img/s, GoogLeNet 19.6k -> 11.6k.
+# Split-K is chosen exactly when a product has few output tiles, so the last-arriving
+# block of each tile reduces s slabs on only `tiles` CUs (e.g. fc6 forward: 64 tiles x 16
+# slabs x 64 KB from memory) where the reduce kernel spreads the same bytes over all 256
+# CUs, and every split block also waits for its sc1 partial stores to reach memory before
+# it may signal (docs/PERF_NOTES.md).
+_FIXUP = os.environ.get("SN_SPLITK_FIXUP", "0") == "1"
+_TILE256_IDS = (6, 7, 8, 9)
+_RING_WORDS = 1 << 22
+_RINGS: dict = {}
+
+
+def _counters(device, n: int) -> int:
+    ring = _RINGS.get(device)
+    if ring is None:
+        ring = _RINGS[device] = [torch.zeros(_RING_WORDS, dtype=torch.int32, device=device), 0]
+    buf, pos = ring
+    assert n <= _RING_WORDS, n
+    if pos + n > _RING_WORDS:
+        pos = 0
+    ring[1] = pos + n
+    return buf.data_ptr() + 4 * pos
 
 
 # --- per-shape autotuning ----------------------------------------------------------------
