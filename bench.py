@@ -51,6 +51,8 @@ def parse():
                    help="fp32 reference engine on the CPU with gloo (tests the launcher / JSON path; not a benchmark)")
     p.add_argument("--host-profile", action="store_true",
                    help="after the timed run, report the host time per step part (stderr)")
+    p.add_argument("--save-tuned", default="",
+                   help="merge this run's GEMM tile / split-K choices into a tuning database (JSON)")
     return p.parse_args()
 
 
@@ -210,6 +212,9 @@ def main():
         print(json.dumps(out), flush=True)
     if args.host_profile and trainer.step_fn is not None:
         host_profile(trainer, dev)
+    if args.save_tuned and rank == 0:
+        from sparknet_amd.ops import gemm as G
+        print(f"tuning database {args.save_tuned}: {G.save_tune_db(args.save_tuned)} entries", file=sys.stderr)
     if comm is not None:
         comm.close()
     return 0

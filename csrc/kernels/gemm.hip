@@ -108,13 +108,6 @@ struct SnGemmArgs {
   unsigned drop_thr;
   float drop_scale;
   float gate_scale;
-  // In-kernel deterministic split-K (gemm_kernel tiles, splits > 1, counters set): every
-  // (tile, split) block stores its fp32 partial to its own BM x BN slab of ws (tile-major:
-  // ws[(g * tiles + tile) * splits + split][BM][BN], sc1 stores), then bumps the tile's
-  // counter; the block whose add returns splits - 1 sums the slabs in split order 0..s-1,
-  // re-arms the counter to 0 and runs the regular epilogue into C — no reduce launch.
-  float* ws;
-  int* counters;
 };
 
 }  // extern "C"
@@ -141,7 +134,6 @@ __device__ __attribute__((aligned(16))) uint32_t g_one16[4] = {0x3F80u, 0u, 0u, 
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 // Global->LDS staging of one operand tile with global_load_lds_dwordx4 (LDS-DMA, no VGPR
 // round trip and no ds_write pass).  One wave-instruction writes 1 KB of LDS linearly
@@ -721,44 +713,6 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
   // Epilogue.  acc[i][j] holds D[n][m] with m = lane&15 (+16j), n = 4(lane>>4)+r (+16i):
   // each lane owns 4 consecutive output columns of one output row.
   const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
-  if (args.counters != nullptr) {
-    // In-kernel split-K hand-off (MI355X_MICROARCH "valid forms", row 1): sc1 partial
-    // stores, every wave's vmcnt(0), a workgroup barrier, ONE agent-scope counter add by
-    // one lane; the last adder's workgroup reads every slab with sc1 loads after a barrier.
-    __shared__ int s_last;
-    const unsigned slab = (unsigned)(grp * tiles + tile) * (unsigned)args.splits * (unsigned)(BM * BN * 4);
-    const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(args.ws, (short)0, 0x7fffffff, 0x00020000);
-    auto pos = [&](int i, int j) { return (unsigned)(((wm0 + 16 * j + mrow_l) * BN + wn0 + 16 * i + ncol_l) * 4); };
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < NFR; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), wsr,
-                                               slab + (unsigned)split * (BM * BN * 4) + pos(i, j), 0, 16);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      int* ctr = args.counters + (grp * tiles + tile);
-      const int last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == args.splits - 1;
-      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next launch
-      s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < NFR; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < args.splits; ++sp) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < NFR; ++i)
-          acc[i][j] += __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(wsr, slab + (unsigned)sp * (BM * BN * 4) + pos(i, j), 0, 16));
-    }
-  }
-  const int split_e = args.counters != nullptr ? 0 : split;
   // fp32 outputs: the bias-gradient column (when routed to bias_out) is not part of C
   const int c_cols = (!epi_bf16<EPI>() && args.bias_out) ? args.ones_col : args.N;
   if constexpr (EPI == EPI_SGD) {
@@ -871,7 +825,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
     for (int i = 0; i < NFR; ++i) {
       const int n = n_blk + wn0 + 16 * i + ncol_l;
       if (n >= args.N) continue;
-      epi_store<EPI, FP8>(args, grp, split_e, m, n, acc[i][j], c_cols);
+      epi_store<EPI, FP8>(args, grp, split, m, n, acc[i][j], c_cols);
     }
   }
 }

@@ -21,6 +21,7 @@ struct LrnP {
   int N, H, W, C, size, pre;
   float alpha, beta, k;
   FDiv fcv;  // C / 8
+  int gate;  // backward: zero dx where x <= 0 (the in-place ReLU that produced x, fused)
 };
 
 SN_DEV float powneg(float s, float beta) { return __expf(-beta * __logf(s)); }
@@ -113,6 +114,7 @@ __global__ void lrn_across_bwd(const bf16_t* __restrict__ x, const bf16_t* __res
 #pragma unroll
       for (int d = -PRE; d <= POST; ++d) acc += r[8 + t - d];
       o[t] = gv[8 + t] - cache_ratio * xv[8 + t] * acc;
+      if (p.gate && !(xv[8 + t] > 0.f)) o[t] = 0.f;
     }
     *reinterpret_cast<uint4*>(dx + base + c0) = pack8(o);
   }
@@ -159,7 +161,8 @@ __global__ void lrn_across_bwd_scalar(const bf16_t* __restrict__ x, const bf16_t
         acc += bf2f(gr[cp]) * bf2f(xr[cp]) * powneg(sc, p.beta + 1.f);
         if (cp == c) own = bf2f(gr[c]) * powneg(sc, p.beta);
       }
-      dx[i * p.C + c] = f2bf(own - cache_ratio * bf2f(xr[c]) * acc);
+      const float v = own - cache_ratio * bf2f(xr[c]) * acc;
+      dx[i * p.C + c] = f2bf(p.gate && !(bf2f(xr[c]) > 0.f) ? 0.f : v);
     }
   }
 }
@@ -233,6 +236,7 @@ static LrnP mk(long long N, long long H, long long W, long long C, long long siz
   p.N = (int)N; p.H = (int)H; p.W = (int)W; p.C = (int)C; p.size = (int)size; p.pre = (int)((size - 1) / 2);
   p.alpha = alpha; p.beta = beta; p.k = k;
   p.fcv = make_fdiv((uint32_t)(C % 8 == 0 ? C / 8 : 1));
+  p.gate = 0;
   return p;
 }
 
@@ -257,8 +261,9 @@ extern "C" int sn_lrn_across_fwd(const bf16_t* x, bf16_t* y, long long N, long l
 
 extern "C" int sn_lrn_across_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, long long N, long long H,
                                  long long W, long long C, long long size, float alpha, float beta, float k,
-                                 hipStream_t st) {
+                                 long long gate, hipStream_t st) {
   LrnP p = mk(N, H, W, C, size, alpha, beta, k);
+  p.gate = (int)gate;
   if (N * H * W * C >= (1ll << 32)) return 8;  // 32-bit index decode
   dim3 g8(sn_blocks(N * H * W * (C / 8), 256, 16384));
   if (C % 8 == 0 && size == 3) {

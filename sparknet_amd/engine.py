@@ -47,7 +47,98 @@ def fuse_relu(net) -> int:
         n += 1
     fuse_relu_backward(net)
     fuse_dropout(net)
+    fuse_concat(net)
     batch_weight_flips(net)
+    return n
+
+
+def _gating_consumers(net, blob: int, after: int):
+    """Layers that would gate the gradient of ``blob`` with its own data if the ReLU
+    backward of ``blob`` were moved into them — every reader after layer ``after``,
+    following Split fan-outs — or None if some reader cannot (in-place readers, layers
+    without a fused gate, net outputs)."""
+    if blob in getattr(net, "output_blob_ids", ()):
+        return None
+    out = []
+    for lj in range(after + 1, len(net.layers)):
+        if blob not in net.bottom_ids[lj]:
+            continue
+        lay = net.layers[lj]
+        if blob in net.top_ids[lj] or not net.layer_need_backward[lj]:
+            return None
+        if lay.type_name == "Split":
+            for t in net.top_ids[lj]:
+                sub = _gating_consumers(net, t, lj)
+                if sub is None:
+                    return None
+                out += sub
+            continue
+        if lay.type_name not in _GATE_CONSUMERS or len(net.bottom_ids[lj]) != 1 or getattr(lay, "relu_gate", False):
+            return None
+        if lay.type_name == "Pooling" and (lay.method not in (0, 1) or len(net.top_ids[lj]) != 1):
+            return None
+        if lay.type_name in ("InnerProduct", "Dropout"):
+            return None  # their gate doubles as the fused-dropout channel (fuse_dropout)
+        out.append(lj)
+    return out
+
+
+def fuse_concat(net) -> int:
+    """Zero-copy channel Concat (GoogLeNet Inception outputs).  Caffe copies every part
+    into the output (concat_layer.cu:9-25) and back out in backward.  Here, when every
+    part is produced by an ungrouped implicit-GEMM Convolution whose only other reader is
+    its fused in-place ReLU, the convolutions write their GEMM output straight into the
+    part's channel slice of one NHWC buffer (ldc = the concat width) and the Concat
+    forward is free.  If, in addition, every reader of the concat output (through Split
+    fan-outs: the next module's convolutions and max-pool, the stage pools, the loss-branch
+    average pools) can apply a ReLU gate, the parts' ReLU backward moves into them (each
+    part is a ReLU output, so the concat output is its own gate) and the Concat backward
+    hands each part a channel-slice view of the output gradient, which the producing
+    convolution's wgrad / dgrad GEMMs read in place.  GPU only; returns the count."""
+    if net.device.type != "cuda" or os.environ.get("SN_ZERO_COPY_CONCAT", "1") == "0":
+        return 0
+    from .layers.common import ConcatSlots
+    from .ops import hip
+    n = 0
+    outputs = set(getattr(net, "output_blob_ids", ()))
+    for lc, cat in enumerate(net.layers):
+        if cat.type_name != "Concat" or len(net.bottom_ids[lc]) < 2 or cat.zero_copy is not None:
+            continue
+        bots = net.bottom_ids[lc]
+        if len(set(bots)) != len(bots) or len(net.bottom_vecs[lc][0].shape) != 4:
+            continue
+        if cat.axis != 1:
+            continue
+        prods = []
+        for bid in bots:
+            writers = [lj for lj in range(lc) if bid in net.top_ids[lj]]
+            readers = [lj for lj in range(len(net.layers)) if bid in net.bottom_ids[lj] and lj != lc]
+            if not writers or bid in outputs:
+                break
+            prod = net.layers[writers[0]]
+            inplace_ok = all(net.layers[lj].type_name == "ReLU" and getattr(net.layers[lj], "fused", False)
+                             and net.top_ids[lj] == [bid] and net.bottom_ids[lj] == [bid] for lj in readers)
+            if (not inplace_ok or set(writers[1:]) != set(readers) or prod.type_name != "Convolution"
+                    or len(net.top_ids[writers[0]]) != 1 or prod.concat_slot is not None
+                    or prod.fp8_slots is not None or prod.folded_input is not None):
+                break
+            s = prod.spec(net.bottom_vecs[writers[0]][0])
+            if not hip._slice_ok(s) or hip._s2d_plan(s) is not None:
+                break
+            prods.append((prod, s.K))
+        if len(prods) != len(bots):
+            continue
+        slots = ConcatSlots([k for _, k in prods])
+        for part, (prod, _) in enumerate(prods):
+            prod.concat_slot = (slots, part)
+        cat.zero_copy = slots
+        gated = _gating_consumers(net, net.top_ids[lc][0], lc)
+        if gated is not None and cat.relu_gate_parts == frozenset(range(len(bots))):
+            for lj in gated:
+                net.layers[lj].relu_gate = True
+            cat.relu_gate_parts = frozenset()
+            cat.zero_copy_bwd = True
+        n += 1
     return n
 
 
@@ -122,14 +213,14 @@ def batch_weight_flips(net) -> int:
     return len(items)
 
 
-_GATE_CONSUMERS = ("Convolution", "InnerProduct", "Dropout", "Pooling")
+_GATE_CONSUMERS = ("Convolution", "InnerProduct", "Dropout", "Pooling", "LRN")
 
 
 def fuse_relu_backward(net) -> int:
     """Fold the backward of every in-place slope-0 ReLU into the backward of the single
     layer that consumes its output (Caffe's ReLU backward is a separate pass over the
     gradient, relu_layer.cu:24-41): conv / inner-product dgrad epilogues, the dropout
-    kernel, the max-pool argmax mask and the channel-concat backward (Inception outputs)
+    kernel, the max-pool argmax mask, the LRN backward and the channel-concat backward (Inception outputs)
     then zero the gradient where the ReLU output is not positive, and the ReLU layer's
     own backward becomes a no-op.  Returns the count."""
     n = 0

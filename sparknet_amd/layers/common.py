@@ -129,6 +129,8 @@ class ConcatLayer(Layer):
         tops[0].reshape(tuple(shape), bottoms[0].dtype)
 
     relu_gate_parts: frozenset = frozenset()  # bottoms whose in-place ReLU backward runs here
+    zero_copy = None       # ConcatSlots: the producers wrote the parts into one buffer (engine.fuse_concat)
+    zero_copy_bwd = False  # ... and the consumers of the output gate its gradient: parts' diffs are views
 
     def _hip_ok(self, bottoms, ax) -> bool:
         """One-launch HIP path: channel concat of NHWC bf16 device blobs, <= 8 parts."""
@@ -140,6 +142,11 @@ class ConcatLayer(Layer):
         if len(bottoms) == 1:
             tops[0].data = bottoms[0].data
             return
+        if self.zero_copy is not None:
+            buf = self.zero_copy.take()
+            if buf is not None and self.zero_copy.holds([b.data for b in bottoms], buf):
+                tops[0].data = buf  # every part already sits in its channel slice: no copy
+                return
         ax = _phys_axis(bottoms[0], self.axis)
         if self._hip_ok(bottoms, ax):
             from ..ops import hip
@@ -164,6 +171,15 @@ class ConcatLayer(Layer):
 
     def backward(self, tops, propagate_down, bottoms):
         ax = _phys_axis(bottoms[0], self.axis)
+        if self.zero_copy_bwd and tops[0].diff.is_cuda and tops[0].diff.is_contiguous():
+            # the output's consumers already applied the parts' ReLU masks: each part's
+            # gradient is a channel-slice view of the output gradient (the producing
+            # convolution reads it in place with the slice's pixel stride)
+            top_d = tops[0].diff
+            for i, (b, (off, c)) in enumerate(zip(bottoms, self.zero_copy.spans)):
+                if propagate_down[i]:
+                    b.diff = top_d[..., off:off + c]
+            return
         gates = [i in self.relu_gate_parts for i in range(len(bottoms))]
         if len(bottoms) > 1 and self._hip_ok(bottoms, ax):
             from ..ops import hip
@@ -189,6 +205,36 @@ class ConcatLayer(Layer):
                     d = top_d.narrow(ax, off, n)
                     b.diff = (d * (b.data > 0).to(d.dtype)) if gates[i] else d.contiguous()
             off += n
+
+
+class ConcatSlots:
+    """Zero-copy channel concat (engine.fuse_concat): the producing convolutions write their
+    outputs straight into channel slices [off, off + c) of one NHWC buffer — Caffe copies
+    every part (concat_layer.cu:9-25).  The buffer is allocated by the first producer of
+    an iteration and handed to the Concat layer's output by take()."""
+
+    def __init__(self, chans):
+        self.spans, off = [], 0
+        for c in chans:
+            self.spans.append((off, c))
+            off += c
+        self.total = off
+        self.buf = None
+
+    def slot(self, part: int, nhw, device) -> torch.Tensor:
+        nhw = tuple(int(v) for v in nhw)
+        if self.buf is None or tuple(self.buf.shape[:3]) != nhw or self.buf.device != device:
+            self.buf = torch.empty(nhw + (self.total,), dtype=torch.bfloat16, device=device)
+        off, c = self.spans[part]
+        return self.buf[..., off:off + c]
+
+    def take(self):
+        b, self.buf = self.buf, None
+        return b
+
+    def holds(self, parts, buf) -> bool:
+        return all(p.dim() == 4 and p.data_ptr() == buf.data_ptr() + 2 * off and p.shape[-1] == c
+                   and p.stride(2) == self.total for p, (off, c) in zip(parts, self.spans))
 
 
 @register("Slice")

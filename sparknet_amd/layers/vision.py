@@ -49,6 +49,7 @@ class ConvolutionLayer(Layer):
     fuse_relu = False  # set by the net's fusion pass when an in-place ReLU follows
     relu_gate = False  # ... and when an in-place ReLU PRODUCES the bottom (backward fused into dgrad)
     folded_input = None  # S2D-folded bottom 0 written by a fused augment (engine.fuse_input_fold)
+    concat_slot = None  # (ConcatSlots, part): top 0 is written into a zero-copy Concat buffer (engine.fuse_concat)
     flipped_weights = None  # dgrad weights flipped at the start of backward (engine.batch_weight_flips)
 
     def layer_setup(self, bottoms, tops):
@@ -100,6 +101,11 @@ class ConvolutionLayer(Layer):
                 t.data = self._forward_fp8(b.data, w, bias, s)
                 continue
             folded = self.folded_input if i == 0 else None
+            if self.concat_slot is not None and i == 0 and b.data.is_cuda:
+                slots, part = self.concat_slot
+                out = slots.slot(part, (s.N, s.P, s.Q), b.data.device)
+                t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i], out=out)
+                continue
             t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i], folded=folded)
 
     fp8_slots = None  # (x slot, w slot) in ctx.fp8 when the forward product runs in e4m3
@@ -324,10 +330,19 @@ class LRNLayer(Layer):
     def forward(self, bottoms, tops):
         tops[0].data = ops.lrn_forward(bottoms[0].data, self.size, self.alpha, self.beta, self.k, self.within)
 
+    relu_gate = False  # engine.fuse_relu_backward: the in-place ReLU producing the bottom
+
     def backward(self, tops, propagate_down, bottoms):
-        if propagate_down[0]:
-            bottoms[0].diff = ops.lrn_backward(tops[0].diff, bottoms[0].data, self.size, self.alpha,
-                                               self.beta, self.k, self.within, tops[0].data)
+        if not propagate_down[0]:
+            return
+        x = bottoms[0].data
+        if self.relu_gate and x.is_cuda:
+            from ..ops import hip
+            bottoms[0].diff = hip.lrn_backward(tops[0].diff, x, self.size, self.alpha, self.beta, self.k,
+                                               self.within, gate=True)
+            return
+        dx = ops.lrn_backward(tops[0].diff, x, self.size, self.alpha, self.beta, self.k, self.within, tops[0].data)
+        bottoms[0].diff = ops.relu_backward(dx, x) if self.relu_gate else dx
 
 
 @register("InnerProduct")

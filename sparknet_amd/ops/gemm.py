@@ -13,7 +13,9 @@ an fp32 workspace and are combined by a deterministic reduce kernel.
 """
 from __future__ import annotations
 
+import ast
 import ctypes as C
+import json
 import os
 from dataclasses import dataclass
 
@@ -93,13 +95,17 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
             "dense operand must be 16-B aligned"
         s = _lib.SnOperand(op.t.data_ptr(), op.ld, op.gstride, _lib.SnConvGeom())
         return s, 0 if op.kcontig else 1, OP_DENSE
-    assert op.x.dtype == elt and op.x.is_contiguous()
     g = op.geom
+    # contiguous NHWC, or a channel slice of a wider NHWC tensor whose pixel stride is g.C
+    assert op.x.dtype == elt and (op.x.is_contiguous() or (
+        op.x.dim() == 4 and op.x.stride(-1) == 1 and op.x.stride(2) == g.C and op.x.shape[-1] <= g.C)), \
+        "implicit conv operand must be NHWC (contiguous or a channel slice with pixel stride C)"
     cm = 16 if fp8 else 8
     assert g.Cg % cm == 0 and g.C % cm == 0, f"implicit conv needs channels % {cm} == 0"
     # the kernel's fp32-reciprocal index division is exact below 2^24
     assert g.N * g.P * g.Q < (1 << 24) and g.N * g.H * g.W < (1 << 24), "conv too large for one launch"
-    assert op.x.numel() < (1 << 31), "implicit conv uses 32-bit element offsets"
+    assert g.N * g.H * g.W * g.C < (1 << 31), "implicit conv uses 32-bit element offsets"
+    assert op.x.data_ptr() % 16 == 0, "implicit conv operand must be 16-B aligned"
     s = _lib.SnOperand(op.x.data_ptr(), 0, op.gstride, g.c_struct())
     return s, 0 if op.kcontig else 1, OP_IM2COL
 
@@ -138,7 +144,7 @@ def _cost(tiles: int, ktiles: int, s: int, out_elems: int, tile: int = 0) -> flo
     kt = -(-ktiles // s)
     t = -(-tiles * s // _SLOTS.get(tile, SLOTS)) * (kt + BLOCK_OVERHEAD) * _KTILE_US.get(tile, KTILE_US)
     if s > 1:
-        t += (out_elems * 4.0 * (s + 1)) / REDUCE_BW * 1e6 + (0.0 if _FIXUP and tile not in _TILE256_IDS else 3.0)
+        t += (out_elems * 4.0 * (s + 1)) / REDUCE_BW * 1e6 + 3.0
     return t
 
 
@@ -261,22 +267,6 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
         return
-    if _FIXUP and tile not in _TILE256_IDS:
-        # in-kernel split-K: tile-major fp32 slabs + per-tile arrival counters; the last
-        # split of each tile sums the slabs (split order) and runs the real epilogue
-        tiles = tm_ * tn_ * groups
-        ws = torch.empty(tiles * splits * bm * bn, dtype=torch.float32, device=out.device)
-        assert ws.numel() * 4 < (1 << 31), "split-K slabs exceed the 2 GB buffer range"
-        ctr = _counters(out.device, tiles)
-        e = EPI_BF16_DROP if (epi == EPI_BF16 and xtra[0]) else epi
-        args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, e,
-                               sa, sb, out.data_ptr(), ldc, c_gstride, 0,
-                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster,
-                               ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), ws.data_ptr(), ctr)
-        _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
-        if _lib.DEBUG_SYNC:
-            _lib.debug_sync("gemm")
-        return
     ldw = -(-N // 4) * 4  # fp32 slabs keep 16-B rows (the ones column makes N odd)
     ws = torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device)
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
@@ -290,36 +280,6 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
               C.c_void_p(rng), int(dstream), float(ratio), float(gscale))
 
 
-# In-kernel split-K (SnGemmArgs.counters): arrival counters come from a per-device ring of
-# zeroed int32 words; every launch leaves its words at zero again (the last split of a tile
-# re-arms its counter), so a region can be reused by any later launch on the same stream,
-# and launches that may run concurrently (branch streams, graph replays) get distinct
-# regions unless the ring wraps within one in-flight window (4M words).
-# Measured SLOWER than the separate reduce kernel and therefore off by default
-# (SN_SPLITK_FIXUP=1 enables it): CaffeNet 102k -> 86k img/s, GoogLeNet 19.6k -> 11.6k.
-# Split-K is chosen exactly when a product has few output tiles, so the last-arriving
-# block of each tile reduces s slabs on only `tiles` CUs (e.g. fc6 forward: 64 tiles x 16
-# slabs x 64 KB from memory) where the reduce kernel spreads the same bytes over all 256
-# CUs, and every split block also waits for its sc1 partial stores to reach memory before
-# it may signal (docs/PERF_NOTES.md).
-_FIXUP = os.environ.get("SN_SPLITK_FIXUP", "0") == "1"
-_TILE256_IDS = (6, 7, 8, 9)
-_RING_WORDS = 1 << 22
-_RINGS: dict = {}
-
-
-def _counters(device, n: int) -> int:
-    ring = _RINGS.get(device)
-    if ring is None:
-        ring = _RINGS[device] = [torch.zeros(_RING_WORDS, dtype=torch.int32, device=device), 0]
-    buf, pos = ring
-    assert n <= _RING_WORDS, n
-    if pos + n > _RING_WORDS:
-        pos = 0
-    ring[1] = pos + n
-    return buf.data_ptr() + 4 * pos
-
-
 # --- per-shape autotuning ----------------------------------------------------------------
 # The cost model picks a tile and split-K factor from the shape alone; the first eager
 # call of every distinct GEMM (shape, operand kinds and geometry, epilogue) instead times
@@ -329,6 +289,51 @@ def _counters(device, n: int) -> int:
 _AUTOTUNE = os.environ.get("SN_GEMM_AUTOTUNE", "1") != "0"
 _TUNED: dict = {}
 _TUNE_LOG = os.environ.get("SN_GEMM_TUNE_LOG", "0") == "1"
+_TUNE_PASSES = int(os.environ.get("SN_GEMM_TUNE_PASSES", "3"))
+# Tuning database: choices measured offline on an MI355X (scripts/build_tune_db.sh, many
+# more timing passes than a first-call tune) are loaded at import so the production
+# models run a fixed, reproducible tile / split-K per GEMM; first-call timing only fills
+# in products the database does not cover.  SN_GEMM_TUNE_DB=0 disables it, a path
+# overrides the packaged file.
+_DB_PATH = os.environ.get("SN_GEMM_TUNE_DB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                          "gemm_tuned.json"))
+
+
+def _key_to_str(key) -> str:
+    return repr(key[:-1] + (str(key[-1]).replace("torch.", ""),))
+
+
+def _key_from_str(s: str):
+    k = ast.literal_eval(s)
+    return k[:-1] + (getattr(torch, k[-1]),)
+
+
+def load_tune_db(path: str | None = None) -> int:
+    """Merge a tuning database (JSON {key: [tile, splits, kchunk]}) into the cache."""
+    path = path or _DB_PATH
+    if not path or path == "0" or not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        db = json.load(f)
+    for k, v in db.items():
+        _TUNED[_key_from_str(k)] = tuple(int(x) for x in v)
+    return len(db)
+
+
+def save_tune_db(path: str) -> int:
+    """Write every cached choice (database entries and first-call tunes) to ``path``,
+    merged over what the file already holds."""
+    db = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            db = json.load(f)
+    db.update({_key_to_str(k): list(v) for k, v in _TUNED.items()})
+    with open(path, "w") as f:
+        json.dump(dict(sorted(db.items())), f, indent=0)
+    return len(db)
+
+
+load_tune_db()
 
 
 def _geom_key(s) -> tuple:
@@ -377,10 +382,11 @@ def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, ga
     splits, kchunk = choose_splits(M, N, K, groups, tile)
     default = (tile, splits, kchunk)
     extent = (groups - 1) * c_gstride + (M - 1) * ldc + (N - (1 if ones >= 0 else 0))
-    if (not _AUTOTUNE or epi == EPI_SGD or not out.is_cuda or not out.is_contiguous() or extent > out.numel()
-            or torch.cuda.is_current_stream_capturing()):
+    if (not _AUTOTUNE or epi == EPI_SGD or not out.is_cuda or torch.cuda.is_current_stream_capturing()
+            or (out.is_contiguous() and extent > out.numel())):
         return default
-    scratch = torch.empty_like(out)
+    # a strided output (a channel slice of a zero-copy concat) is timed on a flat scratch
+    scratch = torch.empty_like(out) if out.is_contiguous() else torch.empty(extent, dtype=out.dtype, device=out.device)
     bscratch = torch.zeros_like(bias_grad) if bias_grad is not None else None
     runs = []
     for cand in _candidates(M, N, K, groups, b_kc_dense, epi):
@@ -399,12 +405,15 @@ def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, ga
     # interleaved passes; the minimum per candidate counts.  A candidate must beat the cost
     # model's pick by 3% to replace it, so timing noise cannot flip a choice.
     times = {c: float("inf") for c, _ in runs}
-    for _ in range(3):
+    # enough back-to-back launches per timed window that it spans >= ~150 us
+    est = _cost(-(-M // TILES[tile][0]) * -(-N // TILES[tile][1]) * groups, -(-K // BK), splits, M * N * groups, tile)
+    reps = max(4, min(32, int(150.0 / max(est, 1.0))))
+    for _ in range(_TUNE_PASSES):
         for cand, run in runs:
             torch.cuda._sleep(1 << 19)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(4):
+            for _ in range(reps):
                 run()
             e1.record()
             e1.synchronize()
@@ -415,7 +424,7 @@ def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, ga
     if _TUNE_LOG:
         print(f"[gemm-tune] M={M} N={N} K={K} g={groups} modes={ops[1:3]}/{ops[4:]} epi={epi} "
               f"default={default} best={best} " +
-              " ".join(f"{c[0]}/{c[1]}:{v * 250:.1f}" for c, v in sorted(times.items())), flush=True)
+              " ".join(f"{c[0]}/{c[1]}:{v * 1000 / reps:.1f}" for c, v in sorted(times.items())), flush=True)
     _TUNED[key] = best
     return best
 

@@ -27,6 +27,21 @@ def _c(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous() else t.contiguous()
 
 
+def chan_stride(t: torch.Tensor) -> int:
+    """Pixel stride (elements) of an NHWC tensor that is either contiguous or a channel
+    slice [..., c0:c0+C] of a contiguous [N, H, W, Ctot] tensor (the zero-copy concat
+    layout: a tower writes / reads its channels in place); 0 for any other layout."""
+    if t.is_contiguous():
+        return t.shape[-1]
+    if t.dim() != 4 or t.stride(-1) != 1:
+        return 0
+    N, H, W, Cc = t.shape
+    ld = t.stride(2)
+    if ld < Cc or t.stride(1) != W * ld or (N > 1 and t.stride(0) != H * W * ld):
+        return 0
+    return ld
+
+
 class WgradStream:
     """Weight gradients on a side stream.  A weight gradient (and, for fused InnerProduct
     layers, the solver update in its epilogue) feeds nothing later in backward, so while
@@ -148,13 +163,27 @@ def _s2d_input(x, s: ConvSpec, plan):
     return x2
 
 
-def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None):
+def _slice_ok(s: ConvSpec) -> bool:
+    """Convs whose input may be / output may go to a channel slice of a wider NHWC
+    tensor: ungrouped implicit-GEMM products (channel offsets stay 16-B aligned)."""
+    return s.groups == 1 and _implicit_ok(s) and s.Kg % 8 == 0
+
+
+def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=None):
     """ws: optional per-layer dict kept from forward to backward (the space-to-depth
     folded input is stored there so the weight-gradient pass does not rebuild it).
     folded: the S2D-folded input already produced upstream (fused augment + fold); x is
-    then not read."""
-    x = _c(x)
+    then not read.  out: a [N, P, Q, K] channel-slice view of a wider NHWC tensor to
+    write the output into (GEMM ldc = its pixel stride: a zero-copy Concat part); x may
+    itself be such a slice."""
+    ldx = chan_stride(x)
+    if not (ldx and _slice_ok(s)):
+        x, ldx = _c(x), s.C
     assert x.dtype == BF16 and w.dtype == BF16, (x.dtype, w.dtype)
+    if out is not None:
+        ldo = chan_stride(out)
+        assert _slice_ok(s) and ldo and tuple(out.shape) == (s.N, s.P, s.Q, s.K) and out.dtype == BF16, \
+            "conv output slice needs an ungrouped implicit conv and an NHWC channel-slice view"
     plan = _s2d_plan(s)
     if plan is not None:
         f, cp, rf, sf, s2 = plan
@@ -165,12 +194,17 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None):
             ws["s2d"] = (x.data_ptr(), x._version, x2)
         return conv_forward(x2, w2, b, s2, relu)
     M = s.N * s.P * s.Q
-    y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device)
+    if out is not None:
+        y, ldy = out, chan_stride(out)
+    else:
+        y, ldy = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device), s.K
     if _implicit_ok(s):
         kred = s.R * s.S * s.Cg
-        A = Im2col(x, _geom(s), kcontig=True, gstride=s.Cg)
+        g = _geom(s)
+        g.C = ldx  # pixel stride of the (possibly channel-sliced) input
+        A = Im2col(x, g, kcontig=True, gstride=s.Cg)
         B = Dense(_c(w.reshape(s.K, kred)), kred, True, gstride=s.Kg * kred)
-        gemm(M, s.Kg, kred, A, B, y, s.K, epi=EPI_BF16, groups=s.groups, c_gstride=s.Kg, bias=b, relu=relu)
+        gemm(M, s.Kg, kred, A, B, y, ldy, epi=EPI_BF16, groups=s.groups, c_gstride=s.Kg, bias=b, relu=relu)
         return y
     wp, kpad = _weight_kpad(w, s)
     y2 = y.view(M, s.K)
@@ -237,25 +271,30 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
     (the backward of a slope-0 in-place ReLU that produced x, fused into the dgrad).
     dw_acc / db_acc False: overwrite the gradient instead of accumulating (its buffer
     was not cleared, see Net.clear_param_diffs(lazy=True))."""
-    dy = _c(dy)
-    x = _c(x)
-    M = s.N * s.P * s.Q
-    dy2 = dy.view(M, s.K)
     kred = s.R * s.S * s.Cg
     plan = _s2d_plan(s) if s.Kg % 8 == 0 else None
+    ldd, ldx = chan_stride(dy), chan_stride(x)
+    if plan is not None or not _slice_ok(s) or not (ldd and ldx):
+        dy, ldd, x, ldx = _c(dy), s.K, _c(x), s.C
+    M = s.N * s.P * s.Q
+    # dy2: the [M, K] gradient matrix (row stride ldd: a channel slice of a zero-copy concat
+    # diff when ldd > K; only the ungrouped implicit paths below see such a view)
+    dy2 = dy.view(M, s.K) if ldd == s.K else dy
     # the bias gradient rides on the weight-gradient GEMM (ones column) on its implicit
     # paths; otherwise (no dw, explicit im2col) it is a separate column sum
     fused_db = db is not None and dw is not None and (
         plan is not None or (_implicit_ok(s) and s.Kg % 8 == 0))
     with wgrad_side():
-        _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc)
+        _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, ldd, ldx)
     if not need_dx:
         return None
-    return _conv_dgrad(dy, x, w, s, M, gate, ws)
+    return _conv_dgrad(dy, x, w, s, M, gate, ws, ldd, ldx)
 
 
-def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc):
+def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, ldd=0, ldx=0):
+    ldd, ldx = ldd or s.K, ldx or s.C
     if db is not None and not fused_db:
+        assert ldd == s.K
         colsum(dy2, db, accumulate=db_acc)
     if dw is not None and plan is not None:
         f, cp, rf, sf, s2 = plan
@@ -272,8 +311,10 @@ def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc):
         dw = None
     if dw is not None:
         if _implicit_ok(s) and s.Kg % 8 == 0:
-            A = Dense(dy2, s.K, kcontig=False, gstride=s.Kg)
-            B = Im2col(x, _geom(s), kcontig=False, gstride=s.Cg)
+            A = Dense(dy2, ldd, kcontig=False, gstride=s.Kg)
+            g = _geom(s)
+            g.C = ldx
+            B = Im2col(x, g, kcontig=False, gstride=s.Cg)
             gemm(s.Kg, kred, M, A, B, dw, kred, epi=EPI_F32_ACC if dw_acc else EPI_F32, groups=s.groups,
                  c_gstride=s.Kg * kred, bias_grad=db if fused_db else None, bias_acc=db_acc)
         else:
@@ -293,15 +334,17 @@ def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc):
                     dw2[g * s.Kg:(g + 1) * s.Kg].copy_(tmp[:s.Kg, :kred])
 
 
-def _conv_dgrad(dy, x, w, s, M, gate, ws):
-    dy2 = dy.view(M, s.K)
+def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0):
+    ldd, ldx = ldd or s.K, ldx or s.C
     dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
+    if gate is not None and ldx != s.C:  # the gate (= x, a channel slice) must share dx's layout
+        gate = _c(gate)
     if s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0:
         # dgrad == forward conv of dy with flipped / transposed weights, pad' = R-1-pad.
         # A flip pass + KC (ds_read_b128) B operand measures faster than reading the
         # weights in place through the FLIPW operand (MC, tr_b16 reads): 81k vs 86k img/s
         # on CaffeNet; FLIPW stays available via DGRAD_INPLACE_WEIGHTS.
-        g2 = ConvGeom(s.N, s.P, s.Q, s.K, s.H, s.W, s.R, s.S, 1, 1, s.R - 1 - s.ph, s.S - 1 - s.pw, 1, 1, s.Kg)
+        g2 = ConvGeom(s.N, s.P, s.Q, ldd, s.H, s.W, s.R, s.S, 1, 1, s.R - 1 - s.ph, s.S - 1 - s.pw, 1, 1, s.Kg)
         kr2 = s.R * s.S * s.Kg
         A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
         pre = ws.get("wt") if ws is not None else None  # flipped once for the net (FlipBatch)
@@ -318,6 +361,8 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws):
              gate=_c(gate) if gate is not None else None)
         return dx
     # generic: dcol = dy_g @ W_g, then col2im (gather, no atomics)
+    assert ldd == s.K
+    dy2 = dy.view(M, s.K)
     wp, kpad = _weight_kpad(w, s)
     kgp = _round8(s.Kg)
     for g in range(s.groups):
@@ -419,7 +464,9 @@ def lrn_forward(x, size, alpha, beta, k, within=False):
     return y
 
 
-def lrn_backward(dy, x, size, alpha, beta, k, within=False, y=None):
+def lrn_backward(dy, x, size, alpha, beta, k, within=False, y=None, gate=False):
+    """gate: also apply the backward of the slope-0 in-place ReLU that produced x (dx = 0
+    where x <= 0) — inside the across-channel kernel, as a pass after the within one."""
     x, dy = _c(x), _c(dy)
     N, H, W, Cc = x.shape
     dx = torch.empty_like(x)
@@ -427,8 +474,10 @@ def lrn_backward(dy, x, size, alpha, beta, k, within=False, y=None):
         sbuf = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         u = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         call("lrn_within_bwd", x, dy, sbuf, u, dx, N, H, W, Cc, size, float(alpha), float(beta))
+        if gate:
+            dx = relu_backward(dx, x)
     else:
-        call("lrn_across_bwd", x, dy, dx, N, H, W, Cc, size, float(alpha), float(beta), float(k))
+        call("lrn_across_bwd", x, dy, dx, N, H, W, Cc, size, float(alpha), float(beta), float(k), int(gate))
     return dx
 
 

@@ -163,6 +163,10 @@ def test_lrn(gpu, within, geo):
     close(y, ref.lrn_forward(x, size, a, bta, k, within))
     dy = rnd(N, H, W, Cc)
     close(hip.lrn_backward(dy, x, size, a, bta, k, within), ref.lrn_backward(dy, x, size, a, bta, k, within))
+    # fused backward of the in-place ReLU that produced x (GoogLeNet conv2/3x3 -> relu -> norm2)
+    xr = torch.relu(x)
+    gated = ref.relu_backward(ref.lrn_backward(dy, xr, size, a, bta, k, within), xr)
+    close(hip.lrn_backward(dy, xr, size, a, bta, k, within, gate=True), gated)
 
 
 def test_relu_dropout(gpu):

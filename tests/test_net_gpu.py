@@ -50,8 +50,9 @@ def test_relu_gate_fusion_on_gpu(gpu):
 
 
 def test_googlenet_concat_gate_on_gpu(gpu):
-    """GoogLeNet: HIP channel concat and the Inception ReLU masks applied in the concat
-    backward, fused vs unfused on the GPU, and the fused GPU pass vs the fp32 CPU engine."""
+    """GoogLeNet: zero-copy channel concat with the Inception ReLU masks applied by the
+    concat outputs' readers, fused vs unfused on the GPU, and the fused GPU pass vs the
+    fp32 CPU engine."""
     n = models.googlenet(train_batch=2, test_batch=2, crop=67, classes=7, aux=False)
     for l in n.layer:
         if l.type == "Dropout":
@@ -62,8 +63,11 @@ def test_googlenet_concat_gate_on_gpu(gpu):
             l.pooling_param.global_pooling = True
     l0, g0, net0 = _run(n, gpu, False)
     l1, g1, net = _run(n, gpu, True, weights=net0.flat_data.detach().float().cpu())
-    gated = sum(len(getattr(l, "relu_gate_parts", ())) for l in net.layers if l.type_name == "Concat")
-    assert gated == 9 * 4, gated
+    cats = [l for l in net.layers if l.type_name == "Concat"]
+    # zero-copy concat (engine.fuse_concat): the parts' ReLU masks moved into the readers
+    # of each concat output; otherwise they are applied in the concat backward
+    assert all(c.zero_copy_bwd and not c.relu_gate_parts for c in cats) or \
+        sum(len(c.relu_gate_parts) for c in cats) == 9 * 4
     assert abs(l0 - l1) <= 1e-3 * max(1.0, abs(l0))
     err = (g0 - g1).abs().max().item() / (g0.abs().max().item() + 1e-12)
     assert err < 1e-2, err
@@ -243,3 +247,44 @@ def test_fused_dropout_matches_standalone(gpu, monkeypatch):
     assert abs(l0 - l1) <= 1e-3 * max(1.0, abs(l0))
     err = (g0 - g1).abs().max().item() / (g0.abs().max().item() + 1e-12)
     assert err < 2e-2, err
+
+
+def test_googlenet_zero_copy_concat_bitwise(gpu, monkeypatch):
+    """engine.fuse_concat: the Inception towers' convolutions write into channel slices of
+    the concat buffer, the ReLU gates move into the readers of the concat output and the
+    parts' gradients are slice views read in place by the wgrad / dgrad GEMMs.  Loss and
+    every parameter gradient are bitwise equal to the copying Concat (same GEMM tiles:
+    autotuning off), and no concat copy kernel runs."""
+    from sparknet_amd.engine import fuse_relu
+    from sparknet_amd.ops import gemm as G
+    monkeypatch.setattr(G, "_AUTOTUNE", False)
+    monkeypatch.setattr(G, "_TUNED", {})  # no tile choices cached by earlier tests
+    n = models.googlenet(train_batch=4, test_batch=4, crop=67, classes=7, aux=True)
+    for l in n.layer:
+        if l.type == "Dropout":
+            l.dropout_param.dropout_ratio = 0.0
+        if l.name in ("pool5/7x7_s1", "loss1/ave_pool", "loss2/ave_pool"):
+            for f in ("kernel_h", "kernel_w", "stride_h", "stride_w", "kernel_size", "stride"):
+                l.pooling_param.ClearField(f)
+            l.pooling_param.global_pooling = True
+    res = {}
+    for mode in ("copy", "zero"):
+        monkeypatch.setenv("SN_ZERO_COPY_CONCAT", "1" if mode == "zero" else "0")
+        net = Net(n, phase=proto.TRAIN, seed=3, device=gpu)
+        fuse_relu(net)
+        cats = [l for l in net.layers if l.type_name == "Concat"]
+        if mode == "zero":
+            assert cats and all(c.zero_copy is not None and c.zero_copy_bwd for c in cats)
+        g = torch.Generator().manual_seed(5)
+        net.blob_by_name("data").set_nchw(torch.randn(4, 3, 67, 67, generator=g) * 20)
+        net.blob_by_name("label").set_nchw(torch.tensor([[1.0], [5.0], [0.0], [6.0]]))
+        out = []
+        for _ in range(2):
+            net.clear_param_diffs()
+            loss = net.forward_backward()
+            torch.cuda.synchronize()
+            out.append((float(loss), net.flat_diff.detach().clone()))
+        res[mode] = out
+    for (la, ga), (lb, gb) in zip(res["copy"], res["zero"]):
+        assert la == lb
+        assert torch.equal(ga, gb)
