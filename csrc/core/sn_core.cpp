@@ -8,11 +8,17 @@
 #include <Python.h>
 #include <dlfcn.h>
 
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
+#include <vector>
 
 #include "sn_core.h"
 
@@ -141,11 +147,245 @@ int parse_file(const char* fn, const char* path, char** out, int* len) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Native step executor.  The reference's solver_step (ccaffe.cpp:230-233) runs Caffe's C++
+// Solver::Step; here sn_solver_step on a GPU state runs its iterations in this loop with no
+// Python involved: CoreState.native_plan (capi.py) captures one full training iteration
+// (every kernel from libsn_kernels) into a hipGraph and returns the handles and device
+// buffers; per iteration this code calls the C data callbacks (the JavaData contract,
+// java_data_layer.cpp:37-44), copies each minibatch into its data blob (pinned staging +
+// sn_stage_nchw_f32_bf16 for NHWC image blobs), stages the learning rate (SGDSolver::
+// GetLearningRate, sgd_solver.cpp:27-63) into the solver's hyper-parameter buffer and
+// launches the graph.  Python is re-entered only for display / snapshot iterations.
+
+typedef int (*stage_fn_t)(const float*, void*, long long, long long, long long, long long, hipStream_t);
+
+struct Feed {
+  void* dev = nullptr;
+  int kind = 0;  // 1: 4-D image blob (bf16 NHWC), 0: fp32 blob copied as is
+  std::vector<int> shape;
+  long long count = 0;
+  sn_data_callback_t cb = nullptr;
+  void* user = nullptr;
+  float* host = nullptr;     // pinned
+  float* staging = nullptr;  // device fp32 NCHW (kind 1)
+};
+
+struct NativeStep {
+  hipGraphExec_t exec = nullptr;
+  hipStream_t stream = nullptr;
+  float* hyper_dev = nullptr;
+  float hyper[16] = {};
+  float last_lr = -1.f;
+  static constexpr int RING = 8;
+  float* hyper_host = nullptr;  // pinned, RING x 16
+  hipEvent_t hyper_ev[RING] = {};
+  int ring_pos = 0;
+  float* loss_dev = nullptr;
+  float* loss_ring = nullptr;  // device, average_loss slots
+  std::vector<float> loss_host;
+  std::vector<Feed> feeds;
+  hipEvent_t fed = nullptr;
+  bool fed_pending = false;
+  int policy = 0, adam = 0, display = 0, snapshot = 0, average_loss = 1;
+  double base_lr = 0, gamma = 0, power = 0, momentum = 0, momentum2 = 0;
+  long long stepsize = 0, max_iter = 0, iter = 0, done = 0;
+  std::vector<long long> stepvalues;
+  stage_fn_t stage = nullptr;
+
+  ~NativeStep() {
+    if (stream) hipStreamSynchronize(stream);
+    for (auto& f : feeds) {
+      if (f.host) hipHostFree(f.host);
+      if (f.staging) hipFree(f.staging);
+    }
+    for (auto& e : hyper_ev)
+      if (e) hipEventDestroy(e);
+    if (fed) hipEventDestroy(fed);
+    if (hyper_host) hipHostFree(hyper_host);
+    if (loss_ring) hipFree(loss_ring);
+  }
+
+  double learning_rate(long long it) const {
+    switch (policy) {
+      case 0: return base_lr;
+      case 1: return base_lr * std::pow(gamma, (double)(it / (stepsize > 0 ? stepsize : 1)));
+      case 2: return base_lr * std::pow(gamma, (double)it);
+      case 3: return base_lr * std::pow(1.0 + gamma * (double)it, -power);
+      case 4: {
+        long long cur = 0;
+        while (cur < (long long)stepvalues.size() && it >= stepvalues[cur]) ++cur;
+        return base_lr * std::pow(gamma, (double)cur);
+      }
+      case 5: return base_lr * std::pow(1.0 - (double)it / (double)max_iter, power);
+      default: return base_lr * (1.0 / (1.0 + std::exp(-gamma * ((double)it - (double)stepsize))));
+    }
+  }
+};
+
+std::mutex g_native_mu;
+std::unordered_map<void*, std::unique_ptr<NativeStep>> g_native;
+
+void drop_native(void* s) {
+  std::lock_guard<std::mutex> lk(g_native_mu);
+  g_native.erase(s);
+}
+
+#define HIPOK(x)                                                   \
+  do {                                                             \
+    hipError_t e_ = (x);                                           \
+    if (e_ != hipSuccess) {                                        \
+      g_err = std::string(#x) + ": " + hipGetErrorString(e_);      \
+      if (g_err_cb) g_err_cb(g_err.c_str());                       \
+      return 1;                                                    \
+    }                                                              \
+  } while (0)
+
+long long dict_ll(PyObject* d, const char* k) {
+  PyObject* v = PyDict_GetItemString(d, k);
+  return v ? PyLong_AsLongLong(v) : 0;
+}
+double dict_f(PyObject* d, const char* k) {
+  PyObject* v = PyDict_GetItemString(d, k);
+  return v ? PyFloat_AsDouble(v) : 0.0;
+}
+
+// Build the executor from CoreState.native_plan() (GIL held).  Returns the iterations the
+// plan's capture already ran, or -1 (g_err set; the caller falls back to Python).
+long long build_native(void* s, std::unique_ptr<NativeStep>& out) {
+  PyObject* r = call(s, "native_plan", nullptr);
+  if (!r) return -1;
+  long long ran = PyLong_AsLongLong(PyTuple_GetItem(r, 0));
+  PyObject* d = PyTuple_GetItem(r, 1);
+  auto ns = std::make_unique<NativeStep>();
+  ns->exec = (hipGraphExec_t)(uintptr_t)dict_ll(d, "exec");
+  ns->stream = (hipStream_t)(uintptr_t)dict_ll(d, "stream");
+  ns->hyper_dev = (float*)(uintptr_t)dict_ll(d, "hyper_dev");
+  ns->loss_dev = (float*)(uintptr_t)dict_ll(d, "loss_dev");
+  ns->iter = dict_ll(d, "iter");
+  ns->policy = (int)dict_ll(d, "policy");
+  ns->base_lr = dict_f(d, "base_lr");
+  ns->gamma = dict_f(d, "gamma");
+  ns->power = dict_f(d, "power");
+  ns->stepsize = dict_ll(d, "stepsize");
+  ns->max_iter = dict_ll(d, "max_iter");
+  ns->adam = (int)dict_ll(d, "adam");
+  ns->momentum = dict_f(d, "momentum");
+  ns->momentum2 = dict_f(d, "momentum2");
+  ns->display = (int)dict_ll(d, "display");
+  ns->snapshot = (int)dict_ll(d, "snapshot");
+  ns->average_loss = (int)dict_ll(d, "average_loss");
+  PyObject* hv = PyDict_GetItemString(d, "hyper");
+  for (int i = 0; i < 16 && hv && i < PyList_Size(hv); ++i) ns->hyper[i] = (float)PyFloat_AsDouble(PyList_GetItem(hv, i));
+  PyObject* sv = PyDict_GetItemString(d, "stepvalues");
+  for (Py_ssize_t i = 0; sv && i < PyList_Size(sv); ++i) ns->stepvalues.push_back(PyLong_AsLongLong(PyList_GetItem(sv, i)));
+  PyObject* fl = PyDict_GetItemString(d, "feeds");
+  for (Py_ssize_t i = 0; fl && i < PyList_Size(fl); ++i) {
+    PyObject* f = PyList_GetItem(fl, i);
+    Feed fd;
+    fd.dev = (void*)(uintptr_t)dict_ll(f, "dev");
+    fd.kind = (int)dict_ll(f, "kind");
+    fd.cb = (sn_data_callback_t)(uintptr_t)dict_ll(f, "cb");
+    fd.user = (void*)(uintptr_t)dict_ll(f, "user");
+    PyObject* sh = PyDict_GetItemString(f, "shape");
+    fd.count = 1;
+    for (Py_ssize_t k = 0; sh && k < PyTuple_Size(sh); ++k) {
+      fd.shape.push_back((int)PyLong_AsLong(PyTuple_GetItem(sh, k)));
+      fd.count *= fd.shape.back();
+    }
+    ns->feeds.push_back(fd);
+  }
+  Py_DECREF(r);
+  if (PyErr_Occurred()) {
+    fetch_error("native_plan");
+    return -1;
+  }
+  ns->stage = (stage_fn_t)dlsym(RTLD_DEFAULT, "sn_stage_nchw_f32_bf16");
+  if (!ns->stage) {
+    g_err = "native step: sn_stage_nchw_f32_bf16 not found (libsn_kernels not loaded)";
+    return -1;
+  }
+  auto fail = [&](hipError_t e, const char* what) {
+    g_err = std::string("native step: ") + what + ": " + hipGetErrorString(e);
+    return -1;
+  };
+  hipError_t e;
+  for (auto& f : ns->feeds) {
+    if ((e = hipHostMalloc((void**)&f.host, sizeof(float) * f.count, 0)) != hipSuccess) return fail(e, "hipHostMalloc");
+    if (f.kind == 1 && (e = hipMalloc((void**)&f.staging, sizeof(float) * f.count)) != hipSuccess)
+      return fail(e, "hipMalloc");
+  }
+  if ((e = hipHostMalloc((void**)&ns->hyper_host, sizeof(float) * 16 * NativeStep::RING, 0)) != hipSuccess)
+    return fail(e, "hipHostMalloc");
+  for (auto& ev : ns->hyper_ev)
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return fail(e, "hipEventCreate");
+  if ((e = hipEventCreateWithFlags(&ns->fed, hipEventDisableTiming)) != hipSuccess) return fail(e, "hipEventCreate");
+  if ((e = hipMalloc((void**)&ns->loss_ring, sizeof(float) * ns->average_loss)) != hipSuccess) return fail(e, "hipMalloc");
+  ns->loss_host.assign(ns->average_loss, 0.f);
+  out = std::move(ns);
+  return ran;
+}
+
+// One training iteration (no GIL needed).
+int native_iteration(NativeStep& ns) {
+  // the host staging buffers are reused: the previous iteration's copies must have left
+  if (ns.fed_pending) HIPOK(hipEventSynchronize(ns.fed));
+  for (auto& f : ns.feeds) f.cb(f.host, f.shape.empty() ? 0 : f.shape[0], (int)f.shape.size(), f.shape.data(), f.user);
+  for (auto& f : ns.feeds) {
+    if (f.kind == 1) {
+      HIPOK(hipMemcpyAsync(f.staging, f.host, sizeof(float) * f.count, hipMemcpyHostToDevice, ns.stream));
+      if (ns.stage(f.staging, f.dev, f.shape[0], f.shape[1], f.shape[2], f.shape[3], ns.stream)) {
+        g_err = "native step: staging kernel launch failed";
+        return 1;
+      }
+    } else {
+      HIPOK(hipMemcpyAsync(f.dev, f.host, sizeof(float) * f.count, hipMemcpyHostToDevice, ns.stream));
+    }
+  }
+  if (!ns.feeds.empty()) {
+    HIPOK(hipEventRecord(ns.fed, ns.stream));
+    ns.fed_pending = true;
+  }
+  // hyper-parameters (Solver.hyper_values layout: 0 lr, 8 Adam correction)
+  const float lr = (float)ns.learning_rate(ns.iter);
+  float corr = ns.hyper[8];
+  if (ns.adam) {
+    const double t = (double)(ns.iter + 1);
+    corr = (float)(std::sqrt(1.0 - std::pow(ns.momentum2, t)) / (1.0 - std::pow(ns.momentum, t)));
+  }
+  if (lr != ns.last_lr || (ns.adam && corr != ns.hyper[8])) {
+    const int slot = ns.ring_pos;
+    ns.ring_pos = (ns.ring_pos + 1) % NativeStep::RING;
+    HIPOK(hipEventSynchronize(ns.hyper_ev[slot]));  // that slot's previous copy has left
+    float* h = ns.hyper_host + 16 * slot;
+    std::memcpy(h, ns.hyper, sizeof(ns.hyper));
+    h[0] = lr;
+    h[8] = corr;
+    h[9] = 0.f;  // H_T: host-side only
+    HIPOK(hipMemcpyAsync(ns.hyper_dev, h, sizeof(float) * 16, hipMemcpyHostToDevice, ns.stream));
+    HIPOK(hipEventRecord(ns.hyper_ev[slot], ns.stream));
+    ns.last_lr = lr;
+    ns.hyper[8] = corr;
+  }
+  HIPOK(hipGraphLaunch(ns.exec, ns.stream));
+  HIPOK(hipMemcpyAsync(ns.loss_ring + (ns.iter % ns.average_loss), ns.loss_dev, sizeof(float),
+                       hipMemcpyDeviceToDevice, ns.stream));
+  ++ns.iter;
+  ++ns.done;
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* sn_last_error(void) { return g_err.c_str(); }
+
+long long sn_native_iterations(void* s) {
+  std::lock_guard<std::mutex> lk(g_native_mu);
+  auto it = g_native.find(s);
+  return it == g_native.end() ? 0 : it->second->done;
+}
 
 void* sn_create_state(void) {
   ensure_interpreter();
@@ -158,16 +398,22 @@ void* sn_create_state(void) {
 
 void sn_destroy_state(void* state) {
   if (!state) return;
+  {
+    std::lock_guard<std::mutex> lk(g_native_mu);
+    g_native.erase(state);  // before the Python state (which owns the captured graph)
+  }
   Gil g;
   Py_DECREF(static_cast<PyObject*>(state));
 }
 
 int sn_set_device(void* s, int device) {
+  drop_native(s);
   Gil g;
   return status(call(s, "set_device", "(i)", device));
 }
 
 int sn_load_solver_from_protobuf(void* s, const char* bytes, int len) {
+  drop_native(s);
   Gil g;
   return status(call(s, "load_solver", "(y#)", bytes, (Py_ssize_t)len));
 }
@@ -184,6 +430,7 @@ static int set_cb(void* s, int test, int layer, sn_data_callback_t cb, void* use
 }
 
 int sn_set_train_data_callback(void* s, int layer, sn_data_callback_t cb, void* user) {
+  drop_native(s);  // the native executor binds the callbacks it was built with
   return set_cb(s, 0, layer, cb, user);
 }
 
@@ -206,8 +453,54 @@ int sn_backward(void* s) {
 }
 
 int sn_solver_step(void* s, int iters) {
+  if (iters <= 0) return 0;
+  NativeStep* ns = nullptr;
+  {
+    Gil g;
+    std::lock_guard<std::mutex> lk(g_native_mu);
+    auto it = g_native.find(s);
+    if (it != g_native.end()) {
+      ns = it->second.get();
+    } else if (std::getenv("SN_NATIVE_STEP") == nullptr || std::strcmp(std::getenv("SN_NATIVE_STEP"), "0") != 0) {
+      PyObject* dev = call(s, "native_eligible", nullptr);
+      const bool ok = dev && PyObject_IsTrue(dev) == 1;
+      Py_XDECREF(dev);
+      PyErr_Clear();
+      if (ok && iters > 3) {
+        std::unique_ptr<NativeStep> built;
+        const long long ran = build_native(s, built);
+        if (ran >= 0) {
+          ns = built.get();
+          g_native[s] = std::move(built);
+          iters -= (int)ran;
+        }
+      }
+    }
+    if (!ns) return status(call(s, "step", "(i)", iters));
+  }
+  // native loop: no GIL; Python only for display / snapshot iterations
+  for (int i = 0; i < iters; ++i) {
+    if (native_iteration(*ns)) return 1;
+    const long long it = ns->iter;
+    const bool disp = ns->display && (it - 1) % ns->display == 0;
+    const bool snap = ns->snapshot && it % ns->snapshot == 0;
+    if (disp || snap) {
+      HIPOK(hipStreamSynchronize(ns->stream));
+      float smoothed = -1.f;
+      if (disp) {
+        const long long n = ns->done < ns->average_loss ? ns->done : ns->average_loss;
+        HIPOK(hipMemcpy(ns->loss_host.data(), ns->loss_ring, sizeof(float) * ns->average_loss, hipMemcpyDeviceToHost));
+        double acc = 0;
+        for (long long k = 0; k < n; ++k) acc += ns->loss_host[(it - 1 - k) % ns->average_loss];
+        smoothed = (float)(acc / (double)(n > 0 ? n : 1));
+      }
+      Gil g;
+      if (status(call(s, "native_event", "(Ldi)", it, (double)smoothed, (int)snap))) return 1;
+    }
+  }
+  HIPOK(hipStreamSynchronize(ns->stream));
   Gil g;
-  return status(call(s, "step", "(i)", iters));
+  return status(call(s, "native_done", "(L)", ns->iter));
 }
 
 int sn_solver_test(void* s, int iters) {

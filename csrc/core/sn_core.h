@@ -28,7 +28,11 @@ int sn_set_test_data_callback(void* state, int layer_index, sn_data_callback_t c
 
 int sn_forward(void* state, float* loss);
 int sn_backward(void* state);
+// On a GPU state the iterations run in a native C++ loop over a captured hipGraph of one
+// training iteration (the first call captures it, running 3 iterations through Python);
+// SN_NATIVE_STEP=0 keeps every iteration on the Python engine.
 int sn_solver_step(void* state, int iters);
+long long sn_native_iterations(void* state);  // iterations run by the native loop so far
 int sn_solver_test(void* state, int iters);  // returns the number of scores (>= 0) or -1
 float sn_get_test_score(void* state, int index);
 

@@ -130,6 +130,30 @@ extern "C" int sn_cast_f32_bf16(const float* src, bf16_t* dst, long long n, hipS
   return SN_CHECK_LAUNCH();
 }
 
+// Host-fed input staging for the native step executor (csrc/core/sn_core.cpp): a logical
+// NCHW fp32 minibatch (the JavaData callback contract, CaffeLibrary.java:12-14) converted
+// to the blob's physical NHWC bf16 layout.  One thread per output element, so the bf16
+// stores are coalesced; the fp32 reads stride by H*W (the minibatch sits in L2).
+__global__ void stage_nchw_f32_bf16(const float* __restrict__ src, bf16_t* __restrict__ dst, int C, int HW,
+                                    long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long pix = i / C;
+    const int c = (int)(i - pix * C);
+    const long long img = pix / HW;
+    const int hw = (int)(pix - img * HW);
+    dst[i] = f2bf(src[(img * C + c) * HW + hw]);
+  }
+}
+
+extern "C" int sn_stage_nchw_f32_bf16(const float* src, bf16_t* dst, long long N, long long C, long long H,
+                                      long long W, hipStream_t st) {
+  const long long n = N * C * H * W;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(stage_nchw_f32_bf16, dim3(sn_blocks(n, 256, 16384)), dim3(256), 0, st, src, dst, (int)C,
+                     (int)(H * W), n);
+  return SN_CHECK_LAUNCH();
+}
+
 // out = sum_k in_k (k <= 8), bf16 with fp32 accumulation; K is a template parameter so
 // the K loads of an iteration are issued together.
 struct Ptrs8 { const bf16_t* p[8]; };

@@ -105,7 +105,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     with cf.ThreadPoolExecutor(jobs) as ex:
         hip_objs = list(ex.map(lambda s: _compile(s, True), hip_srcs))
         cpp_objs = list(ex.map(lambda s: _compile(s, False), cpp_srcs))
-        core_objs = list(ex.map(lambda s: _compile(s, False, [*py_inc, f"-I{CSRC / 'core'}"]), core_srcs))
+        core_objs = list(ex.map(lambda s: _compile(s, False, [*py_inc, f"-I{CSRC / 'core'}", "-D__HIP_PLATFORM_AMD__=1",
+                                                              f"-I{ROCM}/include"]), core_srcs))
     out = {}
     if hip_objs:
         if force or _stale(KERNEL_LIB, hip_objs):
@@ -119,7 +120,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         out["runtime"] = str(RUNTIME_LIB)
     if core_objs:
         if force or _stale(CORE_LIB, core_objs):
-            _run(["g++", "-shared", "-fPIC", "-pthread", *map(str, core_objs), *py_link, "-o", str(CORE_LIB)])
+            _run(["g++", "-shared", "-fPIC", "-pthread", *map(str, core_objs), *py_link, *RUNTIME_LINK, "-ldl",
+                  "-o", str(CORE_LIB)])
         out["core"] = str(CORE_LIB)
     if verbose:
         print(out)

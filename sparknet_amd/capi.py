@@ -96,6 +96,96 @@ class CoreState:
     def step(self, n: int) -> None:
         self.solver.step(n)
 
+    # -- native step executor (csrc/core/sn_core.cpp NativeStep) ---------------------------
+    # On the GPU, sn_solver_step runs training iterations without Python: this method
+    # captures ONE full iteration (forward, backward, fused solver update — every kernel a
+    # HIP kernel of libsn_kernels) into a hipGraph through engine.GraphStep, running
+    # `warmup` eager iterations plus the capture's replay as real iterations fed by the
+    # Python path, and hands the C++ executor the graph-exec handle, the stream, the device
+    # buffers it stages callback data / hyper-parameters into and the solver schedule.
+    # Per iteration the C++ loop then calls the C data callbacks, copies the minibatches
+    # into the data blobs (sn_stage_nchw_f32_bf16 for images), stages the learning rate and
+    # launches the graph; Python is re-entered only at display / snapshot iterations.
+    NATIVE_WARMUP = 2
+
+    def native_eligible(self) -> bool:
+        return self.device.type == "cuda" and self.solver is not None and self.net is self.solver.net
+
+    def native_plan(self) -> tuple:
+        """-> (iterations already run, plan dict of ints / floats) or raises if the
+        state cannot run natively (CPU device, solver features the graph cannot hold)."""
+        from .engine import GraphStep
+        from .layers.data import ExternalDataLayer
+        s = self.solver
+        if self.device.type != "cuda" or s is None:
+            raise RuntimeError("native stepping needs a GPU solver")
+        p = s.param
+        if p.iter_size > 1 or p.clip_gradients > 0 or s.callbacks or s.action_request is not None:
+            raise RuntimeError("native stepping: iter_size / clip_gradients / callbacks / action requests "
+                               "stay on the Python path")
+        net = self.net
+        feeds = []
+        for li, layer in enumerate(net.layers):
+            if isinstance(layer, ExternalDataLayer) and layer.source is not None:
+                if (False, li) not in self._callbacks:
+                    raise RuntimeError(f"data layer {layer.name!r} has a non-C source")
+                fn, user = self._callbacks[(False, li)]
+                top = net.top_vecs[li][0]
+                t = top.data
+                if len(top.shape) == 4:
+                    assert t.dtype == torch.bfloat16 and t.is_contiguous()
+                    kind, dims = 1, tuple(top.shape)
+                else:
+                    assert t.dtype == torch.float32 and t.is_contiguous()
+                    kind, dims = 0, tuple(top.shape)
+                feeds.append((layer, layer.source, {"dev": t.data_ptr(), "kind": kind, "shape": dims,
+                                                    "cb": C.cast(fn, C.c_void_p).value, "user": user or 0}))
+        for layer, _, _ in feeds:
+            layer.set_source(None)  # inside the graph the blobs are already staged (restored below)
+
+        def pre():
+            for layer, src, _ in feeds:
+                src(layer, net.top_vecs[net.layers.index(layer)])
+
+        it0 = s.iter
+        self._graph_step = GraphStep(s, warmup=self.NATIVE_WARMUP, pre=pre, overlap=False)
+        s.stage_hyper()
+        try:
+            loss = self._graph_step.step()  # warmup iterations + capture + one replay
+        finally:
+            for layer, src, _ in feeds:  # the Python verbs (sn_forward, ...) keep their feeds
+                layer.set_source(src)
+        torch.cuda.synchronize(self.device)
+        pol = ["fixed", "step", "exp", "inv", "multistep", "poly", "sigmoid"].index(p.lr_policy)
+        hyper = s.hyper_values(s.get_learning_rate())
+        plan = {
+            "exec": int(self._graph_step.graph.raw_cuda_graph_exec()),
+            "stream": int(torch.cuda.current_stream(self.device).cuda_stream),
+            "hyper_dev": int(s.hyper.data_ptr()), "hyper": [float(v) for v in hyper],
+            "loss_dev": int(loss.data_ptr()), "iter": int(s.iter),
+            "policy": pol, "base_lr": float(p.base_lr), "gamma": float(p.gamma), "power": float(p.power),
+            "stepsize": int(p.stepsize), "max_iter": int(p.max_iter), "stepvalues": [int(v) for v in p.stepvalue],
+            "adam": int(s.type == "Adam"), "momentum": float(p.momentum), "momentum2": float(p.momentum2),
+            "display": int(p.display), "snapshot": int(p.snapshot), "average_loss": max(1, int(p.average_loss)),
+            "feeds": [f for _, _, f in feeds],
+        }
+        return s.iter - it0, plan
+
+    def native_event(self, it: int, smoothed_loss: float, snapshot: int) -> None:
+        """Display / snapshot iteration reached by the native loop (Solver.step's logging
+        and snapshot, solver.cpp:227-262)."""
+        s = self.solver
+        s.iter = it
+        if smoothed_loss == smoothed_loss and smoothed_loss >= 0:
+            import logging
+            s.smoothed_loss = smoothed_loss
+            logging.getLogger("sparknet_amd.solver").info("Iteration %d, loss = %g", it - 1, smoothed_loss)
+        if snapshot:
+            s.snapshot()
+
+    def native_done(self, it: int) -> None:
+        self.solver.iter = it
+
     def test(self, n: int) -> int:
         """solver_test -> TestAndStoreResult (solver.cpp:413-444): sum of every output
         blob over n forwards; returns the number of scores."""

@@ -51,6 +51,7 @@ int main(int argc, char** argv) {
   CHECK(sn_set_train_data_callback(st, 0, data_cb, NULL));
   CHECK(sn_set_train_data_callback(st, 1, label_cb, NULL));
   CHECK(sn_solver_step(st, 5));
+  printf("native=%lld\n", sn_native_iterations(st)); /* > 0 on a GPU: the C++ step loop ran */
   CHECK(sn_load_net_from_protobuf(st, "\xff\xff\xff", 3) == 0); /* garbage bytes must fail cleanly */
   int nl = sn_num_layers(st);
   char name[64];

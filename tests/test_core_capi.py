@@ -39,6 +39,8 @@ def _c_host_program(tmp_path, device):
     r = subprocess.run([str(exe), SOLVER, str(tmp_path / "w.caffemodel"), str(device), str(db)],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout, r.stderr[-3000:])
+    if device < 0:
+        assert "native=0" in r.stdout
     assert "layers=7 layer2=conv1" in r.stdout and "callbacks=6" in r.stdout
     assert "weights2=2" in r.stdout and "blob0=data" in r.stdout
     from sparknet_amd.data.db import DatumReader
@@ -47,10 +49,19 @@ def _c_host_program(tmp_path, device):
     assert len(rd) == 5 and [rd.get(i).label for i in range(5)] == [0, 1, 2, 3, 4]
     assert list(rd.get(3).data[:2]) == [144, 145]
     assert read_mean_binaryproto(str(db) + ".mean.binaryproto").reshape(-1).tolist() == [1.0, 2.0, 3.0]
+    return r.stdout
 
 
 def test_c_host_program(core_lib, tmp_path):
     _c_host_program(tmp_path, -1)
+
+
+@pytest.mark.gpu
+def test_c_host_program_gpu_native_step(core_lib, tmp_path):
+    """The same C host program on the GPU: sn_solver_step captures one iteration and runs
+    the remaining ones in the native C++ loop (sn_native_iterations > 0)."""
+    out = _c_host_program(tmp_path, 0)
+    assert "native=2" in out, out
 
 
 
@@ -90,3 +101,53 @@ def test_ctypes_inside_python(core_lib, tmp_path):
     assert np.isfinite(np.frombuffer(w, dtype=np.float32)).all()
     lib.sn_free(buf)
     lib.sn_destroy_state(st)
+
+
+def _ctypes_train(core_lib, device, iters, native):
+    lib = C.CDLL(core_lib)
+    lib.sn_create_state.restype = C.c_void_p
+    lib.sn_last_error.restype = C.c_char_p
+    lib.sn_num_params.restype = C.c_longlong
+    lib.sn_native_iterations.restype = C.c_longlong
+    os.environ["SN_NATIVE_STEP"] = "1" if native else "0"
+    try:
+        st = C.c_void_p(lib.sn_create_state())
+        buf, n = C.c_char_p(), C.c_int()
+        assert lib.sn_parse_solver_prototxt(SOLVER.encode(), C.byref(buf), C.byref(n)) == 0
+        assert lib.sn_set_device(st, device) == 0
+        assert lib.sn_load_solver_from_protobuf(st, buf, n) == 0, lib.sn_last_error()
+        calls = [0]
+
+        def fill(p, batch, nd, shape, user):
+            cnt = int(np.prod([shape[i] for i in range(nd)]))
+            arr = np.ctypeslib.as_array(p, shape=(cnt,))
+            if nd == 4:
+                arr[:] = np.sin(0.37 * (np.arange(cnt) + 13 * calls[0])).astype(np.float32)
+                calls[0] += 1
+            else:
+                arr[:] = (np.arange(cnt) + calls[0]) % 3
+
+        cb = CB(fill)
+        assert lib.sn_set_train_data_callback(st, 0, cb, None) == 0
+        assert lib.sn_set_train_data_callback(st, 1, cb, None) == 0
+        assert lib.sn_solver_step(st, iters) == 0, lib.sn_last_error()
+        nparam = lib.sn_num_params(st)
+        w = (C.c_float * nparam)()
+        assert lib.sn_get_weights(st, w, C.c_longlong(nparam)) == 0
+        nat = lib.sn_native_iterations(st)
+        lib.sn_free(buf)
+        lib.sn_destroy_state(st)
+        return np.frombuffer(w, dtype=np.float32).copy(), nat, calls[0]
+    finally:
+        os.environ.pop("SN_NATIVE_STEP", None)
+
+
+@pytest.mark.gpu
+def test_native_step_matches_python_step(core_lib):
+    """20 iterations through the native C++ step loop (after its 3 capture iterations) end
+    at the same weights as 20 iterations of the Python solver fed by the same callbacks."""
+    w_py, nat_py, calls_py = _ctypes_train(core_lib, 0, 20, native=False)
+    w_nat, nat, calls_nat = _ctypes_train(core_lib, 0, 20, native=True)
+    assert nat_py == 0 and nat == 17 and calls_py == calls_nat == 20
+    err = np.abs(w_nat - w_py).max() / (np.abs(w_py).max() + 1e-12)
+    assert err < 2e-2, err
