@@ -130,8 +130,10 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
                            scale=scale, mirror=False, train=False, device=dev)
     if args.sync_sgd and comm is not None:
         solver.add_callback(SyncSGDCallback(comm, net))
+    # sync SGD keeps the hipGraph: the bucketed gradient all-reduces are captured with the
+    # iteration (engine.GraphStep runs the solver callbacks inside the captured body)
     trainer = LocalSGDTrainer(solver, None if args.sync_sgd else comm, tau=args.tau, feeder=feeder,
-                              use_graph=dev.type == "cuda" and not args.sync_sgd)
+                              use_graph=dev.type == "cuda")
     if start_round == 0:
         trainer.broadcast_initial()
     trainer.round = start_round

@@ -580,6 +580,11 @@ class GraphStep:
         s = self.solver
         net = s.net
         net.clear_param_diffs(lazy=True)
+        # solver callbacks (P2PSync-style sync SGD, parallel.comm.SyncSGDCallback): their
+        # bucketed gradient all-reduces, launched from backward hooks, are captured with
+        # the iteration (RCCL collectives on the capturing stream become graph nodes)
+        for cb in s.callbacks:
+            getattr(cb, "on_start", lambda: None)()
         if self.overlap is not None:
             self.overlap.begin()
         if self._use_branches and self.branches is None:
@@ -598,6 +603,8 @@ class GraphStep:
                 hip.WgradStream.join()
         net.finish_param_diffs()
         fp8_step(net)
+        for cb in s.callbacks:
+            getattr(cb, "on_gradients_ready", lambda: None)()
         ops.advance_rng(net.ctx.rng_state)
         if self.overlap is not None:
             self.overlap.end()

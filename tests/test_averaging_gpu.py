@@ -87,3 +87,48 @@ def test_graph_trainer_average_updates_masters_shadow_and_next_replay(gpu):
     assert (fc8_graph - fc8_eager).abs().max().item() <= 1e-3 * scale, "replay must read the averaged weights"
     assert (fc8_before - fc8_eager).abs().max().item() > 1e-2 * scale, "averaging must change the forward"
     assert torch.isfinite(net.flat_data).all()
+
+
+def test_sync_sgd_bucketed_allreduce_captured_in_graph(gpu):
+    """Sync-SGD mode keeps the hipGraph: the SyncSGDCallback's bucketed RCCL all-reduces
+    (launched from backward hooks, overlapped with the remaining backward) are captured
+    with the iteration.  On a 1-rank NCCL(RCCL) group the reduction is the identity, so
+    4 captured steps end bitwise equal to 4 captured steps without the callback."""
+    import socket
+
+    import torch.distributed as dist
+
+    from sparknet_amd.engine import GraphStep
+    from sparknet_amd.parallel.comm import Comm, SyncSGDCallback, grad_buckets
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                            device_id=torch.device(gpu))
+    try:
+        res = []
+        for sync in (False, True):
+            solver = _caffenet_solver(torch.device(gpu), batch=2, crop=67)
+            if sync:
+                cb = SyncSGDCallback(Comm(), solver.net)
+                cb.plan, cb.late = grad_buckets(solver.net, 1 << 16)  # force the overlapped buckets
+                solver.net.backward_hooks.append(cb._hook)
+                solver.add_callback(cb)
+                assert sum(len(v) for v in cb.plan.values()) >= 2
+            g = torch.Generator().manual_seed(1)
+            batches = iter([(torch.randn(2, 3, 67, 67, generator=g) * 20, torch.tensor([[1.0], [4.0]]))
+                            for _ in range(6)])
+
+            def pre():
+                x, y = next(batches)
+                solver.net.blob_by_name("data").set_nchw(x)
+                solver.net.blob_by_name("label").set_nchw(y)
+            step = GraphStep(solver, warmup=1, pre=pre, overlap=False, fuse_fc=False)
+            for _ in range(4):
+                step.step()
+            torch.cuda.synchronize()
+            assert step.graph is not None
+            res.append(solver.net.flat_data.detach().clone())
+        assert torch.equal(res[0], res[1])
+    finally:
+        dist.destroy_process_group()
