@@ -304,6 +304,16 @@ struct GStager {
                 r += 1;
               }
             }
+          } else if (g.Cg >= 2 * EPC) {
+            // narrower channel runs (fp8 with 64 channels: VGG conv1_2): the chunk may cross
+            // up to 8 * EPC / Cg taps — a short carry loop instead of two divisions
+            while (c >= g.Cg) {
+              c -= g.Cg;
+              if (++s == g.S) {
+                s = 0;
+                ++r;
+              }
+            }
           } else {
             const int kk = k_tile + ch[e] * EPC;
             const int tap = fdiv(kk, g.Cg, invCg);

@@ -26,7 +26,8 @@ for n in (4096, 8192):
     print(f"dense {n}^3: bf16 {fl / t16 / 1e9:7.1f} TF   fp8 {fl / t8 / 1e9:7.1f} TF", flush=True)
 for name, s in {"vgg conv3_x": ConvSpec(64, 56, 56, 256, 256, 3, 3, 1, 1, 1, 1),
                 "vgg conv4_x": ConvSpec(64, 28, 28, 512, 512, 3, 3, 1, 1, 1, 1),
-                "vgg conv2_x": ConvSpec(64, 112, 112, 128, 128, 3, 3, 1, 1, 1, 1)}.items():
+                "vgg conv2_x": ConvSpec(64, 112, 112, 128, 128, 3, 3, 1, 1, 1, 1),
+                "vgg conv1_2": ConvSpec(64, 224, 224, 64, 64, 3, 3, 1, 1, 1, 1)}.items():
     x = torch.randn(s.N, s.H, s.W, s.C, device=dev)
     w = torch.randn(s.K, s.R, s.S, s.Cg, device=dev) * 0.05
     xb, wb = x.to(torch.bfloat16), w.to(torch.bfloat16)
