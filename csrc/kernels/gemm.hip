@@ -108,6 +108,9 @@ struct SnGemmArgs {
   unsigned drop_thr;
   float drop_scale;
   float gate_scale;
+  // bf16 epilogues of unsplit 4-wave tiles: stage the finished tile through the idle LDS
+  // stages and store it as whole 16-B row chunks (host: ldc % 8 == 0, 16-B aligned C)
+  int lds_store;
 };
 
 }  // extern "C"
@@ -447,16 +450,16 @@ SN_DEV i32x8 read_frag8(const char* lds, int x0, int lane) {
   return r;
 }
 
-// Store one 4-column output fragment v = C[m][n..n+3] (the caller checked m < M, n < N):
-// bias / ReLU / ReLU-backward gate for bf16 outputs, fp32 store / accumulate (+ the
-// bias-gradient column routed to bias_out), or the fused solver update (EPI_SGD).
+// bias / ReLU / ReLU-backward gate / dropout of one 4-column bf16 output fragment
 template <int EPI, bool FP8>
-SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, f32x4 v, int c_cols) {
+SN_DEV void epi_bf16_math(const SnGemmArgs& args, int grp, int m, int n, f32x4 v, int c_cols, float* o) {
   const bool full = (n + 3 < c_cols) && ((args.ldc & 3) == 0);
   if (FP8) v = v * (args.deq_a[0] * args.deq_b[0]);  // per-tensor fp8 scales
-  if (epi_bf16<EPI>()) {
-    bf16_t* C = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride + (long long)m * args.ldc;
-    float o[4] = {v[0], v[1], v[2], v[3]};
+  o[0] = v[0];
+  o[1] = v[1];
+  o[2] = v[2];
+  o[3] = v[3];
+  {
     if (args.bias) {
       const float* bz = args.bias + (long long)grp * args.N;
 #pragma unroll
@@ -496,6 +499,19 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
           o[r] = dropout_keep(args.drop_rng, args.drop_stream, args.drop_thr, e0 + r) ? o[r] * args.drop_scale : 0.f;
       }
     }
+  }
+}
+
+// Store one 4-column output fragment v = C[m][n..n+3] (the caller checked m < M, n < N):
+// bias / ReLU / ReLU-backward gate for bf16 outputs, fp32 store / accumulate (+ the
+// bias-gradient column routed to bias_out), or the fused solver update (EPI_SGD).
+template <int EPI, bool FP8>
+SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, f32x4 v, int c_cols) {
+  const bool full = (n + 3 < c_cols) && ((args.ldc & 3) == 0);
+  if (epi_bf16<EPI>()) {
+    bf16_t* C = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride + (long long)m * args.ldc;
+    float o[4];
+    epi_bf16_math<EPI, FP8>(args, grp, m, n, v, c_cols, o);
     if (full) {
       uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
       *reinterpret_cast<uint2*>(C + n) = pk;
@@ -505,6 +521,7 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
         if (n + r < args.N) C[n + r] = f2bf(o[r]);
     }
   } else {
+    if (FP8) v = v * (args.deq_a[0] * args.deq_b[0]);
     if (args.bias_out && n <= args.ones_col && args.ones_col < n + 4) {
       const int r = args.ones_col - n;
       const float bv = r == 0 ? v[0] : (r == 1 ? v[1] : (r == 2 ? v[2] : v[3]));
@@ -824,6 +841,50 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmAr
           *reinterpret_cast<float4*>(args.sgd_h + o) = make_float4(A[0], A[1], A[2], A[3]);
           *reinterpret_cast<uint2*>(args.sgd_shadow + o) = make_uint2(pack2(W[0], W[1]), pack2(W[2], W[3]));
         }
+      return;
+    }
+  }
+  if constexpr (epi_bf16<EPI>() && NS == 2) {
+    if (args.lds_store) {
+      // The MFMA layout stores 16 rows x 8 B per lane group (32-B row pieces per
+      // wave-instruction); instead stage the finished bf16 tile in the idle LDS stages
+      // (rows of the first M half in smem0, the second in smem1; 16-B row padding keeps
+      // the 8-B fragment writes of 16 consecutive rows on distinct banks) and store it as
+      // whole 16-B chunks, each wave-instruction covering 1 KB of consecutive rows.
+      constexpr int PITCH = BN * 2 + 16, HALF = BM / 2, CPR = BN / 8;
+      static_assert(HALF * PITCH <= STAGE, "staged epilogue half-tile must fit one LDS stage");
+      __builtin_amdgcn_s_barrier();  // every wave is past its last fragment read of the stages
+      char* wbuf = wm0 < HALF ? smem0 : smem1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int lr = wm0 + 16 * j + mrow_l, m = m_blk + lr;
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) {
+          const int nl = wn0 + 16 * i + ncol_l, n = n_blk + nl;
+          float o[4] = {0.f, 0.f, 0.f, 0.f};
+          if (m < args.M && n < args.N) epi_bf16_math<EPI, FP8>(args, grp, m, n, acc[i][j], args.N, o);
+          *reinterpret_cast<uint2*>(wbuf + (lr % HALF) * PITCH + nl * 2) =
+              make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      bf16_t* Cb = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride;
+      for (int q = tid; q < BM * CPR; q += NW * 64) {
+        const int lr = q / CPR, c = q - lr * CPR;
+        const int m = m_blk + lr, n = n_blk + c * 8;
+        if (m >= args.M || n >= args.N) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>((lr < HALF ? smem0 : smem1) + (lr % HALF) * PITCH + c * 16);
+        bf16_t* dst = Cb + (long long)m * args.ldc + n;
+        if (n + 8 <= args.N) {
+          *reinterpret_cast<uint4*>(dst) = v;
+        } else {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (k < args.N - n) dst[k] = (bf16_t)(w[k >> 1] >> (16 * (k & 1)));
+        }
+      }
       return;
     }
   }

@@ -234,6 +234,9 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
 
 
 _NO_XTRA = (0, 0, 0.0, 1.0)
+# bf16 epilogues of the 4-wave tiles store through LDS as whole 16-B row chunks
+# (SnGemmArgs.lds_store); SN_GEMM_LDS_EPI=0 keeps the per-fragment stores (A/B)
+_LDS_EPI = os.environ.get("SN_GEMM_LDS_EPI", "1") != "0"
 
 
 def _drop_fields(xtra):
@@ -259,10 +262,12 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     bg = bias_grad.data_ptr() if bias_grad is not None else 0
     if splits == 1:
         e = EPI_BF16_DROP if (epi == EPI_BF16 and xtra[0]) else epi
+        lds = int(_LDS_EPI and epi == EPI_BF16 and tile in (0, 1, 4, 5) and ldc % 8 == 0 and c_gstride % 8 == 0
+                  and out.data_ptr() % 16 == 0)
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, e,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
                                bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster,
-                               ones, bg, int(bias_acc), *sg, *_drop_fields(xtra))
+                               ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), lds)
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
