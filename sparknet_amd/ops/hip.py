@@ -169,7 +169,35 @@ def _slice_ok(s: ConvSpec) -> bool:
     return s.groups == 1 and _implicit_ok(s) and s.Kg % 8 == 0
 
 
+# The implicit-GEMM index decode (fp32 reciprocal division) is exact below 2^24 pixels per
+# launch; larger batches (e.g. VGG-16 at batch 512, sized for 288 GB of HBM) run as
+# consecutive launches over image chunks — forward / dgrad write disjoint output slices,
+# weight gradients accumulate.
+_MAX_PIX = 1 << 24
+
+
+def _image_chunk(s: ConvSpec) -> int:
+    """Images per launch (s.N when one launch holds the whole batch)."""
+    per = max(s.H * s.W, s.P * s.Q, 1)
+    plan = _s2d_plan(s)
+    if plan is not None:  # the folded input materialises the spatial padding
+        per = max(per, plan[4].H * plan[4].W)
+    return s.N if s.N * per < _MAX_PIX else max(1, (_MAX_PIX - 1) // per)
+
+
 def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=None):
+    nb = _image_chunk(s)
+    if nb < s.N:
+        y = out if out is not None else torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device)
+        for n0 in range(0, s.N, nb):
+            n1 = min(s.N, n0 + nb)
+            conv_forward(x[n0:n1], w, b, s.with_batch(n1 - n0), relu, None,
+                         folded[n0:n1] if folded is not None else None, out=y[n0:n1])
+        return y
+    return _conv_forward(x, w, b, s, relu, ws, folded, out)
+
+
+def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=None):
     """ws: optional per-layer dict kept from forward to backward (the space-to-depth
     folded input is stored there so the weight-gradient pass does not rebuild it).
     folded: the S2D-folded input already produced upstream (fused augment + fold); x is
@@ -182,8 +210,8 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=Non
     assert x.dtype == BF16 and w.dtype == BF16, (x.dtype, w.dtype)
     if out is not None:
         ldo = chan_stride(out)
-        assert _slice_ok(s) and ldo and tuple(out.shape) == (s.N, s.P, s.Q, s.K) and out.dtype == BF16, \
-            "conv output slice needs an ungrouped implicit conv and an NHWC channel-slice view"
+        assert (out.is_contiguous() or _slice_ok(s)) and ldo and tuple(out.shape) == (s.N, s.P, s.Q, s.K) \
+            and out.dtype == BF16, "conv output slice needs an ungrouped implicit conv and an NHWC channel-slice view"
     plan = _s2d_plan(s)
     if plan is not None:
         f, cp, rf, sf, s2 = plan
@@ -192,7 +220,7 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=Non
         x2 = folded if folded is not None else _s2d_input(x, s, plan)
         if ws is not None:
             ws["s2d"] = (x.data_ptr(), x._version, x2)
-        return conv_forward(x2, w2, b, s2, relu)
+        return conv_forward(x2, w2, b, s2, relu, out=out)
     M = s.N * s.P * s.Q
     if out is not None:
         y, ldy = out, chan_stride(out)
@@ -206,6 +234,7 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=Non
         B = Dense(_c(w.reshape(s.K, kred)), kred, True, gstride=s.Kg * kred)
         gemm(M, s.Kg, kred, A, B, y, ldy, epi=EPI_BF16, groups=s.groups, c_gstride=s.Kg, bias=b, relu=relu)
         return y
+    assert ldy == s.K, "explicit im2col path writes contiguous outputs"
     wp, kpad = _weight_kpad(w, s)
     y2 = y.view(M, s.K)
     for g in range(s.groups):
@@ -267,6 +296,22 @@ def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
 
 def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
                   dw_acc=True, db_acc=True):
+    nb = _image_chunk(s)
+    if nb < s.N:
+        dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device) if need_dx else None
+        for n0 in range(0, s.N, nb):
+            n1 = min(s.N, n0 + nb)
+            _conv_backward(dy[n0:n1], x[n0:n1], w, s.with_batch(n1 - n0), need_dx, dw,
+                           db, gate[n0:n1] if gate is not None else None,
+                           {"wt": ws["wt"]} if ws and "wt" in ws else None, dw_acc, db_acc,
+                           dx_out=dx[n0:n1] if need_dx else None)
+            dw_acc = db_acc = True  # later chunks accumulate into the weight gradients
+        return dx
+    return _conv_backward(dy, x, w, s, need_dx, dw, db, gate, ws, dw_acc, db_acc)
+
+
+def _conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
+                   dw_acc=True, db_acc=True, dx_out=None):
     """gate: optional bf16 NHWC tensor shaped like x; dx is zeroed where gate <= 0
     (the backward of a slope-0 in-place ReLU that produced x, fused into the dgrad).
     dw_acc / db_acc False: overwrite the gradient instead of accumulating (its buffer
@@ -288,7 +333,7 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
         _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, ldd, ldx)
     if not need_dx:
         return None
-    return _conv_dgrad(dy, x, w, s, M, gate, ws, ldd, ldx)
+    return _conv_dgrad(dy, x, w, s, M, gate, ws, ldd, ldx, dx_out)
 
 
 def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, ldd=0, ldx=0):
@@ -334,9 +379,9 @@ def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, 
                     dw2[g * s.Kg:(g + 1) * s.Kg].copy_(tmp[:s.Kg, :kred])
 
 
-def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0):
+def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
     ldd, ldx = ldd or s.K, ldx or s.C
-    dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
+    dx = dx_out if dx_out is not None else torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
     if gate is not None and ldx != s.C:  # the gate (= x, a channel slice) must share dx's layout
         gate = _c(gate)
     if s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0:
@@ -377,6 +422,9 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0):
              s.Cg, kpad, g * s.Cg)
     if gate is not None:
         dx = relu_backward(dx, gate)
+        if dx_out is not None:
+            dx_out.copy_(dx)
+            dx = dx_out
     return dx
 
 
@@ -721,6 +769,13 @@ def conv_forward_fp8(xq, wq, b, s: ConvSpec, deq_x, deq_w, relu=False):
     """Implicit-GEMM convolution on e4m3 operands (v_mfma_scale_f32_16x16x128_f8f6f4),
     fp32 accumulation, dequantised + bias + ReLU epilogue, bf16 NHWC output."""
     assert s.Cg % 16 == 0 and s.C % 16 == 0 and xq.dtype == torch.uint8 and wq.dtype == torch.uint8
+    nb = _image_chunk(s)
+    if nb < s.N:
+        y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=xq.device)
+        for n0 in range(0, s.N, nb):
+            n1 = min(s.N, n0 + nb)
+            y[n0:n1] = conv_forward_fp8(xq[n0:n1], wq, b, s.with_batch(n1 - n0), deq_x, deq_w, relu)
+        return y
     M = s.N * s.P * s.Q
     kred = s.R * s.S * s.Cg
     y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=xq.device)

@@ -331,3 +331,26 @@ def test_concat_channels_fwd_bwd_gate(gpu):
         if diffs[i] is not None:
             assert torch.equal(diffs[i], want), i
         off += c
+
+
+def test_conv_image_chunking(gpu, monkeypatch):
+    """Convolutions over more than 2^24 pixels per launch run as image chunks (forward /
+    dgrad slices, accumulated weight gradients): forced small chunk limit vs one launch."""
+    from sparknet_amd.ops import hip
+    from sparknet_amd.ops.spec import ConvSpec
+    s = ConvSpec(6, 20, 20, 16, 32, 3, 3, 1, 1, 1, 1)
+    x = rnd(6, 20, 20, 16)
+    w = rnd(32, 3, 3, 16, scale=0.1)
+    b = torch.randn(32, device="cuda")
+    dy = rnd(6, 20, 20, 32)
+    y0 = hip.conv_forward(x, w, b, s, relu=True)
+    dw0, db0 = torch.zeros(32, 3, 3, 16, device="cuda"), torch.zeros(32, device="cuda")
+    dx0 = hip.conv_backward(dy, x, w, s, True, dw0, db0)
+    monkeypatch.setattr(hip, "_MAX_PIX", 2 * 20 * 20 + 1)  # 2 images per launch
+    assert hip._image_chunk(s) == 2
+    y1 = hip.conv_forward(x, w, b, s, relu=True)
+    dw1, db1 = torch.zeros_like(dw0), torch.zeros_like(db0)
+    dx1 = hip.conv_backward(dy, x, w, s, True, dw1, db1)
+    assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
+    close(dw1, dw0, 1e-3)
+    close(db1, db0, 1e-3)
