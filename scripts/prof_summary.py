@@ -17,7 +17,7 @@ for r in rows[a + 1:b + 1]:
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     tot += d
     n = r['Kernel_Name']
-    k = (n.split('(SnGemmArgs')[0] if 'gemm_kernel' in n else n.split('(')[0])[-60:]
+    k = (n.split("(SnGemmArgs")[0] if "gemm" in n else n.split("(")[0].replace("void ", ""))[-60:]
     agg[k] = agg.get(k, 0) + d
 print("per-iteration kernel time by kernel (us):")
 for k, v in sorted(agg.items(), key=lambda x: -x[1])[:25]:
