@@ -1,0 +1,25 @@
+#!/usr/bin/env python3
+"""Aggregate rocprofv3 --pmc counter CSVs (p*/run_counter_collection.csv) per kernel:
+mean counter value per dispatch of the GEMM kernels."""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+vals = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"]
+        if "gemm" not in k and "splitk" not in k:
+            continue
+        k = k.split("(SnGemmArgs")[0].split("(")[0][-70:]
+        vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in vals.items():
+    print(k)
+    m = {c: sum(v) / len(v) for c, v in cs.items()}
+    for c in sorted(m):
+        print(f"   {c:30s} {m[c]:14.4g}")
+    g = m.get("GRBM_GUI_ACTIVE")
+    if g and "SQ_VALU_MFMA_BUSY_CYCLES" in m and "SQ_BUSY_CU_CYCLES" in m:
+        print(f"   MFMA busy / (GUI_ACTIVE x 256 CU x 4 SIMD) = {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (g * 1024):.3f}")
