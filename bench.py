@@ -61,8 +61,10 @@ DEFAULTS = {  # model: (batch, channels, src hw, crop, classes, mean, input scal
     "caffenet": (256, 3, 256, 227, 1000, [104.0, 117.0, 123.0], 1.0),
     "alexnet": (256, 3, 256, 227, 1000, [104.0, 117.0, 123.0], 1.0),
     "googlenet": (128, 3, 256, 224, 1000, [104.0, 117.0, 123.0], 1.0),
-    # msra-initialised 13-conv stack: unit-scale input keeps the random-init logits finite
-    "vgg16": (64, 3, 256, 224, 1000, [104.0, 117.0, 123.0], 0.017),
+    # msra-initialised 13-conv stack: unit-scale input keeps the random-init logits finite;
+    # BASELINE config 5 sizes the per-GPU batch for the 288 GB of HBM: 512 (38 GB, 7.5k img/s;
+    # 1024: 73 GB, 7.8k; 64: 6.5 GB, 6.1k — profiles/r2_vgg16_batch_sweep.txt)
+    "vgg16": (512, 3, 256, 224, 1000, [104.0, 117.0, 123.0], 0.017),
     "cifar10_quick": (100, 3, 32, 32, 10, [125.0, 123.0, 114.0], 1.0),
     "cifar10_full": (100, 3, 32, 32, 10, [125.0, 123.0, 114.0], 1.0),
 }
