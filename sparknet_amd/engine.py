@@ -14,6 +14,7 @@
 """
 from __future__ import annotations
 
+import gc
 import logging
 import os
 import time
@@ -637,6 +638,13 @@ class GraphStep:
         # the capture did not execute: replay it once as a real iteration
         self.graph.replay()
         s.iter += 1
+        # The replay loop allocates almost nothing, but Python's cyclic collector still runs
+        # full passes over every object built so far (net, captured graph, torch state):
+        # a gen-2 pass stalls the host for ~30 ms while the GPU drains its queue (measured:
+        # the first 100 CaffeNet steps after capture ran at 94k instead of 105k img/s).
+        # Collect once now and move the surviving objects out of the collector's view.
+        gc.collect()
+        gc.freeze()
 
     def step(self):
         s = self.solver
