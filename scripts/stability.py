@@ -42,6 +42,25 @@ if os.environ.get("SPIN"):
     torch.cuda.synchronize()
 if os.environ.get("NOFEED"):  # replay without the per-step H2D minibatch copies (timing only)
     tr.step_fn.pre = None
+f = tr.feeder
+mode = os.environ.get("FEED", "")
+if mode == "nocopy":  # augment from the staged slots every step, no new H2D copy
+    def _pf():
+        f._pending = f.k % len(f.slots)
+        f.events[f._pending] = None
+        f.k += 1
+    f.prefetch = _pf
+elif mode == "samestream":  # the copy on the compute stream itself (no cross-stream events)
+    def _pf():
+        x, y = f.source.next_batch()
+        slot = f.k % len(f.slots)
+        dx, dy = f.slots[slot]
+        dx.copy_(x, non_blocking=True)
+        dy.copy_(y, non_blocking=True)
+        f.events[slot] = None
+        f._pending = slot
+        f.k += 1
+    f.prefetch = _pf
 # GPU-side timing of 10-step slices inside one long un-synchronised run
 evs = [torch.cuda.Event(enable_timing=True) for _ in range(31)]
 evs[0].record()
