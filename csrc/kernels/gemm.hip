@@ -598,7 +598,7 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
 
 template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, bool FP8 = false,
           int NFR = 4>
-__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_kernel(SnGemmArgs args) {
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) gemm_kernel(SnGemmArgs args) {
   // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
   constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
   // B's LDS image holds BNL >= BN rows: whole wave-instructions per wave (a 48-wide tile
@@ -1196,6 +1196,22 @@ int launch_tile96(const SnGemmArgs& a, hipStream_t stream) {
   return 4;
 }
 
+// 128x64 tile (4 waves of 64x32, 48 KB of LDS): three co-resident blocks per CU (three
+// waves per SIMD) to hide the LDS-DMA latency of latency-bound products (few K-steps,
+// narrow outputs) at the price of 1.5x the operand bytes per MFMA of a 128x128 tile.
+int launch_tile64(const SnGemmArgs& a, hipStream_t stream) {
+  const int tiles = ((a.M + 127) / 128) * ((a.N + 63) / 64);
+  dim3 grid(tiles * a.splits * a.groups);
+  const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  switch (key) {
+    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, 128, 64, 4, 2, 2>(a, grid, stream);
+    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, 128, 64, 4, 2, 2>(a, grid, stream);
+    case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE, 128, 64, 4, 2, 2>(a, grid, stream);
+    case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL, 128, 64, 4, 2, 2>(a, grid, stream);
+    default: return 4;
+  }
+}
+
 // 256x48 tile (4 waves of 64x48; B staged as 64 rows): 48-wide outputs such as AlexNet
 // conv2's dgrad (48 input channels per group) without a quarter of dead MFMA columns.
 template <int NS_ = 2>
@@ -1265,6 +1281,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 7: return a.epi == EPI_SGD ? 4 : launch256<128>(a, stream);
     case 8: return a.epi == EPI_SGD ? 4 : launch256<256, 4>(a, stream);  // 4-phase variant (A/B probes)
     case 9: return a.epi == EPI_SGD ? 4 : launch256<128, 4>(a, stream);
+    case 10: return a.epi == EPI_SGD ? 4 : launch_tile64(a, stream);
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

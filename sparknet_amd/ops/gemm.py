@@ -111,13 +111,14 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 
 
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
-         6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128)}
+         6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64)}
 # gemm256_kernel tiles (6, 7) run one 512-thread block per CU
-_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256}
+_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768}
 _KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1}
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
 _RASTER_N = int(os.environ.get("SN_GEMM_RASTER_N", "-1"))  # -1: heuristic
 _TILE256 = os.environ.get("SN_GEMM_TILE256", "1") != "0"  # autotune candidates 6 / 7 (gemm256_kernel)
+_TILE64 = os.environ.get("SN_GEMM_TILE64", "1") != "0"  # autotune candidate 10 (128x64, 3 blocks / CU)
 
 
 def choose_tile(M: int, N: int, b_kcontig: bool = False) -> int:
@@ -262,7 +263,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     bg = bias_grad.data_ptr() if bias_grad is not None else 0
     if splits == 1:
         e = EPI_BF16_DROP if (epi == EPI_BF16 and xtra[0]) else epi
-        lds = int(_LDS_EPI and epi == EPI_BF16 and tile in (0, 1, 4, 5) and ldc % 8 == 0 and c_gstride % 8 == 0
+        lds = int(_LDS_EPI and epi == EPI_BF16 and tile in (0, 1, 4, 5, 10) and ldc % 8 == 0 and c_gstride % 8 == 0
                   and out.data_ptr() % 16 == 0)
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, e,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
@@ -354,6 +355,8 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
         if N > 128:
             tiles.append(6)
     if epi != EPI_SGD:
+        if _TILE64:
+            tiles.append(10)
         if b_kc_dense and N % 96 == 0:
             tiles.append(4)
         if N % 48 == 0 and N <= 96 and M >= 256:

@@ -254,3 +254,27 @@ def test_linear_wgrad_sgd_epilogue(gpu, nesterov, B, O, I):
     _close(w - w0, w_ref - w0, 1e-3)
     assert torch.equal(sh, w.to(torch.bfloat16))
     _close(db, dy.float().sum(0), 1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(304, 64, 640), (1000, 200, 136), (128, 64, 64)])
+def test_tile64_layouts(gpu, M, N, K, monkeypatch):
+    """The 128x64 tile (three blocks per CU): NT / TN dense products and a conv forward
+    + weight gradient against the fp32 reference."""
+    from sparknet_amd.ops import gemm as G, hip
+    from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(G, "_FORCE_TILE", 10)
+    a, b = _bf(M, K, device=gpu), _bf(N, K, device=gpu)
+    bias = torch.randn(N, device=gpu)
+    c = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    G.gemm(M, N, K, G.Dense(a, K, True), G.Dense(b, K, True), c, N, epi=G.EPI_BF16, bias=bias, relu=True)
+    _close(c, torch.relu(a.float() @ b.float().t() + bias))
+    at, bt = _bf(K, M, device=gpu), _bf(K, N, device=gpu)
+    dw = torch.full((M, N), 1.0, device=gpu)
+    G.gemm(M, N, K, G.Dense(at, M, False), G.Dense(bt, N, False), dw, N, epi=G.EPI_F32_ACC, splits=2)
+    _close(dw, 1.0 + at.float().t() @ bt.float(), 1e-2)
+    s = ConvSpec(4, 12, 12, 32, 64, 3, 3, 1, 1, 1, 1)
+    x = _bf(4, 12, 12, 32, device=gpu)
+    w = (torch.randn(64, 3, 3, 32, device=gpu) * 0.1).to(torch.bfloat16)
+    y = hip.conv_forward(x, w, None, s)
+    from sparknet_amd.ops import ref
+    _close(y, ref.conv_forward(x.float().cpu(), w.float().cpu(), None, s).to(gpu))
