@@ -47,6 +47,9 @@ def parse():
                    help="HIP streams for parallel branches (Inception towers) inside the graph; 1 = sequential "
                         "(>= 3 uses the star topology, see engine.BranchStreams; 4 measured 1-2%% faster than 2 "
                         "on GoogLeNet)")
+    p.add_argument("--feed-group", type=int, default=1,
+                   help="H2D minibatch copies issued in groups of this many steps under one copy/compute "
+                        "fence pair (DeviceFeeder group)")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--cpu", action="store_true",
                    help="fp32 reference engine on the CPU with gloo (tests the launcher / JSON path; not a benchmark)")
@@ -124,7 +127,8 @@ def main():
         fuse_relu(net)
     src = SyntheticSource(B, C, HW, HW, classes=classes, pool=3, seed=rank)
     feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
-                          scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev)
+                          scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev,
+                          group=args.feed_group)
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
     n_fp8 = enable_fp8(net) if args.dtype == "fp8" else 0
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph and not args.cpu,

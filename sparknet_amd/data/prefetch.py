@@ -105,8 +105,12 @@ class DeviceFeeder:
 
     def __init__(self, source: HostBatchSource, data_blob, label_blob, *, crop: int | None = None,
                  mean=None, scale: float = 1.0, mirror: bool = False, train: bool = True,
-                 rng_state: torch.Tensor | None = None, device="cuda", slots: int = 2):
+                 rng_state: torch.Tensor | None = None, device="cuda", slots: int = 2, group: int = 1):
         self.source = source
+        # group > 1: the H2D copies of `group` minibatches are issued together, one group
+        # ahead, under ONE copy/compute fence pair (2*group slots), so the per-step
+        # cross-stream synchronisation is amortised (docs/PERF_NOTES.md "Throughput phases").
+        self.group = max(1, int(group))
         self.data_blob, self.label_blob = data_blob, label_blob
         self.device = torch.device(device)
         from .native import NativeLoader
@@ -128,6 +132,10 @@ class DeviceFeeder:
         self.rng_state = rng_state if rng_state is not None else torch.tensor([1, 0], dtype=torch.int64,
                                                                               device=self.device)
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        if self.copy_stream is None or self.native or getattr(source, "submitted", None) is not None:
+            self.group = 1  # ring sources recycle a host slot per copy event: keep one per step
+        if self.group > 1:
+            slots = max(slots, 2 * self.group)
         self.slots = [(torch.empty(self.shape, dtype=torch.uint8, device=self.device),
                        torch.empty((N,), dtype=torch.int32, device=self.device)) for _ in range(slots)]
         self.events = [None] * slots
@@ -143,6 +151,9 @@ class DeviceFeeder:
         """Issue the H2D copy of the next host batch into the next slot (copy stream)."""
         if self.native:
             self._prefetch_native()
+            return
+        if self.group > 1:
+            self._prefetch_group()
             return
         if self._first is not None:
             x, y = self._first
@@ -168,6 +179,46 @@ class DeviceFeeder:
         if done is not None:
             done(x, ev)
         self._pending = slot
+        self.k += 1
+
+    def _next_host(self):
+        if self._first is not None:
+            x, y = self._first
+            self._first = None
+            return x, y
+        return self.source.next_batch()
+
+    def _issue_group(self, start: int) -> None:
+        """Copy minibatches start .. start+group-1 into their slots behind one fence pair."""
+        n = len(self.slots)
+        cur = torch.cuda.current_stream(self.device)
+        # slots (start + j) % n were last read by steps start-n+j, already submitted on cur
+        self.copy_stream.wait_stream(cur)
+        sent = []
+        with torch.cuda.stream(self.copy_stream):
+            for j in range(self.group):
+                x, y = self._next_host()
+                dx, dy = self.slots[(start + j) % n]
+                dx.copy_(x, non_blocking=True)
+                dy.copy_(y, non_blocking=True)
+                sent.append(x)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+        for j in range(self.group):
+            # later slots of the group are ordered behind the first one's wait on the compute stream
+            self.events[(start + j) % n] = ev if j == 0 else None
+        done = getattr(self.source, "submitted", None)
+        if done is not None:
+            for x in sent:
+                done(x, ev)
+
+    def _prefetch_group(self) -> None:
+        k, g = self.k, self.group
+        if k == 0:
+            self._issue_group(0)
+        if k % g == 0:
+            self._issue_group(k + g)  # one group ahead: `group` steps to hide `group` copies
+        self._pending = k % len(self.slots)
         self.k += 1
 
     def _prefetch_native(self) -> None:

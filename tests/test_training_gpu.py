@@ -109,3 +109,30 @@ def test_caffenet_bf16_gpu_loss_trajectory_matches_fp32_cpu(gpu):
     for i, (a, b) in enumerate(zip(lc, lg)):
         assert abs(a - b) <= 0.05 * max(1.0, abs(a)), (i, a, b)
     assert min(lc[-4:]) < lc[0] and min(lg[-4:]) < lg[0], (lc, lg)
+
+
+def test_grouped_feeder_stages_same_sequence(gpu):
+    """DeviceFeeder(group=3) issues its H2D copies three minibatches at a time behind one
+    fence pair; the staged data / labels must be the per-step feeder's, step for step."""
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.data.prefetch import DeviceFeeder, TensorSource
+    x, y = _patterns(160, seed=3)
+    nets, feeders = [], []
+    for group in (1, 3):
+        solver = Solver(models.solver_for("cifar10_quick", train_batch=10, test_batch=10), device=gpu, seed=5,
+                        build_test_nets=False)
+        net = solver.net
+        feeders.append(DeviceFeeder(TensorSource(x, y, 10), net.blob_by_name("data"), net.blob_by_name("label"),
+                                    crop=32, mean=[120.0, 120.0, 120.0], mirror=False, train=False,
+                                    rng_state=net.ctx.rng_state, device=gpu, group=group))
+        nets.append(net)
+    assert feeders[1].group == 3 and len(feeders[1].slots) == 6
+    for step in range(11):
+        outs = []
+        for f, net in zip(feeders, nets):
+            f.stage()
+            f.prefetch()
+            outs.append((net.blob_by_name("data").data.clone(), net.blob_by_name("label").data.clone()))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0][0], outs[1][0]), step
+        assert torch.equal(outs[0][1], outs[1][1]), step
