@@ -47,9 +47,10 @@ def parse():
                    help="HIP streams for parallel branches (Inception towers) inside the graph; 1 = sequential "
                         "(>= 3 uses the star topology, see engine.BranchStreams; 4 measured 1-2%% faster than 2 "
                         "on GoogLeNet)")
-    p.add_argument("--feed-group", type=int, default=1,
+    p.add_argument("--feed-group", type=int, default=2,
                    help="H2D minibatch copies issued in groups of this many steps under one copy/compute "
-                        "fence pair (DeviceFeeder group)")
+                        "fence pair (DeviceFeeder group; 1 = one fence pair per step: 97k vs 102-105k img/s "
+                        "in the 20-step window, profiles/r2_feed_group_ab.txt)")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--cpu", action="store_true",
                    help="fp32 reference engine on the CPU with gloo (tests the launcher / JSON path; not a benchmark)")
@@ -204,7 +205,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
-                "hipgraph": trainer.use_graph, "streams": args.streams, "fused_input_fold": fused_fold, "fp8_layers": n_fp8,
+                "hipgraph": trainer.use_graph, "streams": args.streams, "feed_group": feeder.group, "fused_input_fold": fused_fold, "fp8_layers": n_fp8,
                 "final_loss": round(final_loss, 4),
             },
             "rccl_world": comm.world_size if comm is not None else 1,

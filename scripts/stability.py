@@ -24,7 +24,7 @@ fuse_relu(solver.net)
 feeder = DeviceFeeder(SyntheticSource(B, C, HW, HW, classes=classes, pool=3, seed=0), solver.net.blob_by_name("data"),
                       solver.net.blob_by_name("label"), crop=crop, mean=mean, scale=sc, mirror=True, train=True,
                       rng_state=solver.net.ctx.rng_state, device=dev,
-                      group=int(os.environ.get("GROUP", "1")))
+                      group=int(os.environ.get("GROUP", "2")))
 fuse_input_fold(solver.net, feeder)
 tr = LocalSGDTrainer(solver, None, tau=50, feeder=feeder, use_graph=True)
 for _ in range(20):

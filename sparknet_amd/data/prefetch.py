@@ -105,7 +105,7 @@ class DeviceFeeder:
 
     def __init__(self, source: HostBatchSource, data_blob, label_blob, *, crop: int | None = None,
                  mean=None, scale: float = 1.0, mirror: bool = False, train: bool = True,
-                 rng_state: torch.Tensor | None = None, device="cuda", slots: int = 2, group: int = 1):
+                 rng_state: torch.Tensor | None = None, device="cuda", slots: int = 2, group: int = 2):
         self.source = source
         # group > 1: the H2D copies of `group` minibatches are issued together, one group
         # ahead, under ONE copy/compute fence pair (2*group slots), so the per-step
