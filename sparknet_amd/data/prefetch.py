@@ -132,8 +132,10 @@ class DeviceFeeder:
         self.rng_state = rng_state if rng_state is not None else torch.tensor([1, 0], dtype=torch.int64,
                                                                               device=self.device)
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
-        if self.copy_stream is None or self.native or getattr(source, "submitted", None) is not None:
-            self.group = 1  # ring sources recycle a host slot per copy event: keep one per step
+        if self.copy_stream is None or getattr(source, "submitted", None) is not None:
+            # Python ring sources recycle a host slot only when told about its copy event:
+            # keep one copy per step (the native loader records its own per-copy events)
+            self.group = 1
         if self.group > 1:
             slots = max(slots, 2 * self.group)
         self.slots = [(torch.empty(self.shape, dtype=torch.uint8, device=self.device),
@@ -149,11 +151,11 @@ class DeviceFeeder:
 
     def prefetch(self) -> None:
         """Issue the H2D copy of the next host batch into the next slot (copy stream)."""
-        if self.native:
-            self._prefetch_native()
-            return
         if self.group > 1:
             self._prefetch_group()
+            return
+        if self.native:
+            self._prefetch_native()
             return
         if self._first is not None:
             x, y = self._first
@@ -197,8 +199,11 @@ class DeviceFeeder:
         sent = []
         with torch.cuda.stream(self.copy_stream):
             for j in range(self.group):
-                x, y = self._next_host()
                 dx, dy = self.slots[(start + j) % n]
+                if self.native:  # the C++ loader copies its next pinned slot on this stream
+                    self.source.next_to_device(dx, dy, self.copy_stream)
+                    continue
+                x, y = self._next_host()
                 dx.copy_(x, non_blocking=True)
                 dy.copy_(y, non_blocking=True)
                 sent.append(x)

@@ -126,3 +126,27 @@ def test_next_to_device(gpu, cifar_dir):
             st.synchronize()
             idx = [(seq * 32 + i) % 500 for i in range(32)]
             assert np.array_equal(dx.cpu().numpy(), imgs[idx]) and np.array_equal(dy.cpu().numpy(), labs[idx])
+
+
+@pytest.mark.gpu
+def test_grouped_feeder_over_native_loader(gpu, cifar_dir):
+    """DeviceFeeder(group=3) over the C++ loader: three next_to_device copies per fence
+    pair, staged labels follow the sequential sampler step for step."""
+    from sparknet_amd import models
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.data.prefetch import DeviceFeeder
+    _, labs = _records(cifar_dir)
+    solver = Solver(models.solver_for("cifar10_quick", train_batch=10, test_batch=10), device=gpu, seed=5,
+                    build_test_nets=False)
+    net = solver.net
+    with native.NativeLoader.cifar10(_files(cifar_dir), 10, sampler=native.SAMPLER_SEQUENTIAL, threads=2) as L:
+        f = DeviceFeeder(L, net.blob_by_name("data"), net.blob_by_name("label"), crop=32, mirror=False,
+                         train=False, rng_state=net.ctx.rng_state, device=gpu, group=3)
+        assert f.group == 3 and len(f.slots) == 6
+        for step in range(13):
+            f.stage()
+            f.prefetch()
+            got = net.blob_by_name("label").data.float().cpu().flatten().numpy()
+            want = labs[[(step * 10 + i) % 500 for i in range(10)]].astype(np.float32)
+            assert np.array_equal(got, want), step
+        torch.cuda.synchronize()
