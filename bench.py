@@ -39,6 +39,9 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                    help="fp8: e4m3 forward products with per-tensor delayed scaling (bf16 backward)")
+    p.add_argument("--fp8-min-work", type=float, default=0.0,
+                   help="--dtype fp8: only layers with at least this many forward MACs per input element "
+                        "run e4m3 (engine.enable_fp8 min_macs_per_input)")
     p.add_argument("--overlap-update", action="store_true",
                    help="run large layers' solver updates on a side stream during backward")
     p.add_argument("--no-fuse-fc", action="store_true",
@@ -131,7 +134,7 @@ def main():
                           scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev,
                           group=args.feed_group)
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
-    n_fp8 = enable_fp8(net) if args.dtype == "fp8" else 0
+    n_fp8 = enable_fp8(net, args.fp8_min_work) if args.dtype == "fp8" else 0
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph and not args.cpu,
                               overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc,
                               streams=args.streams)

@@ -336,21 +336,34 @@ def fuse_input_fold(net, feeder) -> bool:
     return True
 
 
-def enable_fp8(net) -> int:
+def fp8_macs_per_input(layer, bottom) -> float:
+    """Forward multiply-adds per input element of a Convolution / InnerProduct layer: the
+    MFMA work the e4m3 path halves, per element of the bf16 -> e4m3 input quantisation
+    pass it costs (a 3-byte-per-element HBM pass)."""
+    if layer.type_name == "Convolution":
+        s = layer.spec(bottom)
+        return (s.K // s.groups) * s.R * s.S / float(s.sh * s.sw)
+    return float(layer.N)
+
+
+def enable_fp8(net, min_macs_per_input: float = 0.0) -> int:
     """Run the forward products of eligible Convolution / InnerProduct layers in OCP e4m3
     (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation) with per-tensor delayed
     scaling: each layer quantises its input and weights with the scale derived from the
     previous iteration's amax (ops.hip.Fp8Scales; updated once per iteration by
     :func:`fp8_step`).  Gradients, masters and checkpoints stay bf16 / fp32.  Layers whose
-    channels are not multiples of 16 (e.g. an RGB input conv) stay bf16.  GPU only;
-    returns the number of fp8 layers."""
+    channels are not multiples of 16 (e.g. an RGB input conv) stay bf16, and so do layers
+    with fewer than ``min_macs_per_input`` forward MACs per input element (where the
+    quantisation pass over a large activation costs more than the faster product saves,
+    e.g. VGG's 64-channel conv1_2).  GPU only; returns the number of fp8 layers."""
     if net.device.type != "cuda":
         return 0
     from .ops import hip
     chosen = []
     for li, layer in enumerate(net.layers):
         if layer.type_name in ("Convolution", "InnerProduct") and len(net.bottom_vecs[li]) == 1:
-            if layer.fp8_eligible(net.bottom_vecs[li][0]):
+            b = net.bottom_vecs[li][0]
+            if layer.fp8_eligible(b) and fp8_macs_per_input(layer, b) >= min_macs_per_input:
                 chosen.append(layer)
     sc = hip.Fp8Scales(2 * len(chosen), net.device)
     for i, layer in enumerate(chosen):
