@@ -378,3 +378,21 @@ def test_branch_stream_plan_respects_dependencies():
                 if (wi & rj) or (wi & wj) or (ri & wj):
                     assert finish[j] - 1 >= finish[i], (order[i], order[j])
         assert max(finish.values()) < len(plan)  # some layers really overlap
+
+
+def test_fp8_macs_per_input_cost_model():
+    """engine.fp8_macs_per_input: forward MACs per input element that the fp8 layer
+    selection (enable_fp8 min_macs_per_input) compares against the quantisation pass."""
+    from sparknet_amd import models
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.engine import fp8_macs_per_input
+    solver = Solver(models.solver_for("caffenet", train_batch=2, test_batch=2), build_test_nets=False)
+    net = solver.net
+    got = {}
+    for li, layer in enumerate(net.layers):
+        if layer.type_name in ("Convolution", "InnerProduct"):
+            got[layer.name] = fp8_macs_per_input(layer, net.bottom_vecs[li][0])
+    assert got["conv1"] == 96 * 11 * 11 / 16.0  # 11x11 stride 4
+    assert got["conv2"] == 128 * 5 * 5  # group 2: 128 outputs per input channel
+    assert got["conv3"] == 384 * 9
+    assert got["fc6"] == 4096 and got["fc8"] == 1000
