@@ -346,7 +346,7 @@ def fp8_macs_per_input(layer, bottom) -> float:
     return float(layer.N)
 
 
-def enable_fp8(net, min_macs_per_input: float = 0.0) -> int:
+def enable_fp8(net, min_macs_per_input: float = 1000.0) -> int:
     """Run the forward products of eligible Convolution / InnerProduct layers in OCP e4m3
     (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation) with per-tensor delayed
     scaling: each layer quantises its input and weights with the scale derived from the

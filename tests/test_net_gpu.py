@@ -158,7 +158,7 @@ def test_fp8_forward_training(gpu):
         solver = Solver(sp, device=torch.device("cuda:0"), seed=5, build_test_nets=False)
         fuse_relu(solver.net)
         if mode == "fp8":
-            assert enable_fp8(solver.net) >= 14  # 12 of 13 convs (not the RGB input) + 3 IPs
+            assert enable_fp8(solver.net, 0.0) >= 14  # 12 of 13 convs (not the RGB input) + 3 IPs
         g = torch.Generator().manual_seed(2)
         x = torch.randn(4, 3, 32, 32, generator=g) * 0.5
         y = torch.tensor([[1.0], [3.0], [5.0], [7.0]])
@@ -288,3 +288,15 @@ def test_googlenet_zero_copy_concat_bitwise(gpu, monkeypatch):
     for (la, ga), (lb, gb) in zip(res["copy"], res["zero"]):
         assert la == lb
         assert torch.equal(ga, gb)
+
+
+def test_fp8_layer_selection_threshold(gpu):
+    """enable_fp8's default cost-model threshold keeps VGG's conv1_2 (576 MACs per input
+    element) and a 10-way fc8 in bf16, everything else eligible in e4m3."""
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.engine import enable_fp8
+    net_p = models.vgg16(train_batch=2, test_batch=2, crop=32, classes=10)
+    solver = Solver(models.zoo.vgg16_solver(net_p), device=torch.device("cuda:0"), seed=5, build_test_nets=False)
+    assert enable_fp8(solver.net) == 13
+    chosen = {layer.name for layer in solver.net.layers if getattr(layer, "fp8_slots", None) is not None}
+    assert "conv1_2" not in chosen and "fc8" not in chosen and "conv2_1" in chosen and "fc6" in chosen
