@@ -94,11 +94,20 @@ def _worker_sync(rank, world, port, q):
     comm.close()
 
 
+def _wrapped(fn, rank, world, port, q):
+    """Run a worker, then leave the gloo group together: a rank that exits while its peer
+    still has async collectives / the gloo transport open can abort the peer (SIGABRT)."""
+    fn(rank, world, port, q)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def _run(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_wrapped, args=(fn, r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=240) for _ in range(world)]
