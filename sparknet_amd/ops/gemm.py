@@ -375,8 +375,24 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
     return list(dict.fromkeys(out))
 
 
+# Experiment knob: cap the split-K factor of every product (0 = no cap).  With several
+# branch streams in flight (Inception) other streams may fill the CUs a split would.
+_MAX_SPLITS = int(os.environ.get("SN_GEMM_MAX_SPLITS", "0"))
+
+
 def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
                   ones, sg, xtra=_NO_XTRA):
+    cfg = _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
+                            ones, sg, xtra)
+    t, s, kc = cfg
+    if _MAX_SPLITS <= 0 or s <= _MAX_SPLITS:
+        return cfg
+    kc = -(-(-(-K // _MAX_SPLITS)) // BK) * BK
+    return (t, max(1, -(-K // kc)), kc)
+
+
+def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
+                      ones, sg, xtra=_NO_XTRA):
     sa, a_mc, a_mode, sb, b_mc, b_mode = ops
     b_kc_dense = b_mc == 0 and b_mode == OP_DENSE
     key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None, bool(xtra[0]),
