@@ -4,9 +4,10 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for m in googlenet caffenet; do
-  for cap in 0 1 4 0 1; do
-    SN_GEMM_MAX_SPLITS=$cap timeout -k 10 240 python bench.py --model $m --steps 20 --warmup 5 > gpurun_out/sk_$m$cap.json 2> gpurun_out/sk_$m$cap.err || { echo "bench $m cap $cap failed"; tail -20 gpurun_out/sk_$m$cap.err; exit 1; }
+CAPVAR=${CAPVAR:-SN_GEMM_MAX_SPLITS}; CAPS=${CAPS:-"0 1 4 0 1"}
+for m in ${MODELS:-googlenet caffenet}; do
+  for cap in $CAPS; do
+    env $CAPVAR=$cap timeout -k 10 240 python bench.py --model $m --steps 20 --warmup 5 > gpurun_out/sk_$m$cap.json 2> gpurun_out/sk_$m$cap.err || { echo "bench $m cap $cap failed"; tail -20 gpurun_out/sk_$m$cap.err; exit 1; }
     python -c "import json; d=json.load(open('gpurun_out/sk_$m$cap.json')); print('$m max_splits=$cap', d['value'], d['ms_per_step'], flush=True)"
   done
 done

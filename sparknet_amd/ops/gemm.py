@@ -378,6 +378,8 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
 # Experiment knob: cap the split-K factor of every product (0 = no cap).  With several
 # branch streams in flight (Inception) other streams may fill the CUs a split would.
 _MAX_SPLITS = int(os.environ.get("SN_GEMM_MAX_SPLITS", "0"))
+# the same cap for bf16-output products only (forward / dgrad), weight gradients untouched
+_MAX_SPLITS_BF16 = int(os.environ.get("SN_GEMM_MAX_SPLITS_BF16", "0"))
 
 
 def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
@@ -385,9 +387,12 @@ def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, ga
     cfg = _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
                             ones, sg, xtra)
     t, s, kc = cfg
-    if _MAX_SPLITS <= 0 or s <= _MAX_SPLITS:
+    cap = _MAX_SPLITS
+    if _MAX_SPLITS_BF16 > 0 and epi in (EPI_BF16, EPI_BF16_DROP):
+        cap = _MAX_SPLITS_BF16 if cap <= 0 else min(cap, _MAX_SPLITS_BF16)
+    if cap <= 0 or s <= cap:
         return cfg
-    kc = -(-(-(-K // _MAX_SPLITS)) // BK) * BK
+    kc = -(-(-(-K // cap)) // BK) * BK
     return (t, max(1, -(-K // kc)), kc)
 
 
