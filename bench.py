@@ -24,6 +24,10 @@ import os
 import sys
 import time
 
+# dmabuf IPC is the only mode the host driver supports; torchrun-launched ranks must get it
+# before their first GPU call exactly like parallel/launch.spawn_local's children
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 BASELINE_IMG_S = 193.2  # CaffeNet training, Caffe no-cuDNN, K40
 
 
@@ -55,6 +59,13 @@ def parse():
                    help="H2D minibatch copies issued in groups of this many steps under one copy/compute "
                         "fence pair (DeviceFeeder group; 1 = one fence pair per step: 97k vs 102-105k img/s "
                         "in the 20-step window, profiles/r2_feed_group_ab.txt)")
+    p.add_argument("--share-gpu", action="store_true",
+                   help="rehearse the N-rank path on ONE GPU: every rank runs on device 0 and the collectives "
+                        "use gloo (RCCL refuses two ranks on one device); everything else is the production "
+                        "path. The img/s of such a run is not a multi-GPU number")
+    p.add_argument("--verify-average", action="store_true",
+                   help="after the timed window, check that every rank holds bitwise-identical averaged "
+                        "masters and that the bf16 shadow the graph reads is bf16(master) (JSON avg_check)")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--cpu", action="store_true",
                    help="fp32 reference engine on the CPU with gloo (tests the launcher / JSON path; not a benchmark)")
@@ -82,6 +93,9 @@ HEADLINE = ("caffenet", "alexnet")
 def main():
     args = parse()
     from sparknet_amd.parallel.launch import launched_world, spawn_local
+    if args.share_gpu:
+        os.environ["SN_SHARE_GPU"] = "1"  # inherited by the ranks spawn_local starts
+    args.share_gpu = args.share_gpu or os.environ.get("SN_SHARE_GPU", "0") == "1"
     world_env = launched_world()
     if world_env is None and args.gpus > 1:
         # `python bench.py --gpus N`: start N ranks (one per GPU) before any GPU call here
@@ -99,10 +113,11 @@ def main():
         dev = torch.device("cpu")
         numa = -1
     else:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        gpu = 0 if args.share_gpu else local_rank
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
         from sparknet_amd.parallel.topology import bind_to_gpu_numa
-        numa = bind_to_gpu_numa(local_rank) if world > 1 else -1
+        numa = bind_to_gpu_numa(gpu) if world > 1 else -1
 
     def sync():
         if dev.type == "cuda":
@@ -117,7 +132,8 @@ def main():
 
     if dev.type == "cuda":
         _lib.kernels()
-    comm = Comm(device=dev if dev.type == "cuda" else None, watchdog=True, timeout_s=600.0) if world > 1 else None
+    comm = (Comm(backend="gloo" if args.share_gpu else None, device=dev if dev.type == "cuda" else None,
+                 watchdog=True, timeout_s=600.0) if world > 1 else None)
     if comm is not None:
         assert comm.world_size == world == args.gpus, (comm.world_size, world, args.gpus)
     B, C, HW, crop, classes, mean, in_scale = DEFAULTS[args.model]
@@ -177,11 +193,15 @@ def main():
     elapsed = elapsed_rank
     per_rank_ms = [round(1000.0 * elapsed_rank / args.steps, 3)]
     avg_ms = [e[0].elapsed_time(e[1]) for e in avg_events if e is not None]
-    comm_info = None
+    comm_info = avg_check = None
     if comm is not None:
         elapsed = comm.max_over_ranks(elapsed_rank)
         per_rank_ms = [round(1000.0 * v / args.steps, 3) for v in comm.allgather_float(elapsed_rank)]
-        comm_info = comm_bench(comm, net.flat_data, dev, sync)
+        avg_check = None
+        if args.verify_average:  # untimed: average once more so the window's last step is averaged
+            trainer.average()
+            avg_check = verify_average(comm, net, dev, sync)
+        comm_info = comm_bench(comm, net.flat_data, dev, sync, iters=1 if args.share_gpu else 4)
     final_loss = float(loss) if loss is not None else float("nan")
 
     ms = 1000.0 * elapsed / args.steps
@@ -213,6 +233,10 @@ def main():
                 "final_loss": round(final_loss, 4),
             },
             "rccl_world": comm.world_size if comm is not None else 1,
+            "comm_backend": comm.backend if comm is not None else None,
+            "share_gpu": bool(args.share_gpu),
+            "average_buckets": (len(comm.bucket_ranges(net.flat_data.numel(), comm.average_bucket_bytes))
+                                if comm is not None else 0),
             "per_rank_ms_per_step": per_rank_ms,
             "averages_in_window": len(avg_events) if comm is not None else 0,
             "allreduce_ms_per_average": round(sum(avg_ms) / len(avg_ms), 3) if avg_ms else None,
@@ -222,6 +246,8 @@ def main():
         }
         if comm_info is not None:
             out["comm_bench"] = comm_info
+        if avg_check is not None:
+            out["avg_check"] = avg_check
         print(json.dumps(out), flush=True)
     if args.host_profile and trainer.step_fn is not None:
         host_profile(trainer, dev)
@@ -231,6 +257,27 @@ def main():
     if comm is not None:
         comm.close()
     return 0
+
+
+def verify_average(comm, net, dev, sync):
+    """The timed window ended with an average (bench loop): every rank must now hold the
+    SAME fp32 masters bit for bit, and the bf16 compute shadow — the buffer the captured
+    graph's next replay reads, at the pointer it was captured with — must be bf16(master)."""
+    import torch
+    sync()
+    flat = net.flat_data.detach()
+    words = flat.view(torch.int32).to(torch.int64)
+    # order-sensitive 64-bit checksum of the bit patterns (exact integer arithmetic)
+    idx = torch.arange(1, words.numel() + 1, device=words.device, dtype=torch.int64) % 1000003
+    digest = [int(words.sum().item()), int((words * idx).sum().item())]
+    shadow_ok = True
+    if net.flat_compute is not net.flat_data:
+        shadow_ok = bool(torch.equal(net.flat_compute, flat.to(net.flat_compute.dtype)))
+    gathered = [comm.allgather_int(d) for d in digest]
+    equal = all(len(set(g)) == 1 for g in gathered)
+    ok_all = comm.allgather_int(int(shadow_ok))
+    return {"masters_equal_across_ranks": equal, "shadow_is_bf16_master": all(ok_all),
+            "digest_rank0": digest, "ranks": comm.world_size}
 
 
 def comm_bench(comm, flat, dev, sync, bucket_mb=(256, 64, 16), iters=4):

@@ -176,6 +176,9 @@ __global__ void __launch_bounds__(256) prelu_bwd_k(const void* __restrict__ x, c
 // ---------------------------------------------------------------------------------------
 // Deterministic axis reduction: out[b][a] (+)= scale * sum_{o, i} f(p[b][o][a][i], q[...])
 //   mode 0: p   1: p q   2: p^2   3: p q [q <= 0] (PReLU slope)   4: |p|
+//   mode 5: (p - q[b][a])^2 with q an fp32 per-(b, a) centre (the mean): the variance of
+//   BatchNorm / MVN as E[(x - EX)^2] (batch_norm_layer.cu:50-59, mvn_layer.cu:31-36) —
+//   E[x^2] - EX^2 cancels when |mean| >> std
 // Pass 1 writes partials part[split][b][a]; pass 2 combines the splits in order.
 // ---------------------------------------------------------------------------------------
 template <int MODE>
@@ -184,6 +187,7 @@ SN_DEV float rf(float a, float b) {
   if (MODE == 1) return a * b;
   if (MODE == 2) return a * a;
   if (MODE == 3) return b <= 0.f ? a * b : 0.f;
+  if (MODE == 5) return (a - b) * (a - b);
   return fabsf(a);
 }
 
@@ -199,9 +203,10 @@ __global__ void __launch_bounds__(256) colred_k(const void* __restrict__ p, cons
   float acc = 0.f;
   if (col < A) {
     const long long base = (long long)b * outer * A;
+    const float cen = MODE == 5 ? reinterpret_cast<const float*>(q)[(long long)b * A + col] : 0.f;
     for (long long r = r0 + rl; r < r1; r += 4) {
       const long long e = base + r * A + col;
-      acc += rf<MODE>(ldv(p, e, dtp), q ? ldv(q, e, dtq) : 0.f);
+      acc += rf<MODE>(ldv(p, e, dtp), MODE == 5 ? cen : (q ? ldv(q, e, dtq) : 0.f));
     }
   }
   __shared__ float red[4][64];
@@ -221,10 +226,11 @@ __global__ void __launch_bounds__(256) segred_k(const void* __restrict__ p, cons
   const long long tot = outer * inner, per = (tot + splits - 1) / splits;
   const long long e0 = s * per, e1 = min(tot, e0 + per);
   float acc = 0.f;
+  const float cen = MODE == 5 ? reinterpret_cast<const float*>(q)[(long long)b * A + a] : 0.f;
   for (long long e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
     const long long o = e / inner, i = e - o * inner;
     const long long idx = (((long long)b * outer + o) * A + a) * inner + i;
-    acc += rf<MODE>(ldv(p, idx, dtp), q ? ldv(q, idx, dtq) : 0.f);
+    acc += rf<MODE>(ldv(p, idx, dtp), MODE == 5 ? cen : (q ? ldv(q, idx, dtq) : 0.f));
   }
   acc = wave_sum(acc);
   __shared__ float red[4];
@@ -279,8 +285,9 @@ __global__ void __launch_bounds__(256) norm_bwd_k(const void* __restrict__ dy, c
   }
 }
 
-// From sums s1 = sum x, s2 = sum x^2 over `count` elements per (b, a):
-//   mean = s1 / count, var = s2 / count - mean^2 (clamped at 0)
+// From sums s1 = sum x and s2 over `count` elements per (b, a): mean = s1 / count and
+//   var = s2 / count (mode & 4: s2 = sum (x - mean)^2, centred — the default now), or
+//   var = s2 / count - mean^2 clamped at 0 (s2 = sum x^2)
 //   mode 0 (BatchNorm): inv = 1 / sqrt(var + eps)     mode 1 (MVN): inv = 1 / (sqrt(var) + eps)
 //   mode 2 (MVN without variance): inv = 1
 __global__ void stats_finalize_k(const float* __restrict__ s1, const float* __restrict__ s2, int n, float inv_count,
@@ -289,7 +296,9 @@ __global__ void stats_finalize_k(const float* __restrict__ s1, const float* __re
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const float m = s1[j] * inv_count;
-  const float v = s2 ? fmaxf(s2[j] * inv_count - m * m, 0.f) : 0.f;
+  const bool centred = (mode & 4) != 0;
+  mode &= 3;
+  const float v = s2 ? (centred ? s2[j] * inv_count : fmaxf(s2[j] * inv_count - m * m, 0.f)) : 0.f;
   mean[j] = m;
   if (var) var[j] = v;
   if (inv) inv[j] = mode == 0 ? rsqrtf(v + eps) : (mode == 1 ? 1.f / (sqrtf(v) + eps) : 1.f);
@@ -817,7 +826,7 @@ int sn_axis_reduce(long long mode, const void* p, const void* q, long long dtp, 
     switch (mode) {
 #define SN_CR(M) \
   case M: hipLaunchKernelGGL(colred_k<M>, grid, dim3(256), 0, st, p, q, (int)dtp, (int)dtq, outer, (int)A, splits, part, (int)B); break;
-      SN_CR(0) SN_CR(1) SN_CR(2) SN_CR(3) SN_CR(4)
+      SN_CR(0) SN_CR(1) SN_CR(2) SN_CR(3) SN_CR(4) SN_CR(5)
 #undef SN_CR
       default: return 2;
     }
@@ -830,7 +839,7 @@ int sn_axis_reduce(long long mode, const void* p, const void* q, long long dtp, 
     hipLaunchKernelGGL(segred_k<M>, grid, dim3(256), 0, st, p, q, (int)dtp, (int)dtq, outer, (int)A, inner, splits, \
                        part, (int)B);                                                                            \
     break;
-      SN_SR(0) SN_SR(1) SN_SR(2) SN_SR(3) SN_SR(4)
+      SN_SR(0) SN_SR(1) SN_SR(2) SN_SR(3) SN_SR(4) SN_SR(5)
 #undef SN_SR
       default: return 2;
     }

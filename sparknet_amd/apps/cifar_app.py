@@ -15,7 +15,7 @@ import sys
 from ..data.loaders import CifarLoader
 from ..data.sampler import shard_range
 from . import runner
-from .common import base_parser, maybe_launch
+from .common import base_parser, bind_device, maybe_launch
 
 
 def main(argv=None):
@@ -30,6 +30,7 @@ def main(argv=None):
     train = test = None
     mean = [125.3, 123.0, 113.9]
     if args.data and not args.synthetic:
+        bind_device(args)  # pinned rings below allocate on the current device
         ld = CifarLoader(args.data, seed=args.seed)
         mean = ld.mean_image()  # full mean image (the reference computed it, then ignored it)
         files = [os.path.join(args.data, f"data_batch_{i}.bin") for i in range(1, 6)]

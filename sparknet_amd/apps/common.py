@@ -31,6 +31,9 @@ def base_parser(desc: str, **defaults) -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu", action="store_true", help="run the fp32 reference path on the CPU")
     p.add_argument("--sync-sgd", action="store_true", help="all-reduce gradients every step (tau=1 semantics)")
+    p.add_argument("--sync-sgd-graph", action="store_true",
+                   help="--sync-sgd inside the captured hipGraph (bucketed RCCL all-reduces as graph nodes); "
+                        "verified bitwise on a 1-rank group only, so the eager step is the default")
     p.add_argument("--log-dir", default=None)
     p.add_argument("--fail-at-round", type=int, default=-1, help="fault injection: a rank exits at round r")
     p.add_argument("--fail-rank", type=int, default=0, help="fault injection: the rank that exits")
@@ -46,20 +49,36 @@ def base_parser(desc: str, **defaults) -> argparse.ArgumentParser:
     return p
 
 
+def share_gpu() -> bool:
+    """SN_SHARE_GPU=1: rehearse an N-rank job on ONE GPU — every rank on device 0, collectives
+    over gloo (RCCL refuses two ranks on one device).  For tests on 1-GPU boxes."""
+    return os.environ.get("SN_SHARE_GPU", "0") == "1"
+
+
+def bind_device(args) -> torch.device:
+    """Make this rank's GPU (LOCAL_RANK) the current device.  Call it before anything that
+    starts HIP — pinning host memory (``pin_memory``) opens a context on the CURRENT device,
+    so a source built before the bind would put every rank's pinned ring (and a context)
+    on GPU 0."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if share_gpu():
+        local = 0
+    if args.cpu or not torch.cuda.is_available():
+        return torch.device("cpu")
+    torch.cuda.set_device(local)
+    return torch.device("cuda", local)
+
+
 def setup(args):
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.cpu or not torch.cuda.is_available():
-        dev = torch.device("cpu")
-    else:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+    dev = bind_device(args)
+    if dev.type == "cuda":
         from ..ops import _lib
         _lib.kernels()
     from ..parallel import Comm
-    comm = (Comm(device=dev if dev.type == "cuda" else None, timeout_s=getattr(args, "pg_timeout", 300.0),
-                 watchdog=True) if world > 1 else None)
+    comm = (Comm(backend="gloo" if share_gpu() else None, device=dev if dev.type == "cuda" else None,
+                 timeout_s=getattr(args, "pg_timeout", 300.0), watchdog=True) if world > 1 else None)
     return rank, world, dev, comm
 
 

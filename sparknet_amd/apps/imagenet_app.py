@@ -15,7 +15,7 @@ import sys
 
 from ..data.loaders import ImageNetLoader
 from . import runner
-from .common import base_parser, maybe_launch
+from .common import base_parser, bind_device, maybe_launch
 
 
 def main(argv=None):
@@ -40,6 +40,7 @@ def main(argv=None):
     train = test = None
     mean = [104.0, 117.0, 123.0]
     if args.data and not args.synthetic:
+        bind_device(args)  # the pinned rings below allocate on the current device
         # bounded-memory streaming ingest (data.stream): compressed records -> decode pool ->
         # ring of pinned minibatches; the mean is one streamed pass over the shard
         from ..data.stream import StreamingJpegSource, streamed_mean

@@ -130,10 +130,13 @@ def run(args, *, model: str, data_shape, crop: int, mean, scale: float, mirror: 
                            scale=scale, mirror=False, train=False, device=dev)
     if args.sync_sgd and comm is not None:
         solver.add_callback(SyncSGDCallback(comm, net))
-    # sync SGD keeps the hipGraph: the bucketed gradient all-reduces are captured with the
-    # iteration (engine.GraphStep runs the solver callbacks inside the captured body)
+    # sync SGD runs the eager step by default: the bucketed gradient all-reduces CAN be
+    # captured with the iteration (engine.GraphStep runs the solver callbacks inside the
+    # captured body; --sync-sgd-graph), but cross-rank collectives inside a replayed graph
+    # have only been verified on a 1-rank RCCL group (tests/test_averaging_gpu.py)
+    graph = dev.type == "cuda" and (not args.sync_sgd or getattr(args, "sync_sgd_graph", False))
     trainer = LocalSGDTrainer(solver, None if args.sync_sgd else comm, tau=args.tau, feeder=feeder,
-                              use_graph=dev.type == "cuda")
+                              use_graph=graph)
     if start_round == 0:
         trainer.broadcast_initial()
     trainer.round = start_round

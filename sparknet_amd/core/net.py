@@ -684,7 +684,12 @@ class Net:
             if src.endswith(".h5"):
                 self.copy_trained_layers_from_hdf5(src)
                 return
-            src = proto.read_net(src)
+            src = proto.read_net(src)  # upgrades V0 / V1 nets (net.cpp:853-858)
+        elif len(src.layers):
+            from ..proto.upgrade import upgrade_net
+            up = proto.NetParameter()
+            up.CopyFrom(src)
+            src = upgrade_net(up)
         for slp in src.layer:
             if slp.name not in self.layer_names_index:
                 continue
@@ -744,20 +749,20 @@ def blob_shape_equals(bp, shape) -> bool:
     """Blob::ShapeEquals (blob.cpp:474-490): a legacy (num, channels, height, width) proto
     matches a target of <= 4 axes padded with leading 1s; otherwise shapes match exactly."""
     shape = tuple(int(s) for s in shape)
-    if not bp.HasField("shape") and (bp.num or bp.channels or bp.height or bp.width):
+    legacy = any(bp.HasField(f) for f in ("num", "channels", "height", "width"))
+    if legacy:
+        # legacy 4-D fields: unset ones read as their default 0, like Blob::LegacyShape
         if len(shape) > 4:
             return False
         return (1,) * (4 - len(shape)) + shape == (bp.num, bp.channels, bp.height, bp.width)
-    if bp.HasField("shape"):
-        return tuple(bp.shape.dim) == shape
-    return (len(bp.data) or len(bp.double_data)) == (shape[0] if len(shape) == 1 else -1)
+    return tuple(bp.shape.dim) == shape  # no shape either: only a 0-axis blob matches
 
 
 def blob_proto_to_tensor(bp) -> torch.Tensor:
     """Blob::FromProto (blob.cpp:446-495): ``shape`` or legacy 4-D fields, float or double."""
     if bp.HasField("shape"):
         shape = tuple(bp.shape.dim)
-    elif bp.num or bp.channels or bp.height or bp.width:
+    elif any(bp.HasField(f) for f in ("num", "channels", "height", "width")):
         shape = (bp.num, bp.channels, bp.height, bp.width)
     else:
         shape = (len(bp.data) or len(bp.double_data),)

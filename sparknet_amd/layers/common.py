@@ -768,8 +768,16 @@ class MVNLayer(Layer):
         tops[0].reshape(bottoms[0].shape, bottoms[0].dtype)
 
     def _dims(self, x):
+        """Reduction dims of one statistic group (mvn_layer.cpp: num = N, or N*C per channel;
+        dim = count / num)."""
         p = self.lp.mvn_param
-        return (1, 2, 3) if p.across_channels else (1, 2)  # NHWC: spatial dims 1,2 (+channel 3)
+        if x.dim() == 4:
+            return (1, 2, 3) if p.across_channels else (1, 2)  # NHWC: spatial dims 1,2 (+channel 3)
+        return tuple(range(1, x.dim())) if p.across_channels else tuple(range(2, x.dim()))
+
+    @staticmethod
+    def _mean(x, dims):
+        return x.mean(dim=dims, keepdim=True) if dims else x  # dim = 1: each element its own group
 
     def _gpu_geom(self, x):
         """[B][outer][A][inner] of the per-statistic groups: (n, c) over (h, w) in NHWC, or
@@ -778,7 +786,7 @@ class MVNLayer(Layer):
         N = x.shape[0]
         if x.dim() == 4 and not p.across_channels:
             return N, x.shape[1] * x.shape[2], x.shape[3], 1
-        if x.dim() != 4 and not p.across_channels and x.dim() > 2:
+        if x.dim() != 4 and not p.across_channels and x.dim() > 1:
             inner = x.numel() // (N * x.shape[1])
             return N, 1, x.shape[1], inner
         return N, 1, 1, x.numel() // N
@@ -790,9 +798,11 @@ class MVNLayer(Layer):
             x = bottoms[0].data
             B, outer, A, inner = self._gpu_geom(x)
             self.geom = (B, outer, A, inner)
-            s1 = lh.axis_reduce(lh.RED_SUM, x, None, B, outer, A, inner)
-            s2 = lh.axis_reduce(lh.RED_SQ, x, None, B, outer, A, inner) if p.normalize_variance else None
-            mean, _, inv = lh.stats_finalize(s1, s2, outer * inner, p.eps, 1 if p.normalize_variance else 2)
+            if p.normalize_variance:
+                mean, _, inv = lh.mean_var(x, B, outer, A, inner, p.eps, 1)
+            else:
+                s1 = lh.axis_reduce(lh.RED_SUM, x, None, B, outer, A, inner)
+                mean, _, inv = lh.stats_finalize(s1, None, outer * inner, p.eps, 2)
             self.inv = inv if p.normalize_variance else None
             y = lh.chan_affine(x, mean, self.inv, outer, A, inner)
             self.y = y
@@ -800,9 +810,9 @@ class MVNLayer(Layer):
             return
         x = bottoms[0].data.float()
         dims = self._dims(x)
-        xm = x - x.mean(dim=dims, keepdim=True)
+        xm = x - self._mean(x, dims)
         if p.normalize_variance:
-            self.std = torch.sqrt((xm * xm).mean(dim=dims, keepdim=True)) + p.eps
+            self.std = torch.sqrt(self._mean(xm * xm, dims)) + p.eps
             y = xm / self.std
         else:
             y = xm
@@ -828,10 +838,10 @@ class MVNLayer(Layer):
         dims = self._dims(dy)
         if p.normalize_variance:
             y = self.y
-            g = dy - dy.mean(dim=dims, keepdim=True) - y * (dy * y).mean(dim=dims, keepdim=True)
+            g = dy - self._mean(dy, dims) - y * self._mean(dy * y, dims)
             g = g / self.std
         else:
-            g = dy - dy.mean(dim=dims, keepdim=True)
+            g = dy - self._mean(dy, dims)
         bottoms[0].diff = g.to(bottoms[0].dtype)
 
 
@@ -879,9 +889,7 @@ class BatchNormLayer(Layer):
             if self.use_global:
                 mean, self.inv_std = lh.bn_global(self.mean.data, self.var.data, self.factor.data, self.eps)
             else:
-                s1 = lh.axis_reduce(lh.RED_SUM, x, None, 1, outer, C_, inner)
-                s2 = lh.axis_reduce(lh.RED_SQ, x, None, 1, outer, C_, inner)
-                mean, var, self.inv_std = lh.stats_finalize(s1, s2, outer * inner, self.eps, 0)
+                mean, var, self.inv_std = lh.mean_var(x, 1, outer, C_, inner, self.eps, 0)
                 m = outer * inner
                 lh.bn_running(self.mean.data, self.var.data, self.factor.data, mean, var, self.frac,
                               m / max(m - 1, 1))

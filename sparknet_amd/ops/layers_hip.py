@@ -17,7 +17,7 @@ from . import _lib
 call = _lib.call
 
 NEURON = {"Sigmoid": 0, "TanH": 1, "AbsVal": 2, "BNLL": 3, "Exp": 4, "Log": 5, "Power": 6, "Threshold": 7}
-RED_SUM, RED_DOT, RED_SQ, RED_PRELU, RED_ABS = 0, 1, 2, 3, 4
+RED_SUM, RED_DOT, RED_SQ, RED_PRELU, RED_ABS, RED_CSQ = 0, 1, 2, 3, 4, 5
 LOSS = {"Euclidean": 0, "HingeL1": 1, "HingeL2": 2, "Multinomial": 3, "Infogain": 4, "SigmoidXent": 5,
         "Contrastive": 6}
 
@@ -92,6 +92,18 @@ def stats_finalize(s1, s2, count, eps, mode):
     inv = torch.empty_like(mean)
     call("stats_finalize", s1, s2, n, 1.0 / max(count, 1), float(eps), mode, mean, var, inv)
     return mean, var, inv
+
+
+def mean_var(x, B, outer, A, inner, eps, mode):
+    """Per-(b, a) mean, variance and inverse scale of x over (outer, inner) in two
+    deterministic passes: the mean, then the CENTRED second moment E[(x - mean)^2]
+    (Caffe's batch_norm_layer.cu:50-59 / mvn_layer.cu:31-36 order, no E[x^2] - EX^2
+    cancellation).  mode as stats_finalize: 0 BatchNorm, 1 MVN."""
+    count = outer * inner
+    s1 = axis_reduce(RED_SUM, x, None, B, outer, A, inner)
+    mean, _, _ = stats_finalize(s1, None, count, eps, 2)
+    s2 = axis_reduce(RED_CSQ, x, mean, B, outer, A, inner)
+    return stats_finalize(s1, s2, count, eps, mode | 4)
 
 
 def chan_affine(x, mean, inv, outer, A, inner, out_dtype=None):

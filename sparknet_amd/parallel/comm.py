@@ -29,6 +29,9 @@ import torch
 import torch.distributed as dist
 
 DEFAULT_BUCKET_BYTES = 256 << 20
+# weight averaging: 64 MB buckets (4 for CaffeNet's 244 MB) so the scale / shadow refresh of
+# one bucket overlaps the next bucket's all-reduce; bench.py's comm_bench measures 256 / 64 / 16
+AVERAGE_BUCKET_BYTES = 64 << 20
 WATCHDOG_EXIT_CODE = 75
 
 
@@ -108,6 +111,7 @@ class Comm:
     def __init__(self, backend: str | None = None, device=None, timeout_s: float = 1800.0,
                  bucket_bytes: int = DEFAULT_BUCKET_BYTES, watchdog: bool = False):
         self.bucket_bytes = bucket_bytes
+        self.average_bucket_bytes = AVERAGE_BUCKET_BYTES
         self.watchdog = None
         if dist.is_available() and dist.is_initialized():
             self.owns = False
@@ -123,6 +127,7 @@ class Comm:
             self.owns = False
         self.world_size = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.backend = dist.get_backend() if dist.is_initialized() else None
         if watchdog and self.world_size > 1 and "MASTER_PORT" in os.environ:
             self.watchdog = Watchdog(self.rank, self.world_size)
 
@@ -149,19 +154,43 @@ class Comm:
         works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=async_op) for b in self._buckets(flat)]
         return works if async_op else None
 
-    def average_params(self, net) -> None:
-        """Model averaging: every rank ends with the exact same mean weights."""
+    def bucket_ranges(self, n: int, bucket_bytes: int | None = None, elem: int = 4):
+        per = max(1, (bucket_bytes or self.bucket_bytes) // elem)
+        return [(s, min(n, s + per)) for s in range(0, n, per)]
+
+    def average_params(self, net, bucket_bytes: int | None = None) -> list[float]:
+        """Model averaging: every rank ends with the exact same mean weights.
+
+        The flat fp32 master buffer is all-reduced in buckets issued together as async
+        collectives; each bucket's 1/N scale + bf16 shadow refresh (``hip.scale_shadow``)
+        is enqueued as soon as THAT bucket's all-reduce is waited for, so on RCCL the
+        scaling of bucket i runs on the compute stream while bucket i+1 is still on the
+        wire.  Returns the host-side issue time per bucket (ms; GPU timing is the
+        caller's, e.g. bench.py's events)."""
         if self.world_size == 1:
-            return
-        self.allreduce_sum(net.flat_data)
+            return []
+        import time
+        flat = net.flat_data
         scale = 1.0 / self.world_size
-        if net.flat_data.is_cuda:
-            from ..ops import hip
-            shadow = net.flat_compute if net.flat_compute is not net.flat_data else None
-            hip.scale_shadow(net.flat_data, shadow, scale)
-        else:
-            net.flat_data.mul_(scale)
+        cuda = flat.is_cuda
+        shadow = net.flat_compute if cuda and net.flat_compute is not net.flat_data else None
+        ranges = self.bucket_ranges(flat.numel(), bucket_bytes or self.average_bucket_bytes)
+        works, t = [], []
+        for s, e in ranges:
+            t0 = time.perf_counter()
+            works.append(self.allreduce_sum(flat[s:e], async_op=True) or ())
+            t.append(1e3 * (time.perf_counter() - t0))
+        for (s, e), ws in zip(ranges, works):
+            for w in ws:
+                w.wait()
+            if cuda:
+                from ..ops import hip
+                hip.scale_shadow(flat[s:e], shadow[s:e] if shadow is not None else None, scale)
+            else:
+                flat[s:e].mul_(scale)
+        if not cuda:
             net.sync_compute()
+        return t
 
     def allreduce_grads(self, net, average: bool = True) -> None:
         """Synchronous data-parallel SGD: sum (or average) the flat gradient buffer."""

@@ -7,8 +7,9 @@ Wire- and text-format compatible with the reference's ``caffe.proto`` (package
 the schema is declared as Python tables and turned into a ``FileDescriptorProto``; the
 generated classes are real protobuf messages (text_format, SerializeToString, ...).
 
-The legacy V0 layer message is not modelled; ``V1LayerParameter`` is (``layers`` field
-of NetParameter), enough to read and upgrade V1-era nets (see ``proto.upgrade``).
+The legacy layer messages are modelled too — ``V1LayerParameter`` (``layers`` field of
+NetParameter) and the V0 ``V0LayerParameter`` nested in it as ``layer`` (caffe.proto:1134-1230)
+— so V0- and V1-era nets and caffemodels parse and are upgraded by ``proto.upgrade``.
 """
 from __future__ import annotations
 
@@ -245,7 +246,25 @@ MESSAGES: dict[str, tuple[dict, list]] = {
         o("softmax_param", 39, "SoftmaxParameter"), o("slice_param", 31, "SliceParameter"),
         o("tanh_param", 37, "TanHParameter"), o("threshold_param", 25, "ThresholdParameter"),
         o("window_data_param", 20, "WindowDataParameter"),
-        o("transform_param", 36, "TransformationParameter"), o("loss_param", 42, "LossParameter")]),
+        o("transform_param", 36, "TransformationParameter"), o("loss_param", 42, "LossParameter"),
+        o("layer", 1, "V0LayerParameter")]),
+    "V0LayerParameter": ({"PoolMethod": POOL3}, [
+        o("name", 1, "string"), o("type", 2, "string"), o("num_output", 3, "uint32"),
+        o("biasterm", 4, "bool", True), o("weight_filler", 5, "FillerParameter"),
+        o("bias_filler", 6, "FillerParameter"), o("pad", 7, "uint32", 0), o("kernelsize", 8, "uint32"),
+        o("group", 9, "uint32", 1), o("stride", 10, "uint32", 1),
+        o("pool", 11, "V0LayerParameter.PoolMethod", "MAX"), o("dropout_ratio", 12, "float", 0.5),
+        o("local_size", 13, "uint32", 5), o("alpha", 14, "float", 1.0), o("beta", 15, "float", 0.75),
+        o("k", 22, "float", 1.0), o("source", 16, "string"), o("scale", 17, "float", 1),
+        o("meanfile", 18, "string"), o("batchsize", 19, "uint32"), o("cropsize", 20, "uint32", 0),
+        o("mirror", 21, "bool", False), r("blobs", 50, "BlobProto"), r("blobs_lr", 51, "float"),
+        r("weight_decay", 52, "float"), o("rand_skip", 53, "uint32", 0),
+        o("det_fg_threshold", 54, "float", 0.5), o("det_bg_threshold", 55, "float", 0.5),
+        o("det_fg_fraction", 56, "float", 0.25), o("det_context_pad", 58, "uint32", 0),
+        o("det_crop_mode", 59, "string", "warp"), o("new_num", 60, "int32", 0),
+        o("new_channels", 61, "int32", 0), o("new_height", 62, "int32", 0), o("new_width", 63, "int32", 0),
+        o("shuffle_images", 64, "bool", False), o("concat_dim", 65, "uint32", 1),
+        o("hdf5_output_param", 1001, "HDF5OutputParameter")]),
 }
 
 

@@ -18,14 +18,17 @@ pytestmark = pytest.mark.gpu
 class FakeComm:
     """world_size = 2; the 'other rank' holds ``other`` (fp32, same layout as flat_data)."""
 
-    def __init__(self, other):
+    def __init__(self, other, bucket_bytes=64 << 20):
         from sparknet_amd.parallel.comm import Comm
         self.other = other
         self.world_size, self.rank = 2, 0
+        self.bucket_bytes = self.average_bucket_bytes = bucket_bytes
+        self.bucket_ranges = Comm.bucket_ranges.__get__(self)
         self._avg = Comm.average_params.__get__(self)
 
     def allreduce_sum(self, flat, async_op=False):
-        flat.add_(self.other)
+        o = flat.storage_offset()  # flat is a bucket view of net.flat_data (offset 0)
+        flat.add_(self.other[o:o + flat.numel()])
 
     def average_params(self, net):
         self._avg(net)
@@ -59,7 +62,7 @@ def test_graph_trainer_average_updates_masters_shadow_and_next_replay(gpu):
     net = solver.net
     g = torch.Generator(device="cpu").manual_seed(7)
     other = (net.flat_data.detach().cpu() * (1.0 + 0.5 * torch.randn(net.flat_data.numel(), generator=g))).to(gpu)
-    comm = FakeComm(other)
+    comm = FakeComm(other, bucket_bytes=4 << 20)  # several buckets: per-bucket scale + shadow
     tr = LocalSGDTrainer(solver, comm, tau=3, use_graph=True)
     assert tr.step_fn is not None
     for _ in range(3):

@@ -39,3 +39,13 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "--gpus 2" in r.stderr
+
+
+def test_bench_verify_average_cpu():
+    """--verify-average on the gloo CPU path: post-average masters bitwise equal on both ranks."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--verify-average", *ARGS], cwd=ROOT,
+                       env=_clean_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["avg_check"]["masters_equal_across_ranks"] and out["avg_check"]["shadow_is_bf16_master"]
+    assert out["comm_backend"] == "gloo" and out["average_buckets"] >= 1

@@ -156,6 +156,7 @@ CASES = {
     "mvn": ('layer { name: "L" type: "MVN" bottom: "x" top: "y" }', {"x": (2, 3, 3, 3)}, {}),
     "mvn_across": ('layer { name: "L" type: "MVN" bottom: "x" top: "y" mvn_param { across_channels: true } }',
                    {"x": (2, 3, 3, 3)}, {}),
+    "mvn_2d_per_channel": ('layer { name: "L" type: "MVN" bottom: "x" top: "y" }', {"x": (3, 4)}, {}),
     "mvn_mean_only": ('layer { name: "L" type: "MVN" bottom: "x" top: "y" mvn_param { normalize_variance: false } }',
                       {"x": (2, 3, 3, 3)}, {}),
     "im2col": ('layer { name: "L" type: "Im2col" bottom: "x" top: "y" convolution_param { kernel_size: 2 '
@@ -263,3 +264,20 @@ def test_dropout_odd_count_train(gpu):
     net.forward()
     y = net.blob_by_name("y").nchw().float().cpu()
     assert set(torch.unique(y).tolist()) <= {0.0, 2.0}
+
+
+@pytest.mark.parametrize("layer", [
+    'layer { name: "L" type: "BatchNorm" bottom: "x" top: "y" batch_norm_param { use_global_stats: false } }',
+    'layer { name: "L" type: "MVN" bottom: "x" top: "y" mvn_param { across_channels: true } }'])
+def test_norm_variance_large_mean(gpu, layer):
+    """|mean| >> std (un-normalised pixels): the variance is the centred second moment
+    E[(x - EX)^2] (batch_norm_layer.cu:50-59, mvn_layer.cu:31-36), not E[x^2] - EX^2,
+    which cancels in fp32 and drives 1 / sqrt(var + eps) towards 1 / sqrt(eps)."""
+    g = torch.Generator().manual_seed(11)
+    shape = (64, 5) if "BatchNorm" in layer else (5, 64)
+    x = 1000.0 + torch.randn(*shape, generator=g)
+    outs = run_both(layer, {"x": shape}, values={"x": x})
+    y = outs["cuda"]["tops"][0]
+    # normalised output: unit variance per channel (BatchNorm) / per row (MVN)
+    dim = 0 if "BatchNorm" in layer else 1
+    assert abs(y.var(dim=dim, unbiased=False).mean().item() - 1.0) < 0.05
