@@ -73,7 +73,9 @@ struct SnGemmArgs {
   const float* bias;  // per output column n (offset by g*N), EPI_BF16 only
   int relu;
   int tile;           // 0: 128x128, 1: 256x64, 4: 128x96, 5: 256x48 (4 waves, 2 stages); 2: 256x128, 3: 128x256 (8 waves, 3 stages);
-                      // 6: 256x256, 7: 256x128 (gemm256_kernel: 8 waves, half-tile phased pipeline)
+                      // 6: 256x256, 7: 256x128 (gemm256_kernel: 8 waves, half-tile phased pipeline);
+                      // 10: 128x64 (4 waves, 3 blocks / CU); 11: 256x256, 12 / 13: 256x128, 14: 256x192
+                      // (gemm_kernel, 8 waves, 2 stages, one block per CU)
   const bf16_t* gate; // EPI_BF16: zero outputs where gate (same layout as C) <= 0 (fused ReLU backward)
   int fp8;            // operands are e4m3 bytes (K-contiguous only); k counts fp8 elements
   const float* deq_a; // fp8: dequantisation factors (1 / quantisation scale) of A and B, device scalars
@@ -111,6 +113,7 @@ struct SnGemmArgs {
   // bf16 epilogues of unsplit 4-wave tiles: stage the finished tile through the idle LDS
   // stages and store it as whole 16-B row chunks (host: ldc % 8 == 0, 16-B aligned C)
   int lds_store;
+  int addr_legacy;  // 1: general per-lane address decode only (A/B probe of the fast DMA paths)
 };
 
 }  // extern "C"
@@ -182,9 +185,25 @@ struct GStager {
   int sn_, sp_, sq_;
   int cdh[MC ? NI : 1], cdw[MC ? NI : 1], colo[MC ? NI : 1];
   bool wave_has_one;
+  // Low-VALU address paths (all decisions wave-uniform, taken once at init):
+  //  KC+IM2COL: kcmode 1 = every K-step lies inside ONE filter tap (Cg % (8*EPC) == 0), so
+  //   the tap offset and its (dh, dw) shift are scalars and a lane's DMA offset is
+  //   rowb[j] + scalar with a two-compare bounds test; kcmode 2 = a K-step straddles at
+  //   most one tap boundary (Cg >= 8*EPC), resolved by one per-lane select per chunk
+  //   parity; kcmode 0 = the general per-lane decode.  rowb[j] = byte offset of the
+  //   lane's pixel corner + its chunk (pixels past the matrix get ph = -2^28: never valid).
+  //  DENSE (KC and MC): fast = the operand spans < 2^31 bytes, so each lane keeps a fixed
+  //   32-bit voffset (its row / column and chunk, or 0x80000000 when outside the matrix)
+  //   and the K advance is the instruction's scalar soffset: no VALU per DMA outside the
+  //   K tail.
+  int kcmode;
+  bool fast;
+  unsigned rowb[NI];  // modular byte arithmetic: operands up to 4 GB (the resource's range)
+  int kch[NI], voff[NI];
 
   SN_DEV void init(const SnOperand& op, int grp, int wave, int lane, int tile_row0, int rows_lim,
-                   int tile_col0, int cols_lim, int ones = -1, int k_start = 0) {
+                   int tile_col0, int cols_lim, int ones = -1, int k_start = 0, int k_lim_hint = 0,
+                   int legacy = 0) {
     ld = op.ld;
     g = op.g;
     ones_col = ones;
@@ -242,6 +261,42 @@ struct GStager {
         colo[j] = (cdh[j] * g.W + cdw[j]) * g.C + coff + cc[j];
       }
     }
+    kcmode = 0;
+    fast = false;
+    if (MODE == OP_IM2COL && !MC) {
+      kcmode = __builtin_amdgcn_readfirstlane(legacy ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        kch[j] = ch[j] * EPC;
+        rowb[j] = (unsigned)(rowoff[j] + kch[j]) * (unsigned)ES;
+        if (!pv[j]) ph[j] = -(1 << 28);
+      }
+    }
+    if (MODE == OP_DENSE) {
+      // element extent of the operand for this group: KC rows x ld, MC (k rows) x ld
+      const long long extent = MC ? (long long)k_lim_hint * ld : (long long)rows_lim * ld;
+      fast = __builtin_amdgcn_readfirstlane((int)(!legacy && extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
+      // built unconditionally from wave-uniform values so it stays in SGPRs
+      const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+      rsrc[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
+      rsrc[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffffu));
+      rsrc[2] = (int)0x80000000u;  // num_records: every valid offset is below 2^31
+      rsrc[3] = 0x00020000;
+      if (fast) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          if (!MC) {
+            const int row = tile_row0 + rr[j];
+            kch[j] = ch[j] * EPC;
+            voff[j] = row < rows_lim ? (int)(((long long)row * ld + kch[j]) * ES) : (int)0x80000000u;
+          } else {
+            const int col = tile_col0 + ch[j] * 8;
+            kch[j] = rr[j];
+            voff[j] = col < cols_lim ? (int)(((long long)rr[j] * ld + col) * 2) : (int)0x80000000u;
+          }
+        }
+      }
+    }
     if (MODE == OP_IM2COL && MC) {
       const int PQ = g.P * g.Q, pix = k_start + rr[0];
       sn_ = fdiv(pix, PQ, invPQ);
@@ -260,14 +315,22 @@ struct GStager {
   // every wait on these DMAs is explicit in the K-loop (counted vmcnt + barrier).
   SN_DEV void dma(const char* src, bool valid, char* lds, bool one = false) {
     const void* s = valid ? (const void*)src : (one ? (const void*)g_one16 : (const void*)g_zero16);
-    const uint32_t m0 = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds));
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(s) : "memory");
   }
   // LDS-DMA through the buffer resource: byte offset off (0xffffffff: out of range -> 0)
   SN_DEV void dma_buf(unsigned off, char* lds) {
-    const uint32_t m0 = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds));
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off),
                  "s"(rsrc)
+                 : "memory");
+  }
+  // ... with a wave-uniform byte offset `so` in the instruction's SGPR offset field
+  // (the per-lane voffset carries the out-of-range marker 0x80000000)
+  SN_DEV void dma_buf_so(unsigned off, unsigned so, char* lds) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds));
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0), "v"(off),
+                 "s"(rsrc), "s"(so)
                  : "memory");
   }
 
@@ -276,6 +339,17 @@ struct GStager {
     char* dst = lds + wave * NI * 1024;
     if (!MC) {
       if (MODE == OP_DENSE) {
+        if (fast) {
+          const bool tail = k_tile + 8 * EPC > k_lim;
+          const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)(k_tile * ES));
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            unsigned o = (unsigned)voff[j];
+            if (tail && k_tile + kch[j] >= k_lim) o = 0x80000000u;
+            dma_buf_so(o, so, dst + j * 1024);
+          }
+          return;
+        }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           int row = tile_rc0 + rr[j], k = k_tile + ch[j] * EPC;
@@ -293,6 +367,43 @@ struct GStager {
             ns = 0;
             ++nr;
           }
+        }
+        if (kcmode != 0) {
+          const bool tail = k_tile + 8 * EPC > k_lim;
+          const int hr0 = r0 * g.dh, ws0 = s0 * g.dw;
+          const unsigned tb0 = (unsigned)((hr0 * g.W + ws0) * g.C + c0) * (unsigned)ES;
+          int hre[2], wse[2];
+          unsigned tbe[2];
+          if (kcmode == 1) {
+            hre[0] = hre[1] = hr0;
+            wse[0] = wse[1] = ws0;
+            tbe[0] = tbe[1] = tb0;
+          } else {
+            // chunks past the tap's last channel belong to the next tap (scalar decode)
+            int r1 = r0, s1 = s0 + 1;
+            if (s1 == g.S) {
+              s1 = 0;
+              ++r1;
+            }
+            const int hr1 = r1 * g.dh, ws1 = s1 * g.dw;
+            const unsigned tb1 = (unsigned)((hr1 * g.W + ws1) * g.C + c0 - g.Cg) * (unsigned)ES;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const bool x = c0 + kch[e] >= g.Cg;
+              hre[e] = x ? hr1 : hr0;
+              wse[e] = x ? ws1 : ws0;
+              tbe[e] = x ? tb1 : tb0;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int e = j & 1;
+            const int h = ph[j] + hre[e], w = pw[j] + wse[e];
+            bool v = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+            if (tail) v = v && k_tile + kch[j] < k_lim;
+            dma_buf(v ? rowb[j] + tbe[e] : 0xffffffffu, dst + j * 1024);
+          }
+          return;
         }
         int kv[2], dh[2], dw[2], toff[2];
 #pragma unroll
@@ -338,7 +449,16 @@ struct GStager {
         }
       }
     } else {
-      if (MODE == OP_DENSE) {
+      if (MODE == OP_DENSE && fast) {
+        const bool tail = k_tile + BK > k_lim;
+        const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)((long long)k_tile * ld * 2));
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          unsigned o = (unsigned)voff[j];
+          if (tail && k_tile + kch[j] >= k_lim) o = 0x80000000u;
+          dma_buf_so(o, so, dst + j * 1024);
+        }
+      } else if (MODE == OP_DENSE) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           int k = k_tile + rr[j], col = tile_rc0 + ch[j] * 8;
@@ -597,7 +717,7 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
 }
 
 template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, bool FP8 = false,
-          int NFR = 4>
+          int NFR = 4, int MFR = 4>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) gemm_kernel(SnGemmArgs args) {
   // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
   constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
@@ -605,9 +725,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   // stages 64 rows, the 16 beyond the tile read the zero page)
   constexpr int BNL = ((BN / 8) % NW == 0) ? BN : (BN + 63) / 64 * 64;
   constexpr int A_BYTES = BM * 128, B_BYTES = BNL * 128, STAGE = A_BYTES + B_BYTES;
-  // waves along N / M; each wave owns 64 rows x (16*NFR) columns (NFR = 4, or 3 for 96-wide tiles)
+  // waves along N / M; each wave owns (16*MFR) rows x (16*NFR) columns: 64 x 64 (NFR = 4, or
+  // 3 for 96-wide tiles), or 128 x (16*NFR) for the 8-wave 256-row tiles (MFR = 8)
   constexpr int WN = BN / (16 * NFR), WM = NW / WN;
-  static_assert(WN * 16 * NFR == BN && WM * 64 == BM && WM * WN == NW, "tile/wave layout mismatch");
+  static_assert(WN * 16 * NFR == BN && WM * 16 * MFR == BM && WM * WN == NW, "tile/wave layout mismatch");
   static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
   // Distinct LDS objects (one per stage): the compiler's alias scopes then prove that
   // the ds_reads of one stage do not depend on the DMA in flight into another, so it
@@ -647,44 +768,64 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   using SB = GStager<BMC, BMODE, BNL, NW, ES>;
   SA sa;
   SB sb;
-  sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, split * args.kchunk);
+  sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, split * args.kchunk, args.K, args.addr_legacy);
   const int n_lim = min(args.N, n_blk + BN);
-  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1, split * args.kchunk);
+  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1, split * args.kchunk, args.K, args.addr_legacy);
 
-  f32x4 acc[NFR][4];
+  f32x4 acc[NFR][MFR];
 #pragma unroll
   for (int i = 0; i < NFR; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int wm0 = (wave % WM) * 64, wn0 = (wave / WM) * (16 * NFR);
+  const int wm0 = (wave % WM) * (16 * MFR), wn0 = (wave / WM) * (16 * NFR);
   const int nk = k1 > k0 ? (k1 - k0 + BKE - 1) / BKE : 0;
 
   auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
     if constexpr (FP8) {
-      i32x8 fa8[4], fb8[NFR];
+      i32x8 fa8[MFR], fb8[NFR];
 #pragma unroll
       for (int i = 0; i < NFR; ++i) fb8[i] = read_frag8(lb, wn0 + 16 * i, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa8[i] = read_frag8(la, wm0 + 16 * i, lane);
+      for (int i = 0; i < MFR; ++i) fa8[i] = read_frag8(la, wm0 + 16 * i, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < NFR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)  // formats 0/0 = e4m3 x e4m3, block scales 2^0 (E8M0 127)
+        for (int j = 0; j < MFR; ++j)  // formats 0/0 = e4m3 x e4m3, block scales 2^0 (E8M0 127)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa8[j], acc[i][j], 0, 0, 0, 127, 0,
                                                                         127);
       __builtin_amdgcn_s_setprio(0);
       return;
     }
-    bf16x8_t fa[2][4], fb[2][NFR];
+    if constexpr (MFR * NFR > 16) {
+      // 128-row wave tiles: fragments of one 32-deep k-substep at a time (the accumulators
+      // already take 4 * MFR * NFR VGPRs)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8_t fa[MFR], fb[NFR];
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) fb[i] = read_frag<BMC, BNL>(lb, wn0 + 16 * i, s, lane);
+#pragma unroll
+        for (int i = 0; i < MFR; ++i) fa[i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < NFR; ++i)
+#pragma unroll
+          for (int j = 0; j < MFR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      return;
+    }
+    bf16x8_t fa[2][MFR], fb[2][NFR];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
       for (int i = 0; i < NFR; ++i) fb[s][i] = read_frag<BMC, BNL>(lb, wn0 + 16 * i, s, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[s][i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
+      for (int i = 0; i < MFR; ++i) fa[s][i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -692,7 +833,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
 #pragma unroll
       for (int i = 0; i < NFR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < MFR; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][i], fa[s][j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
@@ -749,7 +890,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     // the bias column take the per-fragment path below.
     const bool interior = m_blk + BM <= args.M && n_blk + BN <= c_cols && (args.ldc & 3) == 0 &&
                           ((grp * args.c_gstride) & 3) == 0;
-    if constexpr (BM == 128 && BN == 128 && NW == 4 && NFR == 4 && NS == 2 && !FP8) {
+    if constexpr (BM == 128 && BN == 128 && NW == 4 && NFR == 4 && MFR == 4 && NS == 2 && !FP8) {
       // LDS-transposed update (128x128 tiles): the MFMA layout gives each wave-instruction
       // 16 rows x 64 B, which the HBM streams of w / h / shadow serve at ~3.7 TB/s; the
       // gradient tile is instead staged through the (now idle) LDS stages as fp32 row-major
@@ -810,9 +951,9 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       const float* hy = args.sgd_hyper;
       const float rate = hy[0] * args.sgd_lr_mult, mom = hy[1], decay = hy[2] * args.sgd_decay_mult;
       const float gscale = hy[4];
-      float4 Wv[4][NFR], Av[4][NFR];
+      float4 Wv[MFR][NFR], Av[MFR][NFR];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < MFR; ++j)
 #pragma unroll
         for (int i = 0; i < NFR; ++i) {
           const long long o = grp * args.c_gstride + (long long)(m_blk + wm0 + 16 * j + mrow_l) * args.ldc +
@@ -821,7 +962,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
           Av[j][i] = *reinterpret_cast<const float4*>(args.sgd_h + o);
         }
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < MFR; ++j)
 #pragma unroll
         for (int i = 0; i < NFR; ++i) {
           const long long o = grp * args.c_gstride + (long long)(m_blk + wm0 + 16 * j + mrow_l) * args.ldc +
@@ -844,7 +985,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       return;
     }
   }
-  if constexpr (epi_bf16<EPI>() && NS == 2) {
+  if constexpr (epi_bf16<EPI>() && NS == 2 && (BM / 2) * (BN * 2 + 16) <= STAGE) {
     if (args.lds_store) {
       // The MFMA layout stores 16 rows x 8 B per lane group (32-B row pieces per
       // wave-instruction); instead stage the finished bf16 tile in the idle LDS stages
@@ -856,7 +997,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       __builtin_amdgcn_s_barrier();  // every wave is past its last fragment read of the stages
       char* wbuf = wm0 < HALF ? smem0 : smem1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < MFR; ++j) {
         const int lr = wm0 + 16 * j + mrow_l, m = m_blk + lr;
 #pragma unroll
         for (int i = 0; i < NFR; ++i) {
@@ -889,7 +1030,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < MFR; ++j) {
     const int m = m_blk + wm0 + 16 * j + mrow_l;
     if (m >= args.M) continue;
 #pragma unroll
@@ -962,10 +1103,10 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
 
   SA sa_lo, sa_hi;
   SB sb_lo, sb_hi;
-  sa_lo.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, k0);
-  sa_hi.init(args.A, grp, wv, lane, m_blk + HA, args.M, m_blk + HA, args.M, -1, k0);
-  sb_lo.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, ones, k0);
-  sb_hi.init(args.B, grp, wv, lane, n_blk + HB, n_lim, n_blk + HB, n_lim, ones, k0);
+  sa_lo.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, k0, args.K, args.addr_legacy);
+  sa_hi.init(args.A, grp, wv, lane, m_blk + HA, args.M, m_blk + HA, args.M, -1, k0, args.K, args.addr_legacy);
+  sb_lo.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, ones, k0, args.K, args.addr_legacy);
+  sb_hi.init(args.B, grp, wv, lane, n_blk + HB, n_lim, n_blk + HB, n_lim, ones, k0, args.K, args.addr_legacy);
 
   auto A_lo = [&](int b) { return smem + b * STAGE; };
   auto A_hi = [&](int b) { return smem + b * STAGE + A_HALF; };
@@ -1132,24 +1273,24 @@ int launch256(const SnGemmArgs& a, hipStream_t stream) {
   return 4;
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS, int NFR = 4>
+template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS, int NFR = 4, int MFR = 4>
 int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS, false, NFR>), grid,
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS, false, NFR, MFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_BF16_DROP:  // InnerProduct forward only (dense NT)
       if (AMC || AMODE != OP_DENSE || BMC || BMODE != OP_DENSE) return 4;
-      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, NW, NS, false, NFR>), grid,
+      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, NW, NS, false, NFR, MFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS, false, NFR>), grid,
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS, false, NFR, MFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32_ACC:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS, false, NFR>), grid,
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS, false, NFR, MFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     default:
@@ -1180,6 +1321,32 @@ int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
   }
   if (a.a_mc == 0 && a.a_mode == OP_IM2COL && a.b_mc == 1 && a.b_mode == OP_FLIPW)  // conv dgrad
     return launch_epi<0, OP_IM2COL, 1, OP_FLIPW, BM, BN, NW, NS>(a, grid, stream);
+  return 4;
+}
+
+// 8-wave tiles with 256 rows, 2 LDS stages, one block per CU (tiles 11-14): the block
+// tile halves (256x256) or cuts by a quarter to a third (256x128, 256x192) the L2 -> LDS
+// bytes and LDS-DMA instructions per MFMA of the 128x128 tile, whose operand traffic (not
+// its MFMA rate) bounds it on the implicit-conv products.
+template <int BM, int BN, int MFR, int NFR>
+int launch_big(const SnGemmArgs& a, hipStream_t stream) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles * a.splits * a.groups);
+  const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  constexpr bool mc_b_ok = (BN / 8) == 16 || (BN / 8) == 32;  // MC B images need 16 or 32 chunks per row
+  switch (key) {
+    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);   // NT dense
+    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);  // conv fwd/dgrad
+    default: break;
+  }
+  if constexpr (mc_b_ok) {
+    switch (key) {
+      case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);   // NN dense
+      case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);   // TN dense
+      case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);  // conv wgrad
+      default: break;
+    }
+  }
   return 4;
 }
 
@@ -1282,6 +1449,10 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 8: return a.epi == EPI_SGD ? 4 : launch256<256, 4>(a, stream);  // 4-phase variant (A/B probes)
     case 9: return a.epi == EPI_SGD ? 4 : launch256<128, 4>(a, stream);
     case 10: return a.epi == EPI_SGD ? 4 : launch_tile64(a, stream);
+    case 11: return a.epi == EPI_SGD ? 4 : launch_big<256, 256, 8, 4>(a, stream);  // waves 2x4 of 128x64
+    case 12: return a.epi == EPI_SGD ? 4 : launch_big<256, 128, 8, 2>(a, stream);  // waves 2x4 of 128x32
+    case 13: return a.epi == EPI_SGD ? 4 : launch_big<256, 128, 4, 4>(a, stream);  // waves 4x2 of 64x64
+    case 14: return a.epi == EPI_SGD ? 4 : launch_big<256, 192, 8, 3>(a, stream);  // waves 2x4 of 128x48
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

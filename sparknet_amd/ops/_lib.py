@@ -47,7 +47,8 @@ class SnGemmArgs(C.Structure):
                 ("sgd_w", C.c_void_p), ("sgd_h", C.c_void_p), ("sgd_shadow", C.c_void_p), ("sgd_hyper", C.c_void_p),
                 ("sgd_lr_mult", C.c_float), ("sgd_decay_mult", C.c_float), ("sgd_flags", C.c_int),
                 ("drop_rng", C.c_void_p), ("drop_stream", C.c_int), ("drop_thr", C.c_uint),
-                ("drop_scale", C.c_float), ("gate_scale", C.c_float), ("lds_store", C.c_int)]
+                ("drop_scale", C.c_float), ("gate_scale", C.c_float), ("lds_store", C.c_int),
+                ("addr_legacy", C.c_int)]
 
 
 def lib_path(name: str = "libsn_kernels.so") -> Path:

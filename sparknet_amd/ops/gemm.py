@@ -111,10 +111,14 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 
 
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
-         6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64)}
-# gemm256_kernel tiles (6, 7) run one 512-thread block per CU
-_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768}
-_KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1}
+         6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64),
+         11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192)}
+# gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
+# 512-thread block per CU
+_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256}
+_KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55}
+# autotune candidates 11-14 (SN_GEMM_TILE8W=0 drops them)
+_TILE8W = os.environ.get("SN_GEMM_TILE8W", "1") != "0"
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
 _RASTER_N = int(os.environ.get("SN_GEMM_RASTER_N", "-1"))  # -1: heuristic
 _TILE256 = os.environ.get("SN_GEMM_TILE256", "1") != "0"  # autotune candidates 6 / 7 (gemm256_kernel)
@@ -238,6 +242,9 @@ _NO_XTRA = (0, 0, 0.0, 1.0)
 # bf16 epilogues of the 4-wave tiles store through LDS as whole 16-B row chunks
 # (SnGemmArgs.lds_store); SN_GEMM_LDS_EPI=0 keeps the per-fragment stores (A/B)
 _LDS_EPI = os.environ.get("SN_GEMM_LDS_EPI", "1") != "0"
+# SnGemmArgs.addr_legacy: 1 = the general per-lane DMA address decode only (A/B probes of
+# the scalar-offset fast paths; SN_GEMM_LEGACY_ADDR=1)
+_ADDR_LEGACY = int(os.environ.get("SN_GEMM_LEGACY_ADDR", "0"))
 
 
 def _drop_fields(xtra):
@@ -269,6 +276,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
                                bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster,
                                ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), lds)
+        args.addr_legacy = _ADDR_LEGACY
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
@@ -278,6 +286,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
                            sa, sb, ws.data_ptr(), ldw, splits * M * ldw, M * ldw, 0, 0, tile, 0, int(fp8), *dq, raster,
                            ones, 0, 0, *sg, *_drop_fields(_NO_XTRA))
+    args.addr_legacy = _ADDR_LEGACY
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
     rng, dstream, ratio, gscale = xtra
@@ -354,6 +363,12 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
         tiles.append(7)
         if N > 128:
             tiles.append(6)
+    if epi != EPI_SGD and _TILE8W and M >= 256 and N > 64:
+        tiles += [12, 13]
+        if N > 128:
+            tiles.append(11)
+        if N > 128 and (b_kc_dense or N % 192 == 0):
+            tiles.append(14)
     if epi != EPI_SGD:
         if _TILE64:
             tiles.append(10)

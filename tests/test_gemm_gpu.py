@@ -160,10 +160,15 @@ def test_fp8_conv_forward(gpu, case):
 
 
 
-# --- gemm256_kernel (tiles 6 = 256x256, 7 = 256x128): every operand layout, ragged edges,
-# short and long K (the phased DMA pipeline issues zero-page DMAs past the last K-step),
-# split-K, the bias-gradient column and the implicit-GEMM convolutions
-@pytest.mark.parametrize("tile", [6, 7])
+# --- gemm256_kernel (tiles 6 = 256x256, 7 = 256x128) and the 8-wave 2-stage gemm_kernel
+# tiles (11 = 256x256, 12 / 13 = 256x128, 14 = 256x192, K-contiguous B only): every operand
+# layout, ragged edges, short and long K (the phased DMA pipeline issues zero-page DMAs past
+# the last K-step), split-K, the bias-gradient column and the implicit-GEMM convolutions
+BIG_TILES = [6, 7, 11, 12, 13, 14]
+MC_B = {6, 7, 11, 12, 13}  # tiles with an MC (k-strided) B operand instance
+
+
+@pytest.mark.parametrize("tile", BIG_TILES)
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 200, 136), (1000, 384, 2304), (513, 129, 1000), (64, 48, 40)])
 def test_gemm256_layouts(gpu, tile, M, N, K, monkeypatch):
     from sparknet_amd.ops import gemm as G
@@ -171,6 +176,8 @@ def test_gemm256_layouts(gpu, tile, M, N, K, monkeypatch):
     x, w = _bf(M, K, device=gpu), _bf(N, K, device=gpu)
     b = torch.randn(N, device=gpu)
     _close(G.linear_fwd(x, w, b, relu=True), torch.relu(x.float() @ w.float().t() + b))
+    if tile not in MC_B:
+        return
     dy = _bf(M, N, device=gpu)
     w2 = _bf(N, K, device=gpu)
     _close(G.linear_dgrad(dy, w2), dy.float() @ w2.float())
@@ -179,7 +186,7 @@ def test_gemm256_layouts(gpu, tile, M, N, K, monkeypatch):
     _close(dw, 1 + dy.float().t() @ x.float())
 
 
-@pytest.mark.parametrize("tile", [6, 7])
+@pytest.mark.parametrize("tile", sorted(MC_B))
 @pytest.mark.parametrize("splits", [1, 3])
 def test_gemm256_bias_column_and_splitk(gpu, tile, splits, monkeypatch):
     from sparknet_amd.ops import gemm as G
@@ -206,9 +213,10 @@ def _pad(t):
     return out
 
 
-@pytest.mark.parametrize("tile", [6, 7])
+@pytest.mark.parametrize("tile", BIG_TILES)
 @pytest.mark.parametrize("case", [(2, 13, 13, 64, 384, 3, 3, 1, 1, 1), (2, 27, 27, 96, 256, 5, 5, 1, 2, 2),
-                                  (4, 14, 14, 32, 128, 1, 1, 1, 0, 1), (3, 9, 9, 64, 40, 3, 3, 1, 1, 2)])
+                                  (4, 14, 14, 32, 128, 1, 1, 1, 0, 1), (3, 9, 9, 64, 40, 3, 3, 1, 1, 2),
+                                  (2, 7, 7, 192, 96, 3, 3, 1, 1, 2)])
 def test_gemm256_conv(gpu, tile, case, monkeypatch):
     from sparknet_amd.ops import gemm as G, hip, ref
     from sparknet_amd.ops.spec import ConvSpec
@@ -219,6 +227,8 @@ def test_gemm256_conv(gpu, tile, case, monkeypatch):
     w = (torch.randn(K, R, S, Cc // g, device=gpu) * 0.1).to(torch.bfloat16)
     bias = torch.randn(K, device=gpu)
     _close(hip.conv_forward(x, w, bias, s, relu=True), ref.conv_forward(x, w, bias, s, relu=True))
+    if tile not in MC_B:  # forward only; the dgrad / wgrad products need MC B instances
+        return
     dy = _bf(N, s.P, s.Q, K, device=gpu)
     dw, db = torch.zeros(K, R, S, Cc // g, device=gpu), torch.zeros(K, device=gpu)
     dw_r, db_r = torch.zeros_like(dw), torch.zeros_like(db)
@@ -278,3 +288,30 @@ def test_tile64_layouts(gpu, M, N, K, monkeypatch):
     y = hip.conv_forward(x, w, None, s)
     from sparknet_amd.ops import ref
     _close(y, ref.conv_forward(x.float().cpu(), w.float().cpu(), None, s).to(gpu))
+
+
+@pytest.mark.parametrize("tile", [0, 1, 5, 11, 12])
+@pytest.mark.parametrize("case", [(2, 13, 13, 64, 384, 3, 3, 1, 1, 1), (2, 27, 27, 96, 256, 5, 5, 1, 2, 2),
+                                  (2, 7, 7, 192, 96, 3, 3, 1, 1, 2), (3, 9, 9, 32, 40, 3, 3, 2, 1, 1)])
+def test_fast_dma_addressing_bitwise(gpu, tile, case, monkeypatch):
+    """The scalar-offset DMA address paths (uniform-tap / tap-straddle implicit im2col,
+    soffset-advanced dense operands) stage exactly the bytes of the general per-lane
+    decode (SnGemmArgs.addr_legacy = 1): outputs of fwd / dgrad / wgrad are bitwise equal."""
+    from sparknet_amd.ops import gemm as G, hip
+    from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    N, H, W, Cc, K, R, S, st, pd, g = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    x = _bf(N, H, W, Cc, device=gpu)
+    w = (torch.randn(K, R, S, Cc // g, device=gpu) * 0.1).to(torch.bfloat16)
+    dy = _bf(N, s.P, s.Q, K, device=gpu)
+    outs = []
+    for legacy in (0, 1):
+        monkeypatch.setattr(G, "_ADDR_LEGACY", legacy)
+        y = hip.conv_forward(x, w, None, s)
+        dw = torch.zeros(K, R, S, Cc // g, device=gpu)
+        dx = hip.conv_backward(dy, x, w, s, True, dw, None) if tile in (0, 1, 11, 12) else None
+        outs.append((y, dx, dw))
+    for a, b in zip(outs[0], outs[1]):
+        if a is not None:
+            assert torch.equal(a, b)
