@@ -158,6 +158,7 @@ struct GStager {
   static_assert(NI >= 1 && NI * 8 * NW == TILE, "whole wave-instructions per tile");
   static_assert(MC || MODE != OP_IM2COL || NI % 2 == 0, "KC im2col: chunk pattern repeats with period 2 in j");
   static_assert(ES == 2 || !MC, "fp8 operands are K-contiguous");
+  static_assert(!MC || RPI * CPL == 64, "MC images: whole rows per wave-instruction");
   const char* base;  // element offsets below are scaled by ES
   long long ld;
   SnConvGeom g;
@@ -1328,23 +1329,29 @@ int launch_tile(const SnGemmArgs& a, hipStream_t stream) {
 // tile halves (256x256) or cuts by a quarter to a third (256x128, 256x192) the L2 -> LDS
 // bytes and LDS-DMA instructions per MFMA of the 128x128 tile, whose operand traffic (not
 // its MFMA rate) bounds it on the implicit-conv products.
-template <int BM, int BN, int MFR, int NFR>
+template <int BM, int BN, int MFR, int NFR, int NW = 8>
 int launch_big(const SnGemmArgs& a, hipStream_t stream) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles * a.splits * a.groups);
   const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
-  constexpr bool mc_b_ok = (BN / 8) == 16 || (BN / 8) == 32;  // MC B images need 16 or 32 chunks per row
+  constexpr bool mc_b_ok = (BN / 8) == 8 || (BN / 8) == 16 || (BN / 8) == 32;  // MC images: 64 % chunks per row == 0
+  constexpr bool mc_a_ok = (BM / 8) == 8 || (BM / 8) == 16 || (BM / 8) == 32;
   switch (key) {
-    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);   // NT dense
-    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);  // conv fwd/dgrad
+    case 0b0000: return launch_epi<0, OP_DENSE, 0, OP_DENSE, BM, BN, NW, 2, NFR, MFR>(a, grid, stream);   // NT dense
+    case 0b0100: return launch_epi<0, OP_IM2COL, 0, OP_DENSE, BM, BN, NW, 2, NFR, MFR>(a, grid, stream);  // conv fwd/dgrad
     default: break;
   }
   if constexpr (mc_b_ok) {
     switch (key) {
-      case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);   // NN dense
-      case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);   // TN dense
-      case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL, BM, BN, 8, 2, NFR, MFR>(a, grid, stream);  // conv wgrad
+      case 0b0010: return launch_epi<0, OP_DENSE, 1, OP_DENSE, BM, BN, NW, 2, NFR, MFR>(a, grid, stream);   // NN dense
       default: break;
+    }
+    if constexpr (mc_a_ok) {
+      switch (key) {
+        case 0b1010: return launch_epi<1, OP_DENSE, 1, OP_DENSE, BM, BN, NW, 2, NFR, MFR>(a, grid, stream);   // TN dense
+        case 0b1011: return launch_epi<1, OP_DENSE, 1, OP_IM2COL, BM, BN, NW, 2, NFR, MFR>(a, grid, stream);  // conv wgrad
+        default: break;
+      }
     }
   }
   return 4;
@@ -1453,6 +1460,12 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 12: return a.epi == EPI_SGD ? 4 : launch_big<256, 128, 8, 2>(a, stream);  // waves 2x4 of 128x32
     case 13: return a.epi == EPI_SGD ? 4 : launch_big<256, 128, 4, 4>(a, stream);  // waves 4x2 of 64x64
     case 14: return a.epi == EPI_SGD ? 4 : launch_big<256, 192, 8, 3>(a, stream);  // waves 2x4 of 128x48
+    // 4-wave tiles of 320 rows + columns (40 KB LDS stages: two blocks per CU, like 128x128)
+    // with 17 % fewer operand bytes per MFMA than 128x128
+    case 15: return a.epi == EPI_SGD ? 4 : launch_big<128, 192, 4, 6, 4>(a, stream);  // waves 2x2 of 64x96
+    case 16: return a.epi == EPI_SGD ? 4 : launch_big<192, 128, 6, 4, 4>(a, stream);  // waves 2x2 of 96x64
+    case 17: return a.epi == EPI_SGD ? 4 : launch_big<192, 96, 6, 3, 4>(a, stream);   // waves 2x2 of 96x48
+    case 18: return a.epi == EPI_SGD ? 4 : launch_big<192, 64, 6, 2, 4>(a, stream);   // waves 2x2 of 96x32
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

@@ -67,15 +67,28 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, l
     const int r = (int)(i / cols4), c = (int)(i - (long long)r * cols4) * 4;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     const bool vec = (c + 3 < cols) && ((ldw & 3) == 0);
-    for (int s = 0; s < splits; ++s) {
-      const float* p = wsg + s * sstride + (long long)r * ldw + c;
-      if (vec) {
-        float4 v = *reinterpret_cast<const float4*>(p);
-        acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
-      } else {
-        for (int k = 0; k < 4; ++k)
-          if (c + k < cols) acc[k] += p[k];
+    const float* p0 = wsg + (long long)r * ldw + c;
+    if (vec) {
+      // slab loads issued four at a time before they are summed (in split order): a load
+      // inside a per-split branch made each split a dependent L2 round trip
+      int s = 0;
+      for (; s + 3 < splits; s += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p0 + (s + u) * sstride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc[0] += v[u].x; acc[1] += v[u].y; acc[2] += v[u].z; acc[3] += v[u].w;
+        }
       }
+      for (; s < splits; ++s) {
+        const float4 v = *reinterpret_cast<const float4*>(p0 + s * sstride);
+        acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+      }
+    } else {
+      for (int s = 0; s < splits; ++s)
+        for (int k = 0; k < 4; ++k)
+          if (c + k < cols) acc[k] += p0[s * sstride + k];
     }
     reduce_store(o, g, r, c, acc);
   }

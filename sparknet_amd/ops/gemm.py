@@ -112,7 +112,8 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
          6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64),
-         11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192)}
+         11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192), 15: (128, 192), 16: (192, 128),
+         17: (192, 96), 18: (192, 64)}
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
 _SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256}
@@ -369,6 +370,14 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
             tiles.append(11)
         if N > 128 and (b_kc_dense or N % 192 == 0):
             tiles.append(14)
+    if epi != EPI_SGD and _TILE8W and N > 64:
+        tiles.append(16)
+        if b_kc_dense and N > 128:
+            tiles.append(15)
+    if epi != EPI_SGD and _TILE8W and M >= 192:
+        tiles.append(18)
+        if b_kc_dense and N % 96 == 0:
+            tiles.append(17)
     if epi != EPI_SGD:
         if _TILE64:
             tiles.append(10)

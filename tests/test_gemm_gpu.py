@@ -164,8 +164,8 @@ def test_fp8_conv_forward(gpu, case):
 # tiles (11 = 256x256, 12 / 13 = 256x128, 14 = 256x192, K-contiguous B only): every operand
 # layout, ragged edges, short and long K (the phased DMA pipeline issues zero-page DMAs past
 # the last K-step), split-K, the bias-gradient column and the implicit-GEMM convolutions
-BIG_TILES = [6, 7, 11, 12, 13, 14]
-MC_B = {6, 7, 11, 12, 13}  # tiles with an MC (k-strided) B operand instance
+BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18]
+MC_B = {6, 7, 11, 12, 13}  # tiles with MC (k-strided) A and B operand instances
 
 
 @pytest.mark.parametrize("tile", BIG_TILES)
@@ -176,11 +176,12 @@ def test_gemm256_layouts(gpu, tile, M, N, K, monkeypatch):
     x, w = _bf(M, K, device=gpu), _bf(N, K, device=gpu)
     b = torch.randn(N, device=gpu)
     _close(G.linear_fwd(x, w, b, relu=True), torch.relu(x.float() @ w.float().t() + b))
-    if tile not in MC_B:
-        return
     dy = _bf(M, N, device=gpu)
     w2 = _bf(N, K, device=gpu)
-    _close(G.linear_dgrad(dy, w2), dy.float() @ w2.float())
+    if tile in MC_B or tile in (16, 18):  # NN: MC B operand (192-row tiles: MC A excluded)
+        _close(G.linear_dgrad(dy, w2), dy.float() @ w2.float())
+    if tile not in MC_B:
+        return
     dw = torch.ones(N, K, device=gpu)
     G.linear_wgrad(dy, x, dw, accumulate=True)
     _close(dw, 1 + dy.float().t() @ x.float())
