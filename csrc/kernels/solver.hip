@@ -16,13 +16,99 @@
 
 enum { H_LR = 0, H_MOM, H_WD, H_CLIP, H_NORM, H_DELTA, H_MOM2, H_RMS, H_CORR, H_T, H_SUMSQ = 15 };
 
+// Gradient of 4 consecutive parameters of a chunk: from the flat gradient buffer, or —
+// for a chunk whose gradient was left as split-K slabs by its weight-gradient GEMM
+// (engine.fuse_splitk_updates) — the sum of the `splits` fp32 slabs in the order of the
+// reduce kernel the product would otherwise have used (splitk_reduce_kernel: sequential;
+// splitk_reduce_wide: 16 strided lane partials), so no flat gradient write + read and no
+// reduce launch, at bitwise-identical values.
+// src[4 * cid] = {slab byte address of the chunk's first element (0: flat), slab stride
+// (elements), splits, element stride (1: a weight row; ldw: a strided bias column)}.
+SN_DEV void chunk_grad(const float* __restrict__ g, long long o, const long long* __restrict__ src, int cid, int i,
+                       float* G) {
+  const long long sp = src ? src[4 * cid] : 0;
+  if (sp == 0) {
+    const float4 gv = *reinterpret_cast<const float4*>(g + o);
+    G[0] = gv.x; G[1] = gv.y; G[2] = gv.z; G[3] = gv.w;
+    return;
+  }
+  const float* sl = reinterpret_cast<const float*>(sp);
+  const long long ss = src[4 * cid + 1], es = src[4 * cid + 3];
+  const int splits = (int)src[4 * cid + 2];
+  G[0] = G[1] = G[2] = G[3] = 0.f;
+  if (splits >= 16) {
+    // splitk_reduce_wide's order: 16 lane partials over s = l, l+16, ..., then the lanes in
+    // order — the fused and unfused updates stay bitwise equal
+    // (loads issued four at a time, summed in s order: a data-dependent loop around single
+    // loads waits for each one — the update kernel must stay a streaming kernel)
+    if (es == 1) {
+      const float* p = sl + i;
+      for (int l = 0; l < 16; ++l) {
+        float P[4] = {0.f, 0.f, 0.f, 0.f};
+        int s = l;
+        for (; s + 48 < splits; s += 64) {
+          float4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (s + 16 * u) * ss);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            P[0] += v[u].x; P[1] += v[u].y; P[2] += v[u].z; P[3] += v[u].w;
+          }
+        }
+        for (; s < splits; s += 16) {
+          const float4 v = *reinterpret_cast<const float4*>(p + s * ss);
+          P[0] += v.x; P[1] += v.y; P[2] += v.z; P[3] += v.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) G[k] += P[k];
+      }
+    } else {
+      for (int l = 0; l < 16; ++l) {
+        float P[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int s = l; s < splits; s += 16) {
+          float v[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = sl[(long long)(i + k) * es + s * ss];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) P[k] += v[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) G[k] += P[k];
+      }
+    }
+    return;
+  }
+  if (es == 1) {
+    const float* p = sl + i;
+    int s = 0;
+    for (; s + 3 < splits; s += 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (s + u) * ss);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        G[0] += v[u].x; G[1] += v[u].y; G[2] += v[u].z; G[3] += v[u].w;
+      }
+    }
+    for (; s < splits; ++s) {
+      const float4 v = *reinterpret_cast<const float4*>(p + s * ss);
+      G[0] += v.x; G[1] += v.y; G[2] += v.z; G[3] += v.w;
+    }
+  } else {
+    for (int s = 0; s < splits; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) G[k] += sl[(long long)(i + k) * es + s * ss];
+  }
+}
+
 template <int KIND, bool L1, bool CLIP, bool SHADOW>
 __global__ void __launch_bounds__(256) solver_update_kernel(float* __restrict__ w, const float* __restrict__ g,
                                                             float* __restrict__ h0, float* __restrict__ h1,
                                                             bf16_t* __restrict__ shadow,
                                                             const long long* __restrict__ chunk_pos,
                                                             const float* __restrict__ chunk_mult,
-                                                            const float* __restrict__ hyper, int nchunks) {
+                                                            const float* __restrict__ hyper, int nchunks,
+                                                            const long long* __restrict__ chunk_src) {
   // a grid smaller than the chunk table loops over it (a background update running next to
   // the backward GEMMs on a side stream takes only a slice of the CUs)
   for (int cid = blockIdx.x; cid < nchunks; cid += gridDim.x) {
@@ -42,11 +128,12 @@ __global__ void __launch_bounds__(256) solver_update_kernel(float* __restrict__ 
   for (int i = threadIdx.x * 4; i < count; i += blockDim.x * 4) {
     const long long o = start + i;
     float4 wv = *reinterpret_cast<float4*>(w + o);
-    float4 gv = *reinterpret_cast<const float4*>(g + o);
+    float G[4];
+    chunk_grad(g, o, chunk_src, cid, i, G);
     float4 a = *reinterpret_cast<float4*>(h0 + o);
     float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
     if (KIND >= 4) b = *reinterpret_cast<float4*>(h1 + o);
-    float W[4] = {wv.x, wv.y, wv.z, wv.w}, G[4] = {gv.x, gv.y, gv.z, gv.w};
+    float W[4] = {wv.x, wv.y, wv.z, wv.w};
     float A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -120,33 +207,34 @@ __global__ void sumsq_pass2(const float* __restrict__ part, int nparts, float* _
 
 template <int KIND, bool L1, bool CLIP>
 static void launch3(bool shadow, dim3 grid, hipStream_t st, float* w, const float* g, float* h0, float* h1,
-                    bf16_t* sh, const long long* cp, const float* cm, const float* hyper, int n) {
+                    bf16_t* sh, const long long* cp, const float* cm, const float* hyper, int n, const long long* src) {
   if (shadow)
     hipLaunchKernelGGL((solver_update_kernel<KIND, L1, CLIP, true>), grid, dim3(256), 0, st, w, g, h0, h1, sh, cp, cm,
-                       hyper, n);
+                       hyper, n, src);
   else
     hipLaunchKernelGGL((solver_update_kernel<KIND, L1, CLIP, false>), grid, dim3(256), 0, st, w, g, h0, h1, sh, cp,
-                       cm, hyper, n);
+                       cm, hyper, n, src);
 }
 
 template <int KIND>
 static void launch_kind(bool l1, bool clip, bool shadow, dim3 grid, hipStream_t st, float* w, const float* g,
                         float* h0, float* h1, bf16_t* sh, const long long* cp, const float* cm, const float* hyper,
-                        int n) {
+                        int n, const long long* src) {
   if (l1) {
-    if (clip) launch3<KIND, true, true>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n);
-    else launch3<KIND, true, false>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n);
+    if (clip) launch3<KIND, true, true>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n, src);
+    else launch3<KIND, true, false>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n, src);
   } else {
-    if (clip) launch3<KIND, false, true>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n);
-    else launch3<KIND, false, false>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n);
+    if (clip) launch3<KIND, false, true>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n, src);
+    else launch3<KIND, false, false>(shadow, grid, st, w, g, h0, h1, sh, cp, cm, hyper, n, src);
   }
 }
 
 extern "C" int sn_solver_update(long long kind, float* w, const float* g, float* h0, float* h1, bf16_t* shadow,
                                 const long long* chunk_pos, const float* chunk_mult, long long nchunks,
                                 float* hyper, long long l1, long long clip, float* part, long long nparts,
-                                long long total, long long grid_limit, hipStream_t st) {
+                                long long total, long long grid_limit, const long long* chunk_src, hipStream_t st) {
   if (nchunks <= 0) return 0;
+  if (clip && chunk_src) return 9;  // clipping needs every gradient in the flat buffer
   if (clip) {
     hipLaunchKernelGGL(sumsq_pass1, dim3((unsigned)nparts), dim3(256), 0, st, g, total, part);
     hipLaunchKernelGGL(sumsq_pass2, dim3(1), dim3(1024), 0, st, part, (int)nparts, hyper);
@@ -155,12 +243,12 @@ extern "C" int sn_solver_update(long long kind, float* w, const float* g, float*
   bool sh = shadow != nullptr;
   const int n = (int)nchunks;
   switch (kind) {
-    case 0: launch_kind<0>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
-    case 1: launch_kind<1>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
-    case 2: launch_kind<2>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
-    case 3: launch_kind<3>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
-    case 4: launch_kind<4>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
-    case 5: launch_kind<5>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n); break;
+    case 0: launch_kind<0>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n, chunk_src); break;
+    case 1: launch_kind<1>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n, chunk_src); break;
+    case 2: launch_kind<2>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n, chunk_src); break;
+    case 3: launch_kind<3>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n, chunk_src); break;
+    case 4: launch_kind<4>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n, chunk_src); break;
+    case 5: launch_kind<5>(l1, clip, sh, grid, st, w, g, h0, h1, shadow, chunk_pos, chunk_mult, hyper, n, chunk_src); break;
     default: return 8;
   }
   return SN_CHECK_LAUNCH();

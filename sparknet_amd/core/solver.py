@@ -133,9 +133,22 @@ class Solver:
         from .. import ops
         segs = self.net.param_segments()
         self.segments = segs
-        fused = getattr(self, "fused_offsets", set())
+        fused = set(getattr(self, "fused_offsets", set()))
+        for sink in getattr(self, "slab_sinks", ()):
+            if sink.desc is not None:  # updated in backward from its split-K slabs
+                fused.update(p.offset for p in sink.params())
         self._tables = ops.solver_tables([s for s in segs if s[0] not in fused], self.net.num_param_elems,
                                          self.device)
+        self.slab_tables_dirty = False
+
+    def set_slab_sinks(self, sinks) -> None:
+        """Convolution weight gradients left as split-K slabs (engine.fuse_splitk_updates):
+        the update tables are rebuilt whenever a layer's slab layout changes (first pass,
+        a re-tuned split factor) — always before a graph capture."""
+        self.slab_sinks = list(sinks)
+        self.slab_tables_dirty = True
+        if not getattr(self, "fused_offsets", None):
+            self.fused_offsets = set()  # stage hyper-parameters before backward (Solver.iteration)
 
     def set_fused_update(self, offsets) -> None:
         """Declare params whose solver update runs in their layer's weight-gradient GEMM
@@ -253,6 +266,9 @@ class Solver:
         if self.param.regularization_type not in ("L1", "L2"):
             raise ValueError(f"Unknown regularization type: {self.param.regularization_type}")
         net = self.net
+        if getattr(self, "slab_tables_dirty", False):
+            assert not torch.cuda.is_current_stream_capturing(), "split-K slab layout changed during capture"
+            self._build_tables()
         ops.solver_update(SOLVER_KINDS[self.type], net.flat_data, net.flat_diff, self.history,
                           net.flat_compute if net.flat_compute is not net.flat_data else None,
                           self._tables, self.hyper, l1, self.param.clip_gradients > 0)
@@ -261,7 +277,7 @@ class Solver:
     def iteration(self):
         """One training iteration minus bookkeeping: returns the device loss."""
         net = self.net
-        if getattr(self, "fused_offsets", None):
+        if getattr(self, "fused_offsets", None) or getattr(self, "slab_sinks", None):
             self.stage_hyper()  # the in-backward (fused) updates read this iteration's rate
         net.clear_param_diffs(lazy=True)
         for cb in self.callbacks:

@@ -307,6 +307,130 @@ def fuse_fc_updates(solver) -> int:
     return len(offsets)
 
 
+class _SlabGrad:
+    """Split-K slabs of one Convolution's weight gradient (and its bias column) left for
+    the solver: the update kernel sums them in split order per parameter (solver.hip
+    chunk_grad) instead of a splitk_reduce launch writing the flat gradient buffer and the
+    solver reading it back.  The slab buffer is persistent (allocated on the first pass,
+    before any graph capture) so the captured update reads the slabs at a fixed address."""
+
+    def __init__(self, solver, layer):
+        self.solver, self.layer = solver, layer
+        self.buf = None
+        self.desc = None
+        self.key = None
+        self.got = False
+        self.table = None
+
+    # gemm.defer_reduce protocol
+    def begin(self):
+        self.got = False
+
+    def end(self):
+        if not self.got:
+            self._set(None)
+
+    def accepts(self, out, bias_grad) -> bool:
+        ok = out.data_ptr() == self.layer.weight.diff.data_ptr()
+        if ok and bias_grad is not None:
+            ok = self.layer.bias is not None and bias_grad.data_ptr() == self.layer.bias.diff.data_ptr()
+        return ok
+
+    def slab(self, numel: int, device):
+        if self.buf is None or self.buf.numel() < numel:
+            assert not torch.cuda.is_current_stream_capturing(), "split-K slab buffer grown during capture"
+            self.buf = torch.empty(numel, dtype=torch.float32, device=device)
+        return self.buf[:numel]
+
+    def record(self, d):
+        self.got = True
+        self._set(d)
+
+    def _set(self, d):
+        key = None if d is None else (d["ws"].data_ptr(), d["splits"], d["M"], d["N"], d["ldw"], d["groups"],
+                                      d["ones"], d["ldc"], d["c_gstride"])
+        if key != self.key:
+            assert not torch.cuda.is_current_stream_capturing(), "split-K slab layout changed during capture"
+            self.key, self.desc = key, d
+            self.solver.slab_tables_dirty = True
+            self.table = None
+            if d is not None:
+                from . import ops
+                mine = {p.offset for p in self.params()}
+                segs = [sg for sg in self.solver.net.param_segments() if sg[0] in mine]
+                self.table = ops.solver_tables(segs, self.solver.net.num_param_elems, self.solver.device,
+                                               self.chunks())
+
+    def params(self):
+        return [self.layer.weight] + ([self.layer.bias] if self.layer.bias is not None else [])
+
+    def apply(self) -> None:
+        """The layer's solver update, right after its backward (its data gradient has read
+        the old weights): on the layer's own stream, so Inception towers overlap it."""
+        if self.table is not None:
+            self.solver.update_params_segments(self.table)
+
+    def chunks(self) -> dict:
+        """{param offset: [(flat start, count, slab address, slab stride, splits, element
+        stride)]}: one chunk per weight row (g, m) — contiguous (tap, channel) columns of
+        slab row m of group g — and one strided chunk per group for the bias column."""
+        d = self.desc
+        if d is None:
+            return {}
+        M, N, ldw, G, S = d["M"], d["N"], d["ldw"], d["groups"], d["splits"]
+        assert d["ldc"] == N and d["c_gstride"] == M * N, "weight gradient must be the dense [K][RS*Cg] layout"
+        base, ss, gs = d["ws"].data_ptr(), M * ldw, S * M * ldw
+        wp = self.layer.weight
+        out = {wp.offset: [(wp.offset + (g * M + m) * N, N, base + 4 * (g * gs + m * ldw), ss, S, 1)
+                           for g in range(G) for m in range(M)]}
+        bp = self.layer.bias
+        if d["ones"] >= 0 and bp is not None:
+            out[bp.offset] = [(bp.offset + g * M, M, base + 4 * (g * gs + d["ones"]), ss, S, ldw) for g in range(G)]
+        return out
+
+
+def fuse_splitk_updates(solver) -> int:
+    """Let the solver update consume Convolution weight-gradient split-K slabs directly
+    (see :class:`_SlabGrad`): removes every splitk_reduce launch after a conv wgrad product
+    and the flat-gradient round trip of those parameters; the update of such a layer runs
+    right after its backward (like the fused InnerProduct update), on the layer's stream.  Same eligibility as the fused
+    InnerProduct update (no clipping / iter_size accumulation / gradient callbacks / debug
+    info) plus a single-bottom, unshared, unfolded (no space-to-depth input), unchunked
+    convolution.  The per-parameter arithmetic and the split summation order are those
+    of the reduce kernel + solver update; the flat gradient of fused params is not
+    written.  Returns the number of layers.
+
+    Opt-in (SN_FUSE_SPLITK=1): measured on one MI355X, same box, alternating runs, it is
+    2 % slower on CaffeNet and 5 % slower on GoogLeNet than the wide split-K reduce kernel
+    it replaces (docs/PERF_NOTES.md, "split-K slabs consumed by the solver").
+    net = solver.net
+    if (net.device.type != "cuda" or not solver.overlap_eligible() or net.debug_info
+            or os.environ.get("SN_FUSE_SPLITK", "0") != "1"):
+        return 0
+    from .ops import hip
+    users: dict = {}
+    for layer in net.layers:
+        for p in layer.params:
+            users[p.offset] = users.get(p.offset, 0) + 1
+    sinks = []
+    for li, layer in enumerate(net.layers):
+        if layer.type_name != "Convolution" or not net.layer_need_backward[li] or not layer.param_grads_needed(0):
+            continue
+        if len(net.bottom_vecs[li]) != 1 or getattr(layer, "folded_input", None) is not None:
+            continue
+        ps = [layer.weight] + ([layer.bias] if layer.bias is not None else [])
+        if any(p.owner is not None or users.get(p.offset, 0) != 1 for p in ps):
+            continue
+        s = layer.spec(net.bottom_vecs[li][0])
+        if hip.s2d_plan(s) is not None or hip._image_chunk(s) < s.N or not hip._implicit_ok(s) or s.Kg % 8:
+            continue
+        layer.slab_grad = _SlabGrad(solver, layer)
+        sinks.append(layer.slab_grad)
+    if sinks:
+        solver.set_slab_sinks(sinks)
+    return len(sinks)
+
+
 def fuse_input_fold(net, feeder) -> bool:
     """If the feeder's data blob is consumed only by a strided low-channel convolution on
     the space-to-depth path (AlexNet/CaffeNet conv1), make the feeder write the folded
@@ -578,6 +702,7 @@ class GraphStep:
             solver.net.backward_hooks.append(self.overlap.hook)
         elif fuse_fc:
             fuse_fc_updates(solver)
+            fuse_splitk_updates(solver)
         # parallel Inception towers etc.; built lazily, used from the 2nd warmup iteration
         # on (the first one autotunes GEMMs, timed on an otherwise idle GPU).  Two
         # streams by default; more use the star topology (see BranchStreams)

@@ -139,8 +139,20 @@ class ConvolutionLayer(Layer):
                 ws["wt"] = self.flipped_weights
             dw_acc = not (dw is not None and self.grad_overwrite(0))
             db_acc = not (db is not None and self.grad_overwrite(1))
-            dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws,
-                                   dw_acc=dw_acc, db_acc=db_acc)
+            sink = getattr(self, "slab_grad", None)
+            if sink is not None and dw is not None and not dw_acc and not (db is not None and db_acc):
+                # engine.fuse_splitk_updates: the solver sums this product's split-K slabs
+                from ..ops import gemm as _gemm
+                with _gemm.defer_reduce(sink):
+                    dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws,
+                                           dw_acc=dw_acc, db_acc=db_acc)
+                sink.apply()  # after the data gradient, which reads the old weights
+            else:
+                if sink is not None:
+                    sink.begin()
+                    sink.end()  # this pass's gradient went to the flat buffer
+                dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws,
+                                       dw_acc=dw_acc, db_acc=db_acc)
             if propagate_down[i]:
                 b.diff = dx
 

@@ -107,11 +107,13 @@ def advance_rng(rng_state: torch.Tensor) -> None:
         rng_state[1] += 1
 
 
-def solver_tables(segments, total: int, device) -> dict:
-    """Per-element multipliers (CPU reference) or the chunk table of the fused HIP update."""
+def solver_tables(segments, total: int, device, slab_chunks=None) -> dict:
+    """Per-element multipliers (CPU reference) or the chunk table of the fused HIP update
+    (``slab_chunks``: gradients read from split-K slabs, GPU only)."""
     device = torch.device(device)
     if device.type == "cuda":
-        return _hipmod().solver_tables(segments, total, device)
+        return _hipmod().solver_tables(segments, total, device, slab_chunks)
+    assert not slab_chunks
     lr = torch.zeros(max(total, 1))
     dc = torch.zeros(max(total, 1))
     for off, cnt, lm, dm in segments:

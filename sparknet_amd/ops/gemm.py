@@ -283,17 +283,52 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
             _lib.debug_sync("gemm")
         return
     ldw = -(-N // 4) * 4  # fp32 slabs keep 16-B rows (the ones column makes N odd)
-    ws = torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device)
+    sink = _DEFER_SINK
+    deferred = (sink is not None and epi == EPI_F32 and not fp8 and (bias_grad is None or not bias_acc)
+                and sink.accepts(out, bias_grad))
+    ws = (sink.slab(groups * splits * M * ldw, out.device).view(groups, splits, M, ldw) if deferred
+          else torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device))
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
                            sa, sb, ws.data_ptr(), ldw, splits * M * ldw, M * ldw, 0, 0, tile, 0, int(fp8), *dq, raster,
                            ones, 0, 0, *sg, *_drop_fields(_NO_XTRA))
     args.addr_legacy = _ADDR_LEGACY
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
+    if deferred:
+        # the solver update sums these slabs itself (engine.fuse_splitk_updates)
+        sink.record(dict(ws=ws, splits=splits, M=M, N=N - (1 if ones >= 0 else 0), ldw=ldw, groups=groups,
+                         ones=ones, ldc=ldc, c_gstride=c_gstride))
+        return
     mode = {EPI_BF16: 0, EPI_F32: 1, EPI_F32_ACC: 2}[epi]
     rng, dstream, ratio, gscale = xtra
     _lib.call("splitk_reduce", ws, splits, M * ldw, M, N, ldw, out, ldc, mode, bias, int(relu),
               groups, splits * M * ldw, c_gstride, gate, bias_grad, ones, int(bias_acc), M,
               C.c_void_p(rng), int(dstream), float(ratio), float(gscale))
+
+
+# --- deferred split-K reduction ---------------------------------------------------------
+# A weight-gradient product run under ``defer_reduce(sink)`` (a single, overwriting
+# contribution to a parameter's gradient) leaves its fp32 split-K slabs in a persistent
+# buffer owned by ``sink`` instead of reducing them into the gradient; the solver's update
+# kernel then sums the slabs in split order itself (engine.fuse_splitk_updates).  A
+# product that is not split (or accumulates) runs normally and the sink records None.
+_DEFER_SINK = None
+
+
+class defer_reduce:
+    def __init__(self, sink):
+        self.sink = sink
+
+    def __enter__(self):
+        global _DEFER_SINK
+        self.prev, _DEFER_SINK = _DEFER_SINK, self.sink
+        self.sink.begin()
+        return self.sink
+
+    def __exit__(self, *exc):
+        global _DEFER_SINK
+        _DEFER_SINK = self.prev
+        self.sink.end()
+        return False
 
 
 # --- per-shape autotuning ----------------------------------------------------------------

@@ -675,17 +675,31 @@ def accuracy(x2, labels, top_k=1, ignore_label=None):
 CHUNK = 8192
 
 
-def solver_tables(segments, total: int, device) -> dict:
-    pos, mult = [], []
+def solver_tables(segments, total: int, device, slab_chunks=None) -> dict:
+    """Chunk table of the fused update kernel.  ``slab_chunks``: {segment offset: [(start,
+    count, slab byte address, slab stride, splits, element stride), ...]} replaces the
+    flat-gradient chunks of those segments by chunks whose gradient the kernel sums from
+    split-K slabs (engine.fuse_splitk_updates)."""
+    pos, mult, src = [], [], []
+    slab_chunks = slab_chunks or {}
     for off, cnt, lm, dm in segments:
+        if off in slab_chunks:
+            for start, n, ptr, ss, splits, es in slab_chunks[off]:
+                for s in range(0, n, CHUNK):
+                    pos.append((start + s, min(CHUNK, n - s)))
+                    mult.append((lm, dm))
+                    src.append((ptr + 4 * s * es, ss, splits, es))
+            continue
         padded = -(-cnt // 64) * 64
         for s in range(0, padded, CHUNK):
             pos.append((off + s, min(CHUNK, padded - s)))
             mult.append((lm, dm))
+            src.append((0, 0, 0, 0))
     nparts = max(1, min(1024, -(-total // (256 * 16))))
     return {
         "pos": torch.tensor(pos or [(0, 0)], dtype=torch.int64, device=device),
         "mult": torch.tensor(mult or [(0.0, 0.0)], dtype=torch.float32, device=device),
+        "src": (torch.tensor(src, dtype=torch.int64, device=device) if slab_chunks and src else None),
         "n": len(pos),
         "part": torch.empty(nparts, dtype=torch.float32, device=device),
         "total": total,
@@ -696,7 +710,8 @@ def solver_update(kind, data, diff, history, compute, tables, hyper, l1, clip, g
     h0 = history[0]
     h1 = history[1] if len(history) > 1 else history[0]
     call("solver_update", int(kind), data, diff, h0, h1, compute, tables["pos"], tables["mult"], tables["n"],
-         hyper, int(l1), int(clip), tables["part"], tables["part"].numel(), tables["total"], int(grid_limit))
+         hyper, int(l1), int(clip), tables["part"], tables["part"].numel(), tables["total"], int(grid_limit),
+         tables.get("src"))
 
 
 def scale_shadow(flat, shadow, scale: float):
