@@ -275,14 +275,16 @@ class DeviceFeeder:
             x = x - self.mean.view(1, C, H, W)
         c = self.crop
         out = torch.empty((N, C, c, c))
-        g = torch.Generator().manual_seed(int(self.rng_state[0]) * 1000003 + self.k)
+        if self.train and self.rng_state is not None:
+            # the device kernels' Philox draw (ops.ref.augment_params): CPU and GPU feeders
+            # fed the same batches at the same RNG counter produce the same crops
+            from ..ops import ref
+            st = self.rng_state.detach().cpu()
+            params = ref.augment_params(N, int(st[0]), int(st[1]), H, W, c, c, bool(self.mirror))
+        else:
+            params = [((H - c) // 2, (W - c) // 2, False)] * N
         for n in range(N):
-            if self.train:
-                ho = int(torch.randint(0, H - c + 1, (1,), generator=g))
-                wo = int(torch.randint(0, W - c + 1, (1,), generator=g))
-                mir = self.mirror and bool(torch.randint(0, 2, (1,), generator=g))
-            else:
-                ho, wo, mir = (H - c) // 2, (W - c) // 2, False
+            ho, wo, mir = params[n]
             crop = x[n, :, ho:ho + c, wo:wo + c]
             out[n] = crop.flip(-1) if mir else crop
         self.data_blob.set_nchw(out * self.scale)

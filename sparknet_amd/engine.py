@@ -393,16 +393,16 @@ def fuse_splitk_updates(solver) -> int:
     """Let the solver update consume Convolution weight-gradient split-K slabs directly
     (see :class:`_SlabGrad`): removes every splitk_reduce launch after a conv wgrad product
     and the flat-gradient round trip of those parameters; the update of such a layer runs
-    right after its backward (like the fused InnerProduct update), on the layer's stream.  Same eligibility as the fused
-    InnerProduct update (no clipping / iter_size accumulation / gradient callbacks / debug
-    info) plus a single-bottom, unshared, unfolded (no space-to-depth input), unchunked
+    right after its backward (like the fused InnerProduct update), on the layer's stream.
+    Same eligibility as the fused InnerProduct update (no clipping / iter_size
+    accumulation / gradient callbacks / debug info) plus a single-bottom, unshared, unfolded (no space-to-depth input), unchunked
     convolution.  The per-parameter arithmetic and the split summation order are those
     of the reduce kernel + solver update; the flat gradient of fused params is not
     written.  Returns the number of layers.
 
     Opt-in (SN_FUSE_SPLITK=1): measured on one MI355X, same box, alternating runs, it is
     2 % slower on CaffeNet and 5 % slower on GoogLeNet than the wide split-K reduce kernel
-    it replaces (docs/PERF_NOTES.md, "split-K slabs consumed by the solver").
+    it replaces (docs/PERF_NOTES.md, "split-K slabs consumed by the solver")."""
     net = solver.net
     if (net.device.type != "cuda" or not solver.overlap_eligible() or net.debug_info
             or os.environ.get("SN_FUSE_SPLITK", "0") != "1"):

@@ -226,6 +226,35 @@ def _philox4(n4: int, seed: int, counter: int, stream: int) -> torch.Tensor:
     return torch.stack([c0, c1, c2, c3], dim=1)
 
 
+def philox4_counters(seed: int, c0, c1: int, c2: int, c3: int) -> torch.Tensor:
+    """Philox4x32-10 of arbitrary counters (c0 a tensor, c1..c3 scalars): [len(c0), 4]."""
+    c0 = torch.as_tensor(c0, dtype=torch.int64) & _MASK32
+    c1 = torch.full_like(c0, c1 & _MASK32)
+    c2 = torch.full_like(c0, c2 & _MASK32)
+    c3 = torch.full_like(c0, c3 & _MASK32)
+    k0, k1 = seed & _MASK32, (seed >> 32) & _MASK32
+    for _ in range(10):
+        p0 = c0 * _M0
+        p1 = c2 * _M1
+        hi0, lo0 = (p0 >> 32) & _MASK32, p0 & _MASK32
+        hi1, lo1 = (p1 >> 32) & _MASK32, p1 & _MASK32
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = (k0 + _W0) & _MASK32
+        k1 = (k1 + _W1) & _MASK32
+    return torch.stack([c0, c1, c2, c3], dim=1)
+
+
+def augment_params(N: int, seed: int, counter: int, Hs: int, Ws: int, crop_h: int, crop_w: int, mirror: bool):
+    """Per-image (row offset, column offset, mirror) of a training crop — the draw of the
+    augment / augment_s2d kernels (csrc/kernels/augment.hip: Philox(seed) at counter
+    (n, 0xA5A50000, counter)), so a CPU feeder reproduces the device crops exactly."""
+    u = philox4_counters(seed, torch.arange(N), 0xA5A50000, counter & _MASK32, (counter >> 32) & _MASK32)
+    ho = (u[:, 0] % (Hs - crop_h + 1)).tolist()
+    wo = (u[:, 1] % (Ws - crop_w + 1)).tolist()
+    mir = (u[:, 2] & 1).tolist() if mirror else [0] * N
+    return list(zip(ho, wo, [bool(m) for m in mir]))
+
+
 def dropout_mask(shape, ratio, seed, counter, stream, device):
     n = math.prod(shape)
     u = philox_u32(n, seed, counter, stream)
