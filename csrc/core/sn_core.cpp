@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdlib>
@@ -38,9 +39,13 @@ void ensure_interpreter() {
   });
 }
 
+// Every entry into the interpreter goes through a Gil; sn_python_entries() reports how many
+// there were, so a host test can check that the steady-state verbs never enter Python.
+std::atomic<long long> g_py_entries{0};
+
 struct Gil {
   PyGILState_STATE s;
-  Gil() : s(PyGILState_Ensure()) {}
+  Gil() : s(PyGILState_Ensure()) { g_py_entries.fetch_add(1, std::memory_order_relaxed); }
   ~Gil() { PyGILState_Release(s); }
 };
 
@@ -91,12 +96,15 @@ bool import_module() {
   return true;
 }
 
+void sync_python(void* s);
+
 // Call state.method(*args) built from a Py_BuildValue format; returns a new reference.
 PyObject* call(void* state, const char* method, const char* fmt, ...) {
   if (!state) {
     g_err = "null state";
     return nullptr;
   }
+  sync_python(state);
   va_list ap;
   va_start(ap, fmt);
   PyObject* args = fmt && *fmt ? Py_VaBuildValue(fmt, ap) : PyTuple_New(0);
@@ -148,17 +156,48 @@ int parse_file(const char* fn, const char* path, char** out, int* len) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Native step executor.  The reference's solver_step (ccaffe.cpp:230-233) runs Caffe's C++
-// Solver::Step; here sn_solver_step on a GPU state runs its iterations in this loop with no
-// Python involved: CoreState.native_plan (capi.py) captures one full training iteration
-// (every kernel from libsn_kernels) into a hipGraph and returns the handles and device
-// buffers; per iteration this code calls the C data callbacks (the JavaData contract,
-// java_data_layer.cpp:37-44), copies each minibatch into its data blob (pinned staging +
-// sn_stage_nchw_f32_bf16 for NHWC image blobs), stages the learning rate (SGDSolver::
-// GetLearningRate, sgd_solver.cpp:27-63) into the solver's hyper-parameter buffer and
-// launches the graph.  Python is re-entered only for display / snapshot iterations.
+// Native executors.  The reference's verbs run Caffe's C++ Net / Solver directly
+// (ccaffe.cpp:181-187 forward / backward, 218-238 solver_test / solver_step, 240-262
+// get / set data).  Here, on a GPU state:
+//   * sn_solver_step runs its iterations in NativeStep: CoreState.native_plan (capi.py)
+//     captures one full training iteration (every kernel from libsn_kernels) into a
+//     hipGraph and returns the handles and device buffers; per iteration this code calls
+//     the C data callbacks (the JavaData contract, java_data_layer.cpp:37-44), copies each
+//     minibatch into its data blob (pinned staging + sn_stage_nchw_f32_bf16 for NHWC image
+//     blobs), stages the learning rate (SGDSolver::GetLearningRate, sgd_solver.cpp:27-63)
+//     into the solver's hyper-parameter buffer and launches the graph;
+//   * sn_forward / sn_solver_test replay a captured forward-only graph of the train / test
+//     net (NativeForward, CoreState.forward_plan); the test graph adds each output blob's
+//     sum into a device accumulator read once per sn_solver_test (TestAndStoreResult,
+//     solver.cpp:413-444);
+//   * sn_get_weights / sn_set_weights are a hipMemcpy on the flat fp32 master buffer plus,
+//     for set, the sn_cast_f32_bf16 refresh of the bf16 compute shadow (NativeWeights).
+// Each plan is built by one Python call on first use; afterwards these verbs never enter
+// the interpreter (sn_python_entries counts the entries).  Python is re-entered only for
+// display / snapshot iterations, and the solver's iteration counter / the test scores are
+// handed back lazily at the next verb that does enter Python (sync_python).
 
 typedef int (*stage_fn_t)(const float*, void*, long long, long long, long long, long long, hipStream_t);
+typedef int (*cast_fn_t)(const float*, void*, long long, hipStream_t);
+
+#define HIPOK(x)                                                   \
+  do {                                                             \
+    hipError_t e_ = (x);                                           \
+    if (e_ != hipSuccess) {                                        \
+      g_err = std::string(#x) + ": " + hipGetErrorString(e_);      \
+      if (g_err_cb) g_err_cb(g_err.c_str());                       \
+      return 1;                                                    \
+    }                                                              \
+  } while (0)
+
+long long dict_ll(PyObject* d, const char* k) {
+  PyObject* v = PyDict_GetItemString(d, k);
+  return v ? PyLong_AsLongLong(v) : 0;
+}
+double dict_f(PyObject* d, const char* k) {
+  PyObject* v = PyDict_GetItemString(d, k);
+  return v ? PyFloat_AsDouble(v) : 0.0;
+}
 
 struct Feed {
   void* dev = nullptr;
@@ -169,6 +208,86 @@ struct Feed {
   void* user = nullptr;
   float* host = nullptr;     // pinned
   float* staging = nullptr;  // device fp32 NCHW (kind 1)
+};
+
+// The data layers' callback feeds of one captured graph.
+struct Feeds {
+  std::vector<Feed> list;
+  hipEvent_t fed = nullptr;
+  bool pending = false;
+  stage_fn_t stage = nullptr;
+
+  ~Feeds() {
+    for (auto& f : list) {
+      if (f.host) hipHostFree(f.host);
+      if (f.staging) hipFree(f.staging);
+    }
+    if (fed) hipEventDestroy(fed);
+  }
+
+  // from the plan's "feeds" list (GIL held); false with g_err set on failure
+  bool build(PyObject* fl) {
+    for (Py_ssize_t i = 0; fl && i < PyList_Size(fl); ++i) {
+      PyObject* f = PyList_GetItem(fl, i);
+      Feed fd;
+      fd.dev = (void*)(uintptr_t)dict_ll(f, "dev");
+      fd.kind = (int)dict_ll(f, "kind");
+      fd.cb = (sn_data_callback_t)(uintptr_t)dict_ll(f, "cb");
+      fd.user = (void*)(uintptr_t)dict_ll(f, "user");
+      PyObject* sh = PyDict_GetItemString(f, "shape");
+      fd.count = 1;
+      for (Py_ssize_t k = 0; sh && k < PyTuple_Size(sh); ++k) {
+        fd.shape.push_back((int)PyLong_AsLong(PyTuple_GetItem(sh, k)));
+        fd.count *= fd.shape.back();
+      }
+      if (fd.kind == 1 && fd.shape.size() != 4) {
+        g_err = "native feed: image blob is not 4-D";
+        return false;
+      }
+      list.push_back(fd);
+    }
+    stage = (stage_fn_t)dlsym(RTLD_DEFAULT, "sn_stage_nchw_f32_bf16");
+    if (!stage) {
+      g_err = "native feed: sn_stage_nchw_f32_bf16 not found (libsn_kernels not loaded)";
+      return false;
+    }
+    hipError_t e;
+    for (auto& f : list) {
+      if ((e = hipHostMalloc((void**)&f.host, sizeof(float) * f.count, 0)) != hipSuccess ||
+          (f.kind == 1 && (e = hipMalloc((void**)&f.staging, sizeof(float) * f.count)) != hipSuccess)) {
+        g_err = std::string("native feed: allocation: ") + hipGetErrorString(e);
+        return false;
+      }
+    }
+    if ((e = hipEventCreateWithFlags(&fed, hipEventDisableTiming)) != hipSuccess) {
+      g_err = std::string("native feed: hipEventCreate: ") + hipGetErrorString(e);
+      return false;
+    }
+    return true;
+  }
+
+  // call the callbacks and enqueue the copies / staging kernels on `stream`
+  int run(hipStream_t stream) {
+    // the host staging buffers are reused: the previous iteration's copies must have left
+    if (pending) HIPOK(hipEventSynchronize(fed));
+    for (auto& f : list) f.cb(f.host, f.shape.empty() ? 0 : f.shape[0], (int)f.shape.size(), f.shape.data(), f.user);
+    for (auto& f : list) {
+      if (f.kind == 1) {
+        HIPOK(hipMemcpyAsync(f.staging, f.host, sizeof(float) * f.count, hipMemcpyHostToDevice, stream));
+        if (stage(f.staging, f.dev, f.shape[0], f.shape[1], f.shape[2], f.shape[3], stream)) {
+          g_err = "native feed: staging kernel launch failed";
+          return 1;
+        }
+      } else {
+        HIPOK(hipMemcpyAsync(f.dev, f.host, sizeof(float) * f.count, hipMemcpyHostToDevice, stream));
+      }
+    }
+    if (!list.empty()) {
+      HIPOK(hipEventRecord(fed, stream));
+      pending = true;
+    }
+    return 0;
+  }
 };
 
 struct NativeStep {
@@ -184,24 +303,16 @@ struct NativeStep {
   float* loss_dev = nullptr;
   float* loss_ring = nullptr;  // device, average_loss slots
   std::vector<float> loss_host;
-  std::vector<Feed> feeds;
-  hipEvent_t fed = nullptr;
-  bool fed_pending = false;
+  Feeds feeds;
   int policy = 0, adam = 0, display = 0, snapshot = 0, average_loss = 1;
   double base_lr = 0, gamma = 0, power = 0, momentum = 0, momentum2 = 0;
-  long long stepsize = 0, max_iter = 0, iter = 0, done = 0;
+  long long stepsize = 0, max_iter = 0, iter = 0, done = 0, synced_iter = 0;
   std::vector<long long> stepvalues;
-  stage_fn_t stage = nullptr;
 
   ~NativeStep() {
     if (stream) hipStreamSynchronize(stream);
-    for (auto& f : feeds) {
-      if (f.host) hipHostFree(f.host);
-      if (f.staging) hipFree(f.staging);
-    }
     for (auto& e : hyper_ev)
       if (e) hipEventDestroy(e);
-    if (fed) hipEventDestroy(fed);
     if (hyper_host) hipHostFree(hyper_host);
     if (loss_ring) hipFree(loss_ring);
   }
@@ -223,37 +334,122 @@ struct NativeStep {
   }
 };
 
+struct NativeForward {
+  hipGraphExec_t exec = nullptr;
+  hipStream_t stream = nullptr;
+  float* loss_dev = nullptr;
+  float* acc_dev = nullptr;
+  int n_out = 0;
+  float* out_host = nullptr;  // pinned: loss + n_out sums
+  Feeds feeds;
+
+  ~NativeForward() {
+    if (stream) hipStreamSynchronize(stream);
+    if (out_host) hipHostFree(out_host);
+  }
+};
+
+struct NativeWeights {
+  float* data = nullptr;  // flat fp32 masters (device or host memory)
+  long long count = 0;
+  bool cuda = false;
+  void* compute = nullptr;  // bf16 compute shadow (GPU) or null
+  long long compute_count = 0;
+  hipStream_t stream = nullptr;
+  cast_fn_t cast = nullptr;
+};
+
+// Per-state native plans.  A plan that could not be built (CPU state, data layers fed
+// from Python, solver features the graph cannot hold) is remembered as such until the
+// state changes, so an ineligible state costs one Python call, not one per verb.
+struct NativeState {
+  std::unique_ptr<NativeStep> step;
+  std::unique_ptr<NativeForward> fwd[2];  // [0] train net (sn_forward), [1] test net
+  std::unique_ptr<NativeWeights> weights;
+  bool step_failed = false, fwd_failed[2] = {false, false}, weights_failed = false;
+  std::vector<float> scores;  // last native sn_solver_test
+  bool scores_native = false, scores_pending = false;
+};
+
 std::mutex g_native_mu;
-std::unordered_map<void*, std::unique_ptr<NativeStep>> g_native;
+std::unordered_map<void*, std::unique_ptr<NativeState>> g_native;
+
+NativeState& native_state(void* s) {
+  std::lock_guard<std::mutex> lk(g_native_mu);
+  auto& p = g_native[s];
+  if (!p) p = std::make_unique<NativeState>();
+  return *p;
+}
+
+NativeState* find_native(void* s) {
+  std::lock_guard<std::mutex> lk(g_native_mu);
+  auto it = g_native.find(s);
+  return it == g_native.end() ? nullptr : it->second.get();
+}
 
 void drop_native(void* s) {
   std::lock_guard<std::mutex> lk(g_native_mu);
   g_native.erase(s);
 }
 
-#define HIPOK(x)                                                   \
-  do {                                                             \
-    hipError_t e_ = (x);                                           \
-    if (e_ != hipSuccess) {                                        \
-      g_err = std::string(#x) + ": " + hipGetErrorString(e_);      \
-      if (g_err_cb) g_err_cb(g_err.c_str());                       \
-      return 1;                                                    \
-    }                                                              \
-  } while (0)
-
-long long dict_ll(PyObject* d, const char* k) {
-  PyObject* v = PyDict_GetItemString(d, k);
-  return v ? PyLong_AsLongLong(v) : 0;
-}
-double dict_f(PyObject* d, const char* k) {
-  PyObject* v = PyDict_GetItemString(d, k);
-  return v ? PyFloat_AsDouble(v) : 0.0;
+bool native_enabled() {
+  const char* v = std::getenv("SN_NATIVE_STEP");
+  return v == nullptr || std::strcmp(v, "0") != 0;
 }
 
-// Build the executor from CoreState.native_plan() (GIL held).  Returns the iterations the
-// plan's capture already ran, or -1 (g_err set; the caller falls back to Python).
-long long build_native(void* s, std::unique_ptr<NativeStep>& out) {
-  PyObject* r = call(s, "native_plan", nullptr);
+// Hand the native loops' state back to Python before any other Python verb runs on `s`
+// (GIL held): the solver's iteration counter and the scores of a native test.
+void sync_python(void* s) {
+  NativeState* st = find_native(s);
+  if (!st) return;
+  PyObject* obj = static_cast<PyObject*>(s);
+  if (st->step && st->step->synced_iter != st->step->iter) {
+    PyObject* r = PyObject_CallMethod(obj, "native_done", "(L)", st->step->iter);
+    if (r) st->step->synced_iter = st->step->iter;
+    Py_XDECREF(r);
+    PyErr_Clear();
+  }
+  if (st->scores_pending) {
+    PyObject* l = PyList_New((Py_ssize_t)st->scores.size());
+    for (size_t i = 0; l && i < st->scores.size(); ++i) PyList_SetItem(l, (Py_ssize_t)i, PyFloat_FromDouble(st->scores[i]));
+    PyObject* r = l ? PyObject_CallMethod(obj, "set_scores", "(O)", l) : nullptr;
+    if (r) st->scores_pending = false;
+    Py_XDECREF(r);
+    Py_XDECREF(l);
+    PyErr_Clear();
+  }
+}
+
+// Call a plan method without reporting its failure through the error callback (an
+// ineligible state simply stays on the Python path).
+PyObject* call_quiet(void* s, const char* method, const char* fmt, ...) {
+  sync_python(s);
+  va_list ap;
+  va_start(ap, fmt);
+  PyObject* args = fmt && *fmt ? Py_VaBuildValue(fmt, ap) : PyTuple_New(0);
+  va_end(ap);
+  if (args && !PyTuple_Check(args)) {
+    PyObject* t = PyTuple_Pack(1, args);
+    Py_DECREF(args);
+    args = t;
+  }
+  PyObject* fn = args ? PyObject_GetAttrString(static_cast<PyObject*>(s), method) : nullptr;
+  PyObject* r = fn ? PyObject_CallObject(fn, args) : nullptr;
+  Py_XDECREF(fn);
+  Py_XDECREF(args);
+  if (!r) {
+    sn_error_callback_t cb = g_err_cb;
+    g_err_cb = nullptr;
+    fetch_error(method);
+    g_err_cb = cb;
+  }
+  return r;
+}
+
+// Build the step executor from CoreState.native_plan() (GIL held).  Returns the iterations
+// the plan's capture already ran, or -1 (g_err set; the caller falls back to Python).
+long long build_native_step(void* s, std::unique_ptr<NativeStep>& out) {
+  PyObject* r = call_quiet(s, "native_plan", nullptr);
   if (!r) return -1;
   long long ran = PyLong_AsLongLong(PyTuple_GetItem(r, 0));
   PyObject* d = PyTuple_GetItem(r, 1);
@@ -262,7 +458,7 @@ long long build_native(void* s, std::unique_ptr<NativeStep>& out) {
   ns->stream = (hipStream_t)(uintptr_t)dict_ll(d, "stream");
   ns->hyper_dev = (float*)(uintptr_t)dict_ll(d, "hyper_dev");
   ns->loss_dev = (float*)(uintptr_t)dict_ll(d, "loss_dev");
-  ns->iter = dict_ll(d, "iter");
+  ns->iter = ns->synced_iter = dict_ll(d, "iter");
   ns->policy = (int)dict_ll(d, "policy");
   ns->base_lr = dict_f(d, "base_lr");
   ns->gamma = dict_f(d, "gamma");
@@ -279,47 +475,22 @@ long long build_native(void* s, std::unique_ptr<NativeStep>& out) {
   for (int i = 0; i < 16 && hv && i < PyList_Size(hv); ++i) ns->hyper[i] = (float)PyFloat_AsDouble(PyList_GetItem(hv, i));
   PyObject* sv = PyDict_GetItemString(d, "stepvalues");
   for (Py_ssize_t i = 0; sv && i < PyList_Size(sv); ++i) ns->stepvalues.push_back(PyLong_AsLongLong(PyList_GetItem(sv, i)));
-  PyObject* fl = PyDict_GetItemString(d, "feeds");
-  for (Py_ssize_t i = 0; fl && i < PyList_Size(fl); ++i) {
-    PyObject* f = PyList_GetItem(fl, i);
-    Feed fd;
-    fd.dev = (void*)(uintptr_t)dict_ll(f, "dev");
-    fd.kind = (int)dict_ll(f, "kind");
-    fd.cb = (sn_data_callback_t)(uintptr_t)dict_ll(f, "cb");
-    fd.user = (void*)(uintptr_t)dict_ll(f, "user");
-    PyObject* sh = PyDict_GetItemString(f, "shape");
-    fd.count = 1;
-    for (Py_ssize_t k = 0; sh && k < PyTuple_Size(sh); ++k) {
-      fd.shape.push_back((int)PyLong_AsLong(PyTuple_GetItem(sh, k)));
-      fd.count *= fd.shape.back();
-    }
-    ns->feeds.push_back(fd);
-  }
+  const bool fed = ns->feeds.build(PyDict_GetItemString(d, "feeds"));
   Py_DECREF(r);
   if (PyErr_Occurred()) {
     fetch_error("native_plan");
     return -1;
   }
-  ns->stage = (stage_fn_t)dlsym(RTLD_DEFAULT, "sn_stage_nchw_f32_bf16");
-  if (!ns->stage) {
-    g_err = "native step: sn_stage_nchw_f32_bf16 not found (libsn_kernels not loaded)";
-    return -1;
-  }
+  if (!fed) return -1;
   auto fail = [&](hipError_t e, const char* what) {
     g_err = std::string("native step: ") + what + ": " + hipGetErrorString(e);
     return -1;
   };
   hipError_t e;
-  for (auto& f : ns->feeds) {
-    if ((e = hipHostMalloc((void**)&f.host, sizeof(float) * f.count, 0)) != hipSuccess) return fail(e, "hipHostMalloc");
-    if (f.kind == 1 && (e = hipMalloc((void**)&f.staging, sizeof(float) * f.count)) != hipSuccess)
-      return fail(e, "hipMalloc");
-  }
   if ((e = hipHostMalloc((void**)&ns->hyper_host, sizeof(float) * 16 * NativeStep::RING, 0)) != hipSuccess)
     return fail(e, "hipHostMalloc");
   for (auto& ev : ns->hyper_ev)
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return fail(e, "hipEventCreate");
-  if ((e = hipEventCreateWithFlags(&ns->fed, hipEventDisableTiming)) != hipSuccess) return fail(e, "hipEventCreate");
   if ((e = hipMalloc((void**)&ns->loss_ring, sizeof(float) * ns->average_loss)) != hipSuccess) return fail(e, "hipMalloc");
   ns->loss_host.assign(ns->average_loss, 0.f);
   out = std::move(ns);
@@ -328,24 +499,7 @@ long long build_native(void* s, std::unique_ptr<NativeStep>& out) {
 
 // One training iteration (no GIL needed).
 int native_iteration(NativeStep& ns) {
-  // the host staging buffers are reused: the previous iteration's copies must have left
-  if (ns.fed_pending) HIPOK(hipEventSynchronize(ns.fed));
-  for (auto& f : ns.feeds) f.cb(f.host, f.shape.empty() ? 0 : f.shape[0], (int)f.shape.size(), f.shape.data(), f.user);
-  for (auto& f : ns.feeds) {
-    if (f.kind == 1) {
-      HIPOK(hipMemcpyAsync(f.staging, f.host, sizeof(float) * f.count, hipMemcpyHostToDevice, ns.stream));
-      if (ns.stage(f.staging, f.dev, f.shape[0], f.shape[1], f.shape[2], f.shape[3], ns.stream)) {
-        g_err = "native step: staging kernel launch failed";
-        return 1;
-      }
-    } else {
-      HIPOK(hipMemcpyAsync(f.dev, f.host, sizeof(float) * f.count, hipMemcpyHostToDevice, ns.stream));
-    }
-  }
-  if (!ns.feeds.empty()) {
-    HIPOK(hipEventRecord(ns.fed, ns.stream));
-    ns.fed_pending = true;
-  }
+  if (ns.feeds.run(ns.stream)) return 1;
   // hyper-parameters (Solver.hyper_values layout: 0 lr, 8 Adam correction)
   const float lr = (float)ns.learning_rate(ns.iter);
   float corr = ns.hyper[8];
@@ -375,6 +529,81 @@ int native_iteration(NativeStep& ns) {
   return 0;
 }
 
+// The forward executor of the train (test = 0) or test (1) net, if built.
+NativeForward* native_forward(void* s, int test) {
+  NativeState* st = find_native(s);
+  return st && native_enabled() ? st->fwd[test].get() : nullptr;
+}
+
+// Build it right after the Python verb ran that forward eagerly (GIL held): the capture
+// then finds every GEMM tuned, and the first call's side effects happen exactly once.
+void build_forward(void* s, int test) {
+  if (!native_enabled()) return;
+  NativeState& st = native_state(s);
+  if (st.fwd[test] || st.fwd_failed[test]) return;
+  st.fwd_failed[test] = true;
+  PyObject* d = call_quiet(s, "forward_plan", "(i)", test);
+  if (!d) return;
+  auto nf = std::make_unique<NativeForward>();
+  nf->exec = (hipGraphExec_t)(uintptr_t)dict_ll(d, "exec");
+  nf->stream = (hipStream_t)(uintptr_t)dict_ll(d, "stream");
+  nf->loss_dev = (float*)(uintptr_t)dict_ll(d, "loss_dev");
+  nf->acc_dev = (float*)(uintptr_t)dict_ll(d, "acc_dev");
+  nf->n_out = (int)dict_ll(d, "n_out");
+  const bool fed = nf->feeds.build(PyDict_GetItemString(d, "feeds"));
+  Py_DECREF(d);
+  if (PyErr_Occurred()) {
+    fetch_error("forward_plan");
+    return;
+  }
+  if (!fed || hipHostMalloc((void**)&nf->out_host, sizeof(float) * (1 + nf->n_out), 0) != hipSuccess) return;
+  st.fwd_failed[test] = false;
+  st.fwd[test] = std::move(nf);
+}
+
+NativeWeights* native_weights(void* s) {
+  if (!native_enabled()) return nullptr;
+  NativeState& st = native_state(s);
+  if (st.weights) return st.weights.get();
+  if (st.weights_failed) return nullptr;
+  Gil g;
+  st.weights_failed = true;
+  PyObject* d = call_quiet(s, "weights_plan", nullptr);
+  if (!d) return nullptr;
+  auto w = std::make_unique<NativeWeights>();
+  w->data = (float*)(uintptr_t)dict_ll(d, "data");
+  w->count = dict_ll(d, "count");
+  w->cuda = dict_ll(d, "cuda") != 0;
+  w->compute = (void*)(uintptr_t)dict_ll(d, "compute");
+  w->compute_count = dict_ll(d, "compute_count");
+  w->stream = (hipStream_t)(uintptr_t)dict_ll(d, "stream");
+  Py_DECREF(d);
+  if (PyErr_Occurred()) {
+    fetch_error("weights_plan");
+    return nullptr;
+  }
+  if (w->compute) {
+    w->cast = (cast_fn_t)dlsym(RTLD_DEFAULT, "sn_cast_f32_bf16");
+    if (!w->cast) return nullptr;
+  }
+  st.weights_failed = false;
+  st.weights = std::move(w);
+  return st.weights.get();
+}
+
+// Forget the plans that depend on what a verb is about to change.
+enum : unsigned { P_STEP = 1, P_FWD_TRAIN = 2, P_FWD_TEST = 4, P_WEIGHTS = 8, P_SCORES = 16 };
+
+void invalidate(void* s, unsigned what) {
+  NativeState* st = find_native(s);
+  if (!st) return;
+  if (what & P_STEP) st->step.reset(), st->step_failed = false;
+  if (what & P_FWD_TRAIN) st->fwd[0].reset(), st->fwd_failed[0] = false;
+  if (what & P_FWD_TEST) st->fwd[1].reset(), st->fwd_failed[1] = false;
+  if (what & P_WEIGHTS) st->weights.reset(), st->weights_failed = false;
+  if (what & P_SCORES) st->scores_native = st->scores_pending = false;
+}
+
 }  // namespace
 
 extern "C" {
@@ -382,10 +611,11 @@ extern "C" {
 const char* sn_last_error(void) { return g_err.c_str(); }
 
 long long sn_native_iterations(void* s) {
-  std::lock_guard<std::mutex> lk(g_native_mu);
-  auto it = g_native.find(s);
-  return it == g_native.end() ? 0 : it->second->done;
+  NativeState* st = find_native(s);
+  return st && st->step ? st->step->done : 0;
 }
+
+long long sn_python_entries(void) { return g_py_entries.load(std::memory_order_relaxed); }
 
 void* sn_create_state(void) {
   ensure_interpreter();
@@ -398,39 +628,42 @@ void* sn_create_state(void) {
 
 void sn_destroy_state(void* state) {
   if (!state) return;
-  {
-    std::lock_guard<std::mutex> lk(g_native_mu);
-    g_native.erase(state);  // before the Python state (which owns the captured graph)
-  }
+  drop_native(state);  // before the Python state (which owns the captured graphs)
   Gil g;
   Py_DECREF(static_cast<PyObject*>(state));
 }
 
 int sn_set_device(void* s, int device) {
-  drop_native(s);
   Gil g;
+  sync_python(s);
+  drop_native(s);
   return status(call(s, "set_device", "(i)", device));
 }
 
 int sn_load_solver_from_protobuf(void* s, const char* bytes, int len) {
-  drop_native(s);
   Gil g;
+  sync_python(s);
+  drop_native(s);
   return status(call(s, "load_solver", "(y#)", bytes, (Py_ssize_t)len));
 }
 
 int sn_load_net_from_protobuf(void* s, const char* bytes, int len) {
   Gil g;
+  sync_python(s);
+  invalidate(s, P_FWD_TRAIN | P_FWD_TEST | P_WEIGHTS | P_SCORES);
   return status(call(s, "load_net", "(y#)", bytes, (Py_ssize_t)len));
 }
 
 static int set_cb(void* s, int test, int layer, sn_data_callback_t cb, void* user) {
   Gil g;
+  sync_python(s);
+  // the native executors bind the callbacks they were built with
+  invalidate(s, test ? P_FWD_TEST : (P_STEP | P_FWD_TRAIN));
   return status(call(s, "set_data_callback", "(iiKK)", test, layer, (unsigned long long)(uintptr_t)cb,
                      (unsigned long long)(uintptr_t)user));
 }
 
 int sn_set_train_data_callback(void* s, int layer, sn_data_callback_t cb, void* user) {
-  drop_native(s);  // the native executor binds the callbacks it was built with
   return set_cb(s, 0, layer, cb, user);
 }
 
@@ -439,11 +672,24 @@ int sn_set_test_data_callback(void* s, int layer, sn_data_callback_t cb, void* u
 }
 
 int sn_forward(void* s, float* loss) {
+  if (!s) {
+    g_err = "null state";
+    return 1;
+  }
+  if (NativeForward* nf = native_forward(s, 0)) {
+    if (nf->feeds.run(nf->stream)) return 1;
+    HIPOK(hipGraphLaunch(nf->exec, nf->stream));
+    HIPOK(hipMemcpyAsync(nf->out_host, nf->loss_dev, sizeof(float), hipMemcpyDeviceToHost, nf->stream));
+    HIPOK(hipStreamSynchronize(nf->stream));
+    if (loss) *loss = nf->out_host[0];
+    return 0;
+  }
   Gil g;
   PyObject* r = call(s, "forward", nullptr);
   if (!r) return 1;
   if (loss) *loss = (float)PyFloat_AsDouble(r);
   Py_DECREF(r);
+  build_forward(s, 0);
   return 0;
 }
 
@@ -454,26 +700,27 @@ int sn_backward(void* s) {
 
 int sn_solver_step(void* s, int iters) {
   if (iters <= 0) return 0;
-  NativeStep* ns = nullptr;
-  {
+  if (!s) {
+    g_err = "null state";
+    return 1;
+  }
+  NativeState& st = native_state(s);
+  NativeStep* ns = st.step.get();
+  if (!ns) {
     Gil g;
-    std::lock_guard<std::mutex> lk(g_native_mu);
-    auto it = g_native.find(s);
-    if (it != g_native.end()) {
-      ns = it->second.get();
-    } else if (std::getenv("SN_NATIVE_STEP") == nullptr || std::strcmp(std::getenv("SN_NATIVE_STEP"), "0") != 0) {
-      PyObject* dev = call(s, "native_eligible", nullptr);
-      const bool ok = dev && PyObject_IsTrue(dev) == 1;
-      Py_XDECREF(dev);
+    if (native_enabled() && !st.step_failed && iters > 3) {
+      PyObject* ok = call_quiet(s, "native_eligible", nullptr);
+      const bool eligible = ok && PyObject_IsTrue(ok) == 1;
+      Py_XDECREF(ok);
       PyErr_Clear();
-      if (ok && iters > 3) {
-        std::unique_ptr<NativeStep> built;
-        const long long ran = build_native(s, built);
-        if (ran >= 0) {
-          ns = built.get();
-          g_native[s] = std::move(built);
-          iters -= (int)ran;
-        }
+      std::unique_ptr<NativeStep> built;
+      const long long ran = eligible ? build_native_step(s, built) : -1;
+      if (ran >= 0) {
+        ns = built.get();
+        st.step = std::move(built);
+        iters -= (int)ran;
+      } else {
+        st.step_failed = true;
       }
     }
     if (!ns) return status(call(s, "step", "(i)", iters));
@@ -496,32 +743,68 @@ int sn_solver_step(void* s, int iters) {
       }
       Gil g;
       if (status(call(s, "native_event", "(Ldi)", it, (double)smoothed, (int)snap))) return 1;
+      ns->synced_iter = it;
     }
   }
   HIPOK(hipStreamSynchronize(ns->stream));
-  Gil g;
-  return status(call(s, "native_done", "(L)", ns->iter));
+  return 0;  // the solver's iteration counter reaches Python at its next entry (sync_python)
 }
 
 int sn_solver_test(void* s, int iters) {
+  if (!s) {
+    g_err = "null state";
+    return -1;
+  }
+  if (NativeForward* nf = native_forward(s, 1)) {
+    NativeState& st = native_state(s);
+    st.scores.clear();
+    if (iters > 0) {
+      auto check = [&](hipError_t e, const char* what) {
+        if (e == hipSuccess) return true;
+        g_err = std::string("native test: ") + what + ": " + hipGetErrorString(e);
+        if (g_err_cb) g_err_cb(g_err.c_str());
+        return false;
+      };
+      if (!check(hipMemsetAsync(nf->acc_dev, 0, sizeof(float) * (nf->n_out > 0 ? nf->n_out : 1), nf->stream), "memset"))
+        return -1;
+      for (int i = 0; i < iters; ++i) {
+        if (nf->feeds.run(nf->stream)) return -1;
+        if (!check(hipGraphLaunch(nf->exec, nf->stream), "hipGraphLaunch")) return -1;
+      }
+      if (!check(hipMemcpyAsync(nf->out_host + 1, nf->acc_dev, sizeof(float) * nf->n_out, hipMemcpyDeviceToHost,
+                                nf->stream), "hipMemcpyAsync") ||
+          !check(hipStreamSynchronize(nf->stream), "hipStreamSynchronize"))
+        return -1;
+      st.scores.assign(nf->out_host + 1, nf->out_host + 1 + nf->n_out);
+    }
+    st.scores_native = st.scores_pending = true;
+    return (int)st.scores.size();
+  }
   Gil g;
+  invalidate(s, P_SCORES);
   PyObject* r = call(s, "test", "(i)", iters);
   if (!r) return -1;
   long n = PyLong_AsLong(r);
   Py_DECREF(r);
+  if (iters > 0) build_forward(s, 1);
   return (int)n;
 }
 
 float sn_get_test_score(void* s, int index) {
+  NativeState* st = find_native(s);
+  if (st && st->scores_native) return index >= 0 && index < (int)st->scores.size() ? st->scores[index] : 0.f;
   Gil g;
+  sync_python(s);
   PyObject* scores = PyObject_GetAttrString(static_cast<PyObject*>(s), "scores");
   float v = 0.f;
   if (scores && index >= 0 && index < PyList_Size(scores)) v = (float)PyFloat_AsDouble(PyList_GetItem(scores, index));
   Py_XDECREF(scores);
+  PyErr_Clear();
   return v;
 }
 
 long long sn_num_params(void* s) {
+  if (NativeWeights* w = native_weights(s)) return w->count;
   Gil g;
   PyObject* r = call(s, "num_params", nullptr);
   if (!r) return -1;
@@ -531,16 +814,47 @@ long long sn_num_params(void* s) {
 }
 
 int sn_get_weights(void* s, float* out, long long n) {
+  if (NativeWeights* w = native_weights(s)) {
+    if (n < 0 || n > w->count || (n > 0 && !out)) {
+      g_err = "sn_get_weights: buffer size " + std::to_string(n) + " vs " + std::to_string(w->count) + " parameters";
+      return 1;
+    }
+    if (!w->cuda) {
+      std::memcpy(out, w->data, sizeof(float) * n);
+      return 0;
+    }
+    HIPOK(hipMemcpyAsync(out, w->data, sizeof(float) * n, hipMemcpyDeviceToHost, w->stream));
+    HIPOK(hipStreamSynchronize(w->stream));
+    return 0;
+  }
   Gil g;
   return status(call(s, "get_weights", "(KL)", (unsigned long long)(uintptr_t)out, n));
 }
 
 int sn_set_weights(void* s, const float* in, long long n) {
+  if (NativeWeights* w = native_weights(s)) {
+    if (n < 0 || n > w->count || (n > 0 && !in)) {
+      g_err = "sn_set_weights: buffer size " + std::to_string(n) + " vs " + std::to_string(w->count) + " parameters";
+      return 1;
+    }
+    if (!w->cuda) {
+      std::memcpy(w->data, in, sizeof(float) * n);
+      return 0;
+    }
+    HIPOK(hipMemcpyAsync(w->data, in, sizeof(float) * n, hipMemcpyHostToDevice, w->stream));
+    if (w->compute && w->cast(w->data, w->compute, w->compute_count, w->stream)) {
+      g_err = "sn_set_weights: sn_cast_f32_bf16 launch failed";
+      return 1;
+    }
+    HIPOK(hipStreamSynchronize(w->stream));  // `in` may be reused as soon as this returns
+    return 0;
+  }
   Gil g;
   return status(call(s, "set_weights", "(KL)", (unsigned long long)(uintptr_t)in, n));
 }
 
 void* sn_weights_device_ptr(void* s) {
+  if (NativeWeights* w = native_weights(s)) return w->data;
   Gil g;
   PyObject* r = call(s, "weights_device_ptr", nullptr);
   if (!r) return nullptr;
@@ -561,6 +875,8 @@ int sn_load_weights_from_file(void* s, const char* path) {
 
 int sn_restore_solver_from_file(void* s, const char* path) {
   Gil g;
+  sync_python(s);
+  invalidate(s, P_STEP);  // the iteration counter and schedule position change
   return status(call(s, "restore_solver", "(s)", path));
 }
 
@@ -668,6 +984,7 @@ static long long int_call(void* s, const char* method, const char* fmt, ...) {
     g_err = "null state";
     return -1;
   }
+  sync_python(s);
   va_list ap;
   va_start(ap, fmt);
   PyObject* args = fmt && *fmt ? Py_VaBuildValue(fmt, ap) : PyTuple_New(0);
@@ -720,6 +1037,8 @@ int sn_num_output_blobs(void* s) {
 }
 
 int sn_num_test_scores(void* s) {
+  NativeState* st = find_native(s);
+  if (st && st->scores_native) return (int)st->scores.size();
   Gil g;
   return (int)int_call(s, "num_test_scores", "()");
 }

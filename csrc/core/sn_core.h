@@ -33,6 +33,7 @@ int sn_backward(void* state);
 // SN_NATIVE_STEP=0 keeps every iteration on the Python engine.
 int sn_solver_step(void* state, int iters);
 long long sn_native_iterations(void* state);  // iterations run by the native loop so far
+long long sn_python_entries(void);  // interpreter entries so far (0 growth: the verbs ran natively)
 int sn_solver_test(void* state, int iters);  // returns the number of scores (>= 0) or -1
 float sn_get_test_score(void* state, int index);
 

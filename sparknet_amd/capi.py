@@ -111,11 +111,40 @@ class CoreState:
     def native_eligible(self) -> bool:
         return self.device.type == "cuda" and self.solver is not None and self.net is self.solver.net
 
+    def _c_feeds(self, net, test: bool) -> list:
+        """(layer, source, feed dict) for every data layer of ``net``: each must be an
+        ExternalDataLayer fed by a C callback registered for that phase.  The feed dict is
+        what the native loops stage per iteration: device blob pointer, kind (1: 4-D bf16
+        NHWC image blob staged by sn_stage_nchw_f32_bf16, 0: fp32 blob copied as is),
+        logical shape, callback and user pointer."""
+        from .layers.data import ExternalDataLayer
+        feeds = []
+        for li, layer in enumerate(net.layers):
+            if not getattr(layer, "is_data", False):
+                continue
+            if isinstance(layer, ExternalDataLayer) and layer.source is None:
+                continue  # blobs set once by the host (sn_blob_set) stay as they are
+            if not isinstance(layer, ExternalDataLayer) or (test, li) not in self._callbacks:
+                raise RuntimeError(f"data layer {layer.name!r} is not fed by a C callback")
+            fn, user = self._callbacks[(test, li)]
+            top = net.top_vecs[li][0]
+            t = top.data
+            if len(top.shape) == 4:
+                if t.dtype != torch.bfloat16 or not t.is_contiguous():
+                    raise RuntimeError(f"data blob of {layer.name!r} is not a bf16 NHWC image blob")
+                kind = 1
+            else:
+                if t.dtype != torch.float32 or not t.is_contiguous():
+                    raise RuntimeError(f"data blob of {layer.name!r} is not fp32")
+                kind = 0
+            feeds.append((layer, layer.source, {"dev": t.data_ptr(), "kind": kind, "shape": tuple(top.shape),
+                                                "cb": C.cast(fn, C.c_void_p).value, "user": user or 0}))
+        return feeds
+
     def native_plan(self) -> tuple:
         """-> (iterations already run, plan dict of ints / floats) or raises if the
         state cannot run natively (CPU device, solver features the graph cannot hold)."""
         from .engine import GraphStep
-        from .layers.data import ExternalDataLayer
         s = self.solver
         if self.device.type != "cuda" or s is None:
             raise RuntimeError("native stepping needs a GPU solver")
@@ -124,22 +153,7 @@ class CoreState:
             raise RuntimeError("native stepping: iter_size / clip_gradients / callbacks / action requests "
                                "stay on the Python path")
         net = self.net
-        feeds = []
-        for li, layer in enumerate(net.layers):
-            if isinstance(layer, ExternalDataLayer) and layer.source is not None:
-                if (False, li) not in self._callbacks:
-                    raise RuntimeError(f"data layer {layer.name!r} has a non-C source")
-                fn, user = self._callbacks[(False, li)]
-                top = net.top_vecs[li][0]
-                t = top.data
-                if len(top.shape) == 4:
-                    assert t.dtype == torch.bfloat16 and t.is_contiguous()
-                    kind, dims = 1, tuple(top.shape)
-                else:
-                    assert t.dtype == torch.float32 and t.is_contiguous()
-                    kind, dims = 0, tuple(top.shape)
-                feeds.append((layer, layer.source, {"dev": t.data_ptr(), "kind": kind, "shape": dims,
-                                                    "cb": C.cast(fn, C.c_void_p).value, "user": user or 0}))
+        feeds = self._c_feeds(net, False)
         for layer, _, _ in feeds:
             layer.set_source(None)  # inside the graph the blobs are already staged (restored below)
 
@@ -185,6 +199,63 @@ class CoreState:
 
     def native_done(self, it: int) -> None:
         self.solver.iter = it
+
+    # -- native forward / test (csrc/core/sn_core.cpp NativeForward) ------------------------
+    # sn_forward and sn_solver_test on a GPU state replay a captured forward-only graph of
+    # the train net / the test net (ccaffe.cpp:181-187 forward, 218-228 solver_test ->
+    # TestAndStoreResult).  The test graph also adds every output blob's sum into a device
+    # accumulator, so n test iterations are n graph launches and ONE host read at the end.
+    def forward_plan(self, test: bool) -> dict:
+        """Capture (not run) one forward pass; called right after the Python verb ran the
+        same forward eagerly, so every GEMM is already autotuned and no layer state (BN
+        running averages, callbacks) is touched twice."""
+        net = self.test_net if test else self.net
+        if self.device.type != "cuda" or net is None:
+            raise RuntimeError("native forward needs a GPU net")
+        feeds = self._c_feeds(net, test)
+        dev = self.device
+        torch.cuda.synchronize(dev)
+        for layer, _, _ in feeds:
+            layer.set_source(None)
+        outs = net.output_blobs if test else []
+        acc = torch.zeros(max(1, len(outs)), dtype=torch.float32, device=dev)
+        loss_buf = torch.zeros(1, dtype=torch.float32, device=dev)
+        graph = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(graph):
+                loss = net.forward()
+                if torch.is_tensor(loss):
+                    loss_buf.copy_(loss.reshape(1).float())
+                if outs:
+                    acc.add_(torch.stack([b.data.float().sum() for b in outs]))
+        finally:
+            for layer, src, _ in feeds:
+                layer.set_source(src)
+        torch.cuda.synchronize(dev)
+        self.__dict__.setdefault("_fwd_graphs", {})[bool(test)] = (graph, acc, loss_buf)
+        return {"exec": int(graph.raw_cuda_graph_exec()),
+                "stream": int(torch.cuda.current_stream(dev).cuda_stream),
+                "loss_dev": int(loss_buf.data_ptr()), "acc_dev": int(acc.data_ptr()), "n_out": len(outs),
+                "feeds": [f for _, _, f in feeds]}
+
+    def weights_plan(self) -> dict:
+        """Flat fp32 master buffer (device or host memory) and its compute shadow for the
+        native sn_get_weights / sn_set_weights (a hipMemcpy plus, on the GPU, the
+        sn_cast_f32_bf16 refresh of the bf16 shadow that Net.sync_compute does)."""
+        net = self.net
+        data, comp = net.flat_data, net.flat_compute
+        if data is None:
+            raise RuntimeError("net has no parameters")
+        shadow = comp is not None and comp is not data
+        if shadow and (not data.is_cuda or comp.dtype != torch.bfloat16):
+            raise RuntimeError("host nets with a separate compute copy stay on the Python path")
+        return {"data": int(data.data_ptr()), "count": int(net.num_param_elems), "cuda": int(data.is_cuda),
+                "compute": int(comp.data_ptr()) if shadow else 0, "compute_count": int(comp.numel()) if shadow else 0,
+                "stream": int(torch.cuda.current_stream(self.device).cuda_stream) if data.is_cuda else 0}
+
+    def set_scores(self, scores: list) -> None:
+        """Scores of a native sn_solver_test, handed over at the next Python entry."""
+        self.scores = [float(v) for v in scores]
 
     def test(self, n: int) -> int:
         """solver_test -> TestAndStoreResult (solver.cpp:413-444): sum of every output

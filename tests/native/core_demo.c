@@ -52,6 +52,28 @@ int main(int argc, char** argv) {
   CHECK(sn_set_train_data_callback(st, 1, label_cb, NULL));
   CHECK(sn_solver_step(st, 5));
   printf("native=%lld\n", sn_native_iterations(st)); /* > 0 on a GPU: the C++ step loop ran */
+  /* steady state: once each verb has run (its first call builds the native plan), step,
+   * test, forward and get / set weights never enter the interpreter on a GPU state */
+  CHECK(sn_set_test_data_callback(st, 0, data_cb, NULL));
+  CHECK(sn_set_test_data_callback(st, 1, label_cb, NULL));
+  CHECK(sn_solver_test(st, 2) != 1);
+  float warm = 0.f;
+  CHECK(sn_forward(st, &warm));
+  long long np = sn_num_params(st);
+  float* ws = (float*)malloc(sizeof(float) * np);
+  CHECK(sn_get_weights(st, ws, np));
+  const long long py0 = sn_python_entries();
+  CHECK(sn_solver_step(st, 3));
+  CHECK(sn_solver_test(st, 2) != 1);
+  const int nscores = sn_num_test_scores(st);
+  const float score = sn_get_test_score(st, 0);
+  CHECK(sn_get_weights(st, ws, np));
+  CHECK(sn_set_weights(st, ws, np));
+  CHECK(sn_forward(st, &warm));
+  const long long py = sn_python_entries() - py0;
+  free(ws);
+  printf("steady_py=%lld scores=%d score0=%.4f fwd=%.4f\n", py, nscores, score, warm);
+  CHECK(!isfinite(score) || !isfinite(warm) || nscores != 1);
   CHECK(sn_load_net_from_protobuf(st, "\xff\xff\xff", 3) == 0); /* garbage bytes must fail cleanly */
   int nl = sn_num_layers(st);
   char name[64];

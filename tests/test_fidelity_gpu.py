@@ -10,8 +10,8 @@ mirrored by the same Philox draw (ops.ref.augment_params) and dropping the same 
 
 * 60 steps: the bf16 GPU loss trajectory stays within 8 % (relative, per 10-step window
   mean) of the fp32 CPU one, and both decrease.
-* 10 steps: graph replay and the eager GPU step end at the same weights to 1e-5 (relative
-  to the largest weight).
+* 10 steps: graph replay and the eager GPU step (same kernels, EPI_SGD included, launched
+  one by one) end at the same weights to 1e-5 (relative to the largest weight).
 
 Reference: caffe/src/caffe/layers/dropout_layer.cu:10-45 (train-time mask), the
 ImageNetApp crop / mirror / mean transform (src/main/scala/apps/ImageNetApp.scala), and
@@ -73,6 +73,9 @@ def _trainer(dev, w0, x, y, graph):
     if dev.type == "cuda":
         fold = fuse_input_fold(net, feeder)
     tr = LocalSGDTrainer(solver, None, tau=1000, feeder=feeder, use_graph=graph)
+    if dev.type == "cuda" and not graph:
+        from sparknet_amd.engine import fuse_fc_updates
+        fuse_fc_updates(solver)  # the eager GPU step runs the same EPI_SGD kernels as the graph
     return tr, solver, fold
 
 
