@@ -1,0 +1,301 @@
+// Fused 3x3 / stride-2 max pooling + cross-channel LRN on NHWC bf16 — the pool1 -> norm1
+// and pool2 -> norm2 pairs of CaffeNet (and GoogLeNet's pool1 -> norm1).
+//
+// Reference: two layers, each a full pass over HBM (pooling_layer.cu:11-47 MaxPoolForward,
+// 217-260 MaxPoolBackward; lrn_layer.cu:9-177 fill-scale / compute-output / compute-diff).
+// Unfused here they are maxpool_fwd_k + lrn_across_fwd and lrn_across_bwd + pool_bwd_k3s2:
+// the pooled tensor is written, read back by the LRN, and in backward the LRN's input
+// gradient (the pooling layer's top diff) is written and read back by the pooling
+// backward.  Fused:
+//   forward : one workgroup pools a run of output pixels (all channels) into LDS, stores
+//             the pooled tensor (the LRN backward needs it) and the argmax mask, then
+//             normalises across channels out of LDS — the LRN never re-reads HBM;
+//   backward: one workgroup owns RB rows of 2x2 input blocks of one image: it computes the
+//             LRN input gradient of the RB+1 pooled rows those blocks read (one halo row)
+//             into LDS, then gathers the pooling gradient out of LDS — the pooled gradient
+//             never exists in HBM.
+// The arithmetic is the unfused kernels' own, in the same order, on the same bf16-rounded
+// intermediates, so the fused pair is bitwise equal to the two separate launches.
+#include "common.h"
+
+struct PLGeom {
+  int N, H, W, C, P, Q, ph, pw;
+  int gate;         // forward: the pooled input is an in-place ReLU output (mask 255 = no gradient)
+  int pix;          // forward: pooled pixels per workgroup
+  int BH, BW;       // backward: 2x2 input blocks over the padded extent
+  int rows, nb;     // backward: block rows per workgroup, workgroups per image
+  int size;
+  float alpha, beta, k;
+  FDiv fcv, fQ, fP, fQcv, fBWcv;
+};
+
+SN_DEV float plrn_pow(float s, float beta) { return __expf(-beta * __logf(s)); }
+
+template <int SIZE>
+__global__ void __launch_bounds__(256) pool_lrn_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ pooled,
+                                                    uint8_t* __restrict__ mask, bf16_t* __restrict__ y, PLGeom g) {
+  extern __shared__ uint4 tile[];  // g.pix x cv pooled chunks
+  constexpr int PRE = (SIZE - 1) / 2;
+  const int cv = g.C >> 3;
+  const long long npix = (long long)g.N * g.P * g.Q;
+  const long long pix0 = (long long)blockIdx.x * g.pix;
+  const int npx = (int)min((long long)g.pix, npix - pix0);
+  const int items = npx * cv;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const uint32_t lp = udiv((uint32_t)it, g.fcv);
+    const int c0 = (it - (int)lp * cv) * 8;
+    const uint32_t pix = (uint32_t)(pix0 + lp);
+    const uint32_t pq = udiv(pix, g.fQ), n = udiv(pq, g.fP);
+    const int q = (int)(pix - pq * g.Q), p = (int)(pq - n * g.P);
+    const int hs = 2 * p - g.ph, ws = 2 * q - g.pw;
+    uint4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const int h = hs + a, w = ws + b;
+        ok[a * 3 + b] = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+        const int hc = min(max(h, 0), g.H - 1), wc = min(max(w, 0), g.W - 1);
+        v[a * 3 + b] = *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + hc) * g.W + wc) * g.C + c0);
+      }
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { best[t] = -INFINITY; arg[t] = 0; }
+#pragma unroll
+    for (int widx = 0; widx < 9; ++widx) {
+      float f[8];
+      unpack8(v[widx], f);
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (ok[widx] && f[t] > best[t]) { best[t] = f[t]; arg[t] = widx; }
+    }
+    if (g.gate) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (!(best[t] > 0.f)) arg[t] = 255;
+    }
+    const uint4 packed = pack8(best);
+    const long long o = (long long)pix * g.C + c0;
+    *reinterpret_cast<uint4*>(pooled + o) = packed;
+    uint2 m;
+    m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    m.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+    *reinterpret_cast<uint2*>(mask + o) = m;
+    tile[it] = packed;
+  }
+  __syncthreads();
+  const float a = g.alpha / g.size;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const uint32_t lp = udiv((uint32_t)it, g.fcv);
+    const int ch = it - (int)lp * cv;
+    float v[24];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int c = ch - 1 + j;
+      const bool ok = c >= 0 && c < cv;
+      unpack8(tile[(int)lp * cv + min(max(c, 0), cv - 1)], v + 8 * j);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[8 * j + t] = ok ? v[8 * j + t] : 0.f;
+    }
+    float o[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < SIZE; ++d) {
+        float e = v[8 + t - PRE + d];
+        s += e * e;
+      }
+      float sc = g.k + a * s;
+      o[t] = v[8 + t] * plrn_pow(sc, g.beta);
+    }
+    *reinterpret_cast<uint4*>(y + (pix0 + lp) * g.C + ch * 8) = pack8(o);
+  }
+}
+
+// The 24 channels [c0-8, c0+16) of one pixel row as fp32, zero outside [0, C).
+SN_DEV void plrn_load24(const bf16_t* row, int c0, int C, float* v) {
+  uint4 raw[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) raw[j] = *reinterpret_cast<const uint4*>(row + min(max(c0 - 8 + 8 * j, 0), C - 8));
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int c = c0 - 8 + 8 * j;
+    const bool ok = c >= 0 && c < C;
+    unpack8(raw[j], v + 8 * j);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[8 * j + t] = ok ? v[8 * j + t] : 0.f;
+  }
+}
+
+template <int SIZE>
+__global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ xp, const bf16_t* __restrict__ dyn,
+                                                    const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
+                                                    PLGeom g) {
+  extern __shared__ uint4 tile[];  // (rows + 1) x Q x cv chunks of the pooled gradient
+  constexpr int PRE = (SIZE - 1) / 2, POST = SIZE - PRE - 1;
+  const int cv = g.C >> 3;
+  const int n = blockIdx.x / g.nb;
+  const int bh0 = (blockIdx.x - n * g.nb) * g.rows;
+  const int qcv = g.Q * cv;
+  const float a = g.alpha / g.size;
+  const float cache_ratio = 2.f * g.alpha * g.beta / g.size;
+  // phase 1: LRN backward of pooled rows bh0-1 .. bh0+rows-1 (lrn_across_bwd, gate off)
+  const int items1 = (g.rows + 1) * qcv;
+  for (int it = threadIdx.x; it < items1; it += blockDim.x) {
+    const uint32_t r = udiv((uint32_t)it, g.fQcv);
+    const int rem = it - (int)r * qcv;
+    const uint32_t q = udiv((uint32_t)rem, g.fcv);
+    const int c0 = (rem - (int)q * cv) * 8;
+    const int p = bh0 - 1 + (int)r;
+    if (p < 0 || p >= g.P) {
+      tile[it] = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
+    const long long base = (((long long)n * g.P + p) * g.Q + q) * g.C;
+    float xv[24], gv[24];
+    plrn_load24(xp + base, c0, g.C, xv);
+    plrn_load24(dyn + base, c0, g.C, gv);
+    float rr[24];
+#pragma unroll
+    for (int j = 8 - POST; j < 16 + PRE; ++j) {
+      const int c = c0 - 8 + j;
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < SIZE; ++d) {
+        float e = xv[j - PRE + d];
+        s += e * e;
+      }
+      float sc = g.k + a * s;
+      rr[j] = (c >= 0 && c < g.C) ? gv[j] * xv[j] * plrn_pow(sc, g.beta + 1.f) : 0.f;
+      if (j >= 8 && j < 16) gv[j] = gv[j] * plrn_pow(sc, g.beta);
+    }
+    float o[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float acc = 0.f;
+#pragma unroll
+      for (int d = -PRE; d <= POST; ++d) acc += rr[8 + t - d];
+      o[t] = gv[8 + t] - cache_ratio * xv[8 + t] * acc;
+    }
+    tile[it] = pack8(o);
+  }
+  __syncthreads();
+  // phase 2: the 2x2 input blocks of rows bh0 .. bh0+rows-1 (pool_bwd_k3s2<true>)
+  const int bwcv = g.BW * cv;
+  const int items2 = min(g.rows, g.BH - bh0) * bwcv;
+  for (int it = threadIdx.x; it < items2; it += blockDim.x) {
+    const uint32_t r = udiv((uint32_t)it, g.fBWcv);
+    const int rem = it - (int)r * bwcv;
+    const uint32_t bwu = udiv((uint32_t)rem, g.fcv);
+    const int ch = rem - (int)bwu * cv, c0 = ch * 8;
+    const int bw = (int)bwu, bh = bh0 + (int)r;
+    uint4 dv[4];
+    uint2 mv[4];
+    bool ok[4];
+#pragma unroll
+    for (int wa = 0; wa < 2; ++wa)
+#pragma unroll
+      for (int wb = 0; wb < 2; ++wb) {
+        const int p = bh - 1 + wa, q = bw - 1 + wb, t = wa * 2 + wb;
+        ok[t] = p >= 0 && p < g.P && q >= 0 && q < g.Q;
+        const int pc = min(max(p, 0), g.P - 1), qc = min(max(q, 0), g.Q - 1);
+        dv[t] = tile[((int)r + wa) * qcv + qc * cv + ch];
+        mv[t] = *reinterpret_cast<const uint2*>(mask + (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0);
+      }
+    float f[4][8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) unpack8(dv[t], f[t]);
+#pragma unroll
+    for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) {
+        const int h = 2 * bh + ia - g.ph, w = 2 * bw + ib - g.pw;
+        if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int wa = t >> 1, wb = t & 1;
+          if ((wa == 0 && ia == 1) || (wb == 0 && ib == 1)) continue;
+          const int widx = (ia + 2 * (1 - wa)) * 3 + (ib + 2 * (1 - wb));
+          const uint32_t mw[2] = {mv[t].x, mv[t].y};
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+            if (ok[t] && (int)((mw[kk >> 2] >> ((kk & 3) * 8)) & 0xff) == widx) acc[kk] += f[t][kk];
+        }
+        *reinterpret_cast<uint4*>(dx + (((long long)n * g.H + h) * g.W + w) * g.C + c0) = pack8(acc);
+      }
+  }
+}
+
+static PLGeom plgeom(long long N, long long H, long long W, long long C, long long P, long long Q, long long ph,
+                     long long pw, long long size, float alpha, float beta, float k) {
+  PLGeom g{};
+  g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C; g.P = (int)P; g.Q = (int)Q;
+  g.ph = (int)ph; g.pw = (int)pw;
+  g.size = (int)size; g.alpha = alpha; g.beta = beta; g.k = k;
+  g.fcv = make_fdiv((uint32_t)(C / 8));
+  g.fQ = make_fdiv((uint32_t)Q); g.fP = make_fdiv((uint32_t)P);
+  return g;
+}
+
+static bool plrn_ok(long long N, long long H, long long W, long long C, long long P, long long Q, long long ph,
+                    long long pw, long long size) {
+  // 3x3 / stride-2 ceil-mode windows, every window starting inside the padded input
+  return C % 8 == 0 && C >= 8 && (size == 3 || size == 5 || size == 7 || size == 9) && ph < 3 && pw < 3 &&
+         2 * (P - 1) - ph < H && 2 * (Q - 1) - pw < W && N * H * W * C < (1ll << 32);
+}
+
+// Workgroup shapes (host side, shared with the Python eligibility check).
+static int plrn_fwd_pix(long long C) { return (int)(512 / (C / 8) > 0 ? 512 / (C / 8) : 1); }
+static int plrn_bwd_rows(long long Q, long long C) {
+  for (int rows = 4; rows >= 1; --rows)
+    if ((long long)(rows + 1) * Q * (C / 8) * 16 <= 64 * 1024) return rows;
+  return 0;
+}
+
+extern "C" int sn_pool_lrn_fwd(const bf16_t* x, bf16_t* pooled, uint8_t* mask, bf16_t* y, long long N, long long H,
+                               long long W, long long C, long long P, long long Q, long long ph, long long pw,
+                               long long gate, long long size, float alpha, float beta, float k, hipStream_t st) {
+  if (!plrn_ok(N, H, W, C, P, Q, ph, pw, size)) return 4;
+  PLGeom g = plgeom(N, H, W, C, P, Q, ph, pw, size, alpha, beta, k);
+  g.gate = (int)gate;
+  g.pix = plrn_fwd_pix(C);
+  const long long npix = N * P * Q;
+  dim3 grid((unsigned)((npix + g.pix - 1) / g.pix));
+  const size_t lds = (size_t)g.pix * (C / 8) * sizeof(uint4);
+  switch (size) {
+    case 3: hipLaunchKernelGGL(pool_lrn_fwd<3>, grid, dim3(256), lds, st, x, pooled, mask, y, g); break;
+    case 5: hipLaunchKernelGGL(pool_lrn_fwd<5>, grid, dim3(256), lds, st, x, pooled, mask, y, g); break;
+    case 7: hipLaunchKernelGGL(pool_lrn_fwd<7>, grid, dim3(256), lds, st, x, pooled, mask, y, g); break;
+    default: hipLaunchKernelGGL(pool_lrn_fwd<9>, grid, dim3(256), lds, st, x, pooled, mask, y, g); break;
+  }
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_t* mask, bf16_t* dx, long long N,
+                               long long H, long long W, long long C, long long P, long long Q, long long ph,
+                               long long pw, long long size, float alpha, float beta, float k, hipStream_t st) {
+  if (!plrn_ok(N, H, W, C, P, Q, ph, pw, size)) return 4;
+  PLGeom g = plgeom(N, H, W, C, P, Q, ph, pw, size, alpha, beta, k);
+  g.rows = plrn_bwd_rows(Q, C);
+  if (g.rows == 0) return 4;
+  g.BH = (int)((H + ph + 1) / 2);
+  g.BW = (int)((W + pw + 1) / 2);
+  // every pooled row the blocks read exists in the tile: blocks bh read rows bh-1, bh
+  if (g.BH > P + 1 || g.BW > Q + 1) return 4;
+  g.nb = (g.BH + g.rows - 1) / g.rows;
+  g.fQcv = make_fdiv((uint32_t)(Q * (C / 8)));
+  g.fBWcv = make_fdiv((uint32_t)(g.BW * (C / 8)));
+  dim3 grid((unsigned)(N * g.nb));
+  const size_t lds = (size_t)(g.rows + 1) * Q * (C / 8) * sizeof(uint4);
+  switch (size) {
+    case 3: hipLaunchKernelGGL(lrn_pool_bwd<3>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
+    case 5: hipLaunchKernelGGL(lrn_pool_bwd<5>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
+    case 7: hipLaunchKernelGGL(lrn_pool_bwd<7>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
+    default: hipLaunchKernelGGL(lrn_pool_bwd<9>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
+  }
+  return SN_CHECK_LAUNCH();
+}

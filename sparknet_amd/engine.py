@@ -49,7 +49,44 @@ def fuse_relu(net) -> int:
     fuse_relu_backward(net)
     fuse_dropout(net)
     fuse_concat(net)
+    fuse_pool_lrn(net)
     batch_weight_flips(net)
+    return n
+
+
+def fuse_pool_lrn(net) -> int:
+    """Run a cross-channel LRN that reads a 3x3 / stride-2 max pooling's output inside the
+    pooling layer's kernels (csrc/kernels/pool_lrn.hip): CaffeNet's pool1 -> norm1 and
+    pool2 -> norm2, GoogLeNet's pool1 -> norm1.  Caffe runs them as two layers with two
+    passes each way (pooling_layer.cu:11-47,217-260, lrn_layer.cu:9-177); fused, the LRN
+    normalises the pooled tile out of LDS, and in backward the pooled gradient is built in
+    LDS and gathered straight into the pooling input gradient.  Requires the pooled blob to
+    be read by the LRN alone (not a net output, no in-place LRN).  Returns the count."""
+    from .ops import hip
+    if net.device.type != "cuda" or net.debug_info or os.environ.get("SN_FUSE_POOL_LRN", "1") == "0":
+        return 0
+    outputs = set(getattr(net, "output_blob_ids", ()))
+    n = 0
+    for li, pool in enumerate(net.layers):
+        if pool.type_name != "Pooling" or len(net.top_ids[li]) != 1 or pool.global_pooling:
+            continue
+        blob = net.top_ids[li][0]
+        readers = [lj for lj in range(li + 1, len(net.layers)) if blob in net.bottom_ids[lj]]
+        if blob in outputs or len(readers) != 1:
+            continue
+        lj = readers[0]
+        lrn = net.layers[lj]
+        if lrn.type_name != "LRN" or lrn.relu_gate or net.top_ids[lj][0] == blob:
+            continue
+        if net.layer_need_backward[li] != net.layer_need_backward[lj]:
+            continue
+        s = pool.spec(net.bottom_vecs[li][0])
+        if not hip.pool_lrn_eligible(s, lrn.size, lrn.within):
+            continue
+        lrn.pool_fused = True
+        lrn.top = net.top_vecs[lj][0]
+        pool.fused_lrn = lrn
+        n += 1
     return n
 
 

@@ -253,6 +253,7 @@ class PoolingLayer(Layer):
         self.aux = None
 
     relu_gate = False  # backward of the slope-0 in-place ReLU producing the bottom is fused here
+    fused_lrn = None   # the LRN reading this layer's output, run inside its kernels (engine.fuse_pool_lrn)
 
     def spec(self, b) -> PoolSpec:
         N, C, H, W = b.shape
@@ -288,6 +289,12 @@ class PoolingLayer(Layer):
                 # StoPoolForwardTest (pooling_layer.cu:125-155): probability-weighted average
                 tops[0].data = _stochastic_test(x.float().clamp_min(0), s).to(x.dtype)
             return
+        f = self.fused_lrn
+        if f is not None and x.is_cuda:
+            from ..ops import hip
+            tops[0].data, self.aux, f.top.data = hip.pool_lrn_forward(x, s, self.relu_gate, f.size, f.alpha, f.beta,
+                                                                      f.k)
+            return
         y, self.aux = ops.pool_forward_aux(x, s, self.relu_gate)
         tops[0].data = y
         if len(tops) > 1:
@@ -311,6 +318,12 @@ class PoolingLayer(Layer):
                 y = ops.ref._pool_windows(xl, s, 0.0).gather(-1, self.aux).squeeze(-1)
                 g, = torch.autograd.grad(y, xl, ops.ref.nchw(tops[0].diff.float()))
             bottoms[0].diff = g.to(bottoms[0].dtype)
+            return
+        f = self.fused_lrn
+        if f is not None and bottoms[0].data.is_cuda:
+            from ..ops import hip
+            bottoms[0].diff = hip.lrn_pool_backward(f.top.diff, tops[0].data, self.aux, s, f.size, f.alpha, f.beta,
+                                                    f.k)
             return
         bottoms[0].diff = ops.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data,
                                             self.relu_gate)
@@ -340,12 +353,16 @@ class LRNLayer(Layer):
         tops[0].reshape(bottoms[0].shape, self.dtype)
 
     def forward(self, bottoms, tops):
+        if self.pool_fused and bottoms[0].data.is_cuda:
+            return  # written by the pooling layer before it (engine.fuse_pool_lrn)
         tops[0].data = ops.lrn_forward(bottoms[0].data, self.size, self.alpha, self.beta, self.k, self.within)
 
     relu_gate = False  # engine.fuse_relu_backward: the in-place ReLU producing the bottom
+    pool_fused = False  # forward and backward run inside the preceding max pooling's kernels
+    top = None          # this layer's top Blob (set with pool_fused)
 
     def backward(self, tops, propagate_down, bottoms):
-        if not propagate_down[0]:
+        if not propagate_down[0] or (self.pool_fused and bottoms[0].data.is_cuda):
             return
         x = bottoms[0].data
         if self.relu_gate and x.is_cuda:

@@ -501,6 +501,38 @@ def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False):
     return dx
 
 
+def pool_lrn_eligible(s: PoolSpec, size: int, within: bool) -> bool:
+    """Max pooling 3x3 / stride 2 followed by a cross-channel LRN that the fused
+    sn_pool_lrn_fwd / sn_lrn_pool_bwd pair covers (csrc/kernels/pool_lrn.hip)."""
+    if s.method != POOL_MAX or within or (s.kh, s.kw, s.sh, s.sw) != (3, 3, 2, 2) or s.C % 8 or size not in (3, 5, 7, 9):
+        return False
+    if s.ph >= 3 or s.pw >= 3 or s.N * s.H * s.W * s.C >= 1 << 32:
+        return False
+    rows = next((r for r in (4, 3, 2, 1) if (r + 1) * s.Q * (s.C // 8) * 16 <= 64 * 1024), 0)
+    return rows > 0 and (s.H + s.ph + 1) // 2 <= s.P + 1 and (s.W + s.pw + 1) // 2 <= s.Q + 1
+
+
+def pool_lrn_forward(x, s: PoolSpec, gate: bool, size: int, alpha: float, beta: float, k: float):
+    """-> (pooled, argmax mask, LRN output): max pooling and the cross-channel LRN of its
+    output in one launch (the pooled tensor is kept: the LRN backward reads it)."""
+    x = _c(x)
+    pooled = torch.empty((s.N, s.P, s.Q, s.C), dtype=BF16, device=x.device)
+    mask = torch.empty((s.N, s.P, s.Q, s.C), dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(pooled)
+    call("pool_lrn_fwd", x, pooled, mask, y, s.N, s.H, s.W, s.C, s.P, s.Q, s.ph, s.pw, int(gate), int(size),
+         float(alpha), float(beta), float(k))
+    return pooled, mask, y
+
+
+def lrn_pool_backward(dy, pooled, mask, s: PoolSpec, size: int, alpha: float, beta: float, k: float):
+    """Gradient at the pooling input from the gradient at the LRN output (the pooled
+    gradient lives only in LDS)."""
+    dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=dy.device)
+    call("lrn_pool_bwd", _c(pooled), _c(dy), mask, dx, s.N, s.H, s.W, s.C, s.P, s.Q, s.ph, s.pw, int(size),
+         float(alpha), float(beta), float(k))
+    return dx
+
+
 def lrn_forward(x, size, alpha, beta, k, within=False):
     x = _c(x)
     N, H, W, Cc = x.shape

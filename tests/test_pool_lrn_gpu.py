@@ -1,0 +1,90 @@
+"""Fused max-pool + cross-channel LRN (csrc/kernels/pool_lrn.hip, engine.fuse_pool_lrn).
+
+* kernel level: the fused forward (pooled tensor, argmax mask, LRN output) and the fused
+  backward (pooling-input gradient from the LRN-output gradient) are BITWISE equal to the
+  unfused launches (maxpool_fwd_k + lrn_across_fwd, lrn_across_bwd + pool_bwd_k3s2) on
+  CaffeNet's pool1/norm1 and pool2/norm2 shapes, GoogLeNet's pool1/norm1 and a padded
+  odd-sized case, with and without the folded ReLU gate; and they track the fp32 CPU
+  reference (ops.ref);
+* net level: CaffeNet fuses both pairs, and a fused GPU step equals an unfused one.
+Reference: caffe/src/caffe/layers/pooling_layer.cu:11-47,217-260, lrn_layer.cu:9-177."""
+import pytest
+import torch
+
+from sparknet_amd.ops.spec import PoolSpec
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # N, H, W, C, pad, LRN size
+    (4, 55, 55, 96, 0, 5),    # CaffeNet pool1 -> norm1
+    (4, 27, 27, 256, 0, 5),   # CaffeNet pool2 -> norm2
+    (2, 112, 112, 64, 0, 5),  # GoogLeNet pool1/3x3_s2 -> pool1/norm1
+    (3, 14, 15, 40, 1, 3),    # padded, odd sizes, C not a multiple of 16
+]
+
+
+def _inputs(N, H, W, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.randn(N, H, W, C, generator=g) * 2.0).to(torch.bfloat16)
+    return x
+
+
+@pytest.mark.parametrize("gate", [False, True])
+@pytest.mark.parametrize("case", CASES)
+def test_fused_pool_lrn_bitwise(gpu, case, gate):
+    from sparknet_amd.ops import hip
+    N, H, W, C, pad, size = case
+    s = PoolSpec(N, H, W, C, 3, 3, 2, 2, pad, pad)
+    assert hip.pool_lrn_eligible(s, size, False)
+    alpha, beta, k = 1e-4 * 50, 0.75, 1.0  # a large alpha so the normalisation matters
+    x = _inputs(N, H, W, C, 1).to(gpu)
+    if gate:
+        x = x.clamp_min(0)  # the in-place ReLU output the gate stands for
+    pooled, mask, y = hip.pool_lrn_forward(x, s, gate, size, alpha, beta, k)
+    p_ref, m_ref = hip.pool_forward_mask(x, s, gate)
+    y_ref = hip.lrn_forward(p_ref, size, alpha, beta, k)
+    assert torch.equal(pooled, p_ref) and torch.equal(mask, m_ref) and torch.equal(y, y_ref)
+    dy = _inputs(N, s.P, s.Q, C, 2).to(gpu)
+    dx = hip.lrn_pool_backward(dy, pooled, mask, s, size, alpha, beta, k)
+    dp = hip.lrn_backward(dy, p_ref, size, alpha, beta, k)
+    dx_ref = hip.pool_backward(dp, x, s, m_ref, gate=gate)
+    assert torch.equal(dx, dx_ref)
+    # and against the fp32 CPU reference of the two layers
+    from sparknet_amd.ops import ref
+    pr = ref.pool_forward(x.float().cpu(), s)  # NHWC, like the device tensors
+    yr = ref.lrn_forward(pr, size, alpha, beta, k)
+    err = (y.float().cpu() - yr).abs().max() / yr.abs().max()
+    assert err < 2e-2, err
+
+
+def test_caffenet_step_fused_equals_unfused(gpu):
+    from sparknet_amd import engine, models
+    from sparknet_amd.core.solver import Solver
+    results = []
+    for fuse in (True, False):
+        sp = models.zoo.caffenet_solver(models.caffenet(train_batch=8, test_batch=8, crop=227, classes=10))
+        solver = Solver(sp, device=torch.device(gpu), seed=5, build_test_nets=False)
+        net = solver.net
+        if fuse:
+            engine.fuse_relu(net)
+            assert sum(l.fused_lrn is not None for l in net.layers if l.type_name == "Pooling") == 2
+        else:
+            orig = engine.fuse_pool_lrn
+            engine.fuse_pool_lrn = lambda n: 0
+            try:
+                engine.fuse_relu(net)
+            finally:
+                engine.fuse_pool_lrn = orig
+        g = torch.Generator().manual_seed(9)
+        x = torch.randn(8, 3, 227, 227, generator=g) * 50
+        lab = torch.randint(0, 10, (8, 1), generator=g).float()
+        losses = []
+        for _ in range(3):
+            net.blob_by_name("data").set_nchw(x)
+            net.blob_by_name("label").set_nchw(lab)
+            losses.append(float(solver.iteration()))
+            solver.iter += 1
+        torch.cuda.synchronize()
+        results.append((losses, net.flat_data.detach().clone()))
+    assert results[0][0] == results[1][0]
+    assert torch.equal(results[0][1], results[1][1])
