@@ -9,9 +9,15 @@
 // be replayed inside a graph without host involvement; TEST phase uses centre crops.
 #include "common.h"
 
+#include <cstdlib>
+
 __global__ void augment_kernel(const uint8_t* __restrict__ src, bf16_t* __restrict__ dst, int N, int C, int Hs, int Ws,
                                int crop_h, int crop_w, const float* __restrict__ mean, int mean_mode, float scale,
-                               const long long* __restrict__ rng, int train, int mirror, int* __restrict__ offs_out) {
+                               const long long* __restrict__ rng, int train, int mirror, int* __restrict__ offs_out,
+                               const int* __restrict__ labels, float* __restrict__ labels_out) {
+  // the minibatch's labels -> the float label blob (ProtoLoader.scala:53), folded in here
+  if (labels && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < N; i += blockDim.x) labels_out[i] = (float)labels[i];
   const long long total = (long long)N * crop_h * crop_w;
   const unsigned long long seed = rng ? (unsigned long long)rng[0] : 0ull;
   const unsigned long long counter = rng ? (unsigned long long)rng[1] : 0ull;
@@ -51,12 +57,13 @@ __global__ void augment_kernel(const uint8_t* __restrict__ src, bf16_t* __restri
 
 extern "C" int sn_augment(const uint8_t* src, bf16_t* dst, long long N, long long C, long long Hs, long long Ws,
                           long long crop_h, long long crop_w, const float* mean, long long mean_mode, float scale,
-                          const long long* rng, long long train, long long mirror, int* offs_out, hipStream_t st) {
+                          const long long* rng, long long train, long long mirror, int* offs_out,
+                          const int* labels, float* labels_out, hipStream_t st) {
   if (crop_h > Hs || crop_w > Ws) return 9;
   long long total = N * crop_h * crop_w;
   hipLaunchKernelGGL(augment_kernel, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, src, dst, (int)N, (int)C,
                      (int)Hs, (int)Ws, (int)crop_h, (int)crop_w, mean, (int)mean_mode, scale, rng, (int)train,
-                     (int)mirror, offs_out);
+                     (int)mirror, offs_out, labels, labels_out);
   return SN_CHECK_LAUNCH();
 }
 
@@ -69,51 +76,72 @@ extern "C" int sn_augment(const uint8_t* src, bf16_t* dst, long long N, long lon
 // channels); F / CP are compile-time for the common RGB cases so the channel ->
 // (dy, dx, c) decode is shifts, with a runtime fallback.
 template <int F, int CP, int MM>
-__global__ void augment_s2d_kernel(const uint8_t* __restrict__ src, bf16_t* __restrict__ x2, int N, int C, int Hs,
-                                   int Ws, int crop_h, int crop_w, const float* __restrict__ mean, int mean_mode,
-                                   float scale, const long long* __restrict__ rng, int train, int mirror, int H2,
-                                   int W2, int f_rt, int cp_rt, int ph, int pw) {
+__global__ void __launch_bounds__(256) augment_s2d_kernel(const uint8_t* __restrict__ src, bf16_t* __restrict__ x2,
+                                                          int N, int C, int Hs, int Ws, int crop_h, int crop_w,
+                                                          const float* __restrict__ mean, int mean_mode, float scale,
+                                                          const long long* __restrict__ rng, int train, int mirror,
+                                                          int H2, int W2, int f_rt, int cp_rt, int ph, int pw,
+                                                          int direct, const int* __restrict__ labels,
+                                                          float* __restrict__ labels_out) {
+  if (labels && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < N; i += blockDim.x) labels_out[i] = (float)labels[i];
   const int f = F ? F : f_rt, Cp = CP ? CP : cp_rt;
   const int cv = f * f * Cp / 8;
+  const bool staged = F && !direct;
+  // compile-time shapes: the block's 256 consecutive output pixels (contiguous in x2) are
+  // assembled in LDS and stored by consecutive lanes — a per-thread store of its own
+  // cv x 16 B pixel leaves each wave store instruction 64 scattered 16-B pieces
+  constexpr int CVS = F ? F * F * CP / 8 : 1;
+  __shared__ uint4 tile[F ? 256 * CVS : 1];
   const long long total = (long long)N * H2 * W2;
   const unsigned long long seed = rng ? (unsigned long long)rng[0] : 0ull;
   const unsigned long long counter = rng ? (unsigned long long)rng[1] : 0ull;
-  for (long long pix = blockIdx.x * (long long)blockDim.x + threadIdx.x; pix < total;
-       pix += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(pix % W2), r = (int)((pix / W2) % H2), n = (int)(pix / ((long long)W2 * H2));
-    int ho, wo, mir;
-    if (train) {
-      uint4 u = philox4x32(make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)),
-                           make_uint4((uint32_t)n, 0xA5A50000u, (uint32_t)counter, (uint32_t)(counter >> 32)));
-      ho = (int)(u.x % (uint32_t)(Hs - crop_h + 1));
-      wo = (int)(u.y % (uint32_t)(Ws - crop_w + 1));
-      mir = mirror ? (int)(u.z & 1u) : 0;
-    } else {
-      ho = (Hs - crop_h) / 2;
-      wo = (Ws - crop_w) / 2;
-      mir = 0;
-    }
-    uint4* out = reinterpret_cast<uint4*>(x2) + pix * cv;
-#pragma unroll
-    for (int ch = 0; ch < cv; ++ch) {
-      float v[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int e = ch * 8 + t;
-        const int d = e / Cp, c = e - d * Cp;
-        const int h = r * f + d / f - ph, w = j * f + d % f - pw;  // crop coordinates
-        // branch-free: load from a clamped in-image address, then select (a load under a
-        // per-element condition makes hipcc wait vmcnt(0) per element)
-        const bool ok = c < C && (unsigned)h < (unsigned)crop_h && (unsigned)w < (unsigned)crop_w;
-        const int hc = min(max(h, 0), crop_h - 1), wc = min(max(w, 0), crop_w - 1), cc = min(c, C - 1);
-        const int sh = hc + ho, sw = (mir ? (crop_w - 1 - wc) : wc) + wo;
-        float x = (float)src[(((long long)n * C + cc) * Hs + sh) * Ws + sw];
-        if (MM == 1) x -= mean[cc];  // mean mode is a template parameter: no per-element branch
-        if (MM == 2) x -= mean[((long long)cc * Hs + sh) * Ws + sw];
-        x = ok ? x * scale : 0.f;
-        v[t] = x;
+  for (long long base = (long long)blockIdx.x * blockDim.x; base < total; base += (long long)gridDim.x * blockDim.x) {
+    const long long pix = base + threadIdx.x;
+    if (pix < total) {
+      const int j = (int)(pix % W2), r = (int)((pix / W2) % H2), n = (int)(pix / ((long long)W2 * H2));
+      int ho, wo, mir;
+      if (train) {
+        uint4 u = philox4x32(make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)),
+                             make_uint4((uint32_t)n, 0xA5A50000u, (uint32_t)counter, (uint32_t)(counter >> 32)));
+        ho = (int)(u.x % (uint32_t)(Hs - crop_h + 1));
+        wo = (int)(u.y % (uint32_t)(Ws - crop_w + 1));
+        mir = mirror ? (int)(u.z & 1u) : 0;
+      } else {
+        ho = (Hs - crop_h) / 2;
+        wo = (Ws - crop_w) / 2;
+        mir = 0;
       }
-      out[ch] = pack8(v);
+      uint4* out = reinterpret_cast<uint4*>(x2) + pix * cv;
+#pragma unroll
+      for (int ch = 0; ch < cv; ++ch) {
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int e = ch * 8 + t;
+          const int d = e / Cp, c = e - d * Cp;
+          const int h = r * f + d / f - ph, w = j * f + d % f - pw;  // crop coordinates
+          // branch-free: load from a clamped in-image address, then select (a load under a
+          // per-element condition makes hipcc wait vmcnt(0) per element)
+          const bool ok = c < C && (unsigned)h < (unsigned)crop_h && (unsigned)w < (unsigned)crop_w;
+          const int hc = min(max(h, 0), crop_h - 1), wc = min(max(w, 0), crop_w - 1), cc = min(c, C - 1);
+          const int sh = hc + ho, sw = (mir ? (crop_w - 1 - wc) : wc) + wo;
+          float x = (float)src[(((long long)n * C + cc) * Hs + sh) * Ws + sw];
+          if (MM == 1) x -= mean[cc];  // mean mode is a template parameter: no per-element branch
+          if (MM == 2) x -= mean[((long long)cc * Hs + sh) * Ws + sw];
+          x = ok ? x * scale : 0.f;
+          v[t] = x;
+        }
+        if (staged) tile[threadIdx.x * CVS + ch] = pack8(v);
+        else out[ch] = pack8(v);
+      }
+    }
+    if (staged) {
+      __syncthreads();
+      const int n_out = (int)min((long long)blockDim.x, total - base) * CVS;
+      uint4* dst = reinterpret_cast<uint4*>(x2) + base * CVS;
+      for (int k = threadIdx.x; k < n_out; k += blockDim.x) dst[k] = tile[k];
+      __syncthreads();
     }
   }
 }
@@ -121,14 +149,16 @@ __global__ void augment_s2d_kernel(const uint8_t* __restrict__ src, bf16_t* __re
 extern "C" int sn_augment_s2d(const uint8_t* src, bf16_t* x2, long long N, long long C, long long Hs, long long Ws,
                               long long crop_h, long long crop_w, const float* mean, long long mean_mode, float scale,
                               const long long* rng, long long train, long long mirror, long long H2, long long W2,
-                              long long f, long long Cp, long long ph, long long pw, hipStream_t st) {
+                              long long f, long long Cp, long long ph, long long pw, const int* labels,
+                              float* labels_out, hipStream_t st) {
   if (crop_h > Hs || crop_w > Ws || (f * f * Cp) % 8 || Cp < C) return 9;
   long long total = N * H2 * W2;
   dim3 grid(sn_blocks(total, 256, 16384));
+  const int direct = std::getenv("SN_AUGMENT_DIRECT") != nullptr;  // A/B: per-thread pixel stores
 #define SN_AUG_S2D_MM(FF, CC, MM)                                                                               \
   hipLaunchKernelGGL((augment_s2d_kernel<FF, CC, MM>), grid, dim3(256), 0, st, src, x2, (int)N, (int)C, (int)Hs, (int)Ws, \
                      (int)crop_h, (int)crop_w, mean, (int)mean_mode, scale, rng, (int)train, (int)mirror, (int)H2,     \
-                     (int)W2, (int)f, (int)Cp, (int)ph, (int)pw)
+                     (int)W2, (int)f, (int)Cp, (int)ph, (int)pw, direct, labels, labels_out)
 #define SN_AUG_S2D(FF, CC)              \
   do {                                  \
     if (mean_mode == 1)                 \

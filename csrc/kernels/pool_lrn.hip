@@ -10,23 +10,26 @@
 //   forward : one workgroup pools a run of output pixels (all channels) into LDS, stores
 //             the pooled tensor (the LRN backward needs it) and the argmax mask, then
 //             normalises across channels out of LDS — the LRN never re-reads HBM;
-//   backward: one workgroup owns RB rows of 2x2 input blocks of one image: it computes the
-//             LRN input gradient of the RB+1 pooled rows those blocks read (one halo row)
-//             into LDS, then gathers the pooling gradient out of LDS — the pooled gradient
-//             never exists in HBM.
+//   backward: one workgroup owns RB rows of 2x2 input blocks of one image and a group of
+//             channel chunks: it computes the LRN input gradient of the RB+1 pooled rows
+//             those blocks read (one halo row) into LDS, then gathers the pooling gradient
+//             out of LDS — the pooled gradient never exists in HBM.
 // The arithmetic is the unfused kernels' own, in the same order, on the same bf16-rounded
 // intermediates, so the fused pair is bitwise equal to the two separate launches.
 #include "common.h"
+
+#include <cstdlib>
 
 struct PLGeom {
   int N, H, W, C, P, Q, ph, pw;
   int gate;         // forward: the pooled input is an in-place ReLU output (mask 255 = no gradient)
   int pix;          // forward: pooled pixels per workgroup
   int BH, BW;       // backward: 2x2 input blocks over the padded extent
-  int rows, nb;     // backward: block rows per workgroup, workgroups per image
+  int rows, nb;     // backward: block rows per workgroup, row runs per image
+  int cg, ngrp;     // backward: channel chunks per workgroup, channel groups
   int size;
   float alpha, beta, k;
-  FDiv fcv, fQ, fP, fQcv, fBWcv;
+  FDiv fcv, fQ, fP, fcg, fQcg, fBWcg;
 };
 
 SN_DEV float plrn_pow(float s, float beta) { return __expf(-beta * __logf(s)); }
@@ -134,21 +137,26 @@ template <int SIZE>
 __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ xp, const bf16_t* __restrict__ dyn,
                                                     const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
                                                     PLGeom g) {
-  extern __shared__ uint4 tile[];  // (rows + 1) x Q x cv chunks of the pooled gradient
+  // workgroup = (image, run of `rows` block rows, group of `cg` channel chunks): the LRN's
+  // channel window only widens the global loads of phase 1, so channel groups cost no
+  // recomputation; only the one halo pooled row above the run is computed twice
+  extern __shared__ uint4 tile[];  // (rows + 1) x Q x cg chunks of the pooled gradient
   constexpr int PRE = (SIZE - 1) / 2, POST = SIZE - PRE - 1;
-  const int cv = g.C >> 3;
-  const int n = blockIdx.x / g.nb;
-  const int bh0 = (blockIdx.x - n * g.nb) * g.rows;
-  const int qcv = g.Q * cv;
+  const int cg = g.cg;
+  const int wg = blockIdx.x / g.ngrp;
+  const int ch0 = (blockIdx.x - wg * g.ngrp) * cg;
+  const int n = wg / g.nb;
+  const int bh0 = (wg - n * g.nb) * g.rows;
+  const int qcg = g.Q * cg;
   const float a = g.alpha / g.size;
   const float cache_ratio = 2.f * g.alpha * g.beta / g.size;
   // phase 1: LRN backward of pooled rows bh0-1 .. bh0+rows-1 (lrn_across_bwd, gate off)
-  const int items1 = (g.rows + 1) * qcv;
+  const int items1 = (g.rows + 1) * qcg;
   for (int it = threadIdx.x; it < items1; it += blockDim.x) {
-    const uint32_t r = udiv((uint32_t)it, g.fQcv);
-    const int rem = it - (int)r * qcv;
-    const uint32_t q = udiv((uint32_t)rem, g.fcv);
-    const int c0 = (rem - (int)q * cv) * 8;
+    const uint32_t r = udiv((uint32_t)it, g.fQcg);
+    const int rem = it - (int)r * qcg;
+    const uint32_t q = udiv((uint32_t)rem, g.fcg);
+    const int c0 = (ch0 + rem - (int)q * cg) * 8;
     const int p = bh0 - 1 + (int)r;
     if (p < 0 || p >= g.P) {
       tile[it] = make_uint4(0u, 0u, 0u, 0u);
@@ -184,13 +192,13 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
   }
   __syncthreads();
   // phase 2: the 2x2 input blocks of rows bh0 .. bh0+rows-1 (pool_bwd_k3s2<true>)
-  const int bwcv = g.BW * cv;
-  const int items2 = min(g.rows, g.BH - bh0) * bwcv;
+  const int bwcg = g.BW * cg;
+  const int items2 = min(g.rows, g.BH - bh0) * bwcg;
   for (int it = threadIdx.x; it < items2; it += blockDim.x) {
-    const uint32_t r = udiv((uint32_t)it, g.fBWcv);
-    const int rem = it - (int)r * bwcv;
-    const uint32_t bwu = udiv((uint32_t)rem, g.fcv);
-    const int ch = rem - (int)bwu * cv, c0 = ch * 8;
+    const uint32_t r = udiv((uint32_t)it, g.fBWcg);
+    const int rem = it - (int)r * bwcg;
+    const uint32_t bwu = udiv((uint32_t)rem, g.fcg);
+    const int lc = rem - (int)bwu * cg, c0 = (ch0 + lc) * 8;
     const int bw = (int)bwu, bh = bh0 + (int)r;
     uint4 dv[4];
     uint2 mv[4];
@@ -202,7 +210,7 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
         const int p = bh - 1 + wa, q = bw - 1 + wb, t = wa * 2 + wb;
         ok[t] = p >= 0 && p < g.P && q >= 0 && q < g.Q;
         const int pc = min(max(p, 0), g.P - 1), qc = min(max(q, 0), g.Q - 1);
-        dv[t] = tile[((int)r + wa) * qcv + qc * cv + ch];
+        dv[t] = tile[((int)r + wa) * qcg + qc * cg + lc];
         mv[t] = *reinterpret_cast<const uint2*>(mask + (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0);
       }
     float f[4][8];
@@ -250,10 +258,26 @@ static bool plrn_ok(long long N, long long H, long long W, long long C, long lon
 
 // Workgroup shapes (host side, shared with the Python eligibility check).
 static int plrn_fwd_pix(long long C) { return (int)(512 / (C / 8) > 0 ? 512 / (C / 8) : 1); }
-static int plrn_bwd_rows(long long Q, long long C) {
-  for (int rows = 4; rows >= 1; --rows)
-    if ((long long)(rows + 1) * Q * (C / 8) * 16 <= 64 * 1024) return rows;
-  return 0;
+// backward tile: the channel group is the whole pixel or at least 8 chunks (128 B), so
+// the gradient rows are written in full cache lines; then the most block rows (least halo
+// recomputation) whose (rows + 1) x Q x cg tile fits the LDS budget (SN_PLRN_LDS bytes,
+// default 32 KB: several workgroups per CU).  SN_PLRN_CG forces the group size.
+static bool plrn_bwd_tile(long long Q, long long C, int* rows, int* cg) {
+  const int cv = (int)(C / 8);
+  const char* e = std::getenv("SN_PLRN_LDS");
+  const long long budget = e ? std::atoll(e) : 32 * 1024;
+  const char* fc = std::getenv("SN_PLRN_CG");
+  for (int r = 7; r >= 1; --r)
+    for (int c = cv; c >= 1; --c) {
+      if (cv % c) continue;
+      if (fc ? c != std::atoi(fc) : (c != cv && c < 8)) continue;
+      if ((long long)(r + 1) * Q * c * 16 <= budget) {
+        *rows = r;
+        *cg = c;
+        return true;
+      }
+    }
+  return false;
 }
 
 extern "C" int sn_pool_lrn_fwd(const bf16_t* x, bf16_t* pooled, uint8_t* mask, bf16_t* y, long long N, long long H,
@@ -280,17 +304,18 @@ extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_
                                long long pw, long long size, float alpha, float beta, float k, hipStream_t st) {
   if (!plrn_ok(N, H, W, C, P, Q, ph, pw, size)) return 4;
   PLGeom g = plgeom(N, H, W, C, P, Q, ph, pw, size, alpha, beta, k);
-  g.rows = plrn_bwd_rows(Q, C);
-  if (g.rows == 0) return 4;
+  if (!plrn_bwd_tile(Q, C, &g.rows, &g.cg)) return 4;
+  g.ngrp = (int)(C / 8) / g.cg;
   g.BH = (int)((H + ph + 1) / 2);
   g.BW = (int)((W + pw + 1) / 2);
   // every pooled row the blocks read exists in the tile: blocks bh read rows bh-1, bh
   if (g.BH > P + 1 || g.BW > Q + 1) return 4;
   g.nb = (g.BH + g.rows - 1) / g.rows;
-  g.fQcv = make_fdiv((uint32_t)(Q * (C / 8)));
-  g.fBWcv = make_fdiv((uint32_t)(g.BW * (C / 8)));
-  dim3 grid((unsigned)(N * g.nb));
-  const size_t lds = (size_t)(g.rows + 1) * Q * (C / 8) * sizeof(uint4);
+  g.fcg = make_fdiv((uint32_t)g.cg);
+  g.fQcg = make_fdiv((uint32_t)(Q * g.cg));
+  g.fBWcg = make_fdiv((uint32_t)(g.BW * g.cg));
+  dim3 grid((unsigned)(N * g.nb * g.ngrp));
+  const size_t lds = (size_t)(g.rows + 1) * Q * g.cg * sizeof(uint4);
   switch (size) {
     case 3: hipLaunchKernelGGL(lrn_pool_bwd<3>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
     case 5: hipLaunchKernelGGL(lrn_pool_bwd<5>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;

@@ -256,14 +256,18 @@ class DeviceFeeder:
             self._stage_cpu(src, lab)
             return
         from ..ops import hip
+        ld = self.label_blob.data  # labels -> float inside the augment launch
+        fused = ld.dtype == torch.float32 and ld.is_contiguous() and ld.numel() == lab.numel()
+        labels, label_out = (lab, ld) if fused else (None, None)
         if self.fold is not None:
             x2, plan, spec = self.fold
             hip.augment_s2d(src, x2, self.crop, plan, spec, self.mean, self.mean_mode, self.scale, self.rng_state,
-                            self.train, self.mirror)
+                            self.train, self.mirror, labels, label_out)
         else:
             hip.augment(src, self.data_blob.data, self.crop, self.mean, self.mean_mode, self.scale,
-                        self.rng_state, self.train, self.mirror)
-        _lib.call("labels_to_float", lab, self.label_blob.data, lab.numel())
+                        self.rng_state, self.train, self.mirror, labels=labels, label_out=label_out)
+        if not fused:
+            _lib.call("labels_to_float", lab, ld, lab.numel())
 
     def _stage_cpu(self, src, lab) -> None:
         """Reference (CPU) version of the augment kernel semantics."""

@@ -508,8 +508,8 @@ def pool_lrn_eligible(s: PoolSpec, size: int, within: bool) -> bool:
         return False
     if s.ph >= 3 or s.pw >= 3 or s.N * s.H * s.W * s.C >= 1 << 32:
         return False
-    rows = next((r for r in (4, 3, 2, 1) if (r + 1) * s.Q * (s.C // 8) * 16 <= 64 * 1024), 0)
-    return rows > 0 and (s.H + s.ph + 1) // 2 <= s.P + 1 and (s.W + s.pw + 1) // 2 <= s.Q + 1
+    cv = s.C // 8  # backward tile (pool_lrn.hip plrn_bwd_tile): two pooled rows of a 128-B group fit 32 KB
+    return 2 * s.Q * 16 * min(cv, 8) <= 32 * 1024 and (s.H + s.ph + 1) // 2 <= s.P + 1 and (s.W + s.pw + 1) // 2 <= s.Q + 1
 
 
 def pool_lrn_forward(x, s: PoolSpec, gate: bool, size: int, alpha: float, beta: float, k: float):
@@ -758,23 +758,33 @@ def s2d_plan(s: ConvSpec):
     return _s2d_plan(s)
 
 
+def _labels(labels, label_out):
+    if labels is None:
+        return None, None
+    assert labels.dtype == torch.int32 and label_out.dtype == torch.float32 and label_out.numel() == labels.numel()
+    return _c(labels), label_out
+
+
 def augment_s2d(src_u8, x2, crop, plan, s: ConvSpec, mean=None, mean_mode=0, scale=1.0, rng_state=None,
-                train=True, mirror=False):
-    """Fused augment + space-to-depth fold into x2 (see conv_forward(folded=...))."""
+                train=True, mirror=False, labels=None, label_out=None):
+    """Fused augment + space-to-depth fold into x2 (see conv_forward(folded=...)); with
+    ``labels`` (int32 [N]) the same launch also writes them as floats into ``label_out``."""
     N, Cc, Hs, Ws = src_u8.shape
     f, cp, rf, sf, s2 = plan
     assert tuple(x2.shape) == (N, s2.H, s2.W, s2.C) and x2.dtype == BF16 and x2.is_contiguous()
     assert s.C == Cc and s.H == crop and s.W == crop
+    assert labels is None or labels.numel() == N
     call("augment_s2d", _c(src_u8), x2, N, Cc, Hs, Ws, crop, crop, mean, int(mean_mode), float(scale), rng_state,
-         int(train), int(mirror), s2.H, s2.W, f, cp, s.ph, s.pw)
+         int(train), int(mirror), s2.H, s2.W, f, cp, s.ph, s.pw, *_labels(labels, label_out))
     return x2
 
 
 def augment(src_u8, dst, crop, mean=None, mean_mode=0, scale=1.0, rng_state=None, train=True, mirror=False,
-            offs_out=None):
+            offs_out=None, labels=None, label_out=None):
     N, Cc, Hs, Ws = src_u8.shape
+    assert labels is None or labels.numel() == N
     call("augment", _c(src_u8), dst, N, Cc, Hs, Ws, crop, crop, mean, int(mean_mode), float(scale), rng_state,
-         int(train), int(mirror), offs_out)
+         int(train), int(mirror), offs_out, *_labels(labels, label_out))
     return dst
 
 

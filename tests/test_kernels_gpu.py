@@ -280,14 +280,17 @@ def test_cast_and_augment(gpu):
         close(out[n], expect, 1e-2)
 
 
+@pytest.mark.parametrize("src_hw", [(40, 44), (39, 41)])
 @pytest.mark.parametrize("mean_mode", [1, 2])
 @pytest.mark.parametrize("ksp", [(11, 4, 0), (7, 2, 3), (3, 1, 1)])
-def test_augment_s2d_equals_augment_then_fold(gpu, mean_mode, ksp):
-    """The fused augment + space-to-depth kernel is bitwise the two-pass result."""
+def test_augment_s2d_equals_augment_then_fold(gpu, mean_mode, ksp, src_hw, monkeypatch):
+    """The fused augment + space-to-depth kernel (row-tiled LDS path and the per-pixel
+    path) is bitwise the two-pass result; odd source widths take the byte-load staging."""
     from sparknet_amd.ops import hip
     N, crop = 3, 35
-    img = torch.randint(0, 256, (N, 3, 40, 44), dtype=torch.uint8, device="cuda")
-    mean = (torch.rand(3, device="cuda") * 200) if mean_mode == 1 else (torch.rand(3, 40, 44, device="cuda") * 200)
+    Hs, Ws = src_hw
+    img = torch.randint(0, 256, (N, 3, Hs, Ws), dtype=torch.uint8, device="cuda")
+    mean = (torch.rand(3, device="cuda") * 200) if mean_mode == 1 else (torch.rand(3, Hs, Ws, device="cuda") * 200)
     rng = torch.tensor([11, 5], dtype=torch.int64, device="cuda")
     k, st, pd = ksp
     s = ConvSpec(N, crop, crop, 3, 16, k, k, st, st, pd, pd)
@@ -299,6 +302,12 @@ def test_augment_s2d_equals_augment_then_fold(gpu, mean_mode, ksp):
     x2 = torch.empty_like(ref2)
     hip.augment_s2d(img, x2, crop, plan, s, mean, mean_mode, 0.25, rng, True, True)
     assert torch.equal(x2, ref2)
+    monkeypatch.setenv("SN_AUGMENT_DIRECT", "1")
+    x3 = torch.full_like(ref2, 7.0)
+    lab = torch.tensor([4, 0, 9], dtype=torch.int32, device="cuda")
+    lab_out = torch.full((N, 1), -1.0, device="cuda")
+    hip.augment_s2d(img, x3, crop, plan, s, mean, mean_mode, 0.25, rng, True, True, lab, lab_out)
+    assert torch.equal(x3, ref2) and lab_out.flatten().tolist() == [4.0, 0.0, 9.0]
 
 
 @pytest.mark.parametrize("k", [2, 3, 8, 11])
