@@ -22,4 +22,5 @@ for k, cs in vals.items():
         print(f"   {c:30s} {m[c]:14.4g}")
     g = m.get("GRBM_GUI_ACTIVE")
     if g and "SQ_VALU_MFMA_BUSY_CYCLES" in m and "SQ_BUSY_CU_CYCLES" in m:
-        print(f"   MFMA busy / (GUI_ACTIVE x 256 CU x 4 SIMD) = {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (g * 1024):.3f}")
+        # GRBM_GUI_ACTIVE sums the 8 XCDs; busy cycles sum the 1024 SIMDs (scripts/pmc_summary.py)
+        print(f"   MFMA util = MFMA_BUSY / (GUI_ACTIVE / 8 x 1024 SIMD) = {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (g / 8 * 1024):.3f}")

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc passes (gpurun_out/pmc/p*/run_counter_collection.csv): mean
 counter value per kernel instantiation (short name), plus derived metrics:
-MFMA util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * CUs), L2 hit %, LDS conflict
+MFMA util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs) — the one
+normalisation used for every PMC figure in this repo (GRBM_GUI_ACTIVE sums the 8 XCDs'
+active cycles; MFMA busy cycles sum over all 1024 SIMDs), L2 hit %, LDS conflict
 ratio, fetched bytes (FETCH_SIZE is reported x2 per MI355X_MICROARCH.md)."""
 import collections
 import csv
@@ -38,7 +40,7 @@ for k in order:
         continue
     out = [k]
     if "GRBM_GUI_ACTIVE" in d and "SQ_VALU_MFMA_BUSY_CYCLES" in d:
-        out.append(f"mfma_util={100 * d['SQ_VALU_MFMA_BUSY_CYCLES'] / (d['GRBM_GUI_ACTIVE'] * CUS):.1f}%")
+        out.append(f"mfma_util={100 * d['SQ_VALU_MFMA_BUSY_CYCLES'] / (d['GRBM_GUI_ACTIVE'] / 8 * 4 * CUS):.1f}%")
         out.append(f"gui_cycles={d['GRBM_GUI_ACTIVE']:.0f}")
     if "TCC_HIT_sum" in d:
         out.append(f"L2_hit={100 * d['TCC_HIT_sum'] / max(1, d['TCC_HIT_sum'] + d['TCC_MISS_sum']):.1f}%")

@@ -160,11 +160,13 @@ def test_fp8_conv_forward(gpu, case):
 
 
 
-# --- gemm256_kernel (tiles 6 = 256x256, 7 = 256x128) and the 8-wave 2-stage gemm_kernel
-# tiles (11 = 256x256, 12 / 13 = 256x128, 14 = 256x192, K-contiguous B only): every operand
+# --- gemm256_kernel (tiles 6 = 256x256, 7 = 256x128), the 8-wave 2-stage gemm_kernel
+# tiles (11 = 256x256, 12 / 13 = 256x128, 14 = 256x192, K-contiguous B only), the 3-stage
+# 4-wave tiles (19, 20: dense only) and the B-direct tiles (21, 22: gemm_bdir.hip, forward
+# products with a K-contiguous dense B): every operand
 # layout, ragged edges, short and long K (the phased DMA pipeline issues zero-page DMAs past
 # the last K-step), split-K, the bias-gradient column and the implicit-GEMM convolutions
-BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18]
+BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22]
 MC_B = {6, 7, 11, 12, 13}  # tiles with MC (k-strided) A and B operand instances
 
 
@@ -178,7 +180,7 @@ def test_gemm256_layouts(gpu, tile, M, N, K, monkeypatch):
     _close(G.linear_fwd(x, w, b, relu=True), torch.relu(x.float() @ w.float().t() + b))
     dy = _bf(M, N, device=gpu)
     w2 = _bf(N, K, device=gpu)
-    if tile in MC_B or tile in (16, 18):  # NN: MC B operand (192-row tiles: MC A excluded)
+    if tile in MC_B or tile in (16, 18, 19, 20):  # NN: MC B operand (192-row tiles: MC A excluded)
         _close(G.linear_dgrad(dy, w2), dy.float() @ w2.float())
     if tile not in MC_B:
         return
@@ -222,6 +224,8 @@ def test_gemm256_conv(gpu, tile, case, monkeypatch):
     from sparknet_amd.ops import gemm as G, hip, ref
     from sparknet_amd.ops.spec import ConvSpec
     monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    if tile in (19, 20):
+        pytest.skip("3-stage 4-wave tiles: dense operands only")
     N, H, W, Cc, K, R, S, st, pd, g = case
     s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
     x = _bf(N, H, W, Cc, device=gpu)
@@ -301,6 +305,8 @@ def test_fast_dma_addressing_bitwise(gpu, tile, case, monkeypatch):
     from sparknet_amd.ops import gemm as G, hip
     from sparknet_amd.ops.spec import ConvSpec
     monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    if tile in (19, 20):
+        pytest.skip("3-stage 4-wave tiles: dense operands only")
     N, H, W, Cc, K, R, S, st, pd, g = case
     s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
     x = _bf(N, H, W, Cc, device=gpu)
