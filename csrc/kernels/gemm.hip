@@ -110,8 +110,6 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 10:
     case 19:
     case 20: return sn_gemm_tiles_b(a, stream);  // gemm_tiles_b.hip
-    case 21:
-    case 22: return sn_gemm_bdir(a, stream);  // gemm_bdir.hip
     case 4: return launch_tile96(a, stream);
     case 5: return launch_tile48(a, stream);
     case 6:

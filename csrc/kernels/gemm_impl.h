@@ -1364,4 +1364,3 @@ int sn_gemm_tiles_b(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_t256(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big8(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big4(const SnGemmArgs& a, hipStream_t stream);
-int sn_gemm_bdir(const SnGemmArgs& a, hipStream_t stream);

@@ -113,10 +113,10 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
          6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64),
          11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192), 15: (128, 192), 16: (192, 128),
-         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64), 21: (128, 128), 22: (128, 128)}
+         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64)}
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
-_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512, 21: 512, 22: 512}
+_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512}
 _KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55}
 # autotune candidates 11-14 (SN_GEMM_TILE8W=0 drops them)
 _TILE8W = os.environ.get("SN_GEMM_TILE8W", "1") != "0"
@@ -124,7 +124,6 @@ _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experime
 _RASTER_N = int(os.environ.get("SN_GEMM_RASTER_N", "-1"))  # -1: heuristic
 _TILE256 = os.environ.get("SN_GEMM_TILE256", "1") != "0"  # autotune candidates 6 / 7 (gemm256_kernel)
 _TILE64 = os.environ.get("SN_GEMM_TILE64", "1") != "0"  # autotune candidate 10 (128x64, 3 blocks / CU)
-_TILE_BDIR = os.environ.get("SN_GEMM_BDIR", "1") != "0"  # autotune candidates 21 / 22 (gemm_bdir.hip)
 
 
 def choose_tile(M: int, N: int, b_kcontig: bool = False) -> int:
@@ -414,8 +413,6 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
         tiles.append(18)
         if b_kc_dense and N % 96 == 0:
             tiles.append(17)
-    if epi != EPI_SGD and b_kc_dense and _TILE_BDIR:
-        tiles += [21, 22]  # B fragments straight to VGPRs, A through 3 / 4 LDS stages
     if epi != EPI_SGD and not b_kc_dense and N >= 64:
         tiles.append(20)  # 3-stage 128x64 (dense NN: InnerProduct data gradient)
     if epi != EPI_SGD:

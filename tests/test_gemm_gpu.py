@@ -162,11 +162,10 @@ def test_fp8_conv_forward(gpu, case):
 
 # --- gemm256_kernel (tiles 6 = 256x256, 7 = 256x128), the 8-wave 2-stage gemm_kernel
 # tiles (11 = 256x256, 12 / 13 = 256x128, 14 = 256x192, K-contiguous B only), the 3-stage
-# 4-wave tiles (19, 20: dense only) and the B-direct tiles (21, 22: gemm_bdir.hip, forward
-# products with a K-contiguous dense B): every operand
+# 4-wave tiles (19, 20: dense only): every operand
 # layout, ragged edges, short and long K (the phased DMA pipeline issues zero-page DMAs past
 # the last K-step), split-K, the bias-gradient column and the implicit-GEMM convolutions
-BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22]
+BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20]
 MC_B = {6, 7, 11, 12, 13}  # tiles with MC (k-strided) A and B operand instances
 
 
