@@ -243,6 +243,7 @@ _NO_XTRA = (0, 0, 0.0, 1.0)
 # bf16 epilogues of the 4-wave tiles store through LDS as whole 16-B row chunks
 # (SnGemmArgs.lds_store); SN_GEMM_LDS_EPI=0 keeps the per-fragment stores (A/B)
 _LDS_EPI = os.environ.get("SN_GEMM_LDS_EPI", "1") != "0"
+_LDS_EPI_TILES = frozenset(int(t) for t in os.environ.get("SN_GEMM_LDS_EPI_TILES", "0,1,4,5,10,12,13,14,15,16,17,18,19,20").split(","))
 # SnGemmArgs.addr_legacy: 1 = the general per-lane DMA address decode only (A/B probes of
 # the scalar-offset fast paths; SN_GEMM_LEGACY_ADDR=1)
 _ADDR_LEGACY = int(os.environ.get("SN_GEMM_LEGACY_ADDR", "0"))
@@ -271,7 +272,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     bg = bias_grad.data_ptr() if bias_grad is not None else 0
     if splits == 1:
         e = EPI_BF16_DROP if (epi == EPI_BF16 and xtra[0]) else epi
-        lds = int(_LDS_EPI and epi == EPI_BF16 and tile in (0, 1, 4, 5, 10) and ldc % 8 == 0 and c_gstride % 8 == 0
+        lds = int(_LDS_EPI and epi == EPI_BF16 and tile in _LDS_EPI_TILES and ldc % 8 == 0 and c_gstride % 8 == 0
                   and out.data_ptr() % 16 == 0)
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, e,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
