@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes as C
+import dataclasses
 import os
 
 import torch
@@ -477,13 +478,27 @@ def _pool_args(s: PoolSpec):
     return (s.N, s.H, s.W, s.C, s.P, s.Q, s.kh, s.kw, s.sh, s.sw, s.ph, s.pw, s.method)
 
 
+# the pooling / LRN kernels decode NHWC element indices in 32 bits: larger batches run as
+# several launches over image ranges (contiguous NHWC slices)
+_MAX_ELEMS = 1 << 31
+
+
+def _pool_images(s: PoolSpec) -> int:
+    per = s.H * s.W * s.C
+    return s.N if s.N * per < _MAX_ELEMS else max(1, (_MAX_ELEMS - 1) // per)
+
+
 def pool_forward_mask(x, s: PoolSpec, gate: bool = False):
     """gate=True (MAX only): x is the output of a slope-0 in-place ReLU whose backward is
     folded into the argmax mask (windows with max <= 0 pass no gradient)."""
     x = _c(x)
     y = torch.empty((s.N, s.P, s.Q, s.C), dtype=BF16, device=x.device)
     mask = torch.empty((s.N, s.P, s.Q, s.C), dtype=torch.uint8, device=x.device) if s.method == POOL_MAX else None
-    call("pool_fwd", x, y, mask, *_pool_args(s), int(gate and s.method == POOL_MAX))
+    nb = _pool_images(s)
+    for n0 in range(0, s.N, nb):
+        n1 = min(s.N, n0 + nb)
+        call("pool_fwd", x[n0:n1], y[n0:n1], mask[n0:n1] if mask is not None else None,
+             *_pool_args(dataclasses.replace(s, N=n1 - n0)), int(gate and s.method == POOL_MAX))
     return y, mask
 
 
@@ -495,7 +510,12 @@ def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False):
     dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=dy.device)
     if s.method == POOL_MAX and mask is None:
         _, mask = pool_forward_mask(x, s, gate)
-    call("pool_bwd", _c(dy), mask, dx, *_pool_args(s))
+    dy = _c(dy)
+    nb = _pool_images(s)
+    for n0 in range(0, s.N, nb):
+        n1 = min(s.N, n0 + nb)
+        call("pool_bwd", dy[n0:n1], mask[n0:n1] if mask is not None else None, dx[n0:n1],
+             *_pool_args(dataclasses.replace(s, N=n1 - n0)))
     if gate and s.method != POOL_MAX:
         dx = relu_backward(dx, x)
     return dx
