@@ -98,6 +98,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     // e4m3 forward products: A (dense or implicit im2col) and B dense, both K-contiguous
     if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || a.a_mc || a.b_mc || a.b_mode != OP_DENSE || !a.deq_a || !a.deq_b)
       return 3;
+    if (a.tile == 11 || a.tile == 16) return sn_gemm_fp8_big(a, stream);  // gemm_fp8big.hip
     const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     dim3 grid(tiles * a.splits * a.groups);
     return a.a_mode == OP_IM2COL ? launch_fp8<OP_IM2COL>(a, grid, stream) : launch_fp8<OP_DENSE>(a, grid, stream);

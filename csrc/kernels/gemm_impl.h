@@ -761,7 +761,23 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
 
   auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
-    if constexpr (FP8) {
+    if constexpr (FP8 && MFR * NFR > 16) {
+      // large fp8 tiles (gemm_fp8big.hip): B fragments held, A fragments streamed per row
+      // group, so at most NFR + 1 fragments (8 VGPRs each) live beside the accumulators
+      i32x8 fb8[NFR];
+#pragma unroll
+      for (int i = 0; i < NFR; ++i) fb8[i] = read_frag8(lb, wn0 + 16 * i, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < MFR; ++j) {
+        const i32x8 fa = read_frag8(la, wm0 + 16 * j, lane);
+#pragma unroll
+        for (int i = 0; i < NFR; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa, acc[i][j], 0, 0, 0, 127, 0, 127);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      return;
+    } else if constexpr (FP8) {
       i32x8 fa8[MFR], fb8[NFR];
 #pragma unroll
       for (int i = 0; i < NFR; ++i) fb8[i] = read_frag8(lb, wn0 + 16 * i, lane);
@@ -1364,3 +1380,4 @@ int sn_gemm_tiles_b(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_t256(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big8(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big4(const SnGemmArgs& a, hipStream_t stream);
+int sn_gemm_fp8_big(const SnGemmArgs& a, hipStream_t stream);

@@ -223,8 +223,11 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         rng, dstream, ratio = dropout
         xtra = (rng.data_ptr(), int(dstream), float(ratio), float(gate_scale))
     ops = (sa, a_mc, a_mode, sb, b_mc, b_mode)
-    if splits is not None or fp8 or _FORCE_TILE >= 0:
-        tile = 0 if fp8 else (_FORCE_TILE if _FORCE_TILE >= 0 else choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE))
+    if splits is not None or _FORCE_TILE >= 0:
+        if fp8:
+            tile = _FORCE_TILE if _FORCE_TILE in _FP8_TILES else 0
+        else:
+            tile = _FORCE_TILE if _FORCE_TILE >= 0 else choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE)
         if epi == EPI_SGD and tile not in (0, 1, 2, 3):
             tile = 0
         if splits is None:
@@ -234,7 +237,7 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
             kchunk = -(-(-(-K // splits)) // bk) * bk
     else:
         tile, splits, kchunk = _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate,
-                                             bias_grad, bias_acc, ones, sg, xtra)
+                                             bias_grad, bias_acc, ones, sg, xtra, deq)
     _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc, ones, sg,
             tile, splits, kchunk, deq, xtra)
 
@@ -437,6 +440,25 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
     return list(dict.fromkeys(out))
 
 
+# e4m3 forward products: the 128x128 tile (gemm.hip launch_fp8) and the large tiles of
+# gemm_fp8big.hip (bf16 / fp32 epilogues; the fused-dropout epilogue only on 128x128)
+_FP8_TILES = (0, 11, 16)
+
+
+def _candidates_fp8(M, N, K, groups, epi, xtra):
+    out = []
+    for t in _FP8_TILES:
+        if t != 0 and (xtra[0] or epi not in (EPI_BF16, EPI_F32)):
+            continue
+        s, kc = choose_splits(M, N, K // 2, groups, t)
+        for s2 in dict.fromkeys((s, 1)):
+            kc2 = -(-(-(-K // s2)) // 128) * 128
+            s2 = max(1, -(-K // kc2))
+            if s2 * M * N * groups * 4 <= (256 << 20):
+                out.append((t, s2, kc2))
+    return list(dict.fromkeys(out))
+
+
 # Experiment knob: cap the split-K factor of every product (0 = no cap).  With several
 # branch streams in flight (Inception) other streams may fill the CUs a split would.
 _MAX_SPLITS = int(os.environ.get("SN_GEMM_MAX_SPLITS", "0"))
@@ -445,32 +467,39 @@ _MAX_SPLITS_BF16 = int(os.environ.get("SN_GEMM_MAX_SPLITS_BF16", "0"))
 
 
 def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
-                  ones, sg, xtra=_NO_XTRA):
+                  ones, sg, xtra=_NO_XTRA, deq=None):
     cfg = _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
-                            ones, sg, xtra)
+                            ones, sg, xtra, deq)
     t, s, kc = cfg
     cap = _MAX_SPLITS
     if _MAX_SPLITS_BF16 > 0 and epi in (EPI_BF16, EPI_BF16_DROP):
         cap = _MAX_SPLITS_BF16 if cap <= 0 else min(cap, _MAX_SPLITS_BF16)
     if cap <= 0 or s <= cap:
         return cfg
-    kc = -(-(-(-K // cap)) // BK) * BK
+    bk = 128 if deq is not None else BK
+    kc = -(-(-(-K // cap)) // bk) * bk
     return (t, max(1, -(-K // kc)), kc)
 
 
 def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
-                      ones, sg, xtra=_NO_XTRA):
+                      ones, sg, xtra=_NO_XTRA, deq=None):
     sa, a_mc, a_mode, sb, b_mc, b_mode = ops
     b_kc_dense = b_mc == 0 and b_mode == OP_DENSE
+    fp8 = deq is not None
     key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None, bool(xtra[0]),
-           _geom_key(sa), _geom_key(sb), out.dtype)
+           _geom_key(sa), _geom_key(sb)) + (("fp8",) if fp8 else ()) + (out.dtype,)
     hit = _TUNED.get(key)
     if hit is not None:
         return hit
-    tile = choose_tile(M, N, b_kc_dense)
+    tile = 0 if fp8 else choose_tile(M, N, b_kc_dense)
     if epi == EPI_SGD and tile not in (0, 1, 2, 3):
         tile = 0
-    splits, kchunk = choose_splits(M, N, K, groups, tile)
+    if fp8:  # K counts e4m3 elements, 128 per K-step; the cost model counts bf16 K-steps
+        splits, kchunk = choose_splits(M, N, K // 2, groups, tile)
+        kchunk *= 2
+        splits = -(-K // kchunk)
+    else:
+        splits, kchunk = choose_splits(M, N, K, groups, tile)
     default = (tile, splits, kchunk)
     extent = (groups - 1) * c_gstride + (M - 1) * ldc + (N - (1 if ones >= 0 else 0))
     if (not _AUTOTUNE or epi == EPI_SGD or not out.is_cuda or torch.cuda.is_current_stream_capturing()
@@ -480,12 +509,13 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     scratch = torch.empty_like(out) if out.is_contiguous() else torch.empty(extent, dtype=out.dtype, device=out.device)
     bscratch = torch.zeros_like(bias_grad) if bias_grad is not None else None
     runs = []
-    for cand in _candidates(M, N, K, groups, b_kc_dense, epi):
+    cands = _candidates_fp8(M, N, K, groups, epi, xtra) if fp8 else _candidates(M, N, K, groups, b_kc_dense, epi)
+    for cand in cands:
         t, s, kc = cand
 
         def run(t=t, s=s, kc=kc):
             _launch(M, N, K, groups, ops, epi, scratch, ldc, c_gstride, bias, relu, gate, bscratch, bias_acc,
-                    ones, sg, t, s, kc, None, xtra)
+                    ones, sg, t, s, kc, deq, xtra)
         try:
             run()
         except RuntimeError:  # a tile this operand combination has no instance for

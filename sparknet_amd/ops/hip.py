@@ -842,20 +842,22 @@ def quant_fp8(x: torch.Tensor, slot: torch.Tensor, out: torch.Tensor | None = No
     return q
 
 
-def conv_forward_fp8(xq, wq, b, s: ConvSpec, deq_x, deq_w, relu=False):
+def conv_forward_fp8(xq, wq, b, s: ConvSpec, deq_x, deq_w, relu=False, out=None):
     """Implicit-GEMM convolution on e4m3 operands (v_mfma_scale_f32_16x16x128_f8f6f4),
-    fp32 accumulation, dequantised + bias + ReLU epilogue, bf16 NHWC output."""
+    fp32 accumulation, dequantised + bias + ReLU epilogue, bf16 NHWC output (written into
+    ``out`` when given: image chunks of a large batch write their slice in place)."""
     assert s.Cg % 16 == 0 and s.C % 16 == 0 and xq.dtype == torch.uint8 and wq.dtype == torch.uint8
     nb = _image_chunk(s)
     if nb < s.N:
-        y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=xq.device)
+        y = out if out is not None else torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=xq.device)
         for n0 in range(0, s.N, nb):
             n1 = min(s.N, n0 + nb)
-            y[n0:n1] = conv_forward_fp8(xq[n0:n1], wq, b, s.with_batch(n1 - n0), deq_x, deq_w, relu)
+            conv_forward_fp8(xq[n0:n1], wq, b, s.with_batch(n1 - n0), deq_x, deq_w, relu, out=y[n0:n1])
         return y
     M = s.N * s.P * s.Q
     kred = s.R * s.S * s.Cg
-    y = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=xq.device)
+    y = out if out is not None else torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=xq.device)
+    assert y.is_contiguous()
     A = Im2col(xq, _geom(s), kcontig=True, gstride=s.Cg)
     B = Dense(wq.view(s.K, kred), kred, True, gstride=s.Kg * kred)
     gemm(M, s.Kg, kred, A, B, y, s.K, epi=EPI_BF16, groups=s.groups, c_gstride=s.Kg, bias=b, relu=relu,

@@ -129,10 +129,15 @@ def test_quant_fp8_matches_torch(gpu):
     assert sc.slots[0, 1].item() == 0.0
 
 
+FP8_TILES = [0, 11, 16]  # 128x128, and the large tiles of gemm_fp8big.hip
+
+
+@pytest.mark.parametrize("tile", FP8_TILES)
 @pytest.mark.parametrize("M,N,K", [(256, 256, 512), (300, 200, 384), (128, 1000, 4096 + 128)])
-def test_fp8_dense_gemm(gpu, M, N, K):
+def test_fp8_dense_gemm(gpu, M, N, K, tile, monkeypatch):
     """e4m3 x e4m3 -> fp32 on the scaled MFMA: exact products of representable values."""
-    from sparknet_amd.ops import hip
+    from sparknet_amd.ops import gemm as G, hip
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
     aq, af = _f8(torch.randn(M, K, device=gpu) * 8)
     bq, bf = _f8(torch.randn(N, K, device=gpu) * 8)
     da = torch.tensor([0.125], device=gpu)
@@ -143,10 +148,12 @@ def test_fp8_dense_gemm(gpu, M, N, K):
     _close(y, ref, 1e-2)
 
 
+@pytest.mark.parametrize("tile", FP8_TILES)
 @pytest.mark.parametrize("case", [(2, 13, 13, 32, 48, 3, 3, 1, 1, 1), (2, 9, 9, 64, 32, 3, 3, 1, 1, 2),
-                                  (2, 14, 14, 256, 128, 3, 3, 1, 1, 1)])
-def test_fp8_conv_forward(gpu, case):
-    from sparknet_amd.ops import hip
+                                  (2, 14, 14, 256, 128, 3, 3, 1, 1, 1), (3, 20, 20, 128, 320, 3, 3, 1, 1, 1)])
+def test_fp8_conv_forward(gpu, case, tile, monkeypatch):
+    from sparknet_amd.ops import gemm as G, hip
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
     from sparknet_amd.ops.spec import ConvSpec
     import torch.nn.functional as F
     N, H, W, Cc, K, R, S, st, pd, g = case
