@@ -83,7 +83,7 @@ DEFAULTS = {  # model: (batch, channels, src hw, crop, classes, mean, input scal
     # msra-initialised 13-conv stack: unit-scale input keeps the random-init logits finite;
     # BASELINE config 5 sizes the per-GPU batch for the 288 GB of HBM: 512 (38 GB, 7.5k img/s;
     # 1024: 73 GB, 7.8k; 64: 6.5 GB, 6.1k — profiles/r2_vgg16_batch_sweep.txt)
-    "vgg16": (512, 3, 256, 224, 1000, [104.0, 117.0, 123.0], 0.017),
+    "vgg16": (2048, 3, 256, 224, 1000, [104.0, 117.0, 123.0], 0.017),
     "cifar10_quick": (100, 3, 32, 32, 10, [125.0, 123.0, 114.0], 1.0),
     "cifar10_full": (100, 3, 32, 32, 10, [125.0, 123.0, 114.0], 1.0),
 }

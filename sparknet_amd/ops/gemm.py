@@ -454,7 +454,7 @@ def _candidates_fp8(M, N, K, groups, epi, xtra):
         for s2 in dict.fromkeys((s, 1)):
             kc2 = -(-(-(-K // s2)) // 128) * 128
             s2 = max(1, -(-K // kc2))
-            if s2 * M * N * groups * 4 <= (256 << 20):
+            if s2 == 1 or s2 * M * N * groups * 4 <= (256 << 20):  # fp32 slabs only when split
                 out.append((t, s2, kc2))
     return list(dict.fromkeys(out))
 
@@ -518,7 +518,9 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
                     ones, sg, t, s, kc, deq, xtra)
         try:
             run()
-        except RuntimeError:  # a tile this operand combination has no instance for
+        except RuntimeError as e:  # a tile this operand combination has no instance for
+            if _TUNE_LOG:
+                print(f"[gemm-tune] candidate {cand} skipped: {e}", flush=True)
             continue
         runs.append((cand, run))
     # Each candidate is timed over 4 back-to-back launches queued behind a GPU spin (so small
