@@ -417,8 +417,8 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
         tiles.append(18)
         if b_kc_dense and N % 96 == 0:
             tiles.append(17)
-    if epi != EPI_SGD and not b_kc_dense and N >= 64:
-        tiles.append(20)  # 3-stage 128x64 (dense NN: InnerProduct data gradient)
+    if epi != EPI_SGD and N >= 64:
+        tiles.append(20)  # 3-stage 128x64, dense NT / NN only (InnerProduct forward / data gradient)
     if epi != EPI_SGD:
         if _TILE64:
             tiles.append(10)
