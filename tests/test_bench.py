@@ -49,3 +49,21 @@ def test_bench_verify_average_cpu():
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["avg_check"]["masters_equal_across_ranks"] and out["avg_check"]["shadow_is_bf16_master"]
     assert out["comm_backend"] == "gloo" and out["average_buckets"] >= 1
+
+
+def test_bench_under_torchrun_like_the_driver():
+    """The driver's multi-GPU form: `python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...` (ranks
+    from the launcher's env, no self-spawn), here on the gloo CPU path."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", *ARGS],
+                       cwd=ROOT, env=_clean_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints the job line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["config"]["parallelism"] == "dp2"
