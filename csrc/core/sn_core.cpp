@@ -721,6 +721,12 @@ int sn_solver_step(void* s, int iters) {
         iters -= (int)ran;
       } else {
         st.step_failed = true;
+        // a capture that failed after its warmup iterations already advanced the solver
+        PyObject* nr = PyObject_GetAttrString(static_cast<PyObject*>(s), "native_ran");
+        if (nr) iters -= (int)PyLong_AsLong(nr);
+        Py_XDECREF(nr);
+        PyErr_Clear();
+        if (iters <= 0) return 0;
       }
     }
     if (!ns) return status(call(s, "step", "(i)", iters));

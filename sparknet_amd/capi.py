@@ -36,6 +36,7 @@ class CoreState:
         self.test_net: Net | None = None
         self.scores: list[float] = []
         self._callbacks = {}                # (phase, layer index) -> (ctypes fn, user) kept alive
+        self.native_ran = 0                 # iterations a failed native_plan capture had run
 
     # -- construction -------------------------------------------------------------------
     def set_device(self, device: int) -> None:
@@ -145,6 +146,7 @@ class CoreState:
         """-> (iterations already run, plan dict of ints / floats) or raises if the
         state cannot run natively (CPU device, solver features the graph cannot hold)."""
         from .engine import GraphStep
+        self.native_ran = 0
         s = self.solver
         if self.device.type != "cuda" or s is None:
             raise RuntimeError("native stepping needs a GPU solver")
@@ -166,6 +168,11 @@ class CoreState:
         s.stage_hyper()
         try:
             loss = self._graph_step.step()  # warmup iterations + capture + one replay
+        except BaseException:
+            # iterations already run count against the caller's request (sn_core.cpp
+            # subtracts native_ran before falling back to the Python solver)
+            self.native_ran = s.iter - it0
+            raise
         finally:
             for layer, src, _ in feeds:  # the Python verbs (sn_forward, ...) keep their feeds
                 layer.set_source(src)
