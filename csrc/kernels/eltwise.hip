@@ -376,9 +376,7 @@ extern "C" int sn_flip_weights(const bf16_t* w, bf16_t* wt, long long G, long lo
 
 // The same flip for every stride-1 convolution of a net in ONE launch (blockIdx.y =
 // layer), run once at the start of backward: the weights are final for the iteration
-// there, and one launch replaces a launch boundary per layer.  32-bit index decode with
-// multiply-high division; one thread per OUTPUT element (coalesced stores, the scattered
-// 2-B reads of a <= 2 MB weight tensor hit L2).
+// there, and one launch replaces a launch boundary per layer.
 struct FlipDesc {
   const bf16_t* w;
   bf16_t* wt;
@@ -386,21 +384,33 @@ struct FlipDesc {
   FDiv fKg, fS, fR, fCg;
 };
 
-__global__ void flip_weights_multi(const FlipDesc* __restrict__ descs) {
+// For a fixed group g and tap, W[g][k][tap][c] -> Wt[g][c][RS-1-tap][k] is a [Kg x Cg]
+// transpose: one workgroup moves a 64 x 64 tile through LDS so both the reads (along c)
+// and the writes (along k) are coalesced (a per-element gather read 2 B per cache line).
+__global__ void __launch_bounds__(256) flip_weights_multi(const FlipDesc* __restrict__ descs) {
+  __shared__ bf16_t tile[64][66];
   const FlipDesc d = descs[blockIdx.y];
   const int Cg = (int)d.fCg.d, RS = d.R * d.S;
-  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < d.total; o += gridDim.x * blockDim.x) {
-    // o = (((g*Cg + c)*R + rf)*S + sf)*Kg + k
-    uint32_t t = udiv((uint32_t)o, d.fKg);
-    const int k = o - (int)t * d.Kg;
-    uint32_t t2 = udiv(t, d.fS);
-    const int sf = (int)(t - t2 * d.S);
-    t = udiv(t2, d.fR);
-    const int rf = (int)(t2 - t * d.R);
-    t2 = udiv(t, d.fCg);
-    const int c = (int)(t - t2 * Cg), g = (int)t2;
-    const int i = ((g * d.Kg + k) * RS + (d.R - 1 - rf) * d.S + (d.S - 1 - sf)) * Cg + c;
-    d.wt[o] = d.w[i];
+  const int ntk = (d.Kg + 63) >> 6, ntc = (Cg + 63) >> 6;
+  const int per_tap = ntk * ntc;
+  const int G = d.total / (d.Kg * RS * Cg);
+  int b = blockIdx.x;
+  if (b >= G * RS * per_tap) return;  // this descriptor has fewer tiles than the grid
+  const int gt = b / per_tap, tt = b - gt * per_tap;
+  const int g = gt / RS, tap = gt - g * RS;
+  const int k0 = (tt / ntc) * 64, c0 = (tt - (tt / ntc) * ntc) * 64;
+  const int r = threadIdx.x >> 6, x = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = k0 + r + 4 * i, c = c0 + x;
+    if (k < d.Kg && c < Cg) tile[r + 4 * i][x] = d.w[((long long)(g * d.Kg + k) * RS + tap) * Cg + c];
+  }
+  __syncthreads();
+  const int tapf = RS - 1 - tap;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = c0 + r + 4 * i, k = k0 + x;
+    if (k < d.Kg && c < Cg) d.wt[((long long)(g * Cg + c) * RS + tapf) * d.Kg + k] = tile[x][r + 4 * i];
   }
 }
 
@@ -424,9 +434,9 @@ extern "C" int sn_flip_desc(void* out, const bf16_t* w, bf16_t* wt, long long G,
   return 0;
 }
 
-extern "C" int sn_flip_weights_multi(const void* descs, long long n, long long max_total, hipStream_t st) {
-  if (n <= 0) return 0;
-  dim3 grid(sn_blocks(max_total, 256, 4096), (unsigned)n);
+extern "C" int sn_flip_weights_multi(const void* descs, long long n, long long max_tiles, hipStream_t st) {
+  if (n <= 0 || max_tiles <= 0) return 0;
+  dim3 grid((unsigned)max_tiles, (unsigned)n);  // the largest descriptor's 64 x 64 tile count
   hipLaunchKernelGGL(flip_weights_multi, grid, dim3(256), 0, st, reinterpret_cast<const FlipDesc*>(descs));
   return SN_CHECK_LAUNCH();
 }

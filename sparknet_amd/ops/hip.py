@@ -280,13 +280,14 @@ class FlipBatch:
             lib.sn_flip_desc(C.byref(buf, i * size), C.c_void_p(w.data_ptr()), C.c_void_p(wt.data_ptr()),
                              *(C.c_longlong(v) for v in (G, Kg, R, S, Cg)))
         self.descs = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(self.device)
-        self.max_total = max(w.numel() for w, *_ in self.items)
+        # 64 x 64 transpose tiles of the largest descriptor = the launch's grid width
+        self.max_tiles = max(G * R * S * -(-Kg // 64) * -(-Cg // 64) for _, _, G, Kg, R, S, Cg in self.items)
         self.ptrs = self._ptrs()
 
     def run(self) -> None:
         if self._ptrs() != self.ptrs:
             self._build()
-        call("flip_weights_multi", self.descs, len(self.items), self.max_total)
+        call("flip_weights_multi", self.descs, len(self.items), self.max_tiles)
 
 
 def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
