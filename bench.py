@@ -47,6 +47,9 @@ def parse():
                    help="--dtype fp8: only layers with at least this many forward MACs per input element "
                         "run e4m3 (engine.enable_fp8 min_macs_per_input; VGG-16 b512: 0 -> 7.3k, 1000 -> 8.0k, "
                         "bf16 7.6k img/s, profiles/r2_fp8_select_ab.txt)")
+    p.add_argument("--fp8-dgrad", action="store_true",
+                   help="--dtype fp8: also run the data gradients of stride-1 convs as e4m3 products "
+                        "(engine.enable_fp8 dgrad; weight gradients stay bf16)")
     p.add_argument("--overlap-update", action="store_true",
                    help="run large layers' solver updates on a side stream during backward")
     p.add_argument("--no-fuse-fc", action="store_true",
@@ -151,7 +154,7 @@ def main():
                           scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev,
                           group=args.feed_group)
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
-    n_fp8 = enable_fp8(net, args.fp8_min_work) if args.dtype == "fp8" else 0
+    n_fp8 = enable_fp8(net, args.fp8_min_work, dgrad=args.fp8_dgrad) if args.dtype == "fp8" else 0
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph and not args.cpu,
                               overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc,
                               streams=args.streams)
@@ -229,7 +232,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
-                "hipgraph": trainer.use_graph, "streams": args.streams, "feed_group": feeder.group, "fused_input_fold": fused_fold, "fp8_layers": n_fp8,
+                "hipgraph": trainer.use_graph, "streams": args.streams, "feed_group": feeder.group, "fused_input_fold": fused_fold, "fp8_layers": n_fp8, "fp8_dgrad": bool(n_fp8 and args.fp8_dgrad),
                 "final_loss": round(final_loss, 4),
             },
             "rccl_world": comm.world_size if comm is not None else 1,

@@ -4,9 +4,15 @@
 //
 // A scale slot is float[4]: [0] quantisation scale s (x_fp8 = sat(x * s)), [1] amax of the
 // tensors quantised with this slot since the last update (float bits, atomicMax),
-// [2] dequantisation factor 1/s (read by the GEMM epilogue), [3] unused.
+// [2] dequantisation factor 1/s (read by the GEMM epilogue), [3] 1 once a measured amax
+// has been turned into a scale.
 // fp8_update_scales (once per iteration, inside the captured graph) turns the running
 // amax into the next iteration's scale: s = 448 / amax (e4m3 max normal = 448).
+// A slot that has never been updated (the first iteration; or the output gradients of the
+// fp8 data-gradient products, which span orders of magnitude below the unit default
+// scale) is scaled from the CURRENT tensor instead: fp8_init_amax measures its amax first
+// (it returns at once, device-side, for an initialised slot, so a captured graph keeps the
+// launch) and the quantiser derives the scale from it.
 #include "common.h"
 
 namespace {
@@ -20,9 +26,44 @@ SN_DEV uint32_t pack4_fp8(float a, float b, float c, float d) {
   return (uint32_t)w;
 }
 
+SN_DEV void block_amax_to_slot(float amax, float* slot) {
+  // one atomic per block (a per-wave atomic on one address serialises ~30k updates)
+  __shared__ float red[4];
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (amax > 0.f)  // amax >= 0: uint order == float order
+      atomicMax(reinterpret_cast<unsigned int*>(slot + 1), __float_as_uint(amax));
+  }
+}
+
+__global__ void __launch_bounds__(256) fp8_init_amax_kernel(const bf16_t* __restrict__ x, long long n16,
+                                                            float* __restrict__ slot) {
+  if (slot[3] != 0.f) return;  // scale already derived from a measured amax
+  float amax = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x) {
+    float f[16];
+    unpack8(reinterpret_cast<const uint4*>(x)[2 * i], f);
+    unpack8(reinterpret_cast<const uint4*>(x)[2 * i + 1], f + 8);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) amax = fmaxf(amax, fabsf(f[k]));
+  }
+  block_amax_to_slot(amax, slot);
+}
+
 __global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q,
                                                         long long n16, float* __restrict__ slot) {
-  const float sc = slot[0];
+  float sc = slot[0];
+  if (slot[3] == 0.f) {  // uninitialised slot: current scaling from fp8_init_amax's measurement
+    const float am = slot[1];
+    sc = am > 0.f ? E4M3_MAX / am : 1.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // no block reads [0] / [2] in this mode
+      slot[0] = sc;
+      slot[2] = 1.f / sc;
+    }
+  }
   float amax = 0.f;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += (long long)gridDim.x * blockDim.x) {
     const uint4 a = reinterpret_cast<const uint4*>(x)[2 * i];
@@ -42,16 +83,7 @@ __global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict
     o.w = pack4_fp8(f[12], f[13], f[14], f[15]);
     reinterpret_cast<uint4*>(q)[i] = o;
   }
-  // one atomic per block (a per-wave atomic on one address serialises ~30k updates)
-  __shared__ float red[4];
-  amax = wave_max(amax);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (amax > 0.f)  // amax >= 0: uint order == float order
-      atomicMax(reinterpret_cast<unsigned int*>(slot + 1), __float_as_uint(amax));
-  }
+  block_amax_to_slot(amax, slot);
 }
 
 __global__ void fp8_update_scales_kernel(float* __restrict__ slots, int n, float margin) {
@@ -63,6 +95,7 @@ __global__ void fp8_update_scales_kernel(float* __restrict__ slots, int n, float
     const float sc = E4M3_MAX / (amax * margin);
     s[0] = sc;
     s[2] = 1.f / sc;
+    s[3] = 1.f;
   }
   s[1] = 0.f;
 }
@@ -71,6 +104,7 @@ __global__ void fp8_update_scales_kernel(float* __restrict__ slots, int n, float
 
 extern "C" int sn_quant_fp8(const bf16_t* x, uint8_t* q, long long n, float* slot, hipStream_t st) {
   if (n % 16) return 7;
+  hipLaunchKernelGGL(fp8_init_amax_kernel, dim3(sn_blocks(n / 16, 256, 1024)), dim3(256), 0, st, x, n / 16, slot);
   hipLaunchKernelGGL(quant_fp8_kernel, dim3(sn_blocks(n / 16, 256, 1024)), dim3(256), 0, st, x, q, n / 16, slot);
   return SN_CHECK_LAUNCH();
 }

@@ -507,7 +507,14 @@ def fp8_macs_per_input(layer, bottom) -> float:
     return float(layer.N)
 
 
-def enable_fp8(net, min_macs_per_input: float = 1000.0) -> int:
+def fp8_dgrad_macs_per_grad(layer, bottom) -> float:
+    """Data-gradient multiply-adds per output-gradient element of a stride-1 Convolution
+    (the work the e4m3 data gradient halves per element of its dy quantisation pass)."""
+    s = layer.spec(bottom)
+    return float(s.Cg * s.R * s.S)
+
+
+def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False) -> int:
     """Run the forward products of eligible Convolution / InnerProduct layers in OCP e4m3
     (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation) with per-tensor delayed
     scaling: each layer quantises its input and weights with the scale derived from the
@@ -516,21 +523,32 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0) -> int:
     channels are not multiples of 16 (e.g. an RGB input conv) stay bf16, and so do layers
     with fewer than ``min_macs_per_input`` forward MACs per input element (where the
     quantisation pass over a large activation costs more than the faster product saves,
-    e.g. VGG's 64-channel conv1_2).  GPU only; returns the number of fp8 layers."""
+    e.g. VGG's 64-channel conv1_2).
+
+    ``dgrad``: also run the data gradients of stride-1 Convolutions in e4m3 (the output
+    gradient and the flip-transposed weights quantised per tensor; weight gradients stay
+    bf16), for layers with at least ``min_macs_per_input`` data-gradient MACs per output-
+    gradient element (:func:`fp8_dgrad_macs_per_grad`).  GPU only; returns the number of
+    fp8 products (forward + data gradient)."""
     if net.device.type != "cuda":
         return 0
     from .ops import hip
-    chosen = []
+    chosen, chosen_dg = [], []
     for li, layer in enumerate(net.layers):
         if layer.type_name in ("Convolution", "InnerProduct") and len(net.bottom_vecs[li]) == 1:
             b = net.bottom_vecs[li][0]
             if layer.fp8_eligible(b) and fp8_macs_per_input(layer, b) >= min_macs_per_input:
                 chosen.append(layer)
-    sc = hip.Fp8Scales(2 * len(chosen), net.device)
+            if (dgrad and layer.type_name == "Convolution" and layer.fp8_dgrad_eligible(b)
+                    and fp8_dgrad_macs_per_grad(layer, b) >= min_macs_per_input):
+                chosen_dg.append(layer)
+    sc = hip.Fp8Scales(2 * (len(chosen) + len(chosen_dg)), net.device)
     for i, layer in enumerate(chosen):
         layer.fp8_slots = (2 * i, 2 * i + 1)
-    net.ctx.fp8 = sc if chosen else None
-    return len(chosen)
+    for i, layer in enumerate(chosen_dg, start=len(chosen)):
+        layer.fp8_dgrad_slots = (2 * i, 2 * i + 1)
+    net.ctx.fp8 = sc if (chosen or chosen_dg) else None
+    return len(chosen) + len(chosen_dg)
 
 
 def fp8_step(net) -> None:

@@ -109,10 +109,15 @@ class ConvolutionLayer(Layer):
             t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i], folded=folded)
 
     fp8_slots = None  # (x slot, w slot) in ctx.fp8 when the forward product runs in e4m3
+    fp8_dgrad_slots = None  # (dy slot, flipped-w slot) when the data gradient runs in e4m3
 
     def fp8_eligible(self, b) -> bool:
         s = self.spec(b)
         return s.C % 16 == 0 and s.Cg % 16 == 0 and s.dh == 1 and s.dw == 1
+
+    def fp8_dgrad_eligible(self, b) -> bool:
+        from ..ops import hip
+        return hip.fp8_dgrad_ok(self.spec(b))
 
     def _forward_fp8(self, x, w, bias, s):
         """e4m3 forward product (delayed per-tensor scales); backward stays bf16 on the
@@ -137,6 +142,9 @@ class ConvolutionLayer(Layer):
             if self.flipped_weights is not None:  # flipped for the whole net (engine.batch_weight_flips)
                 ws = {} if ws is None else ws
                 ws["wt"] = self.flipped_weights
+            if self.fp8_dgrad_slots is not None and t.diff.is_cuda:  # e4m3 data gradient (engine.enable_fp8)
+                ws = {} if ws is None else ws
+                ws["fp8_dgrad"] = (self.ctx.fp8, *self.fp8_dgrad_slots)
             dw_acc = not (dw is not None and self.grad_overwrite(0))
             db_acc = not (db is not None and self.grad_overwrite(1))
             sink = getattr(self, "slab_grad", None)

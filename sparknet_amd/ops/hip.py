@@ -305,7 +305,7 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
             n1 = min(s.N, n0 + nb)
             _conv_backward(dy[n0:n1], x[n0:n1], w, s.with_batch(n1 - n0), need_dx, dw,
                            db, gate[n0:n1] if gate is not None else None,
-                           {"wt": ws["wt"]} if ws and "wt" in ws else None, dw_acc, db_acc,
+                           {k: ws[k] for k in ("wt", "fp8_dgrad") if k in ws} if ws else None, dw_acc, db_acc,
                            dx_out=dx[n0:n1] if need_dx else None)
             dw_acc = db_acc = True  # later chunks accumulate into the weight gradients
         return dx
@@ -393,8 +393,11 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
         # on CaffeNet; FLIPW stays available via DGRAD_INPLACE_WEIGHTS.
         g2 = ConvGeom(s.N, s.P, s.Q, ldd, s.H, s.W, s.R, s.S, 1, 1, s.R - 1 - s.ph, s.S - 1 - s.pw, 1, 1, s.Kg)
         kr2 = s.R * s.S * s.Kg
-        A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
         pre = ws.get("wt") if ws is not None else None  # flipped once for the net (FlipBatch)
+        f8 = ws.get("fp8_dgrad") if ws is not None else None
+        if f8 is not None and fp8_dgrad_ok(s) and ldd == s.K:
+            return _conv_dgrad_fp8(dy, w, s, g2, kr2, pre, gate, dx, f8)
+        A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
         if DGRAD_INPLACE_WEIGHTS:
             B = FlipW(_c(w), s.Kg, s.R, s.S, s.Cg)
         else:
@@ -427,6 +430,32 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
         if dx_out is not None:
             dx_out.copy_(dx)
             dx = dx_out
+    return dx
+
+
+def fp8_dgrad_ok(s: ConvSpec) -> bool:
+    """Can this conv's data gradient run as an e4m3 product (the flip path with output-
+    gradient channels in whole 16-byte fp8 chunks)?"""
+    return dgrad_uses_flip(s) and s.Kg % 16 == 0 and s.C % 8 == 0
+
+
+def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8):
+    """Data gradient as an e4m3 forward conv of the output gradient with the flip-
+    transposed weights (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation): the output
+    gradient and the flipped weights are quantised per tensor with their own delayed-
+    scaling slots (a slot not yet initialised scales from the current tensor), the
+    epilogue dequantises and applies the ReLU-backward gate, dx stays bf16.  The weight
+    gradient keeps reading the bf16 output gradient."""
+    sc, idy, iwt = f8
+    if wt is None:
+        wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=dy.device)
+        call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
+    dyq = quant_fp8(dy, sc.slot(idy))
+    wtq = quant_fp8(wt, sc.slot(iwt))
+    A = Im2col(dyq, g2, kcontig=True, gstride=s.Kg)
+    B = Dense(wtq.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
+    gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg,
+         gate=_c(gate) if gate is not None else None, deq=(sc.deq(idy), sc.deq(iwt)))
     return dx
 
 

@@ -119,6 +119,7 @@ def test_quant_fp8_matches_torch(gpu):
     x = (torch.randn(64, 48, device=gpu) * 3).to(torch.bfloat16)
     sc = hip.Fp8Scales(1, gpu)
     sc.slots[0, 0] = 20.0
+    sc.slots[0, 3] = 1.0  # an initialised slot: its scale is used as is
     q = hip.quant_fp8(x, sc.slot(0))
     ref, _ = _f8(x.float() * 20.0)
     mism = (q != ref).float().mean().item()
@@ -127,6 +128,30 @@ def test_quant_fp8_matches_torch(gpu):
     sc.update()
     assert abs(sc.slots[0, 0].item() - 448.0 / x.float().abs().max().item()) < 1e-3
     assert sc.slots[0, 1].item() == 0.0
+    assert sc.slots[0, 3].item() == 1.0
+
+
+def test_quant_fp8_uninitialised_slot_uses_current_amax(gpu):
+    """A slot that fp8_update_scales has not initialised yet quantises with the CURRENT
+    tensor's scale (448 / amax), and its dequantisation factor says so — small gradients
+    are not flushed to zero by the unit default scale on the first iteration."""
+    from sparknet_amd.ops import hip
+    x = (torch.randn(4096, 64, device=gpu) * 1e-5).to(torch.bfloat16)
+    sc = hip.Fp8Scales(1, gpu)
+    q = hip.quant_fp8(x, sc.slot(0))
+    amax = x.float().abs().max().item()
+    s = 448.0 / amax
+    assert abs(sc.slots[0, 0].item() / s - 1) < 1e-5 and abs(sc.slots[0, 2].item() * s - 1) < 1e-5
+    ref, _ = _f8(x.float() * s)
+    assert (q != ref).float().mean().item() < 1e-3
+    deq = q.view(torch.float8_e4m3fn).float() * sc.slots[0, 2].item()
+    assert ((deq - x.float()).abs().max() / amax).item() < 0.07
+    # a second quantisation before the update keeps the same scale (image chunks share a slot)
+    sc.slots[0, 0] = 123.0
+    hip.quant_fp8(x, sc.slot(0))
+    assert abs(sc.slots[0, 0].item() / s - 1) < 1e-5
+    sc.update()
+    assert sc.slots[0, 3].item() == 1.0 and abs(sc.slots[0, 0].item() / s - 1) < 1e-3
 
 
 FP8_TILES = [0, 11, 16]  # 128x128, and the large tiles of gemm_fp8big.hip
@@ -165,6 +190,39 @@ def test_fp8_conv_forward(gpu, case, tile, monkeypatch):
     ref = F.conv2d(xf.permute(0, 3, 1, 2), wf.permute(0, 3, 1, 2), stride=st, padding=pd, groups=g) * (0.5 * 0.0625)
     _close(y.permute(0, 3, 1, 2), ref, 1e-2)
 
+
+
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 128, 1, False), (2, 9, 9, 96, 64, 2, True),
+                                  (3, 20, 20, 128, 256, 1, True)])
+def test_fp8_conv_dgrad(gpu, case):
+    """e4m3 data gradient of a stride-1 3x3 conv (ops.hip._conv_dgrad_fp8: quantised output
+    gradient x quantised flip-transposed weights, dequantised + ReLU-gated epilogue) against
+    the fp32 reference; the bf16 path on the same inputs sets the scale of the error."""
+    from sparknet_amd.ops import hip
+    from sparknet_amd.ops.spec import ConvSpec
+    import torch.nn.functional as F
+    N, H, W, Cc, K, g, gated = case
+    s = ConvSpec(N, H, W, Cc, K, 3, 3, 1, 1, 1, 1, 1, 1, g)
+    gen = torch.Generator(device=gpu).manual_seed(3)
+    x = torch.randn(N, H, W, Cc, device=gpu, generator=gen).to(torch.bfloat16)
+    w = (torch.randn(K, 3, 3, Cc // g, device=gpu, generator=gen) * 0.05).to(torch.bfloat16)
+    dy = (torch.randn(N, H, W, K, device=gpu, generator=gen) * 1e-4).to(torch.bfloat16)
+    gate = x if gated else None
+    sc = hip.Fp8Scales(2, gpu)
+    assert hip.fp8_dgrad_ok(s)
+    dx8 = hip.conv_backward(dy, x, w, s, True, ws={"fp8_dgrad": (sc, 0, 1)}, gate=gate)
+    dxb = hip.conv_backward(dy, x, w, s, True, gate=gate)
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1,
+                             groups=g).permute(0, 2, 3, 1)
+    if gated:
+        ref = ref * (x.float() > 0)
+    err8 = ((dx8.float() - ref).norm() / ref.norm()).item()
+    errb = ((dxb.float() - ref).norm() / ref.norm()).item()
+    assert err8 < 0.05, (err8, errb)  # e4m3: 3 mantissa bits on both operands
+    assert errb < 0.01
+    assert sc.slots[0, 2].item() * 448.0 / dy.float().abs().max().item() > 0.99  # current scaling on first use
+    if gated:
+        assert torch.all(dx8[x <= 0] == 0)
 
 
 # --- gemm256_kernel (tiles 6 = 256x256, 7 = 256x128), the 8-wave 2-stage gemm_kernel

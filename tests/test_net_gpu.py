@@ -146,8 +146,10 @@ def test_training_is_bitwise_deterministic(gpu):
     assert torch.equal(a.history[0], b.history[0])
 
 
-def test_fp8_forward_training(gpu):
-    """enable_fp8: e4m3 forward products with delayed scaling track the bf16 net and train."""
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_fp8_forward_training(gpu, dgrad):
+    """enable_fp8: e4m3 forward products (and, with dgrad, e4m3 data gradients of the
+    stride-1 convs) with delayed scaling track the bf16 net and train."""
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.engine import GraphStep, enable_fp8, fuse_relu
     net_p = models.vgg16(train_batch=4, test_batch=4, crop=32, classes=10)
@@ -158,7 +160,12 @@ def test_fp8_forward_training(gpu):
         solver = Solver(sp, device=torch.device("cuda:0"), seed=5, build_test_nets=False)
         fuse_relu(solver.net)
         if mode == "fp8":
-            assert enable_fp8(solver.net, 0.0) >= 14  # 12 of 13 convs (not the RGB input) + 3 IPs
+            n = enable_fp8(solver.net, 0.0, dgrad=dgrad)
+            # 12 of 13 convs (not the RGB input) + 3 IPs; data gradients of the 12 convs
+            # whose output channels fill 16-byte fp8 chunks (conv1_1's dgrad is never needed)
+            assert n >= (14 + 12 if dgrad else 14), n
+            if dgrad:
+                assert sum(getattr(ly, "fp8_dgrad_slots", None) is not None for ly in solver.net.layers) >= 12
         g = torch.Generator().manual_seed(2)
         x = torch.randn(4, 3, 32, 32, generator=g) * 0.5
         y = torch.tensor([[1.0], [3.0], [5.0], [7.0]])
