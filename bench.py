@@ -42,14 +42,17 @@ def parse():
     p.add_argument("--tau", type=int, default=50)
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                   help="fp8: e4m3 forward products with per-tensor delayed scaling (bf16 backward)")
+                   help="fp8: e4m3 forward and data-gradient products with per-tensor delayed scaling (bf16 weight gradients)")
     p.add_argument("--fp8-min-work", type=float, default=1000.0,
                    help="--dtype fp8: only layers with at least this many forward MACs per input element "
                         "run e4m3 (engine.enable_fp8 min_macs_per_input; VGG-16 b512: 0 -> 7.3k, 1000 -> 8.0k, "
                         "bf16 7.6k img/s, profiles/r2_fp8_select_ab.txt)")
-    p.add_argument("--fp8-dgrad", action="store_true",
-                   help="--dtype fp8: also run the data gradients of stride-1 convs as e4m3 products "
-                        "(engine.enable_fp8 dgrad; weight gradients stay bf16)")
+    p.add_argument("--no-fp8-dgrad", dest="fp8_dgrad", action="store_false",
+                   help="--dtype fp8: keep the data gradients in bf16 (default: the data gradients of stride-1 "
+                        "convs run as fp8 products too, engine.enable_fp8 dgrad; weight gradients stay bf16; "
+                        "VGG-16 b2048 8.82k vs 8.47k img/s, profiles/r3_fp8_dgrad.txt)")
+    p.add_argument("--fp8-dgrad-format", default="e4m3", choices=["e4m3", "e5m2"],
+                   help="fp8 data gradients: format of the quantised output gradients")
     p.add_argument("--overlap-update", action="store_true",
                    help="run large layers' solver updates on a side stream during backward")
     p.add_argument("--no-fuse-fc", action="store_true",
@@ -154,7 +157,7 @@ def main():
                           scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev,
                           group=args.feed_group)
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
-    n_fp8 = enable_fp8(net, args.fp8_min_work, dgrad=args.fp8_dgrad) if args.dtype == "fp8" else 0
+    n_fp8 = enable_fp8(net, args.fp8_min_work, dgrad=args.fp8_dgrad, dgrad_format=args.fp8_dgrad_format) if args.dtype == "fp8" else 0
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph and not args.cpu,
                               overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc,
                               streams=args.streams)
@@ -232,7 +235,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
-                "hipgraph": trainer.use_graph, "streams": args.streams, "feed_group": feeder.group, "fused_input_fold": fused_fold, "fp8_layers": n_fp8, "fp8_dgrad": bool(n_fp8 and args.fp8_dgrad),
+                "hipgraph": trainer.use_graph, "streams": args.streams, "feed_group": feeder.group, "fused_input_fold": fused_fold, "fp8_layers": n_fp8, "fp8_dgrad": (args.fp8_dgrad_format if n_fp8 and args.fp8_dgrad else None),
                 "final_loss": round(final_loss, 4),
             },
             "rccl_world": comm.world_size if comm is not None else 1,

@@ -2,12 +2,14 @@
 // (VGG-16 fp8 configuration, SURVEY §7.6-3: fp32 masters, fp32 accumulation, per-tensor
 // scales from an amax history).
 //
-// A scale slot is float[4]: [0] quantisation scale s (x_fp8 = sat(x * s)), [1] amax of the
+// A scale slot is float[8]: [0] quantisation scale s (x_fp8 = sat(x * s)), [1] amax of the
 // tensors quantised with this slot since the last update (float bits, atomicMax),
 // [2] dequantisation factor 1/s (read by the GEMM epilogue), [3] 1 once a measured amax
-// has been turned into a scale.
+// has been turned into a scale, [4] the format's largest normal (e4m3 448, e5m2 57344).
 // fp8_update_scales (once per iteration, inside the captured graph) turns the running
-// amax into the next iteration's scale: s = 448 / amax (e4m3 max normal = 448).
+// amax into the next iteration's scale: s = max / amax.  e4m3 (3 mantissa bits) carries
+// activations and weights; e5m2 (2 mantissa bits, 2^32 of range) is the option for the
+// output gradients of the fp8 data-gradient products.
 // A slot that has never been updated (the first iteration; or the output gradients of the
 // fp8 data-gradient products, which span orders of magnitude below the unit default
 // scale) is scaled from the CURRENT tensor instead: fp8_init_amax measures its amax first
@@ -17,12 +19,19 @@
 
 namespace {
 
-constexpr float E4M3_MAX = 448.f;
+constexpr float E4M3_MAX = 448.f, E5M2_MAX = 57344.f;
+constexpr int SLOT = 8;  // floats per scale slot
 
+template <int E5M2>
 SN_DEV uint32_t pack4_fp8(float a, float b, float c, float d) {
   int w = 0;
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  if (E5M2) {
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, w, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+  } else {
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  }
   return (uint32_t)w;
 }
 
@@ -53,12 +62,14 @@ __global__ void __launch_bounds__(256) fp8_init_amax_kernel(const bf16_t* __rest
   block_amax_to_slot(amax, slot);
 }
 
+template <int E5M2>
 __global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q,
                                                         long long n16, float* __restrict__ slot) {
+  constexpr float FMAX = E5M2 ? E5M2_MAX : E4M3_MAX;
   float sc = slot[0];
   if (slot[3] == 0.f) {  // uninitialised slot: current scaling from fp8_init_amax's measurement
     const float am = slot[1];
-    sc = am > 0.f ? E4M3_MAX / am : 1.f;
+    sc = am > 0.f ? FMAX / am : 1.f;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // no block reads [0] / [2] in this mode
       slot[0] = sc;
       slot[2] = 1.f / sc;
@@ -74,13 +85,13 @@ __global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       amax = fmaxf(amax, fabsf(f[k]));
-      f[k] = fminf(fmaxf(f[k] * sc, -E4M3_MAX), E4M3_MAX);
+      f[k] = fminf(fmaxf(f[k] * sc, -FMAX), FMAX);
     }
     uint4 o;
-    o.x = pack4_fp8(f[0], f[1], f[2], f[3]);
-    o.y = pack4_fp8(f[4], f[5], f[6], f[7]);
-    o.z = pack4_fp8(f[8], f[9], f[10], f[11]);
-    o.w = pack4_fp8(f[12], f[13], f[14], f[15]);
+    o.x = pack4_fp8<E5M2>(f[0], f[1], f[2], f[3]);
+    o.y = pack4_fp8<E5M2>(f[4], f[5], f[6], f[7]);
+    o.z = pack4_fp8<E5M2>(f[8], f[9], f[10], f[11]);
+    o.w = pack4_fp8<E5M2>(f[12], f[13], f[14], f[15]);
     reinterpret_cast<uint4*>(q)[i] = o;
   }
   block_amax_to_slot(amax, slot);
@@ -89,10 +100,10 @@ __global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict
 __global__ void fp8_update_scales_kernel(float* __restrict__ slots, int n, float margin) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float* s = slots + 4 * i;
+  float* s = slots + SLOT * i;
   const float amax = s[1];
   if (amax > 0.f) {
-    const float sc = E4M3_MAX / (amax * margin);
+    const float sc = (s[4] > 0.f ? s[4] : E4M3_MAX) / (amax * margin);
     s[0] = sc;
     s[2] = 1.f / sc;
     s[3] = 1.f;
@@ -102,10 +113,15 @@ __global__ void fp8_update_scales_kernel(float* __restrict__ slots, int n, float
 
 }  // namespace
 
-extern "C" int sn_quant_fp8(const bf16_t* x, uint8_t* q, long long n, float* slot, hipStream_t st) {
+extern "C" int sn_fp8_slot_floats() { return SLOT; }
+
+extern "C" int sn_quant_fp8(const bf16_t* x, uint8_t* q, long long n, float* slot, int e5m2, hipStream_t st) {
   if (n % 16) return 7;
   hipLaunchKernelGGL(fp8_init_amax_kernel, dim3(sn_blocks(n / 16, 256, 1024)), dim3(256), 0, st, x, n / 16, slot);
-  hipLaunchKernelGGL(quant_fp8_kernel, dim3(sn_blocks(n / 16, 256, 1024)), dim3(256), 0, st, x, q, n / 16, slot);
+  if (e5m2)
+    hipLaunchKernelGGL(quant_fp8_kernel<1>, dim3(sn_blocks(n / 16, 256, 1024)), dim3(256), 0, st, x, q, n / 16, slot);
+  else
+    hipLaunchKernelGGL(quant_fp8_kernel<0>, dim3(sn_blocks(n / 16, 256, 1024)), dim3(256), 0, st, x, q, n / 16, slot);
   return SN_CHECK_LAUNCH();
 }
 

@@ -64,19 +64,19 @@ int launch_tile48(const SnGemmArgs& a, hipStream_t stream) {
   return 4;
 }
 
-template <int AMODE>
+template <int AMODE, int FMT>
 int launch_fp8(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_BF16, 128, 128, 4, 2, true>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_BF16, 128, 128, 4, 2, FMT>), grid, dim3(256), 0, st, a);
       break;
     case EPI_BF16_DROP:
-      if (AMODE != OP_DENSE) return 4;
-      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, 128, 128, 4, 2, true>), grid, dim3(256), 0,
+      if (AMODE != OP_DENSE || FMT != 1) return 4;
+      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, 128, 128, 4, 2, 1>), grid, dim3(256), 0,
                          st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_F32, 128, 128, 4, 2, true>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_F32, 128, 128, 4, 2, FMT>), grid, dim3(256), 0, st, a);
       break;
     default:
       return 2;
@@ -101,7 +101,10 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     if (a.tile == 11 || a.tile == 16) return sn_gemm_fp8_big(a, stream);  // gemm_fp8big.hip
     const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     dim3 grid(tiles * a.splits * a.groups);
-    return a.a_mode == OP_IM2COL ? launch_fp8<OP_IM2COL>(a, grid, stream) : launch_fp8<OP_DENSE>(a, grid, stream);
+    if (a.fp8 == 2)  // e5m2 output gradients: the fp8 data-gradient products (implicit im2col A)
+      return a.a_mode == OP_IM2COL ? launch_fp8<OP_IM2COL, 2>(a, grid, stream) : 4;
+    if (a.fp8 != 1) return 4;
+    return a.a_mode == OP_IM2COL ? launch_fp8<OP_IM2COL, 1>(a, grid, stream) : launch_fp8<OP_DENSE, 1>(a, grid, stream);
   }
   if (a.kchunk <= 0 || (a.kchunk % BK) != 0) return 3;
   switch (a.tile) {

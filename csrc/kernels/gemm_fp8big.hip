@@ -7,17 +7,17 @@
 
 namespace {
 
-template <int AMODE, int BM, int BN, int NW, int NFR, int MFR>
+template <int AMODE, int BM, int BN, int NW, int NFR, int MFR, int FMT>
 int launch_fp8_big(const SnGemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles * a.splits * a.groups);
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_BF16, BM, BN, NW, 2, true, NFR, MFR>), grid,
+      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_BF16, BM, BN, NW, 2, FMT, NFR, MFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_F32, BM, BN, NW, 2, true, NFR, MFR>), grid,
+      hipLaunchKernelGGL((gemm_kernel<0, AMODE, 0, OP_DENSE, EPI_F32, BM, BN, NW, 2, FMT, NFR, MFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     default:
@@ -30,13 +30,22 @@ int launch_fp8_big(const SnGemmArgs& a, hipStream_t st) {
 
 int sn_gemm_fp8_big(const SnGemmArgs& a, hipStream_t stream) {
   const bool im2col = a.a_mode == OP_IM2COL;
+  if (a.fp8 == 2) {  // e5m2 A (output gradients of the fp8 data-gradient products): implicit im2col only
+    if (!im2col) return 4;
+    switch (a.tile) {
+      case 11: return launch_fp8_big<OP_IM2COL, 256, 256, 8, 4, 8, 2>(a, stream);
+      case 16: return launch_fp8_big<OP_IM2COL, 192, 128, 4, 4, 6, 2>(a, stream);
+      default: return 4;
+    }
+  }
+  if (a.fp8 != 1) return 4;
   switch (a.tile) {
     case 11:
-      return im2col ? launch_fp8_big<OP_IM2COL, 256, 256, 8, 4, 8>(a, stream)
-                    : launch_fp8_big<OP_DENSE, 256, 256, 8, 4, 8>(a, stream);
+      return im2col ? launch_fp8_big<OP_IM2COL, 256, 256, 8, 4, 8, 1>(a, stream)
+                    : launch_fp8_big<OP_DENSE, 256, 256, 8, 4, 8, 1>(a, stream);
     case 16:
-      return im2col ? launch_fp8_big<OP_IM2COL, 192, 128, 4, 4, 6>(a, stream)
-                    : launch_fp8_big<OP_DENSE, 192, 128, 4, 4, 6>(a, stream);
+      return im2col ? launch_fp8_big<OP_IM2COL, 192, 128, 4, 4, 6, 1>(a, stream)
+                    : launch_fp8_big<OP_DENSE, 192, 128, 4, 4, 6, 1>(a, stream);
     default:
       return 4;
   }

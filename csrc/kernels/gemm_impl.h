@@ -54,7 +54,8 @@ struct SnGemmArgs {
                       // 10: 128x64 (4 waves, 3 blocks / CU); 11: 256x256, 12 / 13: 256x128, 14: 256x192
                       // (gemm_kernel, 8 waves, 2 stages, one block per CU)
   const bf16_t* gate; // EPI_BF16: zero outputs where gate (same layout as C) <= 0 (fused ReLU backward)
-  int fp8;            // operands are e4m3 bytes (K-contiguous only); k counts fp8 elements
+  int fp8;            // operands are fp8 bytes (K-contiguous only; k counts fp8 elements): 1 = e4m3 x e4m3,
+                      // 2 = A e5m2 (bf8: output gradients of the fp8 data-gradient products) x B e4m3
   const float* deq_a; // fp8: dequantisation factors (1 / quantisation scale) of A and B, device scalars
   const float* deq_b;
   int raster_n;       // N-fastest tile order (see gemm_kernel)
@@ -694,11 +695,14 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
   }
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, bool FP8 = false,
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, int FP8 = 0,
           int NFR = 4, int MFR = 4>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) gemm_kernel(SnGemmArgs args) {
   // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
   constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
+  // MFMA operand formats: src A of the instruction is our B fragment (cbsz), src B our A
+  // fragment (blgp); 0 = e4m3, 1 = e5m2
+  constexpr int FMT_A = FP8 == 2 ? 1 : 0;
   // B's LDS image holds BNL >= BN rows: whole wave-instructions per wave (a 48-wide tile
   // stages 64 rows, the 16 beyond the tile read the zero page)
   constexpr int BNL = ((BN / 8) % NW == 0) ? BN : (BN + 63) / 64 * 64;
@@ -773,7 +777,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
         const i32x8 fa = read_frag8(la, wm0 + 16 * j, lane);
 #pragma unroll
         for (int i = 0; i < NFR; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa, acc[i][j], 0, 0, 0, 127, 0, 127);
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa, acc[i][j], 0, FMT_A, 0, 127, 0, 127);
       }
       __builtin_amdgcn_s_setprio(0);
       return;
@@ -787,8 +791,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
 #pragma unroll
       for (int i = 0; i < NFR; ++i)
 #pragma unroll
-        for (int j = 0; j < MFR; ++j)  // formats 0/0 = e4m3 x e4m3, block scales 2^0 (E8M0 127)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa8[j], acc[i][j], 0, 0, 0, 127, 0,
+        for (int j = 0; j < MFR; ++j)  // formats e4m3 (B) x e4m3 / e5m2 (A), block scales 2^0 (E8M0 127)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa8[j], acc[i][j], 0, FMT_A, 0, 127, 0,
                                                                         127);
       __builtin_amdgcn_s_setprio(0);
       return;
@@ -1019,7 +1023,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
         for (int i = 0; i < NFR; ++i) {
           const int nl = wn0 + 16 * i + ncol_l, n = n_blk + nl;
           float o[4] = {0.f, 0.f, 0.f, 0.f};
-          if (m < args.M && n < args.N) epi_bf16_math<EPI, FP8>(args, grp, m, n, acc[i][j], args.N, o);
+          if (m < args.M && n < args.N) epi_bf16_math<EPI, (FP8 != 0)>(args, grp, m, n, acc[i][j], args.N, o);
           *reinterpret_cast<uint2*>(wbuf + (lr % HALF) * PITCH + nl * 2) =
               make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
         }
@@ -1053,7 +1057,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     for (int i = 0; i < NFR; ++i) {
       const int n = n_blk + wn0 + 16 * i + ncol_l;
       if (n >= args.N) continue;
-      epi_store<EPI, FP8>(args, grp, split, m, n, acc[i][j], c_cols);
+      epi_store<EPI, (FP8 != 0)>(args, grp, split, m, n, acc[i][j], c_cols);
     }
   }
 }

@@ -514,7 +514,7 @@ def fp8_dgrad_macs_per_grad(layer, bottom) -> float:
     return float(s.Cg * s.R * s.S)
 
 
-def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False) -> int:
+def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgrad_format: str = "e4m3") -> int:
     """Run the forward products of eligible Convolution / InnerProduct layers in OCP e4m3
     (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation) with per-tensor delayed
     scaling: each layer quantises its input and weights with the scale derived from the
@@ -528,8 +528,9 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False) -> 
     ``dgrad``: also run the data gradients of stride-1 Convolutions in e4m3 (the output
     gradient and the flip-transposed weights quantised per tensor; weight gradients stay
     bf16), for layers with at least ``min_macs_per_input`` data-gradient MACs per output-
-    gradient element (:func:`fp8_dgrad_macs_per_grad`).  GPU only; returns the number of
-    fp8 products (forward + data gradient)."""
+    gradient element (:func:`fp8_dgrad_macs_per_grad`); ``dgrad_format`` "e5m2" quantises
+    the output gradients to e5m2 (2 mantissa bits, 2^32 of range) instead of e4m3.  GPU
+    only; returns the number of fp8 products (forward + data gradient)."""
     if net.device.type != "cuda":
         return 0
     from .ops import hip
@@ -545,8 +546,11 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False) -> 
     sc = hip.Fp8Scales(2 * (len(chosen) + len(chosen_dg)), net.device)
     for i, layer in enumerate(chosen):
         layer.fp8_slots = (2 * i, 2 * i + 1)
+    assert dgrad_format in ("e4m3", "e5m2"), dgrad_format
     for i, layer in enumerate(chosen_dg, start=len(chosen)):
         layer.fp8_dgrad_slots = (2 * i, 2 * i + 1)
+        if dgrad_format == "e5m2":
+            sc.set_e5m2(2 * i)
     net.ctx.fp8 = sc if (chosen or chosen_dg) else None
     return len(chosen) + len(chosen_dg)
 

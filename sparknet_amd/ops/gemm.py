@@ -204,7 +204,9 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
         splits = 1
         sg = (sgd["w"].data_ptr(), sgd["h"].data_ptr(), sgd["shadow"].data_ptr(), sgd["hyper"].data_ptr(),
               float(sgd["lr_mult"]), float(sgd["decay_mult"]), int(sgd["flags"]))
-    fp8 = deq is not None  # e4m3 operands; deq = (1/scale_A, 1/scale_B) device scalars
+    # fp8 operands; deq = (1/scale_A, 1/scale_B[, format]) device scalars, format 1 = e4m3 x e4m3
+    # (default), 2 = e5m2 A x e4m3 B (SnGemmArgs.fp8)
+    fp8 = deq is not None
     sa, a_mc, a_mode = _operand(A, fp8)
     sb, b_mc, b_mode = _operand(B, fp8)
     ones = -1
@@ -268,6 +270,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     bk = 128 if fp8 else BK
     splits = max(1, -(-K // kchunk))
     dq = (deq[0].data_ptr(), deq[1].data_ptr()) if fp8 else (0, 0)
+    f8 = (deq[2] if len(deq) > 2 else 1) if fp8 else 0
     bm, bn = TILES[tile]
     tm_, tn_ = -(-M // bm), -(-N // bn)
     raster = int(_RASTER_N if _RASTER_N >= 0 else (1 < tn_ <= 8 and tm_ >= 8 * tn_))
@@ -279,7 +282,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
                   and out.data_ptr() % 16 == 0)
         args = _lib.SnGemmArgs(M, N, K, groups, 1, max(kchunk, bk), a_mc, a_mode, b_mc, b_mode, e,
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
-                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, int(fp8), *dq, raster,
+                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, f8, *dq, raster,
                                ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), lds)
         args.addr_legacy = _ADDR_LEGACY
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
@@ -293,7 +296,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     ws = (sink.slab(groups * splits * M * ldw, out.device).view(groups, splits, M, ldw) if deferred
           else torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device))
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
-                           sa, sb, ws.data_ptr(), ldw, splits * M * ldw, M * ldw, 0, 0, tile, 0, int(fp8), *dq, raster,
+                           sa, sb, ws.data_ptr(), ldw, splits * M * ldw, M * ldw, 0, 0, tile, 0, f8, *dq, raster,
                            ones, 0, 0, *sg, *_drop_fields(_NO_XTRA))
     args.addr_legacy = _ADDR_LEGACY
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
@@ -487,7 +490,7 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     b_kc_dense = b_mc == 0 and b_mode == OP_DENSE
     fp8 = deq is not None
     key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None, bool(xtra[0]),
-           _geom_key(sa), _geom_key(sb)) + (("fp8",) if fp8 else ()) + (out.dtype,)
+           _geom_key(sa), _geom_key(sb)) + ((("fp8",) if len(deq) < 3 or deq[2] == 1 else ("fp8", deq[2])) if fp8 else ()) + (out.dtype,)
     hit = _TUNED.get(key)
     if hit is not None:
         return hit

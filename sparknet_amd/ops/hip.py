@@ -442,7 +442,8 @@ def fp8_dgrad_ok(s: ConvSpec) -> bool:
 def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8):
     """Data gradient as an e4m3 forward conv of the output gradient with the flip-
     transposed weights (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation): the output
-    gradient and the flipped weights are quantised per tensor with their own delayed-
+    gradient (e4m3, or e5m2 when its slot says so) and the flipped weights are quantised
+    per tensor with their own delayed-
     scaling slots (a slot not yet initialised scales from the current tensor), the
     epilogue dequantises and applies the ReLU-backward gate, dx stays bf16.  The weight
     gradient keeps reading the bf16 output gradient."""
@@ -450,12 +451,13 @@ def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8):
     if wt is None:
         wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=dy.device)
         call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
-    dyq = quant_fp8(dy, sc.slot(idy))
+    e5 = sc.is_e5m2(idy)
+    dyq = quant_fp8(dy, sc.slot(idy), e5m2=e5)
     wtq = quant_fp8(wt, sc.slot(iwt))
     A = Im2col(dyq, g2, kcontig=True, gstride=s.Kg)
     B = Dense(wtq.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
     gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg,
-         gate=_c(gate) if gate is not None else None, deq=(sc.deq(idy), sc.deq(iwt)))
+         gate=_c(gate) if gate is not None else None, deq=(sc.deq(idy), sc.deq(iwt), 2 if e5 else 1))
     return dx
 
 
@@ -845,14 +847,27 @@ def augment(src_u8, dst, crop, mean=None, mean_mode=0, scale=1.0, rng_state=None
 FP8_MARGIN = 1.0  # quantisation scale = 448 / (amax * margin)
 
 
+E4M3_MAX, E5M2_MAX = 448.0, 57344.0
+
+
 class Fp8Scales:
-    """Device-resident scale slots (csrc/kernels/fp8.hip): [n][scale, amax, 1/scale, -]."""
+    """Device-resident scale slots (csrc/kernels/fp8.hip): [n][scale, amax, 1/scale,
+    initialised, format max, -, -, -].  Slots are e4m3 unless :meth:`set_e5m2` is called."""
 
     def __init__(self, n: int, device):
-        self.slots = torch.zeros((max(n, 1), 4), dtype=torch.float32, device=device)
+        self.slots = torch.zeros((max(n, 1), 8), dtype=torch.float32, device=device)
         self.slots[:, 0] = 1.0
         self.slots[:, 2] = 1.0
+        self.slots[:, 4] = E4M3_MAX
         self.n = n
+        self._e5m2 = set()
+
+    def set_e5m2(self, i: int) -> None:
+        self.slots[i, 4] = E5M2_MAX
+        self._e5m2.add(i)
+
+    def is_e5m2(self, i: int) -> bool:
+        return i in self._e5m2
 
     def slot(self, i: int) -> torch.Tensor:
         return self.slots[i]
@@ -864,11 +879,13 @@ class Fp8Scales:
         call("fp8_update_scales", self.slots, self.n, float(FP8_MARGIN))
 
 
-def quant_fp8(x: torch.Tensor, slot: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """e4m3 bytes of bf16 ``x`` scaled by slot[0]; folds |x|max into slot[1]."""
+def quant_fp8(x: torch.Tensor, slot: torch.Tensor, out: torch.Tensor | None = None,
+              e5m2: bool = False) -> torch.Tensor:
+    """e4m3 (or e5m2) bytes of bf16 ``x`` scaled by slot[0]; folds |x|max into slot[1]
+    (an uninitialised slot is scaled from the current tensor, see csrc/kernels/fp8.hip)."""
     x = _c(x)
     q = torch.empty(x.shape, dtype=torch.uint8, device=x.device) if out is None else out
-    call("quant_fp8", x, q, x.numel(), slot)
+    call("quant_fp8", x, q, x.numel(), slot, bool(e5m2))
     return q
 
 

@@ -192,14 +192,16 @@ def test_fp8_conv_forward(gpu, case, tile, monkeypatch):
 
 
 
+@pytest.mark.parametrize("fmt,tile", [("e4m3", -1), ("e5m2", 0), ("e5m2", 11), ("e5m2", 16)])
 @pytest.mark.parametrize("case", [(2, 14, 14, 64, 128, 1, False), (2, 9, 9, 96, 64, 2, True),
                                   (3, 20, 20, 128, 256, 1, True)])
-def test_fp8_conv_dgrad(gpu, case):
-    """e4m3 data gradient of a stride-1 3x3 conv (ops.hip._conv_dgrad_fp8: quantised output
-    gradient x quantised flip-transposed weights, dequantised + ReLU-gated epilogue) against
+def test_fp8_conv_dgrad(gpu, case, fmt, tile, monkeypatch):
+    """fp8 data gradient of a stride-1 3x3 conv (ops.hip._conv_dgrad_fp8: e4m3 / e5m2 output
+    gradient x e4m3 flip-transposed weights, dequantised + ReLU-gated epilogue) against
     the fp32 reference; the bf16 path on the same inputs sets the scale of the error."""
-    from sparknet_amd.ops import hip
+    from sparknet_amd.ops import gemm as G, hip
     from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
     import torch.nn.functional as F
     N, H, W, Cc, K, g, gated = case
     s = ConvSpec(N, H, W, Cc, K, 3, 3, 1, 1, 1, 1, 1, 1, g)
@@ -209,6 +211,8 @@ def test_fp8_conv_dgrad(gpu, case):
     dy = (torch.randn(N, H, W, K, device=gpu, generator=gen) * 1e-4).to(torch.bfloat16)
     gate = x if gated else None
     sc = hip.Fp8Scales(2, gpu)
+    if fmt == "e5m2":
+        sc.set_e5m2(0)
     assert hip.fp8_dgrad_ok(s)
     dx8 = hip.conv_backward(dy, x, w, s, True, ws={"fp8_dgrad": (sc, 0, 1)}, gate=gate)
     dxb = hip.conv_backward(dy, x, w, s, True, gate=gate)
@@ -218,9 +222,11 @@ def test_fp8_conv_dgrad(gpu, case):
         ref = ref * (x.float() > 0)
     err8 = ((dx8.float() - ref).norm() / ref.norm()).item()
     errb = ((dxb.float() - ref).norm() / ref.norm()).item()
-    assert err8 < 0.05, (err8, errb)  # e4m3: 3 mantissa bits on both operands
+    # e4m3: 3 mantissa bits on both operands; e5m2 gradients: 2 bits (rms rounding ~3.6 %)
+    assert err8 < (0.05 if fmt == "e4m3" else 0.08), (err8, errb)
     assert errb < 0.01
-    assert sc.slots[0, 2].item() * 448.0 / dy.float().abs().max().item() > 0.99  # current scaling on first use
+    fmax = 448.0 if fmt == "e4m3" else 57344.0
+    assert abs(sc.slots[0, 2].item() * fmax / dy.float().abs().max().item() - 1) < 1e-3  # current scaling on first use
     if gated:
         assert torch.all(dx8[x <= 0] == 0)
 

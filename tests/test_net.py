@@ -396,3 +396,24 @@ def test_fp8_macs_per_input_cost_model():
     assert got["conv2"] == 128 * 5 * 5  # group 2: 128 outputs per input channel
     assert got["conv3"] == 384 * 9
     assert got["fc6"] == 4096 and got["fc8"] == 1000
+
+
+def test_fp8_dgrad_cost_model_and_eligibility():
+    """engine.fp8_dgrad_macs_per_grad (data-gradient MACs per output-gradient element, the
+    work an fp8 data gradient halves per element of its dy quantisation pass) and the
+    shapes ops.hip.fp8_dgrad_ok accepts: stride-1 implicit convs whose output channels per
+    group fill 16-byte fp8 chunks (CaffeNet conv1 is strided, conv2 has 128 per group)."""
+    from sparknet_amd import models
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.engine import fp8_dgrad_macs_per_grad
+    solver = Solver(models.solver_for("caffenet", train_batch=2, test_batch=2), build_test_nets=False)
+    net = solver.net
+    got, ok = {}, {}
+    for li, layer in enumerate(net.layers):
+        if layer.type_name == "Convolution":
+            b = net.bottom_vecs[li][0]
+            got[layer.name] = fp8_dgrad_macs_per_grad(layer, b)
+            ok[layer.name] = layer.fp8_dgrad_eligible(b)
+    assert got["conv2"] == 48 * 5 * 5 and got["conv3"] == 256 * 9 and got["conv4"] == 192 * 9
+    assert not ok["conv1"]  # 11x11 stride 4: the data gradient is not a stride-1 forward conv
+    assert ok["conv2"] and ok["conv3"] and ok["conv4"] and ok["conv5"]
