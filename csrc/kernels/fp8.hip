@@ -111,9 +111,22 @@ __global__ void fp8_update_scales_kernel(float* __restrict__ slots, int n, float
   s[1] = 0.f;
 }
 
+// fold the GEMM side output's block |max| partials (SnGemmArgs.q_part: 256 floats 128 B
+// apart) into the slot's running amax and clear them for the next iteration
+__global__ void __launch_bounds__(256) fp8_fold_amax_kernel(float* __restrict__ part, float* __restrict__ slot) {
+  float v = part[threadIdx.x * 32];
+  part[threadIdx.x * 32] = 0.f;
+  block_amax_to_slot(v, slot);
+}
+
 }  // namespace
 
 extern "C" int sn_fp8_slot_floats() { return SLOT; }
+
+extern "C" int sn_fp8_fold_amax(float* part, float* slot, hipStream_t st) {
+  hipLaunchKernelGGL(fp8_fold_amax_kernel, dim3(1), dim3(256), 0, st, part, slot);
+  return SN_CHECK_LAUNCH();
+}
 
 extern "C" int sn_quant_fp8(const bf16_t* x, uint8_t* q, long long n, float* slot, int e5m2, hipStream_t st) {
   if (n % 16) return 7;

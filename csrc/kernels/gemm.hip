@@ -94,6 +94,12 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   if (a.ones_col >= 0 && (!a.b_mc || a.b_mode == OP_FLIPW || (a.ones_col & 7) || a.ones_col >= a.N || a.fp8))
     return 5;
   if (a.bias_out && (a.ones_col < 0 || a.epi == EPI_BF16 || a.epi == EPI_BF16_DROP)) return 5;
+  // fused fp8 side output: unsplit bf16 epilogues of gemm_kernel (not gemm256_kernel, tiles
+  // 6-9), whole 8-byte chunks
+  if (a.q_out && (a.splits != 1 || (a.epi != EPI_BF16 && a.epi != EPI_BF16_DROP) || (a.tile >= 6 && a.tile <= 9) ||
+                  (a.N % 8) || (a.q_ld % 8) || (a.q_gstride % 8) || !a.q_slot || !a.q_part ||
+                  (reinterpret_cast<unsigned long long>(a.q_out) & 7)))
+    return 6;
   if (a.fp8) {
     // e4m3 forward products: A (dense or implicit im2col) and B dense, both K-contiguous
     if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || a.a_mc || a.b_mc || a.b_mode != OP_DENSE || !a.deq_a || !a.deq_b)

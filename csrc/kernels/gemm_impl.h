@@ -92,6 +92,20 @@ struct SnGemmArgs {
   // stages and store it as whole 16-B row chunks (host: ldc % 8 == 0, 16-B aligned C)
   int lds_store;
   int addr_legacy;  // 1: general per-lane address decode only (A/B probe of the fast DMA paths)
+  // bf16 epilogues of gemm_kernel, unsplit: also store the finished (bf16-rounded) output as
+  // fp8 bytes q_out[grp * q_gstride + m * q_ld + n] = sat(v * q_slot[0]) and fold its |max|
+  // into q_slot[1] — the quantisation pass of the fp8 product that consumes this output
+  // (the next conv's e4m3 input, or the next lower conv's output gradient) fused into its
+  // producer (engine.fuse_fp8_quant).  q_slot is an initialised delayed-scaling slot
+  // (csrc/kernels/fp8.hip), so the bytes equal what the separate pass would write.
+  unsigned char* q_out;
+  long long q_ld, q_gstride;
+  float* q_slot;
+  int q_e5m2;
+  // block |max| partials: one atomicMax per block on q_part[(block & 255) * 32] (128-B apart;
+  // a single address serialises ~10^5 block atomics), folded into q_slot[1] afterwards by
+  // sn_fp8_fold_amax
+  float* q_part;
 };
 
 }  // extern "C"
@@ -549,6 +563,44 @@ SN_DEV i32x8 read_frag8(const char* lds, int x0, int lane) {
   return r;
 }
 
+// fused fp8 side output (SnGemmArgs.q_out): 4 bf16-rounded values -> 4 fp8 bytes
+SN_DEV uint32_t q_pack4(const SnGemmArgs& args, float sc, const float* v, float& qmax) {
+  const float fmax = args.q_e5m2 ? 57344.f : 448.f;
+  float f[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float b = bf2f(f2bf(v[r]));  // the bf16 value the separate pass would read
+    qmax = fmaxf(qmax, fabsf(b));
+    f[r] = fminf(fmaxf(b * sc, -fmax), fmax);
+  }
+  int w = 0;
+  if (args.q_e5m2) {
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], w, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], w, true);
+  } else {
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
+  }
+  return (uint32_t)w;
+}
+
+// block |max| of the fp8 side output -> one atomicMax on q_slot[1] (every thread calls it).
+// The 32-B scratch is the start of an idle LDS stage, NOT a __shared__ array of its own:
+// the 2-block-per-CU tiles use exactly 160 KB of LDS, one more byte halves their occupancy.
+SN_DEV void q_amax_flush(const SnGemmArgs& args, float qmax, char* lds_scratch) {
+  float* qred = reinterpret_cast<float*>(lds_scratch);
+  qmax = wave_max(qmax);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // every wave is done with the stage (fragment reads / staged stores)
+  if ((threadIdx.x & 63) == 0) qred[w] = qmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, qred[i]);
+    if (m > 0.f) atomicMax(reinterpret_cast<unsigned int*>(args.q_part + (blockIdx.x & 255) * 32), __float_as_uint(m));
+  }
+}
+
 // bias / ReLU / ReLU-backward gate / dropout of one 4-column bf16 output fragment
 template <int EPI, bool FP8>
 SN_DEV void epi_bf16_math(const SnGemmArgs& args, int grp, int m, int n, f32x4 v, int c_cols, float* o) {
@@ -605,12 +657,17 @@ SN_DEV void epi_bf16_math(const SnGemmArgs& args, int grp, int m, int n, f32x4 v
 // bias / ReLU / ReLU-backward gate for bf16 outputs, fp32 store / accumulate (+ the
 // bias-gradient column routed to bias_out), or the fused solver update (EPI_SGD).
 template <int EPI, bool FP8>
-SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, f32x4 v, int c_cols) {
+SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, f32x4 v, int c_cols,
+                      float* qmax = nullptr) {
   const bool full = (n + 3 < c_cols) && ((args.ldc & 3) == 0);
   if (epi_bf16<EPI>()) {
     bf16_t* C = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride + (long long)m * args.ldc;
     float o[4];
     epi_bf16_math<EPI, FP8>(args, grp, m, n, v, c_cols, o);
+    if (qmax && args.q_out) {  // host: q_ld % 4 == 0, N % 4 == 0 (whole 4-byte fragments)
+      const uint32_t w = q_pack4(args, args.q_slot[0], o, *qmax);
+      *reinterpret_cast<uint32_t*>(args.q_out + grp * args.q_gstride + (long long)m * args.q_ld + n) = w;
+    }
     if (full) {
       uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
       *reinterpret_cast<uint2*>(C + n) = pk;
@@ -1031,12 +1088,20 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       bf16_t* Cb = reinterpret_cast<bf16_t*>(args.C) + grp * args.c_gstride;
+      float qmax = 0.f;
+      const float qsc = args.q_out ? args.q_slot[0] : 0.f;
       for (int q = tid; q < BM * CPR; q += NW * 64) {
         const int lr = q / CPR, c = q - lr * CPR;
         const int m = m_blk + lr, n = n_blk + c * 8;
         if (m >= args.M || n >= args.N) continue;
         const uint4 v = *reinterpret_cast<const uint4*>((lr < HALF ? smem0 : smem1) + (lr % HALF) * PITCH + c * 16);
         bf16_t* dst = Cb + (long long)m * args.ldc + n;
+        if (args.q_out) {  // host: N % 8 == 0 with a side output, so the chunk is whole
+          float f[8];
+          unpack8(v, f);
+          const uint2 w = make_uint2(q_pack4(args, qsc, f, qmax), q_pack4(args, qsc, f + 4, qmax));
+          *reinterpret_cast<uint2*>(args.q_out + grp * args.q_gstride + (long long)m * args.q_ld + n) = w;
+        }
         if (n + 8 <= args.N) {
           *reinterpret_cast<uint4*>(dst) = v;
         } else {
@@ -1046,9 +1111,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
             if (k < args.N - n) dst[k] = (bf16_t)(w[k >> 1] >> (16 * (k & 1)));
         }
       }
+      if (args.q_out) q_amax_flush(args, qmax, smem0);
       return;
     }
   }
+  float qmax = 0.f;
 #pragma unroll
   for (int j = 0; j < MFR; ++j) {
     const int m = m_blk + wm0 + 16 * j + mrow_l;
@@ -1057,9 +1124,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     for (int i = 0; i < NFR; ++i) {
       const int n = n_blk + wn0 + 16 * i + ncol_l;
       if (n >= args.N) continue;
-      epi_store<EPI, (FP8 != 0)>(args, grp, split, m, n, acc[i][j], c_cols);
+      epi_store<EPI, (FP8 != 0)>(args, grp, split, m, n, acc[i][j], c_cols, epi_bf16<EPI>() ? &qmax : nullptr);
     }
   }
+  if (epi_bf16<EPI>() && args.q_out) q_amax_flush(args, qmax, smem0);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -541,6 +541,7 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
             if layer.fp8_eligible(b) and fp8_macs_per_input(layer, b) >= min_macs_per_input:
                 chosen.append(layer)
             if (dgrad and layer.type_name == "Convolution" and layer.fp8_dgrad_eligible(b)
+                    and net.bottom_need_backward[li][0]
                     and fp8_dgrad_macs_per_grad(layer, b) >= min_macs_per_input):
                 chosen_dg.append(layer)
     sc = hip.Fp8Scales(2 * (len(chosen) + len(chosen_dg)), net.device)
@@ -552,7 +553,47 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
         if dgrad_format == "e5m2":
             sc.set_e5m2(2 * i)
     net.ctx.fp8 = sc if (chosen or chosen_dg) else None
+    fuse_fp8_quant(net)
     return len(chosen) + len(chosen_dg)
+
+
+def fuse_fp8_quant(net) -> int:
+    """Pair each fp8 product with the conv GEMM that produces its bf16 operand, so that GEMM's
+    epilogue also stores the fp8 bytes (ops.gemm.Fp8Side) and the separate bf16 -> fp8 pass
+    (3 bytes of HBM traffic per element) becomes a 1-byte side store:
+      forward:  conv P (ReLU fused) -> conv Q with an e4m3 forward: P's output GEMM stores Q's
+                e4m3 input (Q's x slot);
+      backward: the same pair with an fp8 data gradient on P: Q's data-gradient GEMM (ReLU
+                gate of P's output fused) stores P's fp8 output gradient (P's dy slot).
+    P's output must be read by Q alone (VGG-16's conv2_2 .. conv5_3 chains; the inputs that
+    come out of pooling layers keep their quantisation pass).  The slots use delayed
+    scaling, so the side stores start once the first fp8_update_scales has initialised them
+    (eager warm-up steps); the bytes equal the separate pass's.  Returns the pairs fused."""
+    if getattr(net.ctx, "fp8", None) is None or os.environ.get("SN_FP8_FUSED_QUANT", "1") == "0":
+        return 0
+    outputs = set(getattr(net, "output_blob_ids", ()))
+    n = 0
+    for pi, prod in enumerate(net.layers):
+        if prod.type_name != "Convolution" or not prod.fuse_relu or len(net.top_ids[pi]) != 1:
+            continue
+        if prod.concat_slot is not None:
+            continue
+        blob = net.top_ids[pi][0]
+        readers = [lj for lj in range(pi + 1, len(net.layers))
+                   if blob in net.bottom_ids[lj] and not getattr(net.layers[lj], "fused", False)]
+        if blob in outputs or len(readers) != 1:
+            continue
+        lq = readers[0]
+        cons = net.layers[lq]
+        if cons.type_name != "Convolution" or len(net.bottom_ids[lq]) != 1:
+            continue
+        if cons.fp8_slots is not None:
+            prod.fp8_out = (cons, cons.fp8_slots[0])
+            n += 1
+        if prod.fp8_dgrad_slots is not None and net.bottom_need_backward[pi][0]:
+            cons.fp8_dx_out = (prod, prod.fp8_dgrad_slots[0])  # (conv1_1's data gradient never runs)
+            n += 1
+    return n
 
 
 def fp8_step(net) -> None:

@@ -97,6 +97,17 @@ class ConvolutionLayer(Layer):
         self._ws = [{} for _ in bottoms]  # forward -> backward scratch (e.g. folded input)
         for i, (b, t) in enumerate(zip(bottoms, tops)):
             s = self.spec(b)
+            side = self._fp8_out_side(s) if i == 0 else None
+            if side is not None:  # the epilogue also stores the output as the consumer's fp8 input
+                from ..ops import gemm as _gemm
+                with _gemm.fp8_side_output(side):
+                    if self.fp8_slots is not None:
+                        t.data = self._forward_fp8(b.data, w, bias, s, out=side.base)
+                    else:
+                        t.data = ops.conv_forward(b.data, w, bias, s, relu=self.fuse_relu, ws=self._ws[i],
+                                                  folded=self.folded_input, out=side.base)
+                self.fp8_out[0]._fp8_x_side = side
+                continue
             if self.fp8_slots is not None and b.data.is_cuda:
                 t.data = self._forward_fp8(b.data, w, bias, s)
                 continue
@@ -110,6 +121,26 @@ class ConvolutionLayer(Layer):
 
     fp8_slots = None  # (x slot, w slot) in ctx.fp8 when the forward product runs in e4m3
     fp8_dgrad_slots = None  # (dy slot, flipped-w slot) when the data gradient runs in e4m3
+    # engine.fuse_fp8_quant: (consumer conv, its x slot) — this layer's output GEMM also stores
+    # the consumer's fp8 input; (producer conv, its dy slot) — this layer's data-gradient GEMM
+    # also stores the producer's fp8 output gradient
+    fp8_out = None
+    fp8_dx_out = None
+    _fp8_x_side = None
+    _fp8_dy_side = None
+
+    def _fp8_ready(self) -> bool:
+        sc = getattr(self.ctx, "fp8", None)
+        return sc is not None and sc.updates > 0  # delayed-scaling slots initialised
+
+    def _fp8_out_side(self, s):
+        if self.fp8_out is None or self.concat_slot is not None or not self._fp8_ready():
+            return None
+        from ..ops import gemm as _gemm
+        cons, ix = self.fp8_out
+        sc = self.ctx.fp8
+        y = torch.empty((s.N, s.P, s.Q, s.K), dtype=torch.bfloat16, device=self.weight.compute.device)
+        return _gemm.Fp8Side(y, sc.slot(ix), sc.is_e5m2(ix))
 
     def fp8_eligible(self, b) -> bool:
         s = self.spec(b)
@@ -119,15 +150,20 @@ class ConvolutionLayer(Layer):
         from ..ops import hip
         return hip.fp8_dgrad_ok(self.spec(b))
 
-    def _forward_fp8(self, x, w, bias, s):
-        """e4m3 forward product (delayed per-tensor scales); backward stays bf16 on the
-        bf16 activations and weights (fp32 masters are untouched)."""
+    def _forward_fp8(self, x, w, bias, s, out=None):
+        """e4m3 forward product (delayed per-tensor scales); the weight gradient stays bf16
+        on the bf16 activations (fp32 masters are untouched).  The input's e4m3 bytes come
+        from the producing conv's epilogue when engine.fuse_fp8_quant paired the two."""
         from ..ops import hip
         sc = self.ctx.fp8
         ix, iw = self.fp8_slots
-        xq = hip.quant_fp8(x, sc.slot(ix))
+        from ..ops import gemm as _gemm
+        side, self._fp8_x_side = self._fp8_x_side, None
+        xq = _gemm.side_bytes(side, x)
+        if xq is None:
+            xq = hip.quant_fp8(x, sc.slot(ix))
         wq = hip.quant_fp8(w, sc.slot(iw))
-        return hip.conv_forward_fp8(xq, wq, bias, s, sc.deq(ix), sc.deq(iw), relu=self.fuse_relu)
+        return hip.conv_forward_fp8(xq, wq, bias, s, sc.deq(ix), sc.deq(iw), relu=self.fuse_relu, out=out)
 
     supports_grad_overwrite = True
 
@@ -144,7 +180,12 @@ class ConvolutionLayer(Layer):
                 ws["wt"] = self.flipped_weights
             if self.fp8_dgrad_slots is not None and t.diff.is_cuda:  # e4m3 data gradient (engine.enable_fp8)
                 ws = {} if ws is None else ws
-                ws["fp8_dgrad"] = (self.ctx.fp8, *self.fp8_dgrad_slots)
+                dy_side, self._fp8_dy_side = self._fp8_dy_side, None
+                ws["fp8_dgrad"] = (self.ctx.fp8, *self.fp8_dgrad_slots, dy_side)
+            if i == 0 and self.fp8_dx_out is not None and propagate_down[i] and self._fp8_ready():
+                ws = {} if ws is None else ws
+                prod, idy = self.fp8_dx_out
+                ws["fp8_dx_side"] = (self.ctx.fp8.slot(idy), self.ctx.fp8.is_e5m2(idy))
             dw_acc = not (dw is not None and self.grad_overwrite(0))
             db_acc = not (db is not None and self.grad_overwrite(1))
             sink = getattr(self, "slab_grad", None)
@@ -161,6 +202,8 @@ class ConvolutionLayer(Layer):
                     sink.end()  # this pass's gradient went to the flat buffer
                 dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws,
                                        dw_acc=dw_acc, db_acc=db_acc)
+            if ws is not None and "fp8_dx_side_out" in ws:
+                self.fp8_dx_out[0]._fp8_dy_side = ws.pop("fp8_dx_side_out")
             if propagate_down[i]:
                 b.diff = dx
 

@@ -14,6 +14,7 @@ an fp32 workspace and are combined by a deterministic reduce kernel.
 from __future__ import annotations
 
 import ast
+import contextlib
 import ctypes as C
 import json
 import os
@@ -285,10 +286,17 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
                                bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, f8, *dq, raster,
                                ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), lds)
         args.addr_legacy = _ADDR_LEGACY
+        side = _SIDE
+        if side is not None and side.covers(out):
+            q = _side_fields(side, out, ldc, c_gstride, N, tile, e, lds)
+            if q is not None:
+                args.q_out, args.q_ld, args.q_gstride, args.q_slot, args.q_e5m2, args.q_part = q
         _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
         if _lib.DEBUG_SYNC:
             _lib.debug_sync("gemm")
         return
+    if _SIDE is not None and _SIDE.covers(out):
+        _SIDE.ok = False  # the split-K reduce writes the bf16 output
     ldw = -(-N // 4) * 4  # fp32 slabs keep 16-B rows (the ones column makes N odd)
     sink = _DEFER_SINK
     deferred = (sink is not None and epi == EPI_F32 and not fp8 and (bias_grad is None or not bias_acc)
@@ -310,6 +318,87 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     _lib.call("splitk_reduce", ws, splits, M * ldw, M, N, ldw, out, ldc, mode, bias, int(relu),
               groups, splits * M * ldw, c_gstride, gate, bias_grad, ones, int(bias_acc), M,
               C.c_void_p(rng), int(dstream), float(ratio), float(gscale))
+
+
+# --- fused fp8 side output ----------------------------------------------------------------
+# A bf16 GEMM output that the next layer quantises for an fp8 product (its e4m3 input, or
+# the e4m3 / e5m2 output gradient of the layer below) can be quantised by the producing
+# GEMM's epilogue instead (SnGemmArgs.q_out): every launch under ``fp8_side_output(side)``
+# whose output lies inside ``side.base`` also stores its fp8 bytes into ``side.q`` and
+# folds the block |max| into the slot.  A launch that cannot (split-K, the 8-wave
+# gemm256 tiles, ragged channel counts) marks the side incomplete and the consumer runs
+# its own quantisation pass.  The slot must be an initialised delayed-scaling slot.
+
+
+class Fp8Side:
+    def __init__(self, base: torch.Tensor, slot: torch.Tensor, e5m2: bool = False):
+        assert base.is_contiguous() and base.dtype == torch.bfloat16
+        self.base = base
+        self.q = torch.empty(base.shape, dtype=torch.uint8, device=base.device)
+        self.slot = slot
+        self.e5m2 = bool(e5m2)
+        self.ok = True
+        self.launches = 0
+        self.part = torch.zeros(256 * 32, dtype=torch.float32, device=base.device)  # block |max| partials
+
+    def finish(self) -> None:
+        """Fold the launches' block |max| partials into the slot (one 256-thread block)."""
+        if self.launches:
+            _lib.call("fp8_fold_amax", self.part, self.slot)
+
+    def covers(self, out: torch.Tensor) -> bool:
+        b = self.base.data_ptr()
+        return out.dtype == torch.bfloat16 and b <= out.data_ptr() < b + 2 * self.base.numel()
+
+    @property
+    def complete(self) -> bool:
+        return self.ok and self.launches > 0
+
+    def matches(self, x: torch.Tensor) -> bool:
+        return self.complete and x.data_ptr() == self.base.data_ptr() and x.numel() == self.base.numel()
+
+
+_SIDE = None
+_SIDE_FRAG = os.environ.get("SN_FP8_SIDE_FRAG", "0") == "1"  # also from the per-fragment epilogue (A/B)
+SIDE_STATS = {"used": 0, "missed": 0}  # consumer lookups of a side output (tests, probes)
+
+
+def side_bytes(side, x: torch.Tensor, e5m2: bool = False):
+    """The fp8 bytes of ``x`` stored by its producer's epilogue, or None (quantise it)."""
+    if side is None:
+        return None
+    if side.matches(x) and side.e5m2 == bool(e5m2):
+        SIDE_STATS["used"] += 1
+        return side.q
+    SIDE_STATS["missed"] += 1
+    return None
+
+
+@contextlib.contextmanager
+def fp8_side_output(side):
+    global _SIDE
+    prev, _SIDE = _SIDE, side
+    try:
+        yield side
+    finally:
+        _SIDE = prev
+    side.finish()
+
+
+def _side_fields(side, out, ldc, c_gstride, N, tile, epi, lds):
+    """(q_out, q_ld, q_gstride, q_slot, q_e5m2) of one unsplit launch, or None when this
+    launch cannot store the side output (the side is then marked incomplete).  Only the
+    LDS-staged epilogue stores it (whole 8-byte row chunks, coalesced along rows): from the
+    per-fragment epilogue (16 rows x 4 bytes per 16 lanes) the partial-line fp8 stores cost
+    more than the quantisation pass they replace (VGG-16 b2048 8.0k vs 8.8k img/s)."""
+    off = (out.data_ptr() - side.base.data_ptr()) // 2
+    qp = side.q.data_ptr() + off
+    if ((not lds and not _SIDE_FRAG) or epi not in (EPI_BF16, EPI_BF16_DROP) or tile in (6, 7, 8, 9) or N % 8 or ldc % 8
+            or c_gstride % 8 or qp % 8):
+        side.ok = False
+        return None
+    side.launches += 1
+    return (qp, ldc, c_gstride, side.slot.data_ptr(), int(side.e5m2), side.part.data_ptr())
 
 
 # --- deferred split-K reduction ---------------------------------------------------------

@@ -298,9 +298,26 @@ def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
 
 def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
                   dw_acc=True, db_acc=True):
+    side_req = ws.pop("fp8_dx_side", None) if ws else None
+    if side_req is not None and need_dx:
+        # the data-gradient GEMM epilogue also stores dx as fp8 for the layer below's fp8 data
+        # gradient (engine.fuse_fp8_quant); ws["fp8_dx_side_out"] is that fp8 copy's Fp8Side
+        from .gemm import Fp8Side, fp8_side_output
+        dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
+        side = Fp8Side(dx, *side_req)
+        with fp8_side_output(side):
+            out = _conv_backward_chunked(dy, x, w, s, need_dx, dw, db, gate, ws, dw_acc, db_acc, dx)
+        ws["fp8_dx_side_out"] = side if out is dx else None
+        return out
+    return _conv_backward_chunked(dy, x, w, s, need_dx, dw, db, gate, ws, dw_acc, db_acc)
+
+
+def _conv_backward_chunked(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
+                           dw_acc=True, db_acc=True, dx=None):
     nb = _image_chunk(s)
     if nb < s.N:
-        dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device) if need_dx else None
+        if dx is None:
+            dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device) if need_dx else None
         for n0 in range(0, s.N, nb):
             n1 = min(s.N, n0 + nb)
             _conv_backward(dy[n0:n1], x[n0:n1], w, s.with_batch(n1 - n0), need_dx, dw,
@@ -309,7 +326,7 @@ def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=N
                            dx_out=dx[n0:n1] if need_dx else None)
             dw_acc = db_acc = True  # later chunks accumulate into the weight gradients
         return dx
-    return _conv_backward(dy, x, w, s, need_dx, dw, db, gate, ws, dw_acc, db_acc)
+    return _conv_backward(dy, x, w, s, need_dx, dw, db, gate, ws, dw_acc, db_acc, dx_out=dx)
 
 
 def _conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
@@ -447,12 +464,16 @@ def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8):
     scaling slots (a slot not yet initialised scales from the current tensor), the
     epilogue dequantises and applies the ReLU-backward gate, dx stays bf16.  The weight
     gradient keeps reading the bf16 output gradient."""
-    sc, idy, iwt = f8
+    sc, idy, iwt = f8[:3]
     if wt is None:
         wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=dy.device)
         call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
     e5 = sc.is_e5m2(idy)
-    dyq = quant_fp8(dy, sc.slot(idy), e5m2=e5)
+    side = f8[3] if len(f8) > 3 else None  # dy's fp8 bytes stored by the layer above's dgrad epilogue
+    from .gemm import side_bytes
+    dyq = side_bytes(side, dy, e5)
+    if dyq is None:
+        dyq = quant_fp8(dy, sc.slot(idy), e5m2=e5)
     wtq = quant_fp8(wt, sc.slot(iwt))
     A = Im2col(dyq, g2, kcontig=True, gstride=s.Kg)
     B = Dense(wtq.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
@@ -855,6 +876,7 @@ class Fp8Scales:
     initialised, format max, -, -, -].  Slots are e4m3 unless :meth:`set_e5m2` is called."""
 
     def __init__(self, n: int, device):
+        self.updates = 0  # fp8_update_scales launches issued (slots are initialised after the first)
         self.slots = torch.zeros((max(n, 1), 8), dtype=torch.float32, device=device)
         self.slots[:, 0] = 1.0
         self.slots[:, 2] = 1.0
@@ -877,6 +899,7 @@ class Fp8Scales:
 
     def update(self) -> None:
         call("fp8_update_scales", self.slots, self.n, float(FP8_MARGIN))
+        self.updates += 1
 
 
 def quant_fp8(x: torch.Tensor, slot: torch.Tensor, out: torch.Tensor | None = None,

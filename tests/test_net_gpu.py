@@ -162,7 +162,7 @@ def test_fp8_forward_training(gpu, dgrad):
         if mode == "fp8":
             n = enable_fp8(solver.net, 0.0, dgrad=dgrad)
             # 12 of 13 convs (not the RGB input) + 3 IPs; data gradients of the 12 convs
-            # whose output channels fill 16-byte fp8 chunks (conv1_1's dgrad is never needed)
+            # that need one (conv1_1's is never computed)
             assert n >= (14 + 12 if dgrad else 14), n
             if dgrad:
                 assert sum(getattr(ly, "fp8_dgrad_slots", None) is not None for ly in solver.net.layers) >= 12
@@ -180,6 +180,48 @@ def test_fp8_forward_training(gpu, dgrad):
     # same data every step: both must fit it; fp8 stays close to bf16
     assert losses["fp8"][-1] < losses["fp8"][0]
     assert abs(losses["fp8"][0] - losses["bf16"][0]) < 0.05 * abs(losses["bf16"][0]) + 0.05
+
+
+def test_fp8_fused_quant_is_bitwise_equal(gpu, monkeypatch):
+    """engine.fuse_fp8_quant: the producing conv GEMMs' epilogues store the consumers' fp8
+    inputs and fp8 output gradients (ops.gemm.Fp8Side) instead of separate quantisation
+    passes — same bytes, same amax — so graph-captured training is bitwise equal with and
+    without the fusion, and the side outputs are really consumed."""
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.engine import GraphStep, enable_fp8, fuse_relu
+    from sparknet_amd.ops import gemm as G
+    net_p = models.vgg16(train_batch=4, test_batch=4, crop=32, classes=10)
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SN_FP8_FUSED_QUANT", fused)
+        sp = models.zoo.vgg16_solver(net_p)
+        sp.base_lr = 0.002
+        solver = Solver(sp, device=torch.device("cuda:0"), seed=5, build_test_nets=False)
+        fuse_relu(solver.net)
+        enable_fp8(solver.net, 0.0, dgrad=True)
+        pairs = sum(ly.fp8_out is not None for ly in solver.net.layers if ly.type_name == "Convolution")
+        pairs_bwd = sum(ly.fp8_dx_out is not None for ly in solver.net.layers if ly.type_name == "Convolution")
+        if fused == "1":
+            assert pairs >= 7 and pairs_bwd >= 7, (pairs, pairs_bwd)  # conv1_2 .. conv5_3 chains
+        else:
+            assert pairs == 0 and pairs_bwd == 0
+        g = torch.Generator().manual_seed(2)
+        x = torch.randn(4, 3, 32, 32, generator=g) * 0.5
+        y = torch.tensor([[1.0], [3.0], [5.0], [7.0]])
+
+        def pre():
+            solver.net.blob_by_name("data").set_nchw(x)
+            solver.net.blob_by_name("label").set_nchw(y)
+        G.SIDE_STATS.update(used=0, missed=0)
+        st = GraphStep(solver, warmup=2, pre=pre, overlap=False)
+        losses = [float(st.step()) for _ in range(6)]
+        res[fused] = (losses, solver.net.flat_data.clone(), dict(G.SIDE_STATS))
+    # tiny deep layers run split-K products (their reduce writes the bf16 output): those
+    # consumers quantise themselves; the large early layers take the side outputs
+    assert res["1"][2]["used"] >= 4, res["1"][2]
+    assert res["0"][2]["used"] == 0
+    assert res["1"][0] == res["0"][0], (res["1"][0], res["0"][0])
+    assert torch.equal(res["1"][1], res["0"][1])
 
 
 def test_googlenet_branch_streams_bitwise(gpu):
