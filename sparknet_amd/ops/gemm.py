@@ -359,7 +359,9 @@ class Fp8Side:
 
 
 _SIDE = None
-_SIDE_FRAG = os.environ.get("SN_FP8_SIDE_FRAG", "0") == "1"  # also from the per-fragment epilogue (A/B)
+# the per-fragment epilogue stores side outputs too (SN_FP8_SIDE_FRAG=0: LDS-staged launches only;
+# VGG-16 b2048 8.98k / 8.97k with vs 8.96k / 8.94k img/s without, profiles/r3_fp8_dgrad.txt)
+_SIDE_FRAG = os.environ.get("SN_FP8_SIDE_FRAG", "1") == "1"
 SIDE_STATS = {"used": 0, "missed": 0}  # consumer lookups of a side output (tests, probes)
 
 
@@ -387,10 +389,7 @@ def fp8_side_output(side):
 
 def _side_fields(side, out, ldc, c_gstride, N, tile, epi, lds):
     """(q_out, q_ld, q_gstride, q_slot, q_e5m2) of one unsplit launch, or None when this
-    launch cannot store the side output (the side is then marked incomplete).  Only the
-    LDS-staged epilogue stores it (whole 8-byte row chunks, coalesced along rows): from the
-    per-fragment epilogue (16 rows x 4 bytes per 16 lanes) the partial-line fp8 stores cost
-    more than the quantisation pass they replace (VGG-16 b2048 8.0k vs 8.8k img/s)."""
+    launch cannot store the side output (the side is then marked incomplete)."""
     off = (out.data_ptr() - side.base.data_ptr()) // 2
     qp = side.q.data_ptr() + off
     if ((not lds and not _SIDE_FRAG) or epi not in (EPI_BF16, EPI_BF16_DROP) or tile in (6, 7, 8, 9) or N % 8 or ldc % 8
