@@ -163,6 +163,52 @@ __global__ void pool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restric
   }
 }
 
+// ---- fp8 side output (engine.fuse_fp8_quant): the pooled output / the input gradient also
+// stored as the fp8 bytes the consuming fp8 product reads (a conv's e4m3 input after a pool,
+// the fp8 output gradient of the conv before a pool), scaled by an initialised delayed-scaling
+// slot; block |max| into one of 256 partials 128 B apart (folded by sn_fp8_fold_amax).
+struct QSide {
+  uint8_t* q;
+  const float* slot;
+  float* part;
+  int e5m2;
+};
+
+SN_DEV uint2 q_pack8(const QSide& qs, float sc, const float* v, float& qmax) {
+  const float fmax = qs.e5m2 ? 57344.f : 448.f;
+  float f[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const float b = bf2f(f2bf(v[r]));  // the stored bf16 value
+    qmax = fmaxf(qmax, fabsf(b));
+    f[r] = fminf(fmaxf(b * sc, -fmax), fmax);
+  }
+  int w0 = 0, w1 = 0;
+  if (qs.e5m2) {
+    w0 = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], w0, false);
+    w0 = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], w0, true);
+    w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], w1, false);
+    w1 = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], w1, true);
+  } else {
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], w0, false);
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w0, true);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], w1, false);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], w1, true);
+  }
+  return make_uint2((uint32_t)w0, (uint32_t)w1);
+}
+
+SN_DEV void q_flush(const QSide& qs, float qmax) {  // every thread of the block calls it
+  __shared__ float red[4];
+  qmax = wave_max(qmax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = qmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f) atomicMax(reinterpret_cast<unsigned int*>(qs.part + (blockIdx.x & 255) * 32), __float_as_uint(m));
+  }
+}
+
 // ---- fixed-window fast paths (VEC, compile-time window) --------------------------------
 // Same semantics as the generic kernels above, but every window load is issued up front
 // from a clamped in-bounds address and masked afterwards: a load inside a data-dependent
@@ -170,8 +216,10 @@ __global__ void pool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restric
 
 template <int KH, int KW>
 __global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
-                              PoolGeom g, int gate) {
+                              PoolGeom g, int gate, QSide qs) {
   const int cv = g.C / 8;
+  float qmax = 0.f;
+  const float qsc = qs.q ? qs.slot[0] : 0.f;
   const long long total = (long long)g.N * g.P * g.Q * cv;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -209,6 +257,7 @@ __global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, bf16_t* __restrict__
     }
     const long long o = (long long)pix * g.C + c0;
     *reinterpret_cast<uint4*>(y + o) = pack8(best);
+    if (qs.q) *reinterpret_cast<uint2*>(qs.q + o) = q_pack8(qs, qsc, best, qmax);
     if (mask) {
       uint2 m;
       m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
@@ -216,13 +265,16 @@ __global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, bf16_t* __restrict__
       *reinterpret_cast<uint2*>(mask + o) = m;
     }
   }
+  if (qs.q) q_flush(qs, qmax);
 }
 
 // NH x NW = max number of windows covering one input pixel (ceil(k / stride) per axis).
 template <int NH, int NW, bool MAX>
 __global__ void pool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
-                           PoolGeom g) {
+                           PoolGeom g, QSide qs) {
   const int cv = g.C / 8;
+  float qmax = 0.f;
+  const float qsc = qs.q ? qs.slot[0] : 0.f;
   const long long total = (long long)g.N * g.H * g.W * cv;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -272,7 +324,9 @@ __global__ void pool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restr
         }
       }
     *reinterpret_cast<uint4*>(dx + (long long)pix * g.C + c0) = pack8(acc);
+    if (qs.q) *reinterpret_cast<uint2*>(qs.q + (long long)pix * g.C + c0) = q_pack8(qs, qsc, acc, qmax);
   }
+  if (qs.q) q_flush(qs, qmax);
 }
 
 // 3x3 / stride-2 windows (AlexNet / CaffeNet / GoogLeNet pools): in padded coordinates
@@ -360,16 +414,19 @@ static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long 
 extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long N, long long H, long long W,
                            long long C, long long P, long long Q, long long kh, long long kw, long long sh,
                            long long sw, long long ph, long long pw, long long method, long long gate,
-                           hipStream_t st) {
+                           uint8_t* q, const float* qslot, float* qpart, long long qe5m2, hipStream_t st) {
   PoolGeom g = mkgeom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const QSide qs{q, qslot, qpart, (int)qe5m2};
+  // fp8 side output: the vectorised fixed-window max-pool only
+  if (q && !(method == 0 && (C % 8) == 0 && kh == kw && (kh == 2 || kh == 3) && qslot && qpart)) return 9;
   if (method == 0 && kh * kw > 254) return 6;
   if (N * H * W * C >= (1ll << 32)) return 8;  // 32-bit index decode
   const bool vec = (C % 8) == 0;
   long long total = N * P * Q * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
   if (method == 0 && vec && kh == kw && (kh == 2 || kh == 3)) {
-    if (kh == 3) hipLaunchKernelGGL((maxpool_fwd_k<3, 3>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
-    else hipLaunchKernelGGL((maxpool_fwd_k<2, 2>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
+    if (kh == 3) hipLaunchKernelGGL((maxpool_fwd_k<3, 3>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate, qs);
+    else hipLaunchKernelGGL((maxpool_fwd_k<2, 2>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate, qs);
   } else if (method == 0) {
     if (vec) hipLaunchKernelGGL(maxpool_fwd<true>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
     else hipLaunchKernelGGL(maxpool_fwd<false>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
@@ -382,13 +439,17 @@ extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long 
 
 extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, long long N, long long H, long long W,
                            long long C, long long P, long long Q, long long kh, long long kw, long long sh,
-                           long long sw, long long ph, long long pw, long long method, hipStream_t st) {
+                           long long sw, long long ph, long long pw, long long method,
+                           uint8_t* q, const float* qslot, float* qpart, long long qe5m2, hipStream_t st) {
   PoolGeom g = mkgeom(N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const QSide qs{q, qslot, qpart, (int)qe5m2};
   if (N * H * W * C >= (1ll << 32)) return 8;  // 32-bit index decode
   const bool vec = (C % 8) == 0;
   long long total = N * H * W * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
   const long long nh = (kh + sh - 1) / sh, nw = (kw + sw - 1) / sw;
+  // fp8 side output: the pool_bwd_k paths only
+  if (q && (!vec || (kh == 3 && kw == 3 && sh == 2 && sw == 2) || nh != nw || nh < 1 || nh > 3)) return 9;
   if (vec && kh == 3 && kw == 3 && sh == 2 && sw == 2) {
     // 2x2 input pixels per thread over the padded extent [0, H + ph) x [0, W + pw)
     const int BH = (int)((H + ph + 1) / 2), BW = (int)((W + pw + 1) / 2);
@@ -401,10 +462,11 @@ extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, lo
       hipLaunchKernelGGL((pool_bwd_k3s2<false>), g2, dim3(256), 0, st, dy, mask, dx, g, make_fdiv((uint32_t)BW),
                          make_fdiv((uint32_t)BH), BW, BH);
   } else if (vec && nh == nw && nh >= 1 && nh <= 3) {
-#define SN_POOL_BWD_K(NN)                                                                             \
-  do {                                                                                                \
-    if (method == 0) hipLaunchKernelGGL((pool_bwd_k<NN, NN, true>), grid, dim3(256), 0, st, dy, mask, dx, g);  \
-    else hipLaunchKernelGGL((pool_bwd_k<NN, NN, false>), grid, dim3(256), 0, st, dy, mask, dx, g);             \
+    if (q && !(qslot && qpart)) return 9;
+#define SN_POOL_BWD_K(NN)                                                                                  \
+  do {                                                                                                     \
+    if (method == 0) hipLaunchKernelGGL((pool_bwd_k<NN, NN, true>), grid, dim3(256), 0, st, dy, mask, dx, g, qs); \
+    else hipLaunchKernelGGL((pool_bwd_k<NN, NN, false>), grid, dim3(256), 0, st, dy, mask, dx, g, qs);            \
   } while (0)
     if (nh == 1) SN_POOL_BWD_K(1);
     else if (nh == 2) SN_POOL_BWD_K(2);

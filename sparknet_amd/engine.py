@@ -571,8 +571,36 @@ def fuse_fp8_quant(net) -> int:
     (eager warm-up steps); the bytes equal the separate pass's.  Returns the pairs fused."""
     if getattr(net.ctx, "fp8", None) is None or os.environ.get("SN_FP8_FUSED_QUANT", "1") == "0":
         return 0
+    from .ops import hip
     outputs = set(getattr(net, "output_blob_ids", ()))
     n = 0
+
+    def sole_reader(pi):
+        blob = net.top_ids[pi][0]
+        readers = [lj for lj in range(pi + 1, len(net.layers))
+                   if blob in net.bottom_ids[lj] and not getattr(net.layers[lj], "fused", False)]
+        return readers[0] if (blob not in outputs and len(readers) == 1) else None
+
+    # pooling in between: conv P (ReLU fused) -> max pool -> conv Q (VGG's block boundaries)
+    for oi, pool in enumerate(net.layers):
+        if (pool.type_name != "Pooling" or len(net.top_ids[oi]) != 1 or pool.fused_lrn is not None
+                or pool.global_pooling):
+            continue
+        s = pool.spec(net.bottom_vecs[oi][0])
+        lq = sole_reader(oi)
+        if lq is not None and net.layers[lq].type_name == "Convolution" and net.layers[lq].fp8_slots is not None \
+                and hip.pool_side_ok(s, False):
+            cons = net.layers[lq]
+            pool.fp8_out = (cons, cons.fp8_slots[0])
+            n += 1
+        bid = net.bottom_ids[oi][0]
+        prods = [pj for pj in range(oi) if bid in net.top_ids[pj] and not getattr(net.layers[pj], "fused", False)]
+        if prods and hip.pool_side_ok(s, True) and net.bottom_need_backward[oi][0]:
+            prod = net.layers[prods[-1]]
+            if (prod.type_name == "Convolution" and prod.fp8_dgrad_slots is not None
+                    and net.bottom_need_backward[prods[-1]][0] and sole_reader(prods[-1]) == oi):
+                pool.fp8_dx_out = (prod, prod.fp8_dgrad_slots[0])
+                n += 1
     for pi, prod in enumerate(net.layers):
         if prod.type_name != "Convolution" or not prod.fuse_relu or len(net.top_ids[pi]) != 1:
             continue

@@ -139,8 +139,18 @@ class ConvolutionLayer(Layer):
         from ..ops import gemm as _gemm
         cons, ix = self.fp8_out
         sc = self.ctx.fp8
-        y = torch.empty((s.N, s.P, s.Q, s.K), dtype=torch.bfloat16, device=self.weight.compute.device)
-        return _gemm.Fp8Side(y, sc.slot(ix), sc.is_e5m2(ix))
+        dev = self.weight.compute.device
+        y = torch.empty((s.N, s.P, s.Q, s.K), dtype=torch.bfloat16, device=dev)
+        return _gemm.Fp8Side(y, sc.slot(ix), sc.is_e5m2(ix), self._side_part("fwd", dev))
+
+    def _side_part(self, key, dev):
+        """Persistent block-|max| partials of this layer's fp8 side output (first allocated
+        by an eager step, before any graph capture)."""
+        parts = self.__dict__.setdefault("_fp8_parts", {})
+        if key not in parts:
+            from ..ops import gemm as _gemm
+            parts[key] = _gemm.new_side_part(dev)
+        return parts[key]
 
     def fp8_eligible(self, b) -> bool:
         s = self.spec(b)
@@ -185,7 +195,8 @@ class ConvolutionLayer(Layer):
             if i == 0 and self.fp8_dx_out is not None and propagate_down[i] and self._fp8_ready():
                 ws = {} if ws is None else ws
                 prod, idy = self.fp8_dx_out
-                ws["fp8_dx_side"] = (self.ctx.fp8.slot(idy), self.ctx.fp8.is_e5m2(idy))
+                ws["fp8_dx_side"] = (self.ctx.fp8.slot(idy), self.ctx.fp8.is_e5m2(idy),
+                                     self._side_part("bwd", t.diff.device))
             dw_acc = not (dw is not None and self.grad_overwrite(0))
             db_acc = not (db is not None and self.grad_overwrite(1))
             sink = getattr(self, "slab_grad", None)
@@ -305,6 +316,22 @@ class PoolingLayer(Layer):
 
     relu_gate = False  # backward of the slope-0 in-place ReLU producing the bottom is fused here
     fused_lrn = None   # the LRN reading this layer's output, run inside its kernels (engine.fuse_pool_lrn)
+    # engine.fuse_fp8_quant: (consumer conv, its x slot) / (producer conv, its dy slot) — the
+    # pooling kernels also store the consumer's e4m3 input / the producer's fp8 output gradient
+    fp8_out = None
+    fp8_dx_out = None
+
+    def _fp8_side(self, pair, shape, key, dev):
+        sc = getattr(self.ctx, "fp8", None)
+        if pair is None or sc is None or sc.updates == 0:
+            return None
+        from ..ops import gemm as _gemm
+        parts = self.__dict__.setdefault("_fp8_parts", {})
+        if key not in parts:
+            parts[key] = _gemm.new_side_part(dev)
+        i = pair[1]
+        return _gemm.Fp8Side(torch.empty(shape, dtype=torch.bfloat16, device=dev), sc.slot(i), sc.is_e5m2(i),
+                             parts[key])
 
     def spec(self, b) -> PoolSpec:
         N, C, H, W = b.shape
@@ -346,7 +373,13 @@ class PoolingLayer(Layer):
             tops[0].data, self.aux, f.top.data = hip.pool_lrn_forward(x, s, self.relu_gate, f.size, f.alpha, f.beta,
                                                                       f.k)
             return
-        y, self.aux = ops.pool_forward_aux(x, s, self.relu_gate)
+        side = self._fp8_side(self.fp8_out, (s.N, s.P, s.Q, s.C), "fwd", x.device) if x.is_cuda else None
+        if side is not None:
+            from ..ops import hip
+            y, self.aux = hip.pool_forward_mask(x, s, self.relu_gate, side=side)
+            self.fp8_out[0]._fp8_x_side = side
+        else:
+            y, self.aux = ops.pool_forward_aux(x, s, self.relu_gate)
         tops[0].data = y
         if len(tops) > 1:
             tops[1].data = (self.aux.to(tops[1].dtype) if self.aux is not None
@@ -375,6 +408,14 @@ class PoolingLayer(Layer):
             from ..ops import hip
             bottoms[0].diff = hip.lrn_pool_backward(f.top.diff, tops[0].data, self.aux, s, f.size, f.alpha, f.beta,
                                                     f.k)
+            return
+        side = (self._fp8_side(self.fp8_dx_out, (s.N, s.H, s.W, s.C), "bwd", bottoms[0].data.device)
+                if bottoms[0].data.is_cuda else None)
+        if side is not None:
+            from ..ops import hip
+            bottoms[0].diff = hip.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data,
+                                                self.relu_gate, side=side)
+            self.fp8_dx_out[0]._fp8_dy_side = side
             return
         bottoms[0].diff = ops.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data,
                                             self.relu_gate)

@@ -331,7 +331,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
 
 
 class Fp8Side:
-    def __init__(self, base: torch.Tensor, slot: torch.Tensor, e5m2: bool = False):
+    def __init__(self, base: torch.Tensor, slot: torch.Tensor, e5m2: bool = False, part: torch.Tensor | None = None):
         assert base.is_contiguous() and base.dtype == torch.bfloat16
         self.base = base
         self.q = torch.empty(base.shape, dtype=torch.uint8, device=base.device)
@@ -339,7 +339,9 @@ class Fp8Side:
         self.e5m2 = bool(e5m2)
         self.ok = True
         self.launches = 0
-        self.part = torch.zeros(256 * 32, dtype=torch.float32, device=base.device)  # block |max| partials
+        # block |max| partials (zero between uses: the fold kernel clears them); pass a persistent
+        # buffer so a captured graph does not re-zero a fresh one every replay
+        self.part = part if part is not None else new_side_part(base.device)
 
     def finish(self) -> None:
         """Fold the launches' block |max| partials into the slot (one 256-thread block)."""
@@ -356,6 +358,10 @@ class Fp8Side:
 
     def matches(self, x: torch.Tensor) -> bool:
         return self.complete and x.data_ptr() == self.base.data_ptr() and x.numel() == self.base.numel()
+
+
+def new_side_part(device) -> torch.Tensor:
+    return torch.zeros(256 * 32, dtype=torch.float32, device=device)
 
 
 _SIDE = None

@@ -541,17 +541,44 @@ def _pool_images(s: PoolSpec) -> int:
     return s.N if s.N * per < _MAX_ELEMS else max(1, (_MAX_ELEMS - 1) // per)
 
 
-def pool_forward_mask(x, s: PoolSpec, gate: bool = False):
+def pool_side_ok(s: PoolSpec, backward: bool) -> bool:
+    """Can the pooling kernels store an fp8 side output (ops.gemm.Fp8Side) of this pool's
+    output (forward: vectorised 2x2 / 3x3 max pooling) or input gradient (backward: the
+    pool_bwd_k gathers, not the 3x3 / stride-2 blocked kernel)?"""
+    if s.C % 8:
+        return False
+    if not backward:
+        return s.method == POOL_MAX and s.kh == s.kw and s.kh in (2, 3)
+    nh, nw = -(-s.kh // s.sh), -(-s.kw // s.sw)
+    return not (s.kh == 3 and s.kw == 3 and s.sh == 2 and s.sw == 2) and nh == nw and 1 <= nh <= 3
+
+
+def _side_args(side, t, n0, n1):
+    if side is None:
+        return (None, None, None, 0)
+    return (side.q[n0:n1], side.slot, side.part, int(side.e5m2))
+
+
+def pool_forward_mask(x, s: PoolSpec, gate: bool = False, side=None):
     """gate=True (MAX only): x is the output of a slope-0 in-place ReLU whose backward is
-    folded into the argmax mask (windows with max <= 0 pass no gradient)."""
+    folded into the argmax mask (windows with max <= 0 pass no gradient).  side: an
+    ops.gemm.Fp8Side over the output (pool_side_ok): the kernel also stores its fp8 bytes."""
     x = _c(x)
-    y = torch.empty((s.N, s.P, s.Q, s.C), dtype=BF16, device=x.device)
+    if side is not None:
+        assert pool_side_ok(s, False) and tuple(side.base.shape) == (s.N, s.P, s.Q, s.C)
+        y = side.base
+    else:
+        y = torch.empty((s.N, s.P, s.Q, s.C), dtype=BF16, device=x.device)
     mask = torch.empty((s.N, s.P, s.Q, s.C), dtype=torch.uint8, device=x.device) if s.method == POOL_MAX else None
     nb = _pool_images(s)
     for n0 in range(0, s.N, nb):
         n1 = min(s.N, n0 + nb)
         call("pool_fwd", x[n0:n1], y[n0:n1], mask[n0:n1] if mask is not None else None,
-             *_pool_args(dataclasses.replace(s, N=n1 - n0)), int(gate and s.method == POOL_MAX))
+             *_pool_args(dataclasses.replace(s, N=n1 - n0)), int(gate and s.method == POOL_MAX),
+             *_side_args(side, y, n0, n1))
+    if side is not None:
+        side.launches += 1
+        side.finish()
     return y, mask
 
 
@@ -559,8 +586,14 @@ def pool_forward(x, s: PoolSpec):
     return pool_forward_mask(x, s)[0]
 
 
-def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False):
-    dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=dy.device)
+def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False, side=None):
+    """side: an ops.gemm.Fp8Side over dx (pool_side_ok backward; not with a non-MAX gate)."""
+    if side is not None:
+        assert pool_side_ok(s, True) and not (gate and s.method != POOL_MAX)
+        assert tuple(side.base.shape) == (s.N, s.H, s.W, s.C)
+        dx = side.base
+    else:
+        dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=dy.device)
     if s.method == POOL_MAX and mask is None:
         _, mask = pool_forward_mask(x, s, gate)
     dy = _c(dy)
@@ -568,7 +601,10 @@ def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False):
     for n0 in range(0, s.N, nb):
         n1 = min(s.N, n0 + nb)
         call("pool_bwd", dy[n0:n1], mask[n0:n1] if mask is not None else None, dx[n0:n1],
-             *_pool_args(dataclasses.replace(s, N=n1 - n0)))
+             *_pool_args(dataclasses.replace(s, N=n1 - n0)), *_side_args(side, dx, n0, n1))
+    if side is not None:
+        side.launches += 1
+        side.finish()
     if gate and s.method != POOL_MAX:
         dx = relu_backward(dx, x)
     return dx
