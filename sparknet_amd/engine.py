@@ -912,16 +912,36 @@ class GraphStep:
         gc.collect()
         gc.freeze()
 
+    # Host run-ahead bound (SN_MAX_AHEAD = D > 0): before issuing step k, wait until step k - D
+    # has finished on the GPU, so at most D captured iterations (and their H2D minibatch
+    # copies) are queued ahead of the device; 0 = unbounded.  Unbounded, the host queues
+    # dozens of iterations and the first ~60 of a run execute at 84-95k instead of 107k
+    # img/s on CaffeNet (the "slow phase" of docs/PERF_NOTES.md); with D = 2 the in-stream
+    # rate is a flat 107k from the first step and the driver-shaped 20-step bench measures
+    # 105.7-106.1k vs 89.2-102.8k unbounded on the same box (scripts/ahead_ab.sh).
+    max_ahead = int(os.environ.get("SN_MAX_AHEAD", "2"))
+
     def step(self):
         s = self.solver
         if self.graph is None:
             self.capture()
             return self.loss
+        d = self.max_ahead
+        if d > 0:
+            ring = self.__dict__.setdefault("_ahead", [None] * d)
+            k = self.__dict__.get("_ahead_k", 0)
+            if ring[k % d] is not None:
+                ring[k % d].synchronize()
         if self.pre:
             self.pre()
         s.stage_hyper()
         self.graph.replay()
         s.iter += 1
+        if d > 0:
+            ev = ring[k % d] or torch.cuda.Event()
+            ev.record()
+            ring[k % d] = ev
+            self._ahead_k = k + 1
         return self.loss
 
 

@@ -202,6 +202,39 @@ def test_maxpool_relu_gate(gpu, geo):
     close(hip.pool_backward(dy, x, s, None, gate=True), ref.pool_backward(dy, x, s, gate=True), 1e-2)
 
 
+@pytest.mark.parametrize("e5m2", [False, True])
+@pytest.mark.parametrize("geo", [(2, 16, 16, 64, 2, 2, 0), (2, 14, 14, 32, 3, 1, 1)])
+def test_pool_fp8_side_output(gpu, geo, e5m2):
+    """The pooling kernels' fp8 side output (engine.fuse_fp8_quant: a pool's output as the
+    next conv's fp8 input, its input gradient as the previous conv's fp8 output gradient)
+    is byte-identical to quantising the bf16 result with the same (initialised) slot, and
+    its block maxima fold into the slot's amax."""
+    from sparknet_amd.ops import gemm as G, hip
+    N, H, W, Cc, k, st, pd = geo
+    s = PoolSpec(N, H, W, Cc, k, k, st, st, pd, pd, POOL_MAX)
+    x = torch.relu(rnd(N, H, W, Cc).float()).to(torch.bfloat16)
+    sc = hip.Fp8Scales(2, gpu)
+    for i in range(2):
+        if e5m2:
+            sc.set_e5m2(i)
+        sc.slots[i, 0], sc.slots[i, 2], sc.slots[i, 3] = 37.0, 1 / 37.0, 1.0  # initialised slots
+    if hip.pool_side_ok(s, False):
+        side = G.Fp8Side(torch.empty((N, s.P, s.Q, Cc), dtype=torch.bfloat16, device=gpu), sc.slot(0), e5m2)
+        y, mask = hip.pool_forward_mask(x, s, gate=True, side=side)
+        assert torch.equal(side.q, hip.quant_fp8(y, sc.slot(1), e5m2=e5m2))
+        assert sc.slots[0, 1].item() == y.float().abs().max().item() and side.part.abs().sum().item() == 0
+    else:
+        y, mask = hip.pool_forward_mask(x, s, gate=True)
+    if hip.pool_side_ok(s, True):
+        sc.slots[:, 1] = 0
+        dy = rnd(N, s.P, s.Q, Cc)
+        side = G.Fp8Side(torch.empty((N, H, W, Cc), dtype=torch.bfloat16, device=gpu), sc.slot(0), e5m2)
+        dx = hip.pool_backward(dy, x, s, mask, gate=True, side=side)
+        close(dx, ref.pool_backward(dy, x, s, gate=True), 1e-2)
+        assert torch.equal(side.q, hip.quant_fp8(dx, sc.slot(1), e5m2=e5m2))
+        assert sc.slots[0, 1].item() == dx.float().abs().max().item()
+
+
 def test_softmax_loss_and_accuracy(gpu):
     from sparknet_amd.ops import hip
     x = rnd(256, 1000, scale=2.0)
