@@ -300,6 +300,12 @@ struct NativeStep {
   float* hyper_host = nullptr;  // pinned, RING x 16
   hipEvent_t hyper_ev[RING] = {};
   int ring_pos = 0;
+  // host run-ahead bound (engine.GraphStep.max_ahead): iteration k is issued once k - AHEAD
+  // has finished, so captured iterations and their feeds are not queued dozens deep (a deep
+  // queue runs the device slower for its first ~60 iterations)
+  static constexpr int AHEAD = 2;
+  hipEvent_t ahead_ev[AHEAD] = {};
+  bool ahead_rec[AHEAD] = {};
   float* loss_dev = nullptr;
   float* loss_ring = nullptr;  // device, average_loss slots
   std::vector<float> loss_host;
@@ -312,6 +318,8 @@ struct NativeStep {
   ~NativeStep() {
     if (stream) hipStreamSynchronize(stream);
     for (auto& e : hyper_ev)
+      if (e) hipEventDestroy(e);
+    for (auto& e : ahead_ev)
       if (e) hipEventDestroy(e);
     if (hyper_host) hipHostFree(hyper_host);
     if (loss_ring) hipFree(loss_ring);
@@ -491,6 +499,8 @@ long long build_native_step(void* s, std::unique_ptr<NativeStep>& out) {
     return fail(e, "hipHostMalloc");
   for (auto& ev : ns->hyper_ev)
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return fail(e, "hipEventCreate");
+  for (auto& ev : ns->ahead_ev)
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return fail(e, "hipEventCreate");
   if ((e = hipMalloc((void**)&ns->loss_ring, sizeof(float) * ns->average_loss)) != hipSuccess) return fail(e, "hipMalloc");
   ns->loss_host.assign(ns->average_loss, 0.f);
   out = std::move(ns);
@@ -499,6 +509,8 @@ long long build_native_step(void* s, std::unique_ptr<NativeStep>& out) {
 
 // One training iteration (no GIL needed).
 int native_iteration(NativeStep& ns) {
+  const int ak = (int)(ns.iter % NativeStep::AHEAD);
+  if (ns.ahead_rec[ak]) HIPOK(hipEventSynchronize(ns.ahead_ev[ak]));
   if (ns.feeds.run(ns.stream)) return 1;
   // hyper-parameters (Solver.hyper_values layout: 0 lr, 8 Adam correction)
   const float lr = (float)ns.learning_rate(ns.iter);
@@ -524,6 +536,8 @@ int native_iteration(NativeStep& ns) {
   HIPOK(hipGraphLaunch(ns.exec, ns.stream));
   HIPOK(hipMemcpyAsync(ns.loss_ring + (ns.iter % ns.average_loss), ns.loss_dev, sizeof(float),
                        hipMemcpyDeviceToDevice, ns.stream));
+  HIPOK(hipEventRecord(ns.ahead_ev[ak], ns.stream));
+  ns.ahead_rec[ak] = true;
   ++ns.iter;
   ++ns.done;
   return 0;
