@@ -73,6 +73,8 @@ def parse():
                    help="after the timed window, check that every rank holds bitwise-identical averaged "
                         "masters and that the bf16 shadow the graph reads is bf16(master) (JSON avg_check)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--step-times", action="store_true",
+                   help="record a GPU event after every timed step and print the per-step ms to stderr")
     p.add_argument("--cpu", action="store_true",
                    help="fp32 reference engine on the CPU with gloo (tests the launcher / JSON path; not a benchmark)")
     p.add_argument("--host-profile", action="store_true",
@@ -174,11 +176,18 @@ def main():
     sync()
 
     avg_events = []
+    step_evs = []
+    if args.step_times and dev.type == "cuda":
+        step_evs.append(torch.cuda.Event(enable_timing=True))
+        step_evs[0].record()
     t0 = time.perf_counter()
     loss = None
     averaged = False
     for k in range(args.steps):
         loss = trainer.local_step()
+        if step_evs:
+            step_evs.append(torch.cuda.Event(enable_timing=True))
+            step_evs[-1].record()
         # every tau-th step averages; a timed window shorter than tau still ends with one
         # average so the collective is always inside the measurement
         if (k + 1) % args.tau == 0 or (k == args.steps - 1 and not averaged):
@@ -197,6 +206,9 @@ def main():
     sync()
     elapsed_rank = time.perf_counter() - t0
     elapsed = elapsed_rank
+    if step_evs:
+        ms = [step_evs[i].elapsed_time(step_evs[i + 1]) for i in range(len(step_evs) - 1)]
+        print(f"rank {rank} step ms: " + " ".join(f"{v:.2f}" for v in ms), file=sys.stderr, flush=True)
     per_rank_ms = [round(1000.0 * elapsed_rank / args.steps, 3)]
     avg_ms = [e[0].elapsed_time(e[1]) for e in avg_events if e is not None]
     comm_info = avg_check = None
