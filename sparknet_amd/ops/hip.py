@@ -194,6 +194,10 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=Non
             n1 = min(s.N, n0 + nb)
             conv_forward(x[n0:n1], w, b, s.with_batch(n1 - n0), relu, None,
                          folded[n0:n1] if folded is not None else None, out=y[n0:n1])
+        if ws is not None and folded is not None:
+            # the chunked weight gradient must read the fused augment's folded input: the
+            # NHWC data blob is not written when the fold is fused (engine.fuse_input_fold)
+            ws["s2d_full"] = (x.data_ptr(), x._version, folded)
         return y
     return _conv_forward(x, w, b, s, relu, ws, folded, out)
 
@@ -318,11 +322,17 @@ def _conv_backward_chunked(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=Non
     if nb < s.N:
         if dx is None:
             dx = torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device) if need_dx else None
+        full = ws.get("s2d_full") if ws else None
+        if full is not None and not (full[0] == x.data_ptr() and full[1] == x._version):
+            full = None
         for n0 in range(0, s.N, nb):
             n1 = min(s.N, n0 + nb)
+            cws = {k: ws[k] for k in ("wt", "fp8_dgrad") if k in ws} if ws else None
+            if full is not None:
+                xc = x[n0:n1]
+                cws["s2d"] = (xc.data_ptr(), xc._version, full[2][n0:n1])
             _conv_backward(dy[n0:n1], x[n0:n1], w, s.with_batch(n1 - n0), need_dx, dw,
-                           db, gate[n0:n1] if gate is not None else None,
-                           {k: ws[k] for k in ("wt", "fp8_dgrad") if k in ws} if ws else None, dw_acc, db_acc,
+                           db, gate[n0:n1] if gate is not None else None, cws, dw_acc, db_acc,
                            dx_out=dx[n0:n1] if need_dx else None)
             dw_acc = db_acc = True  # later chunks accumulate into the weight gradients
         return dx

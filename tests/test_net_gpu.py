@@ -224,6 +224,34 @@ def test_fp8_fused_quant_is_bitwise_equal(gpu, monkeypatch):
     assert torch.equal(res["1"][1], res["0"][1])
 
 
+def test_fused_fold_weight_gradient_with_image_chunks(gpu, monkeypatch):
+    """A conv whose S2D-folded input comes from the fused augment (the data blob itself is
+    never written) and whose batch is split into image chunks (VGG-16 conv1_1 at batch
+    2048): the chunked weight gradient reads the folded chunks, equal to the unchunked one."""
+    from sparknet_amd.ops import hip
+    from sparknet_amd.ops.spec import ConvSpec
+    s = ConvSpec(4, 32, 32, 3, 64, 3, 3, 1, 1, 1, 1, 1, 1, 1)
+    plan = hip.s2d_plan(s)
+    assert plan is not None
+    g = torch.Generator(device=gpu).manual_seed(4)
+    x = torch.randn(4, 32, 32, 3, device=gpu, generator=g).to(torch.bfloat16)
+    w = (torch.randn(64, 3, 3, 3, device=gpu, generator=g) * 0.1).to(torch.bfloat16)
+    dy = torch.randn(4, 32, 32, 64, device=gpu, generator=g).to(torch.bfloat16)
+    folded = hip._s2d_input(x, s, plan)
+    stale = torch.zeros_like(x)  # the data blob the fused augment never writes
+    grads = []
+    for max_pix in (1 << 24, 2 * 34 * 34):  # whole batch / 2-image chunks
+        monkeypatch.setattr(hip, "_MAX_PIX", max_pix)
+        ws = {}
+        hip.conv_forward(stale, w, None, s, ws=ws, folded=folded)
+        dw = torch.zeros(64, 3, 3, 3, device=gpu)
+        hip.conv_backward(dy, stale, w, s, False, dw, None, ws=ws, dw_acc=True)
+        grads.append(dw)
+    assert hip._image_chunk(s) < s.N  # the second pass really chunked
+    assert grads[0].abs().sum() > 0
+    assert torch.allclose(grads[1], grads[0], rtol=1e-3, atol=1e-3), (grads[1] - grads[0]).abs().max()
+
+
 def test_googlenet_branch_streams_bitwise(gpu):
     """engine.BranchStreams runs the Inception towers on 4 HIP streams (eager); loss and
     every parameter gradient are bitwise equal to the sequential schedule; the same holds
