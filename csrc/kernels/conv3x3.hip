@@ -1,0 +1,192 @@
+// Direct 3x3 / stride-1 / pad-1 convolution for 64 input and 64 output channels (VGG-16's
+// conv1_2 forward and data gradient: 64 % of VGG's bf16 conv time outside the fp8 products
+// went to these two thin products on the implicit-GEMM path).
+//
+// Why a separate kernel: the implicit GEMM stages every tap of its A operand from L2 (a
+// 256 x 64 tile reads 256 x 576 x 2 B = 295 KB of im2col rows for 9.4 M MACs, the input
+// pixels 9x over), and with only 64 output columns per A byte that L2 -> LDS stream, not the
+// MFMA pipe, sets the speed.  Here a block keeps the whole weight tensor (9 taps x 64 x 64
+// bf16 = 72 KB) resident in LDS, stages one 18 x 18-pixel input patch (41 KB, 1/7 of the
+// implicit-GEMM bytes) per 16 x 16-pixel output tile and reads the 9 tap-shifted A fragments
+// straight out of the patch.  Blocks are persistent (one per CU, 153 KB of LDS) and
+// double-buffer the patch: the next tile's global loads are in flight in registers while the
+// current tile's 288 MFMAs per wave run.
+//
+// Same XOR-swizzled 128-B-row LDS images as the GEMM engine (a row = one pixel's 64 channels
+// or one output channel's 64 weights), v_mfma_f32_16x16x32_bf16 with fp32 accumulation,
+// epilogue: + bias, ReLU, ReLU-backward gate (dgrad), bf16 NHWC store.
+#include "common.h"
+
+#include <cstdlib>
+
+namespace {
+
+constexpr int TILE = 16, PATCH = TILE + 2, PROWS = PATCH * PATCH;  // 324 patch pixels
+constexpr int ROWB = 128;                                           // 64 bf16 channels
+constexpr int W_BYTES = 9 * 64 * ROWB, P_BYTES = PROWS * ROWB;      // 73728, 41472
+constexpr int CHUNKS = PROWS * 8;                                   // 16-B patch chunks
+
+SN_DEV int kc_off(int row, int kc) { return row * ROWB + ((kc ^ ((row >> 1) & 7)) << 4); }
+
+SN_DEV bf16x8_t frag(const char* lds, int row0, int ks, int lane) {
+  const uint4 v = *reinterpret_cast<const uint4*>(lds + kc_off(row0 + (lane & 15), ks * 4 + (lane >> 4)));
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+struct Geo {
+  int N, H, W, th, tw;
+  long long tiles;
+};
+
+// 16-B chunk q (pixel q / 8, channel chunk q % 8) of tile t's input patch; zeros outside
+SN_DEV uint4 patch_load(const bf16_t* __restrict__ x, const Geo& g, long long t, int q) {
+  const int pix = q >> 3, kc = q & 7;
+  const int per_img = g.th * g.tw;
+  const int n = (int)(t / per_img), r = (int)(t - (long long)n * per_img);
+  const int ty = r / g.tw, tx = r - ty * g.tw;
+  const int py = pix / PATCH, px = pix - py * PATCH;
+  const int h = ty * TILE - 1 + py, w = tx * TILE - 1 + px;
+  if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return make_uint4(0, 0, 0, 0);
+  return *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + h) * g.W + w) * 64 + kc * 8);
+}
+
+// NW = 4: wave w owns output rows 4w..4w+3 x all 64 channels; NW = 8: wave (mi, ni) owns rows
+// 4mi..4mi+3 x channels 32ni..32ni+31 (two waves per SIMD to hide the LDS read latency)
+template <int NW>
+__global__ void __launch_bounds__(NW * 64, 1)
+conv3x3_c64_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const float* __restrict__ bias,
+                   const bf16_t* __restrict__ gate, bf16_t* __restrict__ y, Geo g, int relu) {
+  constexpr int NT = NW * 64, PER_T = (CHUNKS + NT - 1) / NT, NF = NW == 4 ? 4 : 2;  // N fragments per wave
+  __shared__ __attribute__((aligned(16))) char smem[W_BYTES + 2 * P_BYTES];
+  char* wl = smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mi = NW == 4 ? wave : (wave & 3), n0w = NW == 4 ? 0 : (wave >> 2) * 32;
+
+  // resident weights: tap t image, row = output channel n, chunk = 8 input channels
+  for (int q = tid; q < 9 * 64 * 8; q += NT) {
+    const int t = q / 512, rem = q - t * 512, n = rem >> 3, kc = rem & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(w + ((long long)n * 9 + t) * 64 + kc * 8);
+    *reinterpret_cast<uint4*>(wl + t * 64 * ROWB + kc_off(n, kc)) = v;
+  }
+  long long tile = blockIdx.x;
+  if (tile < g.tiles) {
+    for (int i = 0; i < PER_T; ++i) {
+      const int q = tid + i * NT;
+      if (q < CHUNKS) *reinterpret_cast<uint4*>(smem + W_BYTES + kc_off(q >> 3, q & 7)) = patch_load(x, g, tile, q);
+    }
+  }
+  __syncthreads();
+
+  int cur = 0;
+  const int mrow = lane & 15, ncol = (lane >> 4) * 4;
+  for (; tile < g.tiles; tile += gridDim.x) {
+    const long long next = tile + gridDim.x;
+    uint4 pre[PER_T];
+    if (next < g.tiles) {
+#pragma unroll
+      for (int i = 0; i < PER_T; ++i) {
+        const int q = tid + i * NT;
+        pre[i] = q < CHUNKS ? patch_load(x, g, next, q) : make_uint4(0, 0, 0, 0);
+      }
+    }
+    f32x4 acc[NF][4];
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* p = smem + W_BYTES + cur * P_BYTES;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int r = t / 3, s = t - r * 3;
+      const char* wt = wl + t * 64 * ROWB;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t fb[NF], fa[4];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) fb[i] = frag(wt, n0w + 16 * i, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fa[j] = frag(p, (4 * mi + j + r) * PATCH + s, ks, lane);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < NF; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // epilogue: lane holds output channels n .. n+3 of pixel (4 wave + j, mrow) for n = 16 i + ncol
+    const int per_img = g.th * g.tw;
+    const int n_img = (int)(tile / per_img), rr = (int)(tile - (long long)n_img * per_img);
+    const int ty = rr / g.tw, tx = rr - ty * g.tw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int h = ty * TILE + 4 * mi + j, wc = tx * TILE + mrow;
+      if (h >= g.H || wc >= g.W) continue;
+      const long long o = (((long long)n_img * g.H + h) * g.W + wc) * 64;
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        const int n = n0w + 16 * i + ncol;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (bias) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] += bias[n + k];
+        }
+        if (relu) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
+        }
+        if (gate) {
+          const uint2 gv = *reinterpret_cast<const uint2*>(gate + o + n);
+          const uint32_t gw[2] = {gv.x, gv.y};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float gf = __uint_as_float((k & 1) ? (gw[k >> 1] & 0xffff0000u) : (gw[k >> 1] << 16));
+            if (!(gf > 0.f)) v[k] = 0.f;
+          }
+        }
+        *reinterpret_cast<uint2*>(y + o + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+    if (next < g.tiles) {
+      char* pn = smem + W_BYTES + (cur ^ 1) * P_BYTES;
+#pragma unroll
+      for (int i = 0; i < PER_T; ++i) {
+        const int q = tid + i * NT;
+        if (q < CHUNKS) *reinterpret_cast<uint4*>(pn + kc_off(q >> 3, q & 7)) = pre[i];
+      }
+    }
+    __syncthreads();  // next patch in LDS; every wave is done reading this one
+    cur ^= 1;
+  }
+}
+
+}  // namespace
+
+// y[N][H][W][64] = conv3x3(x[N][H][W][64], w[64][3][3][64]) (+ bias, ReLU, gate), pad 1,
+// stride 1 — a forward conv, or a data gradient with flip-transposed weights (pad R-1-1 = 1).
+extern "C" int sn_conv3x3_c64(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* gate, bf16_t* y,
+                              long long N, long long H, long long W, long long relu, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0) return 0;
+  Geo g;
+  g.N = (int)N; g.H = (int)H; g.W = (int)W;
+  g.th = (int)((H + TILE - 1) / TILE);
+  g.tw = (int)((W + TILE - 1) / TILE);
+  g.tiles = N * g.th * g.tw;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
+  static int nw = 0;
+  if (!nw) {
+    const char* e = getenv("SN_C64_WAVES");
+    nw = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  if (nw == 4)
+    hipLaunchKernelGGL(conv3x3_c64_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st, x, w, bias, gate, y, g, (int)relu);
+  else
+    hipLaunchKernelGGL(conv3x3_c64_kernel<8>, dim3((unsigned)grid), dim3(512), 0, st, x, w, bias, gate, y, g, (int)relu);
+  return SN_CHECK_LAUNCH();
+}

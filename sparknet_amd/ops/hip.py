@@ -231,6 +231,9 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
         y, ldy = out, chan_stride(out)
     else:
         y, ldy = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device), s.K
+    if direct_c64_ok(s) and ldx == s.C and ldy == s.K and x.is_contiguous() and not _side_covers(y):
+        call("conv3x3_c64", x, _c(w), b, None, y, s.N, s.H, s.W, int(relu))
+        return y
     if _implicit_ok(s):
         kred = s.R * s.S * s.Cg
         g = _geom(s)
@@ -249,6 +252,21 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
         gemm(M, s.Kg, kpad, Dense(col, kpad, True), Dense(_c(wg), kpad, True), y2[:, g * s.Kg:], s.K,
              epi=EPI_BF16, bias=bg, relu=relu)
     return y
+
+
+# Direct 3x3 conv for 64 -> 64 channels (csrc/kernels/conv3x3.hip: resident weights, patch in
+# LDS) instead of the implicit GEMM: VGG-16's conv1_2 forward and data gradient
+_DIRECT_C64 = os.environ.get("SN_CONV_DIRECT_C64", "1") != "0"
+
+
+def direct_c64_ok(s: ConvSpec) -> bool:
+    return (_DIRECT_C64 and s.C == 64 and s.K == 64 and s.groups == 1 and s.R == 3 and s.S == 3 and s.sh == 1
+            and s.sw == 1 and s.ph == 1 and s.pw == 1 and s.dh == 1 and s.dw == 1)
+
+
+def _side_covers(t: torch.Tensor) -> bool:
+    from . import gemm as G
+    return G._SIDE is not None and G._SIDE.covers(t)  # a fused fp8 side output needs the GEMM epilogue
 
 
 def dgrad_uses_flip(s: ConvSpec) -> bool:
@@ -424,6 +442,13 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
         f8 = ws.get("fp8_dgrad") if ws is not None else None
         if f8 is not None and fp8_dgrad_ok(s) and ldd == s.K:
             return _conv_dgrad_fp8(dy, w, s, g2, kr2, pre, gate, dx, f8)
+        if (direct_c64_ok(s) and ldd == s.K and ldx == s.C and dy.is_contiguous() and dx.is_contiguous()
+                and not DGRAD_INPLACE_WEIGHTS and not _side_covers(dx)):
+            if pre is None:
+                pre = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
+                call("flip_weights", _c(w), pre, s.groups, s.Kg, s.R, s.S, s.Cg)
+            call("conv3x3_c64", dy, pre, None, _c(gate) if gate is not None else None, dx, s.N, s.H, s.W, 0)
+            return dx
         A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
         if DGRAD_INPLACE_WEIGHTS:
             B = FlipW(_c(w), s.Kg, s.R, s.S, s.Cg)

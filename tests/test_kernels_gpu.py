@@ -235,6 +235,34 @@ def test_pool_fp8_side_output(gpu, geo, e5m2):
         assert sc.slots[0, 1].item() == dx.float().abs().max().item()
 
 
+@pytest.mark.parametrize("shape", [(2, 20, 37), (3, 16, 16), (1, 56, 56)])
+def test_conv3x3_c64_direct(gpu, shape, monkeypatch):
+    """The direct 64 -> 64-channel 3x3 conv (csrc/kernels/conv3x3.hip, VGG conv1_2): forward
+    with bias + ReLU and the data gradient with the ReLU gate, against the fp32 reference
+    and the implicit-GEMM path on the same bf16 inputs."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    N, H, W = shape
+    s = ConvSpec(N, H, W, 64, 64, 3, 3, 1, 1, 1, 1, 1, 1, 1)
+    assert hip.direct_c64_ok(s)
+    x = rnd(N, H, W, 64)
+    w = rnd(64, 3, 3, 64, scale=0.1)
+    b = torch.randn(64, device="cuda")
+    dy = rnd(N, H, W, 64)
+    gate = torch.relu(rnd(N, H, W, 64).float()).to(torch.bfloat16)
+    y = hip.conv_forward(x, w, b, s, relu=True)
+    dx = hip.conv_backward(dy, gate, w, s, True, gate=gate)
+    ref = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1))
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+    dref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1)
+    close(dx, (dref.permute(0, 2, 3, 1) * (gate.float() > 0)), 1e-2)
+    monkeypatch.setattr(hip, "_DIRECT_C64", False)
+    y2 = hip.conv_forward(x, w, b, s, relu=True)
+    dx2 = hip.conv_backward(dy, gate, w, s, True, gate=gate)
+    close(y, y2, 1e-2)
+    close(dx, dx2, 1e-2)
+
+
 def test_softmax_loss_and_accuracy(gpu):
     from sparknet_amd.ops import hip
     x = rnd(256, 1000, scale=2.0)
