@@ -34,45 +34,61 @@ SN_DEV bf16x8_t frag(const char* lds, int row0, int ks, int lane) {
 }
 
 struct Geo {
-  int N, H, W, th, tw;
+  int N, H, W;   // input
+  int P, Q;      // output (P = H + 2 pad - 2)
+  int C, pad;    // input channels (<= 64, multiple of 8: stored as 128-B rows, zero-filled), padding
+  int th, tw;    // output tiles per image
   long long tiles;
 };
 
-// 16-B chunk q (pixel q / 8, channel chunk q % 8) of tile t's input patch; zeros outside
-SN_DEV uint4 patch_load(const bf16_t* __restrict__ x, const Geo& g, long long t, int q) {
-  const int pix = q >> 3, kc = q & 7;
+SN_DEV void tile_coords(const Geo& g, long long t, int& n, int& ty, int& tx) {
   const int per_img = g.th * g.tw;
-  const int n = (int)(t / per_img), r = (int)(t - (long long)n * per_img);
-  const int ty = r / g.tw, tx = r - ty * g.tw;
-  const int py = pix / PATCH, px = pix - py * PATCH;
-  const int h = ty * TILE - 1 + py, w = tx * TILE - 1 + px;
-  if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return make_uint4(0, 0, 0, 0);
-  return *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + h) * g.W + w) * 64 + kc * 8);
+  n = (int)(t / per_img);
+  const int r = (int)(t - (long long)n * per_img);
+  ty = r / g.tw;
+  tx = r - ty * g.tw;
 }
 
-// NW = 4: wave w owns output rows 4w..4w+3 x all 64 channels; NW = 8: wave (mi, ni) owns rows
-// 4mi..4mi+3 x channels 32ni..32ni+31 (two waves per SIMD to hide the LDS read latency)
-template <int NW>
+// 16-B chunk q (pixel q / 8, channel chunk q % 8) of tile t's input patch; zeros outside the
+// image and beyond the C input channels
+SN_DEV uint4 patch_load(const bf16_t* __restrict__ x, const Geo& g, long long t, int q) {
+  const int pix = q >> 3, kc = q & 7;
+  int n, ty, tx;
+  tile_coords(g, t, n, ty, tx);
+  const int py = pix / PATCH, px = pix - py * PATCH;
+  const int h = ty * TILE - g.pad + py, w = tx * TILE - g.pad + px;
+  if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W || kc * 8 >= g.C) return make_uint4(0, 0, 0, 0);
+  return *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + h) * g.W + w) * g.C + kc * 8);
+}
+
+// NW = 4: wave w owns output rows 4w..4w+3 x all KOUT channels; NW = 8: wave (mi, ni) owns rows
+// 4mi..4mi+3 x channels ni*KOUT/2 .. (two waves per SIMD to hide the LDS read latency).
+// DBUF: double-buffered patch (KOUT = 64); KOUT = 96 weights (108 KB) leave room for one
+// patch, written after a barrier while the next tile's loads wait in registers.
+template <int NW, int KOUT, bool DBUF>
 __global__ void __launch_bounds__(NW * 64, 1)
-conv3x3_c64_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const float* __restrict__ bias,
-                   const bf16_t* __restrict__ gate, bf16_t* __restrict__ y, Geo g, int relu) {
-  constexpr int NT = NW * 64, PER_T = (CHUNKS + NT - 1) / NT, NF = NW == 4 ? 4 : 2;  // N fragments per wave
-  __shared__ __attribute__((aligned(16))) char smem[W_BYTES + 2 * P_BYTES];
+conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const float* __restrict__ bias,
+               const bf16_t* __restrict__ gate, bf16_t* __restrict__ y, Geo g, int relu) {
+  constexpr int NT = NW * 64, PER_T = (CHUNKS + NT - 1) / NT;
+  constexpr int NF = (NW == 4 ? KOUT : KOUT / 2) / 16;  // N fragments per wave
+  constexpr int WB = 9 * KOUT * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[WB + (DBUF ? 2 : 1) * P_BYTES];
   char* wl = smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int mi = NW == 4 ? wave : (wave & 3), n0w = NW == 4 ? 0 : (wave >> 2) * 32;
+  const int mi = NW == 4 ? wave : (wave & 3), n0w = NW == 4 ? 0 : (wave >> 2) * (KOUT / 2);
 
-  // resident weights: tap t image, row = output channel n, chunk = 8 input channels
-  for (int q = tid; q < 9 * 64 * 8; q += NT) {
-    const int t = q / 512, rem = q - t * 512, n = rem >> 3, kc = rem & 7;
-    const uint4 v = *reinterpret_cast<const uint4*>(w + ((long long)n * 9 + t) * 64 + kc * 8);
-    *reinterpret_cast<uint4*>(wl + t * 64 * ROWB + kc_off(n, kc)) = v;
+  // resident weights w[KOUT][3][3][C]: tap t image, row = output channel n, chunk = 8 inputs
+  for (int q = tid; q < 9 * KOUT * 8; q += NT) {
+    const int t = q / (KOUT * 8), rem = q - t * (KOUT * 8), n = rem >> 3, kc = rem & 7;
+    const uint4 v = kc * 8 < g.C ? *reinterpret_cast<const uint4*>(w + ((long long)n * 9 + t) * g.C + kc * 8)
+                                 : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(wl + t * KOUT * ROWB + kc_off(n, kc)) = v;
   }
   long long tile = blockIdx.x;
   if (tile < g.tiles) {
     for (int i = 0; i < PER_T; ++i) {
       const int q = tid + i * NT;
-      if (q < CHUNKS) *reinterpret_cast<uint4*>(smem + W_BYTES + kc_off(q >> 3, q & 7)) = patch_load(x, g, tile, q);
+      if (q < CHUNKS) *reinterpret_cast<uint4*>(smem + WB + kc_off(q >> 3, q & 7)) = patch_load(x, g, tile, q);
     }
   }
   __syncthreads();
@@ -94,11 +110,11 @@ conv3x3_c64_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
     for (int i = 0; i < NF; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const char* p = smem + W_BYTES + cur * P_BYTES;
+    const char* p = smem + WB + cur * P_BYTES;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int r = t / 3, s = t - r * 3;
-      const char* wt = wl + t * 64 * ROWB;
+      const char* wt = wl + t * KOUT * ROWB;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t fb[NF], fa[4];
@@ -114,15 +130,14 @@ conv3x3_c64_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
         __builtin_amdgcn_s_setprio(0);
       }
     }
-    // epilogue: lane holds output channels n .. n+3 of pixel (4 wave + j, mrow) for n = 16 i + ncol
-    const int per_img = g.th * g.tw;
-    const int n_img = (int)(tile / per_img), rr = (int)(tile - (long long)n_img * per_img);
-    const int ty = rr / g.tw, tx = rr - ty * g.tw;
+    // epilogue: lane holds output channels n .. n+3 of pixel (4 mi + j, mrow)
+    int n_img, ty, tx;
+    tile_coords(g, tile, n_img, ty, tx);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int h = ty * TILE + 4 * mi + j, wc = tx * TILE + mrow;
-      if (h >= g.H || wc >= g.W) continue;
-      const long long o = (((long long)n_img * g.H + h) * g.W + wc) * 64;
+      if (h >= g.P || wc >= g.Q) continue;
+      const long long o = (((long long)n_img * g.P + h) * g.Q + wc) * KOUT;
 #pragma unroll
       for (int i = 0; i < NF; ++i) {
         const int n = n0w + 16 * i + ncol;
@@ -147,46 +162,64 @@ conv3x3_c64_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
         *reinterpret_cast<uint2*>(y + o + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
     }
+    if (!DBUF) __syncthreads();  // single patch buffer: every wave is done reading it
     if (next < g.tiles) {
-      char* pn = smem + W_BYTES + (cur ^ 1) * P_BYTES;
+      char* pn = smem + WB + (DBUF ? (cur ^ 1) : 0) * P_BYTES;
 #pragma unroll
       for (int i = 0; i < PER_T; ++i) {
         const int q = tid + i * NT;
         if (q < CHUNKS) *reinterpret_cast<uint4*>(pn + kc_off(q >> 3, q & 7)) = pre[i];
       }
     }
-    __syncthreads();  // next patch in LDS; every wave is done reading this one
-    cur ^= 1;
+    __syncthreads();  // next patch in LDS (DBUF: and every wave is done reading this one)
+    if (DBUF) cur ^= 1;
   }
 }
 
 }  // namespace
 
-// y[N][H][W][64] = conv3x3(x[N][H][W][64], w[64][3][3][64]) (+ bias, ReLU, gate), pad 1,
-// stride 1 — a forward conv, or a data gradient with flip-transposed weights (pad R-1-1 = 1).
-extern "C" int sn_conv3x3_c64(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* gate, bf16_t* y,
-                              long long N, long long H, long long W, long long relu, hipStream_t st) {
-  if (N <= 0 || H <= 0 || W <= 0) return 0;
-  Geo g;
-  g.N = (int)N; g.H = (int)H; g.W = (int)W;
-  g.th = (int)((H + TILE - 1) / TILE);
-  g.tw = (int)((W + TILE - 1) / TILE);
-  g.tiles = N * g.th * g.tw;
+static int cu_count() {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   }
+  return cus;
+}
+
+// y[N][P][Q][K] = conv3x3(x[N][H][W][C], w[K][3][3][C]) (+ bias, ReLU, gate), stride 1, pad
+// 0 or 1 (P = H + 2 pad - 2) — a forward conv, or a data gradient with flip-transposed
+// weights.  K = 64 (VGG-16 conv1_2: C = 64, pad 1) or 96 (CaffeNet / AlexNet conv1 after the
+// space-to-depth fold: C = 48, pad 0); C <= 64, multiple of 8.
+extern "C" int sn_conv3x3_direct(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* gate, bf16_t* y,
+                                 long long N, long long H, long long W, long long C, long long K, long long pad,
+                                 long long relu, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0) return 0;
+  if (C <= 0 || C > 64 || C % 8 || (K != 64 && K != 96) || (pad != 0 && pad != 1)) return 3;
+  Geo g;
+  g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C; g.pad = (int)pad;
+  g.P = (int)(H + 2 * pad - 2);
+  g.Q = (int)(W + 2 * pad - 2);
+  if (g.P <= 0 || g.Q <= 0) return 3;
+  g.th = (g.P + TILE - 1) / TILE;
+  g.tw = (g.Q + TILE - 1) / TILE;
+  g.tiles = N * g.th * g.tw;
+  const int cus = cu_count();
   const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
   static int nw = 0;
   if (!nw) {
     const char* e = getenv("SN_C64_WAVES");
     nw = (e && atoi(e) == 4) ? 4 : 8;
   }
-  if (nw == 4)
-    hipLaunchKernelGGL(conv3x3_c64_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st, x, w, bias, gate, y, g, (int)relu);
+  if (K == 96)
+    hipLaunchKernelGGL((conv3x3_kernel<8, 96, false>), dim3((unsigned)grid), dim3(512), 0, st, x, w, bias, gate, y, g,
+                       (int)relu);
+  else if (nw == 4)
+    hipLaunchKernelGGL((conv3x3_kernel<4, 64, true>), dim3((unsigned)grid), dim3(256), 0, st, x, w, bias, gate, y, g,
+                       (int)relu);
   else
-    hipLaunchKernelGGL(conv3x3_c64_kernel<8>, dim3((unsigned)grid), dim3(512), 0, st, x, w, bias, gate, y, g, (int)relu);
+    hipLaunchKernelGGL((conv3x3_kernel<8, 64, true>), dim3((unsigned)grid), dim3(512), 0, st, x, w, bias, gate, y, g,
+                       (int)relu);
   return SN_CHECK_LAUNCH();
 }

@@ -231,8 +231,8 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
         y, ldy = out, chan_stride(out)
     else:
         y, ldy = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device), s.K
-    if direct_c64_ok(s) and ldx == s.C and ldy == s.K and x.is_contiguous() and not _side_covers(y):
-        call("conv3x3_c64", x, _c(w), b, None, y, s.N, s.H, s.W, int(relu))
+    if direct_conv_ok(s) and ldx == s.C and ldy == s.K and x.is_contiguous() and not _side_covers(y):
+        call("conv3x3_direct", x, _c(w), b, None, y, s.N, s.H, s.W, s.C, s.K, s.ph, int(relu))
         return y
     if _implicit_ok(s):
         kred = s.R * s.S * s.Cg
@@ -254,14 +254,25 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
     return y
 
 
-# Direct 3x3 conv for 64 -> 64 channels (csrc/kernels/conv3x3.hip: resident weights, patch in
-# LDS) instead of the implicit GEMM: VGG-16's conv1_2 forward and data gradient
+# Direct 3x3 / stride-1 conv (csrc/kernels/conv3x3.hip: resident weights, input patch in LDS)
+# instead of the implicit GEMM for two thin shapes: 64 -> 64 channels with pad 1 (VGG-16's
+# conv1_2 forward and data gradient) and 48 -> 96 with pad 0 (CaffeNet / AlexNet conv1 after
+# the space-to-depth fold)
 _DIRECT_C64 = os.environ.get("SN_CONV_DIRECT_C64", "1") != "0"
+_DIRECT_K96 = os.environ.get("SN_CONV_DIRECT_K96", "0") == "1"
 
 
 def direct_c64_ok(s: ConvSpec) -> bool:
     return (_DIRECT_C64 and s.C == 64 and s.K == 64 and s.groups == 1 and s.R == 3 and s.S == 3 and s.sh == 1
             and s.sw == 1 and s.ph == 1 and s.pw == 1 and s.dh == 1 and s.dw == 1)
+
+
+def direct_conv_ok(s: ConvSpec) -> bool:
+    """Forward products the direct kernel takes (the data gradient: direct_c64_ok only)."""
+    if direct_c64_ok(s):
+        return True
+    return (_DIRECT_K96 and s.C == 48 and s.K == 96 and s.groups == 1 and s.R == 3 and s.S == 3 and s.sh == 1
+            and s.sw == 1 and s.ph == 0 and s.pw == 0 and s.dh == 1 and s.dw == 1)
 
 
 def _side_covers(t: torch.Tensor) -> bool:
@@ -447,7 +458,8 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
             if pre is None:
                 pre = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
                 call("flip_weights", _c(w), pre, s.groups, s.Kg, s.R, s.S, s.Cg)
-            call("conv3x3_c64", dy, pre, None, _c(gate) if gate is not None else None, dx, s.N, s.H, s.W, 0)
+            call("conv3x3_direct", dy, pre, None, _c(gate) if gate is not None else None, dx, s.N, s.H, s.W, 64, 64, 1,
+                 0)
             return dx
         A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
         if DGRAD_INPLACE_WEIGHTS:

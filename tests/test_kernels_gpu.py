@@ -263,6 +263,26 @@ def test_conv3x3_c64_direct(gpu, shape, monkeypatch):
     close(dx, dx2, 1e-2)
 
 
+@pytest.mark.parametrize("shape", [(2, 57, 57), (1, 20, 35)])
+def test_conv3x3_k96_direct(gpu, shape, monkeypatch):
+    """The direct 3x3 conv for 48 -> 96 channels, pad 0 (CaffeNet conv1 after the
+    space-to-depth fold) with bias + ReLU, against the fp32 reference and the GEMM path."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    N, H, W = shape
+    s = ConvSpec(N, H, W, 48, 96, 3, 3, 1, 1, 0, 0, 1, 1, 1)
+    monkeypatch.setattr(hip, "_DIRECT_K96", True)
+    assert hip.direct_conv_ok(s)
+    x = rnd(N, H, W, 48)
+    w = rnd(96, 3, 3, 48, scale=0.1)
+    b = torch.randn(96, device="cuda")
+    y = hip.conv_forward(x, w, b, s, relu=True)
+    ref = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b))
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+    monkeypatch.setattr(hip, "_DIRECT_K96", False)
+    close(y, hip.conv_forward(x, w, b, s, relu=True), 1e-2)
+
+
 def test_softmax_loss_and_accuracy(gpu):
     from sparknet_amd.ops import hip
     x = rnd(256, 1000, scale=2.0)
