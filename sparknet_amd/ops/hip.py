@@ -259,7 +259,7 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
 # conv1_2 forward and data gradient) and 48 -> 96 with pad 0 (CaffeNet / AlexNet conv1 after
 # the space-to-depth fold)
 _DIRECT_C64 = os.environ.get("SN_CONV_DIRECT_C64", "1") != "0"
-_DIRECT_K96 = os.environ.get("SN_CONV_DIRECT_K96", "0") == "1"
+_DIRECT_K96 = os.environ.get("SN_CONV_DIRECT_K96", "1") != "0"
 
 
 def direct_c64_ok(s: ConvSpec) -> bool:
