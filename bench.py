@@ -138,12 +138,21 @@ def main():
     from sparknet_amd.ops import _lib
     from sparknet_amd.parallel import Comm
 
+    from sparknet_amd.parallel import diag
+    rccl_log = None
+    if world > 1 and dev.type == "cuda" and not args.share_gpu:
+        rccl_log = diag.rccl_debug_env()  # channels / transports for the JSON (RCCL debug log)
     if dev.type == "cuda":
         _lib.kernels()
     comm = (Comm(backend="gloo" if args.share_gpu else None, device=dev if dev.type == "cuda" else None,
                  watchdog=True, timeout_s=600.0) if world > 1 else None)
-    if comm is not None:
-        assert comm.world_size == world == args.gpus, (comm.world_size, world, args.gpus)
+    bad = diag.check_placement(comm, args.gpus, args.share_gpu or dev.type != "cuda",
+                               torch.cuda.current_device() if dev.type == "cuda" else local_rank, local_rank)
+    if bad is not None:
+        print(f"bench.py rank {rank}: FATAL placement error: {bad}", file=sys.stderr, flush=True)
+        if comm is not None:
+            comm.abort()
+        return 3
     B, C, HW, crop, classes, mean, in_scale = DEFAULTS[args.model]
     B = args.batch or B
     kw = dict(train_batch=B, test_batch=max(1, min(B, 50)))
@@ -211,7 +220,7 @@ def main():
         print(f"rank {rank} step ms: " + " ".join(f"{v:.2f}" for v in ms), file=sys.stderr, flush=True)
     per_rank_ms = [round(1000.0 * elapsed_rank / args.steps, 3)]
     avg_ms = [e[0].elapsed_time(e[1]) for e in avg_events if e is not None]
-    comm_info = avg_check = None
+    comm_info = avg_check = bucket_ms = numa_all = None
     if comm is not None:
         elapsed = comm.max_over_ranks(elapsed_rank)
         per_rank_ms = [round(1000.0 * v / args.steps, 3) for v in comm.allgather_float(elapsed_rank)]
@@ -220,6 +229,8 @@ def main():
             trainer.average()
             avg_check = verify_average(comm, net, dev, sync)
         comm_info = comm_bench(comm, net.flat_data, dev, sync, iters=1 if args.share_gpu else 4)
+        bucket_ms = diag.timed_bucket_allreduce(comm, net.flat_data, comm.average_bucket_bytes, sync)
+        numa_all = comm.allgather_int(int(numa))
     final_loss = float(loss) if loss is not None else float("nan")
 
     ms = 1000.0 * elapsed / args.steps
@@ -262,6 +273,14 @@ def main():
             "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2) if dev.type == "cuda" else None,
             "numa_node_rank0": numa,
         }
+        if comm is not None:
+            out["diag"] = {
+                "rccl_version": diag.rccl_version() if comm.backend == "nccl" else None,
+                "rccl_log_rank0": diag.read_rccl_logs(rccl_log),
+                "bucket_allreduce_ms": bucket_ms,
+                "numa_node_per_rank": numa_all,
+                "step_spread_pct": round(100.0 * (max(per_rank_ms) / max(min(per_rank_ms), 1e-9) - 1.0), 2),
+            }
         if comm_info is not None:
             out["comm_bench"] = comm_info
         if avg_check is not None:

@@ -704,6 +704,13 @@ int sn_forward(void* s, float* loss) {
   if (loss) *loss = (float)PyFloat_AsDouble(r);
   Py_DECREF(r);
   build_forward(s, 0);
+  if (NativeForward* nf = native_forward(s, 0)) {
+    // forward_plan replayed the captured graph once, so the net's blobs hold THAT forward:
+    // report its loss (differs from the eager one only through fresh dropout draws)
+    HIPOK(hipMemcpyAsync(nf->out_host, nf->loss_dev, sizeof(float), hipMemcpyDeviceToHost, nf->stream));
+    HIPOK(hipStreamSynchronize(nf->stream));
+    if (loss) *loss = nf->out_host[0];
+  }
   return 0;
 }
 
@@ -718,6 +725,10 @@ int sn_solver_step(void* s, int iters) {
     g_err = "null state";
     return 1;
   }
+  // steps (eager Python iterations, or the step graph's capture / replays) rebind or
+  // rewrite the train net's blobs: a forward plan's buffers are no longer what the net
+  // (sn_backward, sn_blob_get) sees
+  invalidate(s, P_FWD_TRAIN);
   NativeState& st = native_state(s);
   NativeStep* ns = st.step.get();
   if (!ns) {

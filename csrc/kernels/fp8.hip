@@ -5,7 +5,8 @@
 // A scale slot is float[8]: [0] quantisation scale s (x_fp8 = sat(x * s)), [1] amax of the
 // tensors quantised with this slot since the last update (float bits, atomicMax),
 // [2] dequantisation factor 1/s (read by the GEMM epilogue), [3] 1 once a measured amax
-// has been turned into a scale, [4] the format's largest normal (e4m3 448, e5m2 57344).
+// has been turned into a scale, [4] the format's largest normal (e4m3 448, e5m2 57344),
+// [5] write position of the slot's amax-history ring (fp8_update_scales_kernel).
 // fp8_update_scales (once per iteration, inside the captured graph) turns the running
 // amax into the next iteration's scale: s = max / amax.  e4m3 (3 mantissa bits) carries
 // activations and weights; e5m2 (2 mantissa bits, 2^32 of range) is the option for the
@@ -97,11 +98,25 @@ __global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict
   block_amax_to_slot(amax, slot);
 }
 
-__global__ void fp8_update_scales_kernel(float* __restrict__ slots, int n, float margin) {
+// Delayed scaling with an amax HISTORY: the iteration's measured amax goes into a ring of
+// the last `hist_len` amaxes (hist[i][pos], pos = slot[5]) and the next scale is derived
+// from the ring's maximum times `margin`, so one quiet iteration after a spike (or one
+// spike) does not swing the scale and saturate / flush the next iteration's values.
+// hist_len == 0: the one-iteration delayed scale (the ring is not used).
+__global__ void fp8_update_scales_kernel(float* __restrict__ slots, float* __restrict__ hist, int hist_len, int n,
+                                         float margin) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float* s = slots + SLOT * i;
-  const float amax = s[1];
+  float amax = s[1];
+  if (hist_len > 0 && amax > 0.f) {
+    float* h = hist + (long long)i * hist_len;
+    int pos = (int)s[5];
+    pos = pos >= 0 && pos < hist_len ? pos : 0;
+    h[pos] = amax;
+    s[5] = (float)(pos + 1 == hist_len ? 0 : pos + 1);
+    for (int k = 0; k < hist_len; ++k) amax = fmaxf(amax, h[k]);
+  }
   if (amax > 0.f) {
     const float sc = (s[4] > 0.f ? s[4] : E4M3_MAX) / (amax * margin);
     s[0] = sc;
@@ -138,9 +153,11 @@ extern "C" int sn_quant_fp8(const bf16_t* x, uint8_t* q, long long n, float* slo
   return SN_CHECK_LAUNCH();
 }
 
-extern "C" int sn_fp8_update_scales(float* slots, long long n, float margin, hipStream_t st) {
+extern "C" int sn_fp8_update_scales(float* slots, float* hist, long long hist_len, long long n, float margin,
+                                    hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, slots, (int)n,
-                     margin);
+  if (hist_len > 0 && !hist) return 7;
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, slots, hist,
+                     (int)hist_len, (int)n, margin);
   return SN_CHECK_LAUNCH();
 }

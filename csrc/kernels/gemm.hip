@@ -97,6 +97,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   // fused fp8 side output: unsplit bf16 epilogues of gemm_kernel (not gemm256_kernel, tiles
   // 6-9), whole 8-byte chunks
   if (a.q_out && (a.splits != 1 || (a.epi != EPI_BF16 && a.epi != EPI_BF16_DROP) || (a.tile >= 6 && a.tile <= 9) ||
+                  a.tile >= 30 ||
                   (a.N % 8) || (a.q_ld % 8) || (a.q_gstride % 8) || !a.q_slot || !a.q_part ||
                   (reinterpret_cast<unsigned long long>(a.q_out) & 7)))
     return 6;
@@ -134,6 +135,12 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 16:
     case 17:
     case 18: return a.epi == EPI_SGD ? 4 : sn_gemm_big4(a, stream);  // gemm_big4.hip
+    case 30:
+    case 31:
+    case 32: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_a(a, stream);  // gemm_pk.hip (persistent ring)
+    case 33:
+    case 34:
+    case 36: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_b(a, stream);  // gemm_pk2.hip
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

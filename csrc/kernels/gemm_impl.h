@@ -1453,3 +1453,5 @@ int sn_gemm_t256(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big8(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big4(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_fp8_big(const SnGemmArgs& a, hipStream_t stream);
+int sn_gemm_pk_a(const SnGemmArgs& a, hipStream_t stream);
+int sn_gemm_pk_b(const SnGemmArgs& a, hipStream_t stream);

@@ -32,6 +32,7 @@ p.add_argument("--lr", type=float, default=0.005)
 p.add_argument("--modes", default="bf16,fp8,fp8dg,fp8dg5")
 p.add_argument("--window", type=int, default=20)
 p.add_argument("--noise", type=float, default=0.8)
+p.add_argument("--seed", type=int, default=12)
 args = p.parse_args()
 dev = torch.device("cuda:0")
 
@@ -40,7 +41,7 @@ templates = torch.randn(args.classes, 3, args.crop, args.crop, generator=g0)
 
 
 def batches():
-    g = torch.Generator().manual_seed(12)
+    g = torch.Generator().manual_seed(args.seed)
     while True:
         y = torch.randint(0, args.classes, (args.batch,), generator=g)
         x = templates[y] + args.noise * torch.randn(args.batch, 3, args.crop, args.crop, generator=g)
@@ -54,7 +55,11 @@ def run(mode):
     solver = Solver(sp, device=dev, seed=5, build_test_nets=False)
     fuse_relu(solver.net)
     n8 = 0
-    if mode != "bf16":
+    # bf16alt: bf16 with every GEMM on the 128x128 tile and cost-model split-K (a different
+    # fp32 accumulation order): how far two bf16 runs drift apart on their own (chaos floor)
+    from sparknet_amd.ops import gemm as _G
+    _G._FORCE_TILE = 0 if mode == "bf16alt" else -1
+    if mode not in ("bf16", "bf16alt"):
         n8 = enable_fp8(solver.net, 0.0, dgrad=mode.startswith("fp8dg"),
                         dgrad_format="e5m2" if mode == "fp8dg5" else "e4m3")
     it = batches()

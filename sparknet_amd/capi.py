@@ -210,12 +210,19 @@ class CoreState:
     # -- native forward / test (csrc/core/sn_core.cpp NativeForward) ------------------------
     # sn_forward and sn_solver_test on a GPU state replay a captured forward-only graph of
     # the train net / the test net (ccaffe.cpp:181-187 forward, 218-228 solver_test ->
-    # TestAndStoreResult).  The test graph also adds every output blob's sum into a device
-    # accumulator, so n test iterations are n graph launches and ONE host read at the end.
+    # TestAndStoreResult).  The test graph also adds every element of every output blob
+    # into a device accumulator (one score per element, solver.cpp:427-440), so n test
+    # iterations are n graph launches and ONE host read at the end.
+    #
+    # Capturing rebinds the Python-visible blobs and saved layer buffers (masks, folds,
+    # loss state) to the graph's own memory, which the capture itself never writes: the
+    # plan therefore replays the graph once on the same staged batch, so the net is left
+    # in the state of that replay (sn_backward, blob reads), and the caller reports the
+    # replay's loss.  Any later Python forward of the same net rebinds the blobs again,
+    # so sn_core.cpp drops the plan whenever one can run (invalidate(P_FWD_*)).
     def forward_plan(self, test: bool) -> dict:
-        """Capture (not run) one forward pass; called right after the Python verb ran the
-        same forward eagerly, so every GEMM is already autotuned and no layer state (BN
-        running averages, callbacks) is touched twice."""
+        """Capture one forward pass and replay it once; called right after the Python
+        verb ran the same forward eagerly, so every GEMM is already autotuned."""
         net = self.test_net if test else self.net
         if self.device.type != "cuda" or net is None:
             raise RuntimeError("native forward needs a GPU net")
@@ -225,7 +232,8 @@ class CoreState:
         for layer, _, _ in feeds:
             layer.set_source(None)
         outs = net.output_blobs if test else []
-        acc = torch.zeros(max(1, len(outs)), dtype=torch.float32, device=dev)
+        n_out = sum(int(b.count) for b in outs)
+        acc = torch.zeros(max(1, n_out), dtype=torch.float32, device=dev)
         loss_buf = torch.zeros(1, dtype=torch.float32, device=dev)
         graph = torch.cuda.CUDAGraph()
         try:
@@ -234,15 +242,17 @@ class CoreState:
                 if torch.is_tensor(loss):
                     loss_buf.copy_(loss.reshape(1).float())
                 if outs:
-                    acc.add_(torch.stack([b.data.float().sum() for b in outs]))
+                    acc.add_(torch.cat([b.nchw().float().reshape(-1) for b in outs]))
         finally:
             for layer, src, _ in feeds:
                 layer.set_source(src)
+        graph.replay()  # the blobs now hold a real forward of the staged batch (see above)
         torch.cuda.synchronize(dev)
+        acc.zero_()
         self.__dict__.setdefault("_fwd_graphs", {})[bool(test)] = (graph, acc, loss_buf)
         return {"exec": int(graph.raw_cuda_graph_exec()),
                 "stream": int(torch.cuda.current_stream(dev).cuda_stream),
-                "loss_dev": int(loss_buf.data_ptr()), "acc_dev": int(acc.data_ptr()), "n_out": len(outs),
+                "loss_dev": int(loss_buf.data_ptr()), "acc_dev": int(acc.data_ptr()), "n_out": n_out,
                 "feeds": [f for _, _, f in feeds]}
 
     def weights_plan(self) -> dict:
@@ -265,15 +275,17 @@ class CoreState:
         self.scores = [float(v) for v in scores]
 
     def test(self, n: int) -> int:
-        """solver_test -> TestAndStoreResult (solver.cpp:413-444): sum of every output
-        blob over n forwards; returns the number of scores."""
+        """solver_test -> TestAndStoreResult (solver.cpp:413-444): one score per ELEMENT
+        of every output blob (Caffe's NCHW element order), summed over n forwards;
+        returns the number of scores."""
         net = self.test_net
         sums = None
         for _ in range(n):
             net.forward()
-            v = [float(b.data.float().sum()) for b in net.output_blobs]
-            sums = v if sums is None else [a + b for a, b in zip(sums, v)]
-        self.scores = sums or []
+            v = torch.cat([b.nchw().float().reshape(-1) for b in net.output_blobs]) if net.output_blobs else None
+            if v is not None:
+                sums = v.clone() if sums is None else sums + v
+        self.scores = [float(x) for x in sums.cpu()] if sums is not None else []
         return len(self.scores)
 
     # -- weights --------------------------------------------------------------------------------

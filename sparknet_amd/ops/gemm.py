@@ -114,11 +114,16 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
          6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64),
          11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192), 15: (128, 192), 16: (192, 128),
-         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64)}
+         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64),
+         # persistent ring-pipelined tiles (csrc/kernels/gemm_pk.h): one 512-thread block per CU
+         30: (256, 128), 31: (256, 64), 32: (256, 96), 33: (128, 128), 34: (256, 192), 36: (128, 256)}
+PK_TILES = frozenset((30, 31, 32, 33, 34, 36))
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
-_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512}
-_KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55}
+_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512,
+          30: 256, 31: 256, 32: 256, 33: 256, 34: 256, 36: 256}
+_KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55,
+             30: 0.75, 31: 0.45, 32: 0.6, 33: 0.45, 34: 1.1, 36: 0.75}
 # autotune candidates 11-14 (SN_GEMM_TILE8W=0 drops them)
 _TILE8W = os.environ.get("SN_GEMM_TILE8W", "1") != "0"
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
@@ -398,7 +403,8 @@ def _side_fields(side, out, ldc, c_gstride, N, tile, epi, lds):
     launch cannot store the side output (the side is then marked incomplete)."""
     off = (out.data_ptr() - side.base.data_ptr()) // 2
     qp = side.q.data_ptr() + off
-    if ((not lds and not _SIDE_FRAG) or epi not in (EPI_BF16, EPI_BF16_DROP) or tile in (6, 7, 8, 9) or N % 8 or ldc % 8
+    if ((not lds and not _SIDE_FRAG) or epi not in (EPI_BF16, EPI_BF16_DROP) or tile in (6, 7, 8, 9) or tile in PK_TILES
+            or N % 8 or ldc % 8
             or c_gstride % 8 or qp % 8):
         side.ok = False
         return None

@@ -948,7 +948,9 @@ def augment(src_u8, dst, crop, mean=None, mean_mode=0, scale=1.0, rng_state=None
 # FP8 (e4m3) forward products with per-tensor delayed scaling
 # --------------------------------------------------------------------------------------
 
-FP8_MARGIN = 1.0  # quantisation scale = 448 / (amax * margin)
+FP8_MARGIN = float(os.environ.get("SN_FP8_MARGIN", "1.0"))  # quantisation scale = 448 / (amax * margin)
+# delayed scaling over the max of the last FP8_HISTORY iterations' amaxes (0: last iteration only)
+FP8_HISTORY = int(os.environ.get("SN_FP8_HISTORY", "16"))
 
 
 E4M3_MAX, E5M2_MAX = 448.0, 57344.0
@@ -966,6 +968,8 @@ class Fp8Scales:
         self.slots[:, 4] = E4M3_MAX
         self.n = n
         self._e5m2 = set()
+        self.history = FP8_HISTORY
+        self.hist = torch.zeros((max(n, 1), max(1, self.history)), dtype=torch.float32, device=device)
 
     def set_e5m2(self, i: int) -> None:
         self.slots[i, 4] = E5M2_MAX
@@ -981,7 +985,7 @@ class Fp8Scales:
         return self.slots[i, 2:3]
 
     def update(self) -> None:
-        call("fp8_update_scales", self.slots, self.n, float(FP8_MARGIN))
+        call("fp8_update_scales", self.slots, self.hist, int(self.history), self.n, float(FP8_MARGIN))
         self.updates += 1
 
 

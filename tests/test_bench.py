@@ -31,6 +31,9 @@ def test_bench_spawns_n_ranks_and_reports_job_json():
     assert out["steps"] == 3 and out["averages_in_window"] >= 1
     assert out["ms_per_step"] >= max(out["per_rank_ms_per_step"]) - 1e-3  # slowest rank's clock
     assert set(out["comm_bench"]) == {"bucket_256MB", "bucket_64MB", "bucket_16MB"}
+    d = out["diag"]  # self-diagnosis block of every N > 1 run (parallel/diag.py)
+    assert len(d["bucket_allreduce_ms"]) >= 1 and all(v >= 0 for v in d["bucket_allreduce_ms"])
+    assert len(d["numa_node_per_rank"]) == 2 and d["step_spread_pct"] >= 0
 
 
 def test_bench_refuses_world_mismatch():

@@ -219,3 +219,68 @@ def test_native_test_forward_weights_match_python(core_lib):
     np.testing.assert_allclose(s_nat, s_py, rtol=1e-3)
     np.testing.assert_allclose(l_nat, l_py, rtol=1e-3)
     assert np.array_equal(w_nat, w_py)
+
+
+def _blob(lib, st, layer, index, diff):
+    nd = lib.sn_blob_num_axes(st, layer, index)
+    cnt = int(np.prod([lib.sn_blob_axis_shape(st, layer, index, a) for a in range(nd)])) if nd > 0 else 1
+    buf = (C.c_float * cnt)()
+    assert lib.sn_blob_get(st, layer, index, diff, buf, C.c_longlong(cnt)) == 0, lib.sn_last_error()
+    return np.frombuffer(buf, dtype=np.float32).copy()
+
+
+def _ctypes_fwd_bwd(core_lib, native_verbs):
+    """sn_forward -> sn_backward -> blob / parameter-gradient reads, on the first call and
+    again after an intervening sn_solver_step (a captured forward plan must
+    leave the net's blobs holding a real forward, and be dropped once a step rebinds them)."""
+    lib = C.CDLL(core_lib)
+    lib.sn_create_state.restype = C.c_void_p
+    lib.sn_last_error.restype = C.c_char_p
+    os.environ["SN_NATIVE_STEP"] = "0"
+    try:
+        st = C.c_void_p(lib.sn_create_state())
+        buf, n = C.c_char_p(), C.c_int()
+        assert lib.sn_parse_solver_prototxt(SOLVER.encode(), C.byref(buf), C.byref(n)) == 0
+        assert lib.sn_set_device(st, 0) == 0
+        assert lib.sn_load_solver_from_protobuf(st, buf, n) == 0, lib.sn_last_error()
+        calls = [0]
+
+        def fill(p, batch, nd, shape, user):
+            cnt = int(np.prod([shape[i] for i in range(nd)]))
+            arr = np.ctypeslib.as_array(p, shape=(cnt,))
+            if nd == 4:
+                arr[:] = np.cos(0.31 * (np.arange(cnt) + 5 * calls[0])).astype(np.float32)
+                calls[0] += 1
+            else:
+                arr[:] = (np.arange(cnt) + calls[0]) % 3
+        cb = CB(fill)
+        assert lib.sn_set_train_data_callback(st, 0, cb, None) == 0
+        assert lib.sn_set_train_data_callback(st, 1, cb, None) == 0
+        assert lib.sn_solver_step(st, 3) == 0, lib.sn_last_error()
+        os.environ["SN_NATIVE_STEP"] = "1" if native_verbs else "0"
+        out = []
+        for rnd in range(3):
+            for _ in range(2):  # the first sn_forward builds the plan, the second replays it
+                loss = C.c_float()
+                assert lib.sn_forward(st, C.byref(loss)) == 0, lib.sn_last_error()
+                assert lib.sn_backward(st) == 0, lib.sn_last_error()
+                out.append((loss.value, _blob(lib, st, -1, 4, 0), _blob(lib, st, -1, 3, 0),
+                            _blob(lib, st, 5, 0, 1), _blob(lib, st, 2, 0, 1)))
+            assert lib.sn_solver_step(st, 2 if rnd == 0 else 5) == 0, lib.sn_last_error()
+        lib.sn_free(buf)
+        lib.sn_destroy_state(st)
+        return out, calls[0]
+    finally:
+        os.environ.pop("SN_NATIVE_STEP", None)
+
+
+@pytest.mark.gpu
+def test_native_forward_then_backward_and_blob_reads(core_lib):
+    py, c_py = _ctypes_fwd_bwd(core_lib, False)
+    nat, c_nat = _ctypes_fwd_bwd(core_lib, True)
+    assert c_py == c_nat
+    for a, b in zip(py, nat):
+        np.testing.assert_allclose(b[0], a[0], rtol=1e-3)
+        for x, y in zip(a[1:], b[1:]):
+            assert np.isfinite(y).all()
+            np.testing.assert_allclose(y, x, rtol=2e-2, atol=2e-2 * (np.abs(x).max() + 1e-6))
