@@ -51,6 +51,9 @@ def parse():
                    help="--dtype fp8: keep the data gradients in bf16 (default: the data gradients of stride-1 "
                         "convs run as fp8 products too, engine.enable_fp8 dgrad; weight gradients stay bf16; "
                         "VGG-16 b2048 8.82k vs 8.47k img/s, profiles/r3_fp8_dgrad.txt)")
+    p.add_argument("--no-fp8-wgrad", dest="fp8_wgrad", action="store_false",
+                   help="--dtype fp8: keep the weight gradients in bf16 (default: layers with an fp8 forward AND an "
+                        "fp8 data gradient also run their weight gradient as an fp8 product, reduction over pixels)")
     p.add_argument("--fp8-dgrad-format", default="e4m3", choices=["e4m3", "e5m2"],
                    help="fp8 data gradients: format of the quantised output gradients")
     p.add_argument("--overlap-update", action="store_true",
@@ -168,7 +171,8 @@ def main():
                           scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev,
                           group=args.feed_group)
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
-    n_fp8 = enable_fp8(net, args.fp8_min_work, dgrad=args.fp8_dgrad, dgrad_format=args.fp8_dgrad_format) if args.dtype == "fp8" else 0
+    n_fp8 = (enable_fp8(net, args.fp8_min_work, dgrad=args.fp8_dgrad, dgrad_format=args.fp8_dgrad_format,
+                        wgrad=args.fp8_dgrad and args.fp8_wgrad) if args.dtype == "fp8" else 0)
     trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph and not args.cpu,
                               overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc,
                               streams=args.streams)
@@ -258,7 +262,7 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "algorithm": f"local SGD, tau={args.tau}, RCCL all-reduce weight averaging",
-                "hipgraph": trainer.use_graph, "streams": args.streams, "feed_group": feeder.group, "fused_input_fold": fused_fold, "fp8_layers": n_fp8, "fp8_dgrad": (args.fp8_dgrad_format if n_fp8 and args.fp8_dgrad else None),
+                "hipgraph": trainer.use_graph, "streams": args.streams, "feed_group": feeder.group, "fused_input_fold": fused_fold, "fp8_layers": n_fp8, "fp8_dgrad": (args.fp8_dgrad_format if n_fp8 and args.fp8_dgrad else None), "fp8_wgrad": bool(n_fp8 and args.fp8_dgrad and args.fp8_wgrad),
                 "final_loss": round(final_loss, 4),
             },
             "rccl_world": comm.world_size if comm is not None else 1,

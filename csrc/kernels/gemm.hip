@@ -84,6 +84,25 @@ int launch_fp8(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   return SN_CHECK_LAUNCH();
 }
 
+// fp8 weight gradients: dy^T (MC dense, e4m3 / e5m2) x x (MC: implicit im2col of the
+// layer input, or a dense activation matrix), reduction over the pixel / batch rows, fp32
+// (split-K slab / accumulate) epilogues only; 128x128 tile (read_frag8_mc)
+template <int BMODE, int FMT>
+int launch_fp8_mc(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
+  switch (a.epi) {
+    case EPI_F32:
+      hipLaunchKernelGGL((gemm_kernel<1, OP_DENSE, 1, BMODE, EPI_F32, 128, 128, 4, 2, FMT>), grid, dim3(256), 0, st, a);
+      break;
+    case EPI_F32_ACC:
+      hipLaunchKernelGGL((gemm_kernel<1, OP_DENSE, 1, BMODE, EPI_F32_ACC, 128, 128, 4, 2, FMT>), grid, dim3(256), 0, st,
+                         a);
+      break;
+    default:
+      return 2;
+  }
+  return SN_CHECK_LAUNCH();
+}
+
 }  // namespace
 
 
@@ -102,9 +121,19 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
                   (reinterpret_cast<unsigned long long>(a.q_out) & 7)))
     return 6;
   if (a.fp8) {
+    if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || !a.deq_a || !a.deq_b) return 3;
+    if (a.a_mc || a.b_mc) {
+      if (!a.a_mc || a.a_mode != OP_DENSE || !a.b_mc || (a.b_mode != OP_IM2COL && a.b_mode != OP_DENSE) ||
+          a.ones_col >= 0 || (a.fp8 != 1 && a.fp8 != 2))
+        return 3;
+      const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
+      dim3 grid(tiles * a.splits * a.groups);
+      if (a.b_mode == OP_IM2COL)
+        return a.fp8 == 1 ? launch_fp8_mc<OP_IM2COL, 1>(a, grid, stream) : launch_fp8_mc<OP_IM2COL, 2>(a, grid, stream);
+      return a.fp8 == 1 ? launch_fp8_mc<OP_DENSE, 1>(a, grid, stream) : launch_fp8_mc<OP_DENSE, 2>(a, grid, stream);
+    }
     // e4m3 forward products: A (dense or implicit im2col) and B dense, both K-contiguous
-    if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || a.a_mc || a.b_mc || a.b_mode != OP_DENSE || !a.deq_a || !a.deq_b)
-      return 3;
+    if (a.b_mode != OP_DENSE) return 3;
     if (a.tile == 11 || a.tile == 16) return sn_gemm_fp8_big(a, stream);  // gemm_fp8big.hip
     const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     dim3 grid(tiles * a.splits * a.groups);
@@ -140,7 +169,9 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 32: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_a(a, stream);  // gemm_pk.hip (persistent ring)
     case 33:
     case 34:
-    case 36: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_b(a, stream);  // gemm_pk2.hip
+    case 36:
+    case 37:
+    case 38: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_b(a, stream);  // gemm_pk2.hip
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

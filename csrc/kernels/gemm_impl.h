@@ -125,6 +125,11 @@ SN_DEV int swz_mc(int k) {
 template <int TILE>
 SN_DEV int mc_off(int k, int mc) { return k * (TILE * 2) + ((mc << 4) ^ swz_mc<TILE>(k)); }
 
+// fp8 MC tile: [128 k rows][128 cols] bytes (128-B rows).  16-B chunk index XOR f(k) so the
+// 16 rows {8r+q, 32+8r+q} a 32-lane half reads with ds_read_b64_tr_b8 (read_frag8_mc)
+// cover all 64 banks once: f(k) = ((k >> 1) & 3) | (((k >> 5) & 1) << 2).
+SN_DEV int swz_mc8(int k) { return ((k >> 1) & 3) | (((k >> 5) & 1) << 2); }
+
 // Zero source for LDS-DMA lanes that fall outside the matrix (padding, ragged edges), and
 // the ones page of the bias-gradient column (bf16 1.0 then seven zeros).
 __device__ __attribute__((aligned(16))) uint4 g_zero16[1];
@@ -144,12 +149,16 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 template <int MC, int MODE, int TILE, int NW, int ES = 2>
 struct GStager {
   static constexpr int NI = TILE / (8 * NW);      // wave-instructions per wave per tile
-  static constexpr int CPL = MC ? TILE / 8 : 8;   // 16-B chunks per LDS row
+  static constexpr int CPL = MC ? TILE * ES / 16 : 8;  // 16-B chunks per LDS row
   static constexpr int RPI = 64 / CPL;            // LDS rows per wave-instruction
   static constexpr int EPC = 16 / ES;             // elements per 16-B chunk (8 bf16, 16 fp8)
+  static constexpr int BKE = 128 / ES;            // reduction elements per K-step (64 bf16, 128 fp8)
   static_assert(NI >= 1 && NI * 8 * NW == TILE, "whole wave-instructions per tile");
-  static_assert(MC || MODE != OP_IM2COL || NI % 2 == 0, "KC im2col: chunk pattern repeats with period 2 in j");
-  static_assert(ES == 2 || !MC, "fp8 operands are K-contiguous");
+  // KC im2col: the chunk pattern of instruction j repeats with period 2 in j (row parity of
+  // (wave * NI + j) differs between j and j' iff j - j' is odd), so instructions 0 and 1
+  // describe all of them — for any NI >= 2, odd NI included
+  static_assert(MC || MODE != OP_IM2COL || NI >= 2, "KC im2col: at least two instructions per wave");
+  static_assert(ES == 2 || !MC || (TILE == 128 && MODE != OP_FLIPW), "fp8 MC images: 128 x 128-B rows");
   static_assert(!MC || RPI * CPL == 64, "MC images: whole rows per wave-instruction");
   const char* base;  // element offsets below are scaled by ES
   long long ld;
@@ -230,7 +239,7 @@ struct GStager {
     for (int j = 0; j < NI; ++j) {
       const int row = (wave * NI + j) * RPI + lane / CPL, pos = lane % CPL;
       rr[j] = row;
-      ch[j] = MC ? (pos ^ (swz_mc<TILE>(row) >> 4)) : (pos ^ ((row >> 1) & 7));
+      ch[j] = MC ? (pos ^ (ES == 1 ? swz_mc8(row) : (swz_mc<TILE>(row) >> 4))) : (pos ^ ((row >> 1) & 7));
       if (MODE == OP_IM2COL && !MC) {
         const int PQ = g.P * g.Q;
         int pix = tile_row0 + row;
@@ -242,7 +251,7 @@ struct GStager {
         rowoff[j] = ((n * g.H + ph[j]) * g.W + pw[j]) * g.C + coff;  // host guarantees < 2^31 elements
       }
       if (MODE == OP_IM2COL && MC) {
-        int col = tile_col0 + ch[j] * 8;
+        int col = tile_col0 + ch[j] * EPC;
         co[j] = col == ones_col && col < cols_lim;
         cv[j] = col < cols_lim && col != ones_col;
         int tap = col / g.Cg;
@@ -283,9 +292,9 @@ struct GStager {
             kch[j] = ch[j] * EPC;
             voff[j] = row < rows_lim ? (int)(((long long)row * ld + kch[j]) * ES) : (int)0x80000000u;
           } else {
-            const int col = tile_col0 + ch[j] * 8;
+            const int col = tile_col0 + ch[j] * EPC;
             kch[j] = rr[j];
-            voff[j] = col < cols_lim ? (int)(((long long)rr[j] * ld + col) * 2) : (int)0x80000000u;
+            voff[j] = col < cols_lim ? (int)(((long long)rr[j] * ld + col) * ES) : (int)0x80000000u;
           }
         }
       }
@@ -443,8 +452,8 @@ struct GStager {
       }
     } else {
       if (MODE == OP_DENSE && fast) {
-        const bool tail = k_tile + BK > k_lim;
-        const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)((long long)k_tile * ld * 2));
+        const bool tail = k_tile + BKE > k_lim;
+        const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)((long long)k_tile * ld * ES));
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           unsigned o = (unsigned)voff[j];
@@ -454,9 +463,9 @@ struct GStager {
       } else if (MODE == OP_DENSE) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          int k = k_tile + rr[j], col = tile_rc0 + ch[j] * 8;
+          int k = k_tile + rr[j], col = tile_rc0 + ch[j] * EPC;
           const bool one = col == ones_col && col < rc_lim && k < k_lim;
-          dma(base + ((long long)k * ld + col) * 2, k < k_lim && col < rc_lim && col != ones_col, dst + j * 1024,
+          dma(base + ((long long)k * ld + col) * ES, k < k_lim && col < rc_lim && col != ones_col, dst + j * 1024,
               one);
         }
       } else if (MODE == OP_FLIPW) {
@@ -496,14 +505,14 @@ struct GStager {
         }
         if (!wave_has_one) {
 #pragma unroll
-          for (int j = 0; j < NI; ++j) dma_buf(val[j] ? (unsigned)off[j] * 2u : 0xffffffffu, dst + j * 1024);
+          for (int j = 0; j < NI; ++j) dma_buf(val[j] ? (unsigned)off[j] * (unsigned)ES : 0xffffffffu, dst + j * 1024);
         } else {
 #pragma unroll
           for (int j = 0; j < NI; ++j)
-            dma(base + (long long)off[j] * 2, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
+            dma(base + (long long)off[j] * ES, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
         }
-        // next tile: BK pixels on
-        sq_ += BK;
+        // next tile: BKE pixels on
+        sq_ += BKE;
         const int dp = fdiv(sq_, g.Q, invQ);
         sq_ -= dp * g.Q;
         sp_ += dp;
@@ -561,6 +570,34 @@ SN_DEV i32x8 read_frag8(const char* lds, int x0, int lane) {
   const uint4 v1 = *reinterpret_cast<const uint4*>(lds + kc_off(row, kc + 1));
   i32x8 r = {(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
   return r;
+}
+
+// fp8 fragment of a 16-column subtile (columns x0..x0+15, x0 % 16 == 0) of an MC image
+// ([128 k][128 cols] bytes, swz_mc8): lane l needs X[k = 32(l>>4) + j][x0 + (l&15)],
+// j = 0..31, i.e. one column down 32 rows.  ds_read_b64_tr_b8 transposes an 8-row x 16-byte
+// block per 16-lane group (lane 2q+p addresses row q, bytes 8p..8p+7; lane i receives column
+// i of the 8 rows: tests/test_gemm_fp8_mc_gpu.py pins this), so four reads = 32 k values.
+SN_DEV i32x8 read_frag8_mc(const char* lds, int x0, int lane) {
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  const int g = lane >> 4, i = lane & 15, q = i >> 1, p = i & 1, c = x0 >> 4;
+  i32x8 r;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int k = 32 * g + 8 * rr + q;
+    const char* a = lds + k * 128 + ((c ^ swz_mc8(k)) << 4) + 8 * p;
+    const v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)a);
+    r[2 * rr] = v[0];
+    r[2 * rr + 1] = v[1];
+  }
+  return r;
+}
+template <int MC>
+SN_DEV i32x8 read_frag8x(const char* lds, int x0, int lane) {
+  if constexpr (MC)
+    return read_frag8_mc(lds, x0, lane);
+  else
+    return read_frag8(lds, x0, lane);
 }
 
 // fused fp8 side output (SnGemmArgs.q_out): 4 bf16-rounded values -> 4 fp8 bytes
@@ -827,11 +864,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       // group, so at most NFR + 1 fragments (8 VGPRs each) live beside the accumulators
       i32x8 fb8[NFR];
 #pragma unroll
-      for (int i = 0; i < NFR; ++i) fb8[i] = read_frag8(lb, wn0 + 16 * i, lane);
+      for (int i = 0; i < NFR; ++i) fb8[i] = read_frag8x<BMC>(lb, wn0 + 16 * i, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < MFR; ++j) {
-        const i32x8 fa = read_frag8(la, wm0 + 16 * j, lane);
+        const i32x8 fa = read_frag8x<AMC>(la, wm0 + 16 * j, lane);
 #pragma unroll
         for (int i = 0; i < NFR; ++i)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[i], fa, acc[i][j], 0, FMT_A, 0, 127, 0, 127);
@@ -841,9 +878,9 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     } else if constexpr (FP8) {
       i32x8 fa8[MFR], fb8[NFR];
 #pragma unroll
-      for (int i = 0; i < NFR; ++i) fb8[i] = read_frag8(lb, wn0 + 16 * i, lane);
+      for (int i = 0; i < NFR; ++i) fb8[i] = read_frag8x<BMC>(lb, wn0 + 16 * i, lane);
 #pragma unroll
-      for (int i = 0; i < MFR; ++i) fa8[i] = read_frag8(la, wm0 + 16 * i, lane);
+      for (int i = 0; i < MFR; ++i) fa8[i] = read_frag8x<AMC>(la, wm0 + 16 * i, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < NFR; ++i)

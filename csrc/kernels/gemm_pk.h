@@ -11,8 +11,13 @@
 //     flight during the current tile's last K-steps and its epilogue;
 //   * every wait is a counted vmcnt followed by a raw s_barrier (no vmcnt(0) in the
 //     loop: cdna_hip_programming.md §5 "Pipelining across barriers");
-//   * a block's tiles are a contiguous run of the XCD's share of the tile order, so the
-//     32 blocks of one XCD work on neighbouring tiles that share operand panels in its L2.
+//   * the 32 blocks of one XCD stride through a contiguous share of the tile order, so the
+//     tiles in flight on an XCD at any time are neighbours that share operand panels in its
+//     L2 (a contiguous run PER BLOCK measured 10-40 % slower: 32 distant panels per L2);
+//   * the fragments of the next K-step's first half are read from LDS right after its
+//     barrier, while the MFMAs of the current K-step's second half are in the pipe: the
+//     two waves of a SIMD belong to the same block and would otherwise both sit in the
+//     read phase with the matrix pipe idle.
 // The reference runs these products as per-image im2col + SGEMM
 // (caffe/src/caffe/layers/base_conv_layer.cpp:312-376, conv_layer.cu:14-56,
 //  inner_product_layer.cu:22-54).
@@ -87,11 +92,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pk_kernel(SnGemmArgs args) {
     const int q = total >> 3, r = total & 7;
     const int cstart = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
     const int csize = q + (xcd < r ? 1 : 0);
-    // contiguous run: loc's share of the chunk
-    const int per = csize / nloc, extra = csize % nloc;
-    first = cstart + loc * per + min(loc, extra);
-    count = per + (loc < extra ? 1 : 0);
-    stride = 1;
+    first = cstart + loc;
+    stride = nloc;
+    count = loc < csize ? (csize - loc + nloc - 1) / nloc : 0;
   } else {
     first = blockIdx.x;
     stride = G;
@@ -133,24 +136,23 @@ __global__ void __launch_bounds__(512, 1) gemm_pk_kernel(SnGemmArgs args) {
 #pragma unroll
     for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](const char* la) {
+  // fragments of one 32-deep k-substep: F[0] = A (MFR), F[1..] = B (NFR)
+  struct Frags {
+    bf16x8_t a[MFR], b[NFR];
+  };
+  auto read_sub = [&](Frags& f, const char* la, int sub) {
     const char* lb = la + A_BYTES;
-    bf16x8_t fa[2][MFR], fb[2][NFR];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int i = 0; i < NFR; ++i) f.b[i] = read_frag<BMC, BNL>(lb, wn0 + 16 * i, sub, lane);
 #pragma unroll
-      for (int i = 0; i < NFR; ++i) fb[s][i] = read_frag<BMC, BNL>(lb, wn0 + 16 * i, s, lane);
-#pragma unroll
-      for (int i = 0; i < MFR; ++i) fa[s][i] = read_frag<AMC, BM>(la, wm0 + 16 * i, s, lane);
-    }
+    for (int i = 0; i < MFR; ++i) f.a[i] = read_frag<AMC, BM>(la, wm0 + 16 * i, sub, lane);
+  };
+  auto mma_sub = [&](const Frags& f) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int i = 0; i < NFR; ++i)
 #pragma unroll
-      for (int i = 0; i < NFR; ++i)
-#pragma unroll
-        for (int j = 0; j < MFR; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][i], fa[s][j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < MFR; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[i], f.a[j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -163,40 +165,74 @@ __global__ void __launch_bounds__(512, 1) gemm_pk_kernel(SnGemmArgs args) {
   PkItem Cc = pk_decode(args, first, BM, BN);
   const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
   const int c_cols = (!epi_bf16<EPI>() && args.bias_out) ? args.ones_col : args.N;
-  int slot = 0;  // ring slot of `step`
-  while (c_ord < count) {
-    // stage `step` landed for this wave's DMAs; `issued - step - 1` younger stages may fly
-    pk_wait_stages<P>(issued - step - 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's DMAs of `step` landed; slot step-1 is free
-    {
-      const int ns = slot == 0 ? NS - 1 : slot - 1;  // (step + D) % NS
-      issued += issue_next(smem + ns * STAGE);
-    }
-    compute(smem + slot * STAGE);
-    ++step;
-    slot = slot == NS - 1 ? 0 : slot + 1;
-    if (++c_k >= Cc.nk) {
-      // epilogue of item c_ord (the next items' first stages are already in flight)
+  auto epilogue = [&]() {
 #pragma unroll
-      for (int j = 0; j < MFR; ++j) {
-        const int m = Cc.m_blk + wm0 + 16 * j + mrow_l;
-        if (m >= args.M) continue;
+    for (int j = 0; j < MFR; ++j) {
+      const int m = Cc.m_blk + wm0 + 16 * j + mrow_l;
+      if (m >= args.M) continue;
 #pragma unroll
-        for (int i = 0; i < NFR; ++i) {
-          const int n = Cc.n_blk + wn0 + 16 * i + ncol_l;
-          if (n >= args.N) continue;
-          epi_store<EPI, false>(args, Cc.grp, Cc.split, m, n, acc[i][j], c_cols);
-        }
+      for (int i = 0; i < NFR; ++i) {
+        const int n = Cc.n_blk + wn0 + 16 * i + ncol_l;
+        if (n >= args.N) continue;
+        epi_store<EPI, false>(args, Cc.grp, Cc.split, m, n, acc[i][j], c_cols);
       }
+    }
 #pragma unroll
-      for (int i = 0; i < NFR; ++i)
+    for (int i = 0; i < NFR; ++i)
 #pragma unroll
-        for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // Two wave groups staggered by one barrier (cdna_hip_programming.md §5, the 256^2
+  // template's `if (wr == 1) s_barrier`; MI355X_MICROARCH.md "Two waves per SIMD", item 9):
+  // waves 0-3 and 4-7 sit on different SIMDs in pairs, and every K-step is two phases per
+  // k-substep, R (fragment reads [+ the ring refill]) | barrier | C (MFMAs) | barrier.  With
+  // group B one barrier behind, each SIMD runs group A's C beside group B's R and vice
+  // versa, so the matrix pipe is not idle while fragments are read.
+  //   stage k is read in phases 2k, 2k+1; group A's first read of it follows global barrier
+  //   4k+1, so EVERY wave retires its own DMAs of stage k before arriving there: group A at
+  //   the end of C(2k-1), group B at the end of R(2k-1).  The refill of stage k's slot
+  //   (stage k + NS) is issued in the R phase of step k+1, after group B's last read of
+  //   stage k (R(2k+1)) has passed a barrier.
+  const bool gB = wv >= 4;
+  Frags f;
+  pk_wait_stages<P>(issued - 1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // stage 0 landed for every wave
+  if (gB) __builtin_amdgcn_s_barrier();  // the stagger
+  int slot = 0, pslot = NS - 1;  // ring slots of `step` and of step - 1
+  while (true) {
+    const char* cur = smem + slot * STAGE;
+    const bool last_k = c_k + 1 >= Cc.nk;
+    const bool more = !last_k || c_ord + 1 < count;
+    // ---- k-substep 0 ----
+    issued += issue_next(smem + pslot * STAGE);  // stage step + NS - 1 into step - 1's slot
+    read_sub(f, cur, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    mma_sub(f);
+    __builtin_amdgcn_s_barrier();
+    // ---- k-substep 1 ----
+    read_sub(f, cur, 1);
+    if (gB) pk_wait_stages<P>(issued - step - 2);  // stage step + 1 (group B: end of R)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    mma_sub(f);
+    if (!gB) pk_wait_stages<P>(issued - step - 2);  // stage step + 1 (group A: end of C)
+    __builtin_amdgcn_s_barrier();
+    if (last_k) {
+      epilogue();  // item c_ord; the next items' first stages are already in flight
       c_k = 0;
       if (++c_ord < count) Cc = pk_decode(args, first + c_ord * stride, BM, BN);
+    } else {
+      ++c_k;
     }
+    if (!more) break;
+    ++step;
+    pslot = slot;
+    slot = slot == NS - 1 ? 0 : slot + 1;
   }
+  if (!gB) __builtin_amdgcn_s_barrier();  // both groups execute the same number of barriers
   // nothing may still be landing in LDS when the workgroup retires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }

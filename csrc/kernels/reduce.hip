@@ -287,3 +287,30 @@ extern "C" int sn_vsum(const float* x, long long n, float* out, float scale, lon
   hipLaunchKernelGGL(vsum_kernel, dim3(1), dim3(1024), 0, st, x, n, out, scale, (int)accumulate);
   return SN_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------------------
+// Probe of the ds_read_b64_tr_b8 lane mapping (tests/test_gemm_fp8_mc_gpu.py): a 16 x 16
+// byte image b[row][col] = row * 16 + col in LDS; lane l (group g = l >> 4, i = l & 15)
+// addresses row 8 (g & 1) + (i >> 1), bytes 8 (i & 1) .. +7 and stores the 8 bytes it gets.
+// Under the mapping read_frag8_mc assumes, lane i receives column i of the 8 rows.
+namespace {
+__global__ void probe_tr8_kernel(unsigned* out) {
+  __shared__ __attribute__((aligned(16))) unsigned char img[256];
+  const int l = threadIdx.x;
+  for (int e = l; e < 256; e += 64) img[e] = (unsigned char)e;
+  __syncthreads();
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  const int g = l >> 4, i = l & 15;
+  const int row = 8 * (g & 1) + (i >> 1);
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  const v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+      (lds_v2i*)((__attribute__((address_space(3))) unsigned char*)img + row * 16 + 8 * (i & 1)));
+  out[2 * l] = (unsigned)v[0];
+  out[2 * l + 1] = (unsigned)v[1];
+}
+}  // namespace
+
+extern "C" int sn_probe_tr8(unsigned* out, hipStream_t st) {
+  hipLaunchKernelGGL(probe_tr8_kernel, dim3(1), dim3(64), 0, st, out);
+  return SN_CHECK_LAUNCH();
+}

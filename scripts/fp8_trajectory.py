@@ -29,7 +29,8 @@ p.add_argument("--batch", type=int, default=64)
 p.add_argument("--crop", type=int, default=64)
 p.add_argument("--classes", type=int, default=10)
 p.add_argument("--lr", type=float, default=0.005)
-p.add_argument("--modes", default="bf16,fp8,fp8dg,fp8dg5")
+p.add_argument("--modes", default="bf16,fp8,fp8dg,fp8dg5", help="bf16, bf16alt (chaos floor), fp8, fp8dg, fp8dg5, "
+               "and fp8dgw / fp8dg5w (+ fp8 weight gradients)")
 p.add_argument("--window", type=int, default=20)
 p.add_argument("--noise", type=float, default=0.8)
 p.add_argument("--seed", type=int, default=12)
@@ -61,7 +62,7 @@ def run(mode):
     _G._FORCE_TILE = 0 if mode == "bf16alt" else -1
     if mode not in ("bf16", "bf16alt"):
         n8 = enable_fp8(solver.net, 0.0, dgrad=mode.startswith("fp8dg"),
-                        dgrad_format="e5m2" if mode == "fp8dg5" else "e4m3")
+                        dgrad_format="e5m2" if mode.startswith("fp8dg5") else "e4m3", wgrad=mode.endswith("w"))
     it = batches()
 
     def pre():

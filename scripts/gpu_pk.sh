@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gemm_pk_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pk_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gemm_fp8_mc_gpu.py tests/test_gemm_pk_gpu.py -q --timeout 120 --timeout-method thread > gpurun_out/pk_tests.log 2>&1
 rc=$?
 tail -5 gpurun_out/pk_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc, stopping"; exit $rc; fi

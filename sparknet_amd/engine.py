@@ -514,7 +514,8 @@ def fp8_dgrad_macs_per_grad(layer, bottom) -> float:
     return float(s.Cg * s.R * s.S)
 
 
-def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgrad_format: str = "e4m3") -> int:
+def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgrad_format: str = "e4m3",
+               wgrad: bool = False) -> int:
     """Run the forward products of eligible Convolution / InnerProduct layers in OCP e4m3
     (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation) with per-tensor delayed
     scaling: each layer quantises its input and weights with the scale derived from the
@@ -529,8 +530,13 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
     gradient and the flip-transposed weights quantised per tensor; weight gradients stay
     bf16), for layers with at least ``min_macs_per_input`` data-gradient MACs per output-
     gradient element (:func:`fp8_dgrad_macs_per_grad`); ``dgrad_format`` "e5m2" quantises
-    the output gradients to e5m2 (2 mantissa bits, 2^32 of range) instead of e4m3.  GPU
-    only; returns the number of fp8 products (forward + data gradient)."""
+    the output gradients to e5m2 (2 mantissa bits, 2^32 of range) instead of e4m3.
+
+    ``wgrad`` (with ``dgrad``): the weight gradients of the layers that run BOTH an fp8
+    forward and an fp8 data gradient become fp8 products as well (reduction over pixels:
+    the output gradient's fp8 copy, shared with the data gradient, against the forward's
+    e4m3 input kept for the backward; ops.hip._conv_wgrad_fp8).  GPU only; returns the
+    number of fp8 products (forward + data gradient + weight gradient)."""
     if net.device.type != "cuda":
         return 0
     from .ops import hip
@@ -552,9 +558,16 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
         layer.fp8_dgrad_slots = (2 * i, 2 * i + 1)
         if dgrad_format == "e5m2":
             sc.set_e5m2(2 * i)
+    n_wg = 0
+    if wgrad:
+        both = set(map(id, chosen)) & set(map(id, chosen_dg))
+        for li, layer in enumerate(net.layers):
+            if id(layer) in both and hip.fp8_wgrad_ok(layer.spec(net.bottom_vecs[li][0])):
+                layer.fp8_wgrad = True
+                n_wg += 1
     net.ctx.fp8 = sc if (chosen or chosen_dg) else None
     fuse_fp8_quant(net)
-    return len(chosen) + len(chosen_dg)
+    return len(chosen) + len(chosen_dg) + n_wg
 
 
 def fuse_fp8_quant(net) -> int:

@@ -121,6 +121,10 @@ class ConvolutionLayer(Layer):
 
     fp8_slots = None  # (x slot, w slot) in ctx.fp8 when the forward product runs in e4m3
     fp8_dgrad_slots = None  # (dy slot, flipped-w slot) when the data gradient runs in e4m3
+    # the weight gradient runs as an fp8 product too (engine.enable_fp8 wgrad): the forward
+    # keeps its e4m3 input (_fp8_xq) for it, and dy's fp8 copy is shared with the data gradient
+    fp8_wgrad = False
+    _fp8_xq = None
     # engine.fuse_fp8_quant: (consumer conv, its x slot) — this layer's output GEMM also stores
     # the consumer's fp8 input; (producer conv, its dy slot) — this layer's data-gradient GEMM
     # also stores the producer's fp8 output gradient
@@ -172,6 +176,8 @@ class ConvolutionLayer(Layer):
         xq = _gemm.side_bytes(side, x)
         if xq is None:
             xq = hip.quant_fp8(x, sc.slot(ix))
+        if self.fp8_wgrad:
+            self._fp8_xq = xq
         wq = hip.quant_fp8(w, sc.slot(iw))
         return hip.conv_forward_fp8(xq, wq, bias, s, sc.deq(ix), sc.deq(iw), relu=self.fuse_relu, out=out)
 
@@ -192,6 +198,9 @@ class ConvolutionLayer(Layer):
                 ws = {} if ws is None else ws
                 dy_side, self._fp8_dy_side = self._fp8_dy_side, None
                 ws["fp8_dgrad"] = (self.ctx.fp8, *self.fp8_dgrad_slots, dy_side)
+                xq, self._fp8_xq = self._fp8_xq, None
+                if self.fp8_wgrad and xq is not None and dw is not None and i == 0:
+                    ws["fp8_wgrad"] = (self.ctx.fp8, self.fp8_slots[0], xq, self.fp8_dgrad_slots[0])
             if i == 0 and self.fp8_dx_out is not None and propagate_down[i] and self._fp8_ready():
                 ws = {} if ws is None else ws
                 prod, idy = self.fp8_dx_out

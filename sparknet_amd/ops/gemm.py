@@ -116,14 +116,15 @@ TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96)
          11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192), 15: (128, 192), 16: (192, 128),
          17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64),
          # persistent ring-pipelined tiles (csrc/kernels/gemm_pk.h): one 512-thread block per CU
-         30: (256, 128), 31: (256, 64), 32: (256, 96), 33: (128, 128), 34: (256, 192), 36: (128, 256)}
-PK_TILES = frozenset((30, 31, 32, 33, 34, 36))
+         30: (256, 128), 31: (256, 64), 32: (256, 96), 33: (128, 128), 34: (256, 192), 36: (128, 256),
+         37: (192, 384), 38: (256, 256)}
+PK_TILES = frozenset((30, 31, 32, 33, 34, 36, 37, 38))
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
 _SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512,
-          30: 256, 31: 256, 32: 256, 33: 256, 34: 256, 36: 256}
+          30: 256, 31: 256, 32: 256, 33: 256, 34: 256, 36: 256, 37: 256, 38: 256}
 _KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55,
-             30: 0.75, 31: 0.45, 32: 0.6, 33: 0.45, 34: 1.1, 36: 0.75}
+             30: 0.75, 31: 0.45, 32: 0.6, 33: 0.45, 34: 1.1, 36: 0.75, 37: 1.3, 38: 1.2}
 # autotune candidates 11-14 (SN_GEMM_TILE8W=0 drops them)
 _TILE8W = os.environ.get("SN_GEMM_TILE8W", "1") != "0"
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
@@ -233,7 +234,7 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
     ops = (sa, a_mc, a_mode, sb, b_mc, b_mode)
     if splits is not None or _FORCE_TILE >= 0:
         if fp8:
-            tile = _FORCE_TILE if _FORCE_TILE in _FP8_TILES else 0
+            tile = _FORCE_TILE if (_FORCE_TILE in _FP8_TILES and not (a_mc or b_mc)) else 0
         else:
             tile = _FORCE_TILE if _FORCE_TILE >= 0 else choose_tile(M, N, b_mc == 0 and b_mode == OP_DENSE)
         if epi == EPI_SGD and tile not in (0, 1, 2, 3):
@@ -548,9 +549,9 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
 _FP8_TILES = (0, 11, 16)
 
 
-def _candidates_fp8(M, N, K, groups, epi, xtra):
+def _candidates_fp8(M, N, K, groups, epi, xtra, mc=False):
     out = []
-    for t in _FP8_TILES:
+    for t in ((0,) if mc else _FP8_TILES):  # fp8 MC operands (weight gradients): 128x128 only
         if t != 0 and (xtra[0] or epi not in (EPI_BF16, EPI_F32)):
             continue
         s, kc = choose_splits(M, N, K // 2, groups, t)
@@ -612,7 +613,8 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     scratch = torch.empty_like(out) if out.is_contiguous() else torch.empty(extent, dtype=out.dtype, device=out.device)
     bscratch = torch.zeros_like(bias_grad) if bias_grad is not None else None
     runs = []
-    cands = _candidates_fp8(M, N, K, groups, epi, xtra) if fp8 else _candidates(M, N, K, groups, b_kc_dense, epi)
+    cands = (_candidates_fp8(M, N, K, groups, epi, xtra, bool(a_mc or b_mc)) if fp8
+             else _candidates(M, N, K, groups, b_kc_dense, epi))
     for cand in cands:
         t, s, kc = cand
 

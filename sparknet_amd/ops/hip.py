@@ -354,9 +354,15 @@ def _conv_backward_chunked(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=Non
         full = ws.get("s2d_full") if ws else None
         if full is not None and not (full[0] == x.data_ptr() and full[1] == x._version):
             full = None
+        dyq_full = _fp8_dyq(dy, ws, s) if ws else None  # one fp8 copy of dy shared by the chunks
         for n0 in range(0, s.N, nb):
             n1 = min(s.N, n0 + nb)
             cws = {k: ws[k] for k in ("wt", "fp8_dgrad") if k in ws} if ws else None
+            if dyq_full is not None:
+                cws["fp8_dyq"] = dyq_full[n0:n1]
+            if ws and "fp8_wgrad" in ws:
+                sc, ix, xq, idy = ws["fp8_wgrad"]
+                cws["fp8_wgrad"] = (sc, ix, xq[n0:n1], idy)
             if full is not None:
                 xc = x[n0:n1]
                 cws["s2d"] = (xc.data_ptr(), xc._version, full[2][n0:n1])
@@ -387,6 +393,17 @@ def _conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=
     # paths; otherwise (no dw, explicit im2col) it is a separate column sum
     fused_db = db is not None and dw is not None and (
         plan is not None or (_implicit_ok(s) and s.Kg % 8 == 0))
+    f8w = ws.get("fp8_wgrad") if ws is not None else None
+    if (f8w is not None and dw is not None and plan is None and ldd == s.K and ldx == s.C
+            and fp8_wgrad_ok(s) and f8w[2].shape[0] == s.N):
+        dyq = ws.get("fp8_dyq")
+        if dyq is None:
+            dyq = ws["fp8_dyq"] = _fp8_dyq(dy, ws, s)
+        with wgrad_side():
+            _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc)
+        dw = None
+        if db is not None:
+            db, fused_db = None, False
     with wgrad_side():
         _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, ldd, ldx)
     if not need_dx:
@@ -437,6 +454,46 @@ def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, 
                     dw2[g * s.Kg:(g + 1) * s.Kg].copy_(tmp[:s.Kg, :kred])
 
 
+def fp8_wgrad_ok(s: ConvSpec) -> bool:
+    """Can this conv's weight gradient run as an e4m3 / e5m2 product (fp8 MC operands read
+    with ds_read_b64_tr_b8: whole 16-channel chunks on both sides, implicit im2col of x)?"""
+    return _implicit_ok(s) and s.Kg % 16 == 0 and s.Cg % 16 == 0 and s.C % 16 == 0 and s.K % 16 == 0
+
+
+def _fp8_dyq(dy, ws, s):
+    """fp8 bytes of the output gradient for this layer's fp8 data / weight gradients: the
+    side output of the layer above's dgrad epilogue when it covers dy, else one pass."""
+    f8 = ws.get("fp8_dgrad") if ws else None
+    f8w = ws.get("fp8_wgrad") if ws else None
+    if f8 is None and f8w is None:
+        return None
+    if f8 is not None:
+        sc, idy = f8[0], f8[1]
+        side = f8[3] if len(f8) > 3 else None
+    else:
+        sc, idy, side = f8w[0], f8w[3], None
+    e5 = sc.is_e5m2(idy)
+    from .gemm import side_bytes
+    dyq = side_bytes(side, dy, e5)
+    return dyq if dyq is not None else quant_fp8(_c(dy), sc.slot(idy), e5m2=e5)
+
+
+def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc):
+    """Weight gradient as an fp8 product with the reduction over pixels: A = the output
+    gradient (e4m3 / e5m2, MC: [pixels][K]), B = the implicit im2col of the layer input's
+    e4m3 copy kept from the forward (MC), both read transposed from LDS by
+    ds_read_b64_tr_b8; fp32 accumulation, split-K slabs, dequantised epilogue.  The bias
+    gradient stays an exact bf16 column sum (reference: base_conv_layer.cpp:338-376,
+    conv_layer.cu:35-53)."""
+    sc, ix, xq, idy = f8w
+    if db is not None:
+        colsum(dy2, db, accumulate=db_acc)
+    A = Dense(dyq.view(M, s.K), s.K, kcontig=False, gstride=s.Kg)
+    B = Im2col(xq, _geom(s), kcontig=False, gstride=s.Cg)
+    gemm(s.Kg, kred, M, A, B, dw, kred, epi=EPI_F32_ACC if dw_acc else EPI_F32, groups=s.groups,
+         c_gstride=s.Kg * kred, deq=(sc.deq(idy), sc.deq(ix), 2 if sc.is_e5m2(idy) else 1))
+
+
 def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
     ldd, ldx = ldd or s.K, ldx or s.C
     dx = dx_out if dx_out is not None else torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
@@ -452,7 +509,7 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
         pre = ws.get("wt") if ws is not None else None  # flipped once for the net (FlipBatch)
         f8 = ws.get("fp8_dgrad") if ws is not None else None
         if f8 is not None and fp8_dgrad_ok(s) and ldd == s.K:
-            return _conv_dgrad_fp8(dy, w, s, g2, kr2, pre, gate, dx, f8)
+            return _conv_dgrad_fp8(dy, w, s, g2, kr2, pre, gate, dx, f8, ws.get("fp8_dyq"))
         if (direct_c64_ok(s) and ldd == s.K and ldx == s.C and dy.is_contiguous() and dx.is_contiguous()
                 and not DGRAD_INPLACE_WEIGHTS and not _side_covers(dx)):
             if pre is None:
@@ -503,7 +560,7 @@ def fp8_dgrad_ok(s: ConvSpec) -> bool:
     return dgrad_uses_flip(s) and s.Kg % 16 == 0 and s.C % 8 == 0
 
 
-def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8):
+def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8, ws_dyq=None):
     """Data gradient as an e4m3 forward conv of the output gradient with the flip-
     transposed weights (v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulation): the output
     gradient (e4m3, or e5m2 when its slot says so) and the flipped weights are quantised
@@ -516,9 +573,11 @@ def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8):
         wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=dy.device)
         call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
     e5 = sc.is_e5m2(idy)
-    side = f8[3] if len(f8) > 3 else None  # dy's fp8 bytes stored by the layer above's dgrad epilogue
-    from .gemm import side_bytes
-    dyq = side_bytes(side, dy, e5)
+    dyq = ws_dyq
+    if dyq is None:
+        side = f8[3] if len(f8) > 3 else None  # dy's fp8 bytes stored by the layer above's dgrad epilogue
+        from .gemm import side_bytes
+        dyq = side_bytes(side, dy, e5)
     if dyq is None:
         dyq = quant_fp8(dy, sc.slot(idy), e5m2=e5)
     wtq = quant_fp8(wt, sc.slot(iwt))

@@ -8,8 +8,10 @@ epilogues (Philox), and the InnerProduct SGD update inside the weight-gradient G
 mirrored by the same Philox draw (ops.ref.augment_params) and dropping the same units
 (ops.ref dropout shares the Philox stream).
 
-* 60 steps: the bf16 GPU loss trajectory stays within 8 % (relative, per 10-step window
-  mean) of the fp32 CPU one, and both decrease.
+* 60 steps at batch 32 with the full-width fc6 / fc7 (4096): the production tiles, the
+  split-K weight gradients and the 4096-wide EPI_SGD update tiles are the ones exercised.
+  The bf16 GPU loss trajectory stays within 4 % (relative, per 10-step window mean) of the
+  fp32 CPU one, and both decrease.
 * 10 steps: graph replay and the eager GPU step (same kernels, EPI_SGD included, launched
   one by one) end at the same weights to 1e-5 (relative to the largest weight).
 
@@ -26,11 +28,11 @@ from sparknet_amd import models
 
 pytestmark = pytest.mark.gpu
 
-B, CLASSES, SRC = 8, 10, 256
+B, CLASSES, SRC = 32, 10, 256
 MEAN = [104.0, 117.0, 123.0]
 
 
-def _data(n=64, seed=0):
+def _data(n=256, seed=0):
     """Learnable uint8 256x256 images: class colour + oriented stripes + noise."""
     g = torch.Generator().manual_seed(seed)
     y = torch.randint(0, CLASSES, (n,), generator=g)
@@ -47,11 +49,7 @@ def _data(n=64, seed=0):
 
 
 def _net():
-    n = models.caffenet(train_batch=B, test_batch=B, crop=227, classes=CLASSES)
-    for l in n.layer:
-        if l.type == "InnerProduct" and l.name in ("fc6", "fc7"):
-            l.inner_product_param.num_output = 256  # dropout stays at 0.5
-    return n
+    return models.caffenet(train_batch=B, test_batch=B, crop=227, classes=CLASSES)  # fc6 / fc7: 4096 wide
 
 
 def _trainer(dev, w0, x, y, graph):
@@ -85,6 +83,7 @@ def _initial_weights():
     return s.net.flat_data.detach().clone()
 
 
+@pytest.mark.timeout(900)
 def test_caffenet_production_path_tracks_fp32_cpu(gpu):
     x, y = _data()
     w0 = _initial_weights()
@@ -106,10 +105,11 @@ def test_caffenet_production_path_tracks_fp32_cpu(gpu):
     for w in range(0, len(gl) - 9, 10):
         a = sum(cl_aligned[w:w + 10]) / 10
         b = sum(gl[w:w + 10]) / 10
-        assert abs(a - b) <= 0.08 * max(1.0, abs(a)), (w, a, b, cl_aligned, gl)
+        assert abs(a - b) <= 0.04 * max(1.0, abs(a)), (w, a, b, cl_aligned, gl)
     assert sum(gl[-10:]) < sum(gl[:10]) and sum(cl_aligned[-10:]) < sum(cl_aligned[:10]), (cl_aligned, gl)
 
 
+@pytest.mark.timeout(300)
 def test_caffenet_graph_replay_matches_eager_gpu(gpu):
     x, y = _data()
     w0 = _initial_weights()

@@ -9,7 +9,7 @@ def _bf(*shape, device):
     return (torch.randn(*shape, device=device) * 0.5).to(torch.bfloat16)
 
 
-def _close(a, b, tol=2e-2):
+def _close(a, b, tol=8e-3):
     err = (a.float() - b.float()).abs().max().item()
     scale = b.float().abs().max().item() + 1e-6
     assert err / scale < tol, f"rel err {err/scale:.3e}"
@@ -392,3 +392,46 @@ def test_fast_dma_addressing_bitwise(gpu, tile, case, monkeypatch):
     for a, b in zip(outs[0], outs[1]):
         if a is not None:
             assert torch.equal(a, b)
+
+
+def _db_tiles():
+    """Every tile the packaged tuning database selects for a production product."""
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "sparknet_amd", "ops",
+                     "gemm_tuned.json")
+    with open(p) as f:
+        return sorted({int(v[0]) for v in json.load(f).values()})
+
+
+# shapes with a ragged M / N edge and a K tail (K % 64 != 0) for every tile; wide / tall
+# enough for two tiles along each axis
+_EDGE = [(lambda bm, bn: (2 * bm + 17, 2 * bn + 8, 64 * 5 + 24)), (lambda bm, bn: (bm - 3, bn - 8, 64 * 33 + 8)),
+         (lambda bm, bn: (3 * bm + 1, bn + 24, 136))]
+
+
+@pytest.mark.parametrize("tile", _db_tiles())
+@pytest.mark.parametrize("shape", range(len(_EDGE)))
+def test_db_tiles_edges_and_k_tail(gpu, tile, shape, monkeypatch):
+    """every tuned tile at 8e-3 on ragged M / N edges and K tails, through the
+    NT (forward), NN (data gradient) and TN (weight gradient) layouts it has instances for."""
+    from sparknet_amd.ops import gemm as G
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    bm, bn = G.TILES[tile]
+    M, N, K = _EDGE[shape](bm, bn)
+    x, w = _bf(M, K, device=gpu), _bf(N, K, device=gpu)
+    b = torch.randn(N, device=gpu)
+    _close(G.linear_fwd(x, w, b, relu=True), torch.relu(x.float() @ w.float().t() + b))
+    dy = _bf(M, N, device=gpu)
+    try:
+        dx = G.linear_dgrad(dy, w)
+    except RuntimeError:
+        dx = None  # no MC-B instance for this tile
+    if dx is not None:
+        _close(dx, dy.float() @ w.float())
+    dw = torch.ones(N, K, device=gpu)
+    try:
+        G.linear_wgrad(dy, x, dw, accumulate=True)
+    except RuntimeError:
+        return
+    _close(dw, 1 + dy.float().t() @ x.float())

@@ -8,8 +8,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-PK = [30, 31, 32, 33, 34, 36]
-MC_B = {30, 31, 32, 33, 36}  # tiles whose B image accepts k-strided (MC) operands
+PK = [30, 31, 32, 33, 34, 36, 37, 38]
+MC_B = {30, 31, 32, 33, 36, 38}  # tiles whose B image accepts k-strided (MC) operands
 TOL = 8e-3
 
 
