@@ -166,7 +166,8 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 18: return a.epi == EPI_SGD ? 4 : sn_gemm_big4(a, stream);  // gemm_big4.hip
     case 30:
     case 31:
-    case 32: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_a(a, stream);  // gemm_pk.hip (persistent ring)
+    case 32:
+    case 39: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_a(a, stream);  // gemm_pk.hip (persistent ring)
     case 33:
     case 34:
     case 36:

@@ -63,7 +63,10 @@ SN_DEV PkItem pk_decode(const SnGemmArgs& a, int it, int BMv, int BNv) {
 
 // BM x BN block tile, 8 waves laid out WM (along M) x 8/WM (along N), each wave owning
 // (16 MFR) x (16 NFR) outputs; NS LDS stages of (BM + BNL) x 128 B.
-template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int WM, int MFR, int NFR, int NS>
+// LOOP 0: two wave groups staggered by one barrier (below); 1: one barrier per K-step,
+// fragments of the whole K-step read, then its MFMAs (A/B probe of the stagger)
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int WM, int MFR, int NFR, int NS,
+          int LOOP = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pk_kernel(SnGemmArgs args) {
   constexpr int NW = 8, WN = NW / WM;
   constexpr int BNL = (BN + 63) / 64 * 64;
@@ -194,6 +197,31 @@ __global__ void __launch_bounds__(512, 1) gemm_pk_kernel(SnGemmArgs args) {
   //   the end of C(2k-1), group B at the end of R(2k-1).  The refill of stage k's slot
   //   (stage k + NS) is issued in the R phase of step k+1, after group B's last read of
   //   stage k (R(2k+1)) has passed a barrier.
+  if constexpr (LOOP == 1) {
+    Frags g0, g1;
+    while (c_ord < count) {
+      pk_wait_stages<P>(issued - step - 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      {
+        const int ns = step % NS == 0 ? NS - 1 : step % NS - 1;  // (step + D) % NS
+        issued += issue_next(smem + ns * STAGE);
+      }
+      const char* cur = smem + (step % NS) * STAGE;
+      read_sub(g0, cur, 0);
+      read_sub(g1, cur, 1);
+      mma_sub(g0);
+      mma_sub(g1);
+      ++step;
+      if (++c_k >= Cc.nk) {
+        epilogue();
+        c_k = 0;
+        if (++c_ord < count) Cc = pk_decode(args, first + c_ord * stride, BM, BN);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
   const bool gB = wv >= 4;
   Frags f;
   pk_wait_stages<P>(issued - 1);
@@ -249,7 +277,7 @@ int pk_grid_cap() {
   return cus;
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int WM, int MFR, int NFR, int NS>
+template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int WM, int MFR, int NFR, int NS, int LOOP = 0>
 int pk_launch_epi(const SnGemmArgs& a, hipStream_t st) {
   const long long tiles = (long long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const long long total = tiles * a.splits * a.groups;
@@ -258,20 +286,20 @@ int pk_launch_epi(const SnGemmArgs& a, hipStream_t st) {
   const dim3 grid((unsigned)(total < cap ? total : cap));
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_pk_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, WM, MFR, NFR, NS>), grid, dim3(512),
+      hipLaunchKernelGGL((gemm_pk_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, WM, MFR, NFR, NS, LOOP>), grid, dim3(512),
                          0, st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_pk_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, WM, MFR, NFR, NS>), grid, dim3(512),
+      hipLaunchKernelGGL((gemm_pk_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, WM, MFR, NFR, NS, LOOP>), grid, dim3(512),
                          0, st, a);
       break;
     case EPI_F32_ACC:
-      hipLaunchKernelGGL((gemm_pk_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, WM, MFR, NFR, NS>), grid,
+      hipLaunchKernelGGL((gemm_pk_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, WM, MFR, NFR, NS, LOOP>), grid,
                          dim3(512), 0, st, a);
       break;
     case EPI_BF16_DROP:  // InnerProduct forward only (dense NT)
       if constexpr (AMC == 0 && AMODE == OP_DENSE && BMC == 0 && BMODE == OP_DENSE) {
-        hipLaunchKernelGGL((gemm_pk_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, WM, MFR, NFR, NS>), grid,
+        hipLaunchKernelGGL((gemm_pk_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, WM, MFR, NFR, NS, LOOP>), grid,
                            dim3(512), 0, st, a);
         break;
       }
@@ -280,6 +308,15 @@ int pk_launch_epi(const SnGemmArgs& a, hipStream_t st) {
       return 2;
   }
   return SN_CHECK_LAUNCH();
+}
+
+// LOOP 1 probe instances: NT dense and conv fwd only
+template <int BM, int BN, int WM, int MFR, int NFR, int NS>
+int pk_launch_probe(const SnGemmArgs& a, hipStream_t stream) {
+  const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  if (key == 0b0000) return pk_launch_epi<0, OP_DENSE, 0, OP_DENSE, BM, BN, WM, MFR, NFR, NS, 1>(a, stream);
+  if (key == 0b0100) return pk_launch_epi<0, OP_IM2COL, 0, OP_DENSE, BM, BN, WM, MFR, NFR, NS, 1>(a, stream);
+  return 4;
 }
 
 // operand combinations: NT dense, conv fwd / dgrad (implicit im2col A x K-contiguous
