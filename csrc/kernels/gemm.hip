@@ -110,7 +110,9 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   const SnGemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
   // the ones column is a whole 16-B chunk of an MC B operand, inside the product's N
-  if (a.ones_col >= 0 && (!a.b_mc || a.b_mode == OP_FLIPW || (a.ones_col & 7) || a.ones_col >= a.N || a.fp8))
+  // (fp8: MC weight-gradient products only, the column on a 16-byte chunk boundary)
+  if (a.ones_col >= 0 && (!a.b_mc || a.b_mode == OP_FLIPW || (a.ones_col & (a.fp8 ? 15 : 7)) || a.ones_col >= a.N ||
+                          (a.fp8 && !a.a_mc)))
     return 5;
   if (a.bias_out && (a.ones_col < 0 || a.epi == EPI_BF16 || a.epi == EPI_BF16_DROP)) return 5;
   // fused fp8 side output: unsplit bf16 epilogues of gemm_kernel (not gemm256_kernel, tiles
@@ -124,7 +126,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     if (a.kchunk <= 0 || (a.kchunk % 128) != 0 || !a.deq_a || !a.deq_b) return 3;
     if (a.a_mc || a.b_mc) {
       if (!a.a_mc || a.a_mode != OP_DENSE || !a.b_mc || (a.b_mode != OP_IM2COL && a.b_mode != OP_DENSE) ||
-          a.ones_col >= 0 || (a.fp8 != 1 && a.fp8 != 2))
+          (a.fp8 != 1 && a.fp8 != 2))
         return 3;
       const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
       dim3 grid(tiles * a.splits * a.groups);
@@ -160,6 +162,8 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 12:
     case 13:
     case 14: return a.epi == EPI_SGD ? 4 : sn_gemm_big8(a, stream);  // gemm_big8.hip
+    case 21:
+    case 22: return sn_gemm_tiles_c(a, stream);  // gemm_tiles_c.hip (64-row tiles)
     case 15:
     case 16:
     case 17:

@@ -134,6 +134,8 @@ SN_DEV int swz_mc8(int k) { return ((k >> 1) & 3) | (((k >> 5) & 1) << 2); }
 // the ones page of the bias-gradient column (bf16 1.0 then seven zeros).
 __device__ __attribute__((aligned(16))) uint4 g_zero16[1];
 __device__ __attribute__((aligned(16))) uint32_t g_one16[4] = {0x3F80u, 0u, 0u, 0u};
+// the same for fp8 operands: e4m3 1.0 (0x38) then fifteen zero bytes
+__device__ __attribute__((aligned(16))) uint32_t g_one16_f8[4] = {0x38u, 0u, 0u, 0u};
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -316,7 +318,8 @@ struct GStager {
   // LDS write it cannot disambiguate (it would drain vmcnt(0) before the next ds_read);
   // every wait on these DMAs is explicit in the K-loop (counted vmcnt + barrier).
   SN_DEV void dma(const char* src, bool valid, char* lds, bool one = false) {
-    const void* s = valid ? (const void*)src : (one ? (const void*)g_one16 : (const void*)g_zero16);
+    const void* s = valid ? (const void*)src
+                          : (one ? (ES == 1 ? (const void*)g_one16_f8 : (const void*)g_one16) : (const void*)g_zero16);
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds));
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(s) : "memory");
   }
@@ -714,7 +717,13 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
         if (n + r < args.N) C[n + r] = f2bf(o[r]);
     }
   } else {
-    if (FP8) v = v * (args.deq_a[0] * args.deq_b[0]);
+    if (FP8) {
+      // per-tensor fp8 scales; the virtual ones column (bias gradient of an fp8 weight
+      // gradient) holds an UNSCALED e4m3 1.0, so it takes A's dequantisation only
+      const float dab = args.deq_a[0] * args.deq_b[0], da = args.deq_a[0];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] *= (n + r == args.ones_col) ? da : dab;
+    }
     if (args.bias_out && n <= args.ones_col && args.ones_col < n + 4) {
       const int r = args.ones_col - n;
       const float bv = r == 0 ? v[0] : (r == 1 ? v[1] : (r == 2 ? v[2] : v[3]));
@@ -1491,4 +1500,5 @@ int sn_gemm_big8(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big4(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_fp8_big(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_pk_a(const SnGemmArgs& a, hipStream_t stream);
+int sn_gemm_tiles_c(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_pk_b(const SnGemmArgs& a, hipStream_t stream);

@@ -114,14 +114,15 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
          6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64),
          11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192), 15: (128, 192), 16: (192, 128),
-         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64),
+         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64), 21: (64, 256), 22: (64, 128),
          # persistent ring-pipelined tiles (csrc/kernels/gemm_pk.h): one 512-thread block per CU
          30: (256, 128), 31: (256, 64), 32: (256, 96), 33: (128, 128), 34: (256, 192), 36: (128, 256),
          37: (192, 384), 38: (256, 256), 39: (256, 128)}
 PK_TILES = frozenset((30, 31, 32, 33, 34, 36, 37, 38))
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
-_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512,
+_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512, 21: 512,
+          22: 768,
           30: 256, 31: 256, 32: 256, 33: 256, 34: 256, 36: 256, 37: 256, 38: 256, 39: 256}
 _KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55,
              30: 0.75, 31: 0.45, 32: 0.6, 33: 0.45, 34: 1.1, 36: 0.75, 37: 1.3, 38: 1.2}
@@ -218,7 +219,8 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
     sb, b_mc, b_mode = _operand(B, fp8)
     ones = -1
     if bias_grad is not None:
-        assert epi in (EPI_F32, EPI_F32_ACC, EPI_SGD) and b_mc == 1 and b_mode != OP_FLIPW and N % 8 == 0 and not fp8
+        assert epi in (EPI_F32, EPI_F32_ACC, EPI_SGD) and b_mc == 1 and b_mode != OP_FLIPW and N % 8 == 0
+        assert not fp8 or (a_mc == 1 and N % 16 == 0)  # fp8: the MC weight-gradient products
         assert bias_grad.dtype == torch.float32 and bias_grad.is_contiguous() and bias_grad.numel() == groups * M
         ones, N = N, N + 1
     bk = 128 if fp8 else BK
@@ -449,6 +451,10 @@ _AUTOTUNE = os.environ.get("SN_GEMM_AUTOTUNE", "1") != "0"
 _TUNED: dict = {}
 _TUNE_LOG = os.environ.get("SN_GEMM_TUNE_LOG", "0") == "1"
 _TUNE_PASSES = int(os.environ.get("SN_GEMM_TUNE_PASSES", "3"))
+# products with M <= 64 re-time their database choice against the 64-row tiles (21, 22) on
+# first use (SN_GEMM_THIN_RETUNE=0: keep the database entry)
+_THIN_RETUNE = os.environ.get("SN_GEMM_THIN_RETUNE", "1") != "0"
+_THIN_DONE: set = set()
 # Tuning database: choices measured offline on an MI355X (scripts/build_tune_db.sh, many
 # more timing passes than a first-call tune) are loaded at import so the production
 # models run a fixed, reproducible tile / split-K per GEMM; first-call timing only fills
@@ -523,6 +529,8 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
             tiles.append(17)
     if epi != EPI_SGD and N >= 64:
         tiles.append(20)  # 3-stage 128x64, dense NT / NN only (InnerProduct forward / data gradient)
+    if M <= 64:  # 64-row tiles: thin weight gradients (64-channel convs, Inception reduce layers)
+        tiles += [21, 22]
     if epi != EPI_SGD:
         if _TILE64:
             tiles.append(10)
@@ -593,7 +601,8 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None, bool(xtra[0]),
            _geom_key(sa), _geom_key(sb)) + ((("fp8",) if len(deq) < 3 or deq[2] == 1 else ("fp8", deq[2])) if fp8 else ()) + (out.dtype,)
     hit = _TUNED.get(key)
-    if hit is not None:
+    if hit is not None and not (_THIN_RETUNE and M <= 64 and hit[0] not in (21, 22) and key not in _THIN_DONE
+                                and not fp8 and epi != EPI_SGD):
         return hit
     tile = 0 if fp8 else choose_tile(M, N, b_kc_dense)
     if epi == EPI_SGD and tile not in (0, 1, 2, 3):
@@ -604,7 +613,7 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
         splits = -(-K // kchunk)
     else:
         splits, kchunk = choose_splits(M, N, K, groups, tile)
-    default = (tile, splits, kchunk)
+    default = (tile, splits, kchunk) if hit is None else hit  # a thin re-tune must beat the database entry
     extent = (groups - 1) * c_gstride + (M - 1) * ldc + (N - (1 if ones >= 0 else 0))
     if (not _AUTOTUNE or epi == EPI_SGD or not out.is_cuda or torch.cuda.is_current_stream_capturing()
             or (out.is_contiguous() and extent > out.numel())):
@@ -615,6 +624,8 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     runs = []
     cands = (_candidates_fp8(M, N, K, groups, epi, xtra, bool(a_mc or b_mc)) if fp8
              else _candidates(M, N, K, groups, b_kc_dense, epi))
+    if hit is not None and hit not in cands:
+        cands = [hit] + cands
     for cand in cands:
         t, s, kc = cand
 
@@ -649,6 +660,7 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     best = min(times, key=times.get) if times else default
     if default in times and times[best] > 0.97 * times[default]:
         best = default
+    _THIN_DONE.add(key)
     if _TUNE_LOG:
         print(f"[gemm-tune] M={M} N={N} K={K} g={groups} modes={ops[1:3]}/{ops[4:]} epi={epi} "
               f"default={default} best={best} " +

@@ -454,6 +454,9 @@ def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, 
                     dw2[g * s.Kg:(g + 1) * s.Kg].copy_(tmp[:s.Kg, :kred])
 
 
+FP8_WGRAD_BIAS = os.environ.get("SN_FP8_WGRAD_BIAS", "1") != "0"
+
+
 def fp8_wgrad_ok(s: ConvSpec) -> bool:
     """Can this conv's weight gradient run as an e4m3 / e5m2 product (fp8 MC operands read
     with ds_read_b64_tr_b8: whole 16-channel chunks on both sides, implicit im2col of x)?"""
@@ -486,12 +489,17 @@ def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc):
     gradient stays an exact bf16 column sum (reference: base_conv_layer.cpp:338-376,
     conv_layer.cu:35-53)."""
     sc, ix, xq, idy = f8w
-    if db is not None:
+    # the bias gradient rides on the product as a virtual ones column of B (an e4m3 1.0,
+    # dequantised by dy's factor only): the column sum of the QUANTISED output gradient,
+    # instead of a separate bf16 pass over dy (SN_FP8_WGRAD_BIAS=0 keeps that pass)
+    fused_db = db is not None and kred % 16 == 0 and FP8_WGRAD_BIAS
+    if db is not None and not fused_db:
         colsum(dy2, db, accumulate=db_acc)
     A = Dense(dyq.view(M, s.K), s.K, kcontig=False, gstride=s.Kg)
     B = Im2col(xq, _geom(s), kcontig=False, gstride=s.Cg)
     gemm(s.Kg, kred, M, A, B, dw, kred, epi=EPI_F32_ACC if dw_acc else EPI_F32, groups=s.groups,
-         c_gstride=s.Kg * kred, deq=(sc.deq(idy), sc.deq(ix), 2 if sc.is_e5m2(idy) else 1))
+         c_gstride=s.Kg * kred, deq=(sc.deq(idy), sc.deq(ix), 2 if sc.is_e5m2(idy) else 1),
+         bias_grad=db if fused_db else None, bias_acc=db_acc)
 
 
 def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):

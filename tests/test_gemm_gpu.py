@@ -435,3 +435,44 @@ def test_db_tiles_edges_and_k_tail(gpu, tile, shape, monkeypatch):
     except RuntimeError:
         return
     _close(dw, 1 + dy.float().t() @ x.float())
+
+
+@pytest.mark.parametrize("tile", [21, 22])
+@pytest.mark.parametrize("M,N,K", [(64, 576, 64 * 40), (48, 1200, 333 * 8), (17, 200, 1000), (64, 4096, 256)])
+def test_thin_tiles(gpu, tile, M, N, K, monkeypatch):
+    """64-row tiles (gemm_tiles_c.hip): NT / NN / TN dense products, split-K, the bias column."""
+    from sparknet_amd.ops import gemm as G
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    x, w = _bf(M, K, device=gpu), _bf(N, K, device=gpu)
+    _close(G.linear_fwd(x, w), x.float() @ w.float().t())
+    dy = _bf(M, N, device=gpu)
+    _close(G.linear_dgrad(dy, w), dy.float() @ w.float())
+    a, b = _bf(K, M, device=gpu), _bf(K, N, device=gpu)
+    dw = torch.full((M, N), 3.0, device=gpu)
+    db = torch.full((M,), -2.0, device=gpu)
+    G.gemm(M, N, K, G.Dense(a, M, False), G.Dense(b, N, False), dw, N, epi=G.EPI_F32_ACC, splits=3,
+           bias_grad=db, bias_acc=True)
+    _close(dw, 3.0 + a.float().t() @ b.float())
+    _close(db, -2.0 + a.float().sum(0), 1e-3)
+
+
+@pytest.mark.parametrize("tile", [21, 22])
+@pytest.mark.parametrize("case", [(2, 20, 20, 64, 64, 3, 3, 1, 1, 1), (3, 14, 14, 192, 16, 1, 1, 1, 0, 1),
+                                  (2, 9, 9, 64, 48, 3, 3, 1, 1, 1)])
+def test_thin_tiles_conv(gpu, tile, case, monkeypatch):
+    from sparknet_amd.ops import gemm as G, hip, ref
+    from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    N, H, W, Cc, K, R, S, st, pd, g = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    x = _bf(N, H, W, Cc, device=gpu)
+    w = (torch.randn(K, R, S, Cc // g, device=gpu) * 0.1).to(torch.bfloat16)
+    bias = torch.randn(K, device=gpu)
+    _close(hip.conv_forward(x, w, bias, s, relu=True), ref.conv_forward(x, w, bias, s, relu=True))
+    dy = _bf(N, s.P, s.Q, K, device=gpu)
+    dw, db = torch.zeros(K, R, S, Cc // g, device=gpu), torch.zeros(K, device=gpu)
+    dw_r, db_r = torch.zeros_like(dw), torch.zeros_like(db)
+    hip.conv_backward(dy, x, w, s, False, dw, db)
+    ref.conv_backward(dy, x, w, s, False, dw_r, db_r)
+    _close(dw, dw_r)
+    _close(db, db_r, 1e-3)
