@@ -112,6 +112,24 @@ struct SnGemmArgs {
 
 namespace {
 
+// a * b + c on the full-rate 24-bit multiplier (a, b < 2^24; the low 32 bits of the sum).
+// Inline asm: the compiler otherwise forms quarter-rate v_mad_u64_u32 from __umul24 + add,
+// and sinks the address arithmetic of an LDS-DMA into a branch on the lane's validity.
+SN_DEV unsigned mad24(unsigned a, unsigned b, unsigned c) {
+  unsigned d;
+  asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+// floor(n / d) for 0 <= n < 2^23 (fp32 reciprocal estimate, one correction step), with the
+// back-multiply on the full-rate 24-bit multiplier
+SN_DEV int fdiv24(int n, int d, float inv) {
+  int q = __float2int_rz((float)n * inv);
+  const int r = n - (int)__umul24((unsigned)q, (unsigned)d);
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
 // KC tile: [TILE rows][64 k] bf16, 128-B rows, 16-B chunk index XOR (row>>1)&7.
 SN_DEV int kc_off(int row, int kc) { return row * 128 + ((kc ^ ((row >> 1) & 7)) << 4); }
 
@@ -173,7 +191,7 @@ struct GStager {
   bool pv[NI];                     // element offset of the (h=ph, w=pw) corner, may be < 0
   int cr[NI], cs[NI], cc[NI];  // MC+IM2COL: column decode (cols fixed across k)
   bool cv[NI], co[NI];         //   column valid / column is the ones column
-  float invPQ, invQ, invCg, invS, invKg;
+  float invPQ, invQ, invP, invCg, invS, invKg;
   // KC+IM2COL: (tap row, tap col, channel) of the NEXT tile to issue — tiles are issued in
   // order, so the decode advances by one K-step per issue (wave-uniform, scalar) instead
   // of dividing k_tile by Cg and S every time; and a raw buffer resource over the input
@@ -187,7 +205,7 @@ struct GStager {
   // per-instruction column terms, and whether this wave holds a ones-column lane (then it
   // stages through global loads and the ones page; otherwise through the buffer resource)
   int sn_, sp_, sq_;
-  int cdh[MC ? NI : 1], cdw[MC ? NI : 1], colo[MC ? NI : 1];
+  int cdh[MC ? NI : 1], cdw[MC ? NI : 1], ccol[MC ? NI : 1];
   bool wave_has_one;
   // Low-VALU address paths (all decisions wave-uniform, taken once at init):
   //  KC+IM2COL: kcmode 1 = every K-step lies inside ONE filter tap (Cg % (8*EPC) == 0), so
@@ -204,6 +222,10 @@ struct GStager {
   bool fast;
   unsigned rowb[NI];  // modular byte arithmetic: operands up to 4 GB (the resource's range)
   int kch[NI], voff[NI];
+  // kcmode 1: the lane's valid filter taps, bit r (h = ph + r*dh inside the image) and bit
+  // 16 + s (w = pw + s*dw inside), 0 for rows past the matrix: a DMA is valid iff both bits
+  // of its tap are set — one v_and + v_cmp instead of two adds and two range compares
+  unsigned vrs[NI];
 
   SN_DEV void init(const SnOperand& op, int grp, int wave, int lane, int tile_row0, int rows_lim,
                    int tile_col0, int cols_lim, int ones = -1, int k_start = 0, int k_lim_hint = 0,
@@ -235,6 +257,7 @@ struct GStager {
     invKg = MODE == OP_FLIPW ? 1.f / (float)g.C : 0.f;
     invPQ = 1.f / (float)(g.P * g.Q);
     invQ = 1.f / (float)g.Q;
+    invP = 1.f / (float)g.P;
     invCg = 1.f / (float)g.Cg;
     invS = 1.f / (float)g.S;
 #pragma unroll
@@ -262,18 +285,25 @@ struct GStager {
         cs[j] = tap - cr[j] * g.S;
         cdh[j] = cr[j] * g.dh;
         cdw[j] = cs[j] * g.dw;
-        colo[j] = (cdh[j] * g.W + cdw[j]) * g.C + coff + cc[j];
+        ccol[j] = coff + cc[j];
       }
     }
     kcmode = 0;
     fast = false;
     if (MODE == OP_IM2COL && !MC) {
       kcmode = __builtin_amdgcn_readfirstlane(legacy ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
+      if (kcmode == 1 && (g.R > 16 || g.S > 16)) kcmode = 2;  // the tap masks hold 16 rows / cols
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         kch[j] = ch[j] * EPC;
         rowb[j] = (unsigned)(rowoff[j] + kch[j]) * (unsigned)ES;
         if (!pv[j]) ph[j] = -(1 << 28);
+        unsigned m = 0;
+        if (kcmode == 1 && pv[j]) {
+          for (int r = 0; r < g.R; ++r) m |= (unsigned)((unsigned)(ph[j] + r * g.dh) < (unsigned)g.H) << r;
+          for (int t = 0; t < g.S; ++t) m |= (unsigned)((unsigned)(pw[j] + t * g.dw) < (unsigned)g.W) << (16 + t);
+        }
+        vrs[j] = m;
       }
     }
     if (MODE == OP_DENSE) {
@@ -314,18 +344,24 @@ struct GStager {
     }
   }
 
+  // M0 of an LDS-DMA: the LDS byte address of the destination.  The low 32 bits of a generic
+  // pointer into LDS are that address (shared aperture), so no address-space cast (whose
+  // null check costs two SALU per DMA).
+  static SN_DEV uint32_t lds_m0(const char* lds) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  }
   // The DMA is issued from inline asm so the compiler's wait-count pass does not see an
   // LDS write it cannot disambiguate (it would drain vmcnt(0) before the next ds_read);
   // every wait on these DMAs is explicit in the K-loop (counted vmcnt + barrier).
   SN_DEV void dma(const char* src, bool valid, char* lds, bool one = false) {
     const void* s = valid ? (const void*)src
                           : (one ? (ES == 1 ? (const void*)g_one16_f8 : (const void*)g_one16) : (const void*)g_zero16);
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds));
+    const uint32_t m0 = lds_m0(lds);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(s) : "memory");
   }
   // LDS-DMA through the buffer resource: byte offset off (0xffffffff: out of range -> 0)
   SN_DEV void dma_buf(unsigned off, char* lds) {
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds));
+    const uint32_t m0 = lds_m0(lds);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off),
                  "s"(rsrc)
                  : "memory");
@@ -333,7 +369,7 @@ struct GStager {
   // ... with a wave-uniform byte offset `so` in the instruction's SGPR offset field
   // (the per-lane voffset carries the out-of-range marker 0x80000000)
   SN_DEV void dma_buf_so(unsigned off, unsigned so, char* lds) {
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds));
+    const uint32_t m0 = lds_m0(lds);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0), "v"(off),
                  "s"(rsrc), "s"(so)
                  : "memory");
@@ -345,14 +381,15 @@ struct GStager {
     if (!MC) {
       if (MODE == OP_DENSE) {
         if (fast) {
-          const bool tail = k_tile + 8 * EPC > k_lim;
           const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)(k_tile * ES));
+          if (k_tile + 8 * EPC <= k_lim) {  // no K tail: fixed per-lane offsets, no VALU
 #pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            unsigned o = (unsigned)voff[j];
-            if (tail && k_tile + kch[j] >= k_lim) o = 0x80000000u;
-            dma_buf_so(o, so, dst + j * 1024);
+            for (int j = 0; j < NI; ++j) dma_buf_so((unsigned)voff[j], so, dst + j * 1024);
+            return;
           }
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            dma_buf_so(k_tile + kch[j] >= k_lim ? 0x80000000u : (unsigned)voff[j], so, dst + j * 1024);
           return;
         }
 #pragma unroll
@@ -372,6 +409,21 @@ struct GStager {
             ns = 0;
             ++nr;
           }
+        }
+        if (kcmode == 1) {
+          // one tap per K-step: scalar tap offset and tap mask; per DMA v_and + v_cmp (tap
+          // inside the image), v_add + v_cndmask (offset, or out of range -> zeros)
+          const unsigned tb0 = (unsigned)(((r0 * g.dh) * g.W + s0 * g.dw) * g.C + c0) * (unsigned)ES;
+          const unsigned msk = (1u << r0) | (1u << (16 + s0));
+          if (k_tile + 8 * EPC <= k_lim) {
+#pragma unroll
+            for (int j = 0; j < NI; ++j) dma_buf((vrs[j] & msk) == msk ? rowb[j] + tb0 : 0xffffffffu, dst + j * 1024);
+            return;
+          }
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            dma_buf((vrs[j] & msk) == msk && k_tile + kch[j] < k_lim ? rowb[j] + tb0 : 0xffffffffu, dst + j * 1024);
+          return;
         }
         if (kcmode != 0) {
           const bool tail = k_tile + 8 * EPC > k_lim;
@@ -455,13 +507,14 @@ struct GStager {
       }
     } else {
       if (MODE == OP_DENSE && fast) {
-        const bool tail = k_tile + BKE > k_lim;
         const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)((long long)k_tile * ld * ES));
+        if (k_tile + BKE <= k_lim) {
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          unsigned o = (unsigned)voff[j];
-          if (tail && k_tile + kch[j] >= k_lim) o = 0x80000000u;
-          dma_buf_so(o, so, dst + j * 1024);
+          for (int j = 0; j < NI; ++j) dma_buf_so((unsigned)voff[j], so, dst + j * 1024);
+        } else {
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            dma_buf_so(k_tile + kch[j] >= k_lim ? 0x80000000u : (unsigned)voff[j], so, dst + j * 1024);
         }
       } else if (MODE == OP_DENSE) {
 #pragma unroll
@@ -488,23 +541,65 @@ struct GStager {
         int n = sn_, p = sp_, q = sq_;
         int off[NI];
         bool val[NI];
+        // Q >= RPI (every conv but a tiny spatial extent): a step of RPI pixels wraps q at most
+        // once and p at most once — selects, not per-lane (divergent) carry loops
+        const bool wrap1 = g.Q >= RPI;
+        if (wrap1 && !wave_has_one) {
+          // the common case as its own straight-line code: buffer-resource DMAs, the K tail
+          // test only in the last K-step, 24-bit address arithmetic
+          // rows past the K range read zeros (relative row limit; no row is past it before the
+          // last K-step)
+          const int krel = k_lim - k_tile;
+          const unsigned cb = (unsigned)(g.C * ES);
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            if (j > 0) {
+              q += RPI;
+              const bool wq = q >= g.Q;
+              q -= wq ? g.Q : 0;
+              p += wq;
+              const bool wp = p >= g.P;
+              p -= wp ? g.P : 0;
+              n += wp;
+            }
+            const int h = (int)mad24((unsigned)p, (unsigned)g.sh, (unsigned)(cdh[j] - g.ph));
+            const int w = (int)mad24((unsigned)q, (unsigned)g.sw, (unsigned)(cdw[j] - g.pw));
+            const bool v = cv[j] & ((unsigned)h < (unsigned)g.H) & ((unsigned)w < (unsigned)g.W) & (rr[j] < krel);
+            const unsigned pix = mad24(mad24((unsigned)n, (unsigned)g.H, (unsigned)h), (unsigned)g.W, (unsigned)w);
+            const unsigned o = mad24(pix, cb, (unsigned)(ccol[j] * ES));
+            dma_buf(v ? o : 0xffffffffu, dst + j * 1024);
+          }
+        } else {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           if (j > 0) {
             q += RPI;
-            while (q >= g.Q) {
-              q -= g.Q;
-              ++p;
-            }
-            while (p >= g.P) {
-              p -= g.P;
-              ++n;
+            if (wrap1) {
+              const bool wq = q >= g.Q;
+              q -= wq ? g.Q : 0;
+              p += wq;
+              const bool wp = p >= g.P;
+              p -= wp ? g.P : 0;
+              n += wp;
+            } else {
+              while (q >= g.Q) {
+                q -= g.Q;
+                ++p;
+              }
+              while (p >= g.P) {
+                p -= g.P;
+                ++n;
+              }
             }
           }
-          const int hrow = p * g.sh - g.ph, wrow = q * g.sw - g.pw;
-          val[j] = cv[j] && k_tile + rr[j] < k_lim && (unsigned)(hrow + cdh[j]) < (unsigned)g.H &&
-                   (unsigned)(wrow + cdw[j]) < (unsigned)g.W;
-          off[j] = ((n * g.H + hrow) * g.W + wrow) * g.C + colo[j];
+          // 24-bit multiplies (full-rate v_mad_u32_u24, not the quarter-rate 32-bit ones): for
+          // a valid lane every factor is below 2^24 (host: < 2^24 pixels per launch), an
+          // invalid lane's offset is never used
+          const int h = (int)__umul24((unsigned)p, (unsigned)g.sh) - g.ph + cdh[j];
+          const int w = (int)__umul24((unsigned)q, (unsigned)g.sw) - g.pw + cdw[j];
+          val[j] = cv[j] && k_tile + rr[j] < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          const unsigned pix = __umul24(__umul24((unsigned)n, (unsigned)g.H) + (unsigned)h, (unsigned)g.W) + (unsigned)w;
+          off[j] = (int)(__umul24(pix, (unsigned)g.C) + (unsigned)ccol[j]);
         }
         if (!wave_has_one) {
 #pragma unroll
@@ -514,15 +609,15 @@ struct GStager {
           for (int j = 0; j < NI; ++j)
             dma(base + (long long)off[j] * ES, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
         }
+        }
         // next tile: BKE pixels on
         sq_ += BKE;
-        const int dp = fdiv(sq_, g.Q, invQ);
-        sq_ -= dp * g.Q;
+        const int dp = fdiv24(sq_, g.Q, invQ);
+        sq_ -= (int)__umul24((unsigned)dp, (unsigned)g.Q);
         sp_ += dp;
-        while (sp_ >= g.P) {
-          sp_ -= g.P;
-          ++sn_;
-        }
+        const int dn = fdiv24(sp_, g.P, invP);
+        sp_ -= (int)__umul24((unsigned)dn, (unsigned)g.P);
+        sn_ += dn;
       }
     }
   }
@@ -866,7 +961,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   const int wm0 = (wave % WM) * (16 * MFR), wn0 = (wave / WM) * (16 * NFR);
   const int nk = k1 > k0 ? (k1 - k0 + BKE - 1) / BKE : 0;
 
-  auto compute = [&](const char* la) {
+  auto compute = [&](const char* la) __attribute__((always_inline)) {
     const char* lb = la + A_BYTES;
     if constexpr (FP8 && MFR * NFR > 16) {
       // large fp8 tiles (gemm_fp8big.hip): B fragments held, A fragments streamed per row
@@ -938,7 +1033,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][i], fa[s][j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  auto issue = [&](char* st, int kt) {
+  auto issue = [&](char* st, int kt) __attribute__((always_inline)) {
     sa.issue(st, wv, k0 + kt * BKE, k1, m_blk, args.M);
     sb.issue(st + A_BYTES, wv, k0 + kt * BKE, k1, n_blk, n_lim);
   };
@@ -969,7 +1064,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     // One barrier per K-step: retire this wave's DMA of tile kt, barrier (all waves' DMAs
     // landed AND all reads of the other stage from step kt-1 are done), then start the
     // DMA of tile kt+1 into the other stage and run the MFMAs of tile kt under it.
-    auto step = [&](char* cur, char* nxt, int kt) {
+    auto step = [&](char* cur, char* nxt, int kt) __attribute__((always_inline)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (kt + 1 < nk) issue(nxt, kt + 1);
@@ -982,7 +1077,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     }
   } else {
     constexpr int PER_TILE = SA::NI + SB::NI;  // LDS-DMA instructions per wave per tile
-    auto step = [&](char* cur, char* nxt2, int kt) {
+    auto step = [&](char* cur, char* nxt2, int kt) __attribute__((always_inline)) {
       // retire tile kt; tile kt+1 (if any) stays in flight
       if (kt + 1 < nk)
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(PER_TILE));

@@ -52,7 +52,7 @@ def dense(args):
         gemm._FORCE_TILE = -1
         t_def = timed(lambda: gemm.linear_fwd(x, w), reps)
         t_blas = timed(lambda: torch.matmul(x, w.t()), reps)
-        for t in [0, 11, 13, 16] + sorted(gemm.PK_TILES):
+        for t in ([0, 11, 13, 16] + sorted(gemm.PK_TILES) if args.tiles is None else args.tiles):
             gemm._FORCE_TILE = t
             try:
                 y = gemm.linear_fwd(x, w)
@@ -151,7 +151,7 @@ def model(args):
         scale = ref.abs().max().item() + 1e-6
         best = (t_old, tile, splits, 0.0)
         alls = []
-        for t in sorted(gemm.PK_TILES):
+        for t in (sorted(gemm.PK_TILES) if args.tiles is None else args.tiles):
             for s in dict.fromkeys((1, splits, gemm.choose_splits(M, N, K, groups, t)[0])):
                 kc = -(-(-(-K // s)) // 64) * 64
                 s2 = max(1, -(-K // kc))
@@ -180,7 +180,10 @@ def main():
     ap.add_argument("--model", default="")
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--dense", action="store_true")
+    ap.add_argument("--tiles", default=None, help="comma-separated candidate tiles ('' = time the recorded configs only)")
     args = ap.parse_args()
+    if args.tiles is not None:
+        args.tiles = [int(t) for t in args.tiles.split(",") if t]
     from sparknet_amd.ops import _lib
     _lib.kernels()
     if args.dense:

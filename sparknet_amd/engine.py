@@ -523,8 +523,9 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
     :func:`fp8_step`).  Gradients, masters and checkpoints stay bf16 / fp32.  Layers whose
     channels are not multiples of 16 (e.g. an RGB input conv) stay bf16, and so do layers
     with fewer than ``min_macs_per_input`` forward MACs per input element (where the
-    quantisation pass over a large activation costs more than the faster product saves,
-    e.g. VGG's 64-channel conv1_2).
+    quantisation pass over a large activation costs more than the faster product saves),
+    except 64 -> 64 3x3 convs (VGG's conv1_2), which run the e4m3 direct kernel
+    (ops.hip.direct_fp8_ok; SN_CONV_DIRECT_FP8=0 returns them to bf16).
 
     ``dgrad``: also run the data gradients of stride-1 Convolutions in e4m3 (the output
     gradient and the flip-transposed weights quantised per tensor; weight gradients stay
@@ -544,11 +545,15 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
     for li, layer in enumerate(net.layers):
         if layer.type_name in ("Convolution", "InnerProduct") and len(net.bottom_vecs[li]) == 1:
             b = net.bottom_vecs[li][0]
-            if layer.fp8_eligible(b) and fp8_macs_per_input(layer, b) >= min_macs_per_input:
+            # 64 -> 64 3x3 convs run the e4m3 direct kernel (no idle MFMA columns), worth it below
+            # the MAC threshold too
+            direct = layer.type_name == "Convolution" and hip.direct_fp8_ok(layer.spec(b))
+            if layer.fp8_eligible(b) and (direct or fp8_macs_per_input(layer, b) >= min_macs_per_input):
                 chosen.append(layer)
             if (dgrad and layer.type_name == "Convolution" and layer.fp8_dgrad_eligible(b)
                     and net.bottom_need_backward[li][0]
-                    and fp8_dgrad_macs_per_grad(layer, b) >= min_macs_per_input):
+                    and ((direct and dgrad_format == "e4m3")
+                         or fp8_dgrad_macs_per_grad(layer, b) >= min_macs_per_input)):
                 chosen_dg.append(layer)
     sc = hip.Fp8Scales(2 * (len(chosen) + len(chosen_dg)), net.device)
     for i, layer in enumerate(chosen):

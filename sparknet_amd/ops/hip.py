@@ -275,6 +275,15 @@ def direct_conv_ok(s: ConvSpec) -> bool:
             and s.sw == 1 and s.ph == 0 and s.pw == 0 and s.dh == 1 and s.dw == 1)
 
 
+# the e4m3 direct kernel (csrc/kernels/conv3x3_fp8.hip) for the same 64 -> 64 products under
+# engine.enable_fp8 (forward, and the data gradient with an e4m3 output gradient)
+_DIRECT_FP8 = os.environ.get("SN_CONV_DIRECT_FP8", "1") != "0"
+
+
+def direct_fp8_ok(s: ConvSpec) -> bool:
+    return _DIRECT_FP8 and direct_c64_ok(s)
+
+
 def _side_covers(t: torch.Tensor) -> bool:
     from . import gemm as G
     return G._SIDE is not None and G._SIDE.covers(t)  # a fused fp8 side output needs the GEMM epilogue
@@ -589,6 +598,10 @@ def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8, ws_dyq=None):
     if dyq is None:
         dyq = quant_fp8(dy, sc.slot(idy), e5m2=e5)
     wtq = quant_fp8(wt, sc.slot(iwt))
+    if direct_fp8_ok(s) and not e5 and dx.is_contiguous() and not _side_covers(dx):
+        call("conv3x3_fp8", _c(dyq), wtq, sc.deq(idy), sc.deq(iwt), None, _c(gate) if gate is not None else None, dx,
+             s.N, s.H, s.W, 0)
+        return dx
     A = Im2col(dyq, g2, kcontig=True, gstride=s.Kg)
     B = Dense(wtq.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
     gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg,
@@ -1082,6 +1095,9 @@ def conv_forward_fp8(xq, wq, b, s: ConvSpec, deq_x, deq_w, relu=False, out=None)
     kred = s.R * s.S * s.Cg
     y = out if out is not None else torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=xq.device)
     assert y.is_contiguous()
+    if direct_fp8_ok(s) and not _side_covers(y):
+        call("conv3x3_fp8", _c(xq), _c(wq), deq_x, deq_w, b, None, y, s.N, s.H, s.W, int(relu))
+        return y
     A = Im2col(xq, _geom(s), kcontig=True, gstride=s.Cg)
     B = Dense(wq.view(s.K, kred), kred, True, gstride=s.Kg * kred)
     gemm(M, s.Kg, kred, A, B, y, s.K, epi=EPI_BF16, groups=s.groups, c_gstride=s.Kg, bias=b, relu=relu,
