@@ -475,6 +475,21 @@ struct GStager {
                 r += 1;
               }
             }
+          } else if (g.Cg > 2 * EPC && g.S >= 2) {
+            // Cg in (16, 64) bf16 channels (AlexNet conv2's 48 per group, GoogLeNet's reduce
+            // widths): c < Cg + 6 EPC < 4 Cg, so the chunk crosses at most three tap boundaries
+            // and the tap column wraps at most twice — compares and selects, not a per-lane
+            // (divergent) carry loop
+            const int d = (c >= g.Cg) + (c >= 2 * g.Cg) + (c >= 3 * g.Cg);
+            c -= (int)__umul24((unsigned)d, (unsigned)g.Cg);
+            s += d;
+            const bool ws = s >= g.S;
+            s -= ws ? g.S : 0;
+            r += ws;
+            if (s >= g.S) {  // S == 2 and three crossings
+              s -= g.S;
+              ++r;
+            }
           } else if (g.Cg >= 2 * EPC) {
             // narrower channel runs (fp8 with 64 channels: VGG conv1_2): the chunk may cross
             // up to 8 * EPC / Cg taps — a short carry loop instead of two divisions
@@ -493,9 +508,9 @@ struct GStager {
             s = tap - r * g.S;
           }
           kv[e] = k_tile + ch[e] * EPC < k_lim;
-          dh[e] = r * g.dh;
-          dw[e] = s * g.dw;
-          toff[e] = (dh[e] * g.W + dw[e]) * g.C + c;
+          dh[e] = (int)__umul24((unsigned)r, (unsigned)g.dh);
+          dw[e] = (int)__umul24((unsigned)s, (unsigned)g.dw);
+          toff[e] = (int)mad24(mad24((unsigned)dh[e], (unsigned)g.W, (unsigned)dw[e]), (unsigned)g.C, (unsigned)c);
         }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
@@ -1381,6 +1396,66 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
     __builtin_amdgcn_s_setprio(0);
   };
 
+  if constexpr (PH == 8) {
+    // The 8-phase schedule (cdna_hip_programming "The 256^2 8-phase template"): four phases
+    // per K-tile, one C-quadrant of 16 (BN 256) MFMAs per phase, two barriers per phase; each
+    // phase issues its fragment reads and ONE half-tile LDS-DMA before its first barrier and
+    // its MFMAs after it.  Half-tile stream: phase q of K-tile t stages
+    //   q0: B_lo(t+1)   q1: A_lo(t+2)   q2: B_hi(t+2)   q3: A_hi(t+2)
+    // each into a region whose last read was the phase before (WAR: the previous phase's
+    // second barrier); q3 waits vmcnt(A_lo + B_hi + A_hi loads) before its first barrier, which
+    // retires every half of K-tile t+1 (read from the next phase on).  DMAs past the K range
+    // read zeros (same instruction count, so the counted waits hold).
+    constexpr int VM3 = 2 * H_A + H_B;
+    if (nk > 0) {
+      dma_a_lo(0);
+      dma_b_hi(0);
+      dma_a_hi(0);
+      dma_b_lo(0);
+      dma_a_lo(1);
+      dma_b_hi(1);
+      dma_a_hi(1);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM3));
+      __builtin_amdgcn_s_barrier();
+      auto ktile = [&](int t, int b) __attribute__((always_inline)) {
+        // q0: (A_lo, B_lo)
+        read_a(A_lo(b));
+        read_b(fbl, B_lo(b));
+        dma_b_lo(t + 1);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mma(acc[0][0], fbl);
+        __builtin_amdgcn_s_barrier();
+        // q1: (A_lo, B_hi)
+        read_b(fbh, B_hi(b));
+        dma_a_lo(t + 2);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mma(acc[0][1], fbh);
+        __builtin_amdgcn_s_barrier();
+        // q2: (A_hi, B_hi)
+        read_a(A_hi(b));
+        dma_b_hi(t + 2);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mma(acc[1][1], fbh);
+        __builtin_amdgcn_s_barrier();
+        // q3: (A_hi, B_lo)
+        read_b(fbl, B_lo(b));
+        dma_a_hi(t + 2);
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM3));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mma(acc[1][0], fbl);
+        __builtin_amdgcn_s_barrier();
+      };
+      for (int t = 0; t < nk; t += 2) {
+        ktile(t, 0);
+        if (t + 1 < nk) ktile(t + 1, 1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else
   if (nk > 0) {
     // prologue: K-step 0 whole, K-step 1 without A_hi (issued in P1(0))
     dma_a_lo(0);
@@ -1596,4 +1671,5 @@ int sn_gemm_big4(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_fp8_big(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_pk_a(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_tiles_c(const SnGemmArgs& a, hipStream_t stream);
+int sn_gemm_t256p8(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_pk_b(const SnGemmArgs& a, hipStream_t stream);

@@ -117,15 +117,17 @@ TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96)
          17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64), 21: (64, 256), 22: (64, 128),
          # persistent ring-pipelined tiles (csrc/kernels/gemm_pk.h): one 512-thread block per CU
          30: (256, 128), 31: (256, 64), 32: (256, 96), 33: (128, 128), 34: (256, 192), 36: (128, 256),
-         37: (192, 384), 38: (256, 256), 39: (256, 128)}
+         37: (192, 384), 38: (256, 256), 39: (256, 128),
+         # gemm256_kernel with the 8-phase schedule (csrc/kernels/gemm_t256p8.hip)
+         40: (256, 256), 41: (256, 128)}
 PK_TILES = frozenset((30, 31, 32, 33, 34, 36, 37, 38))
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
 _SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512, 21: 512,
           22: 768,
-          30: 256, 31: 256, 32: 256, 33: 256, 34: 256, 36: 256, 37: 256, 38: 256, 39: 256}
+          30: 256, 31: 256, 32: 256, 33: 256, 34: 256, 36: 256, 37: 256, 38: 256, 39: 256, 40: 256, 41: 256}
 _KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55,
-             30: 0.75, 31: 0.45, 32: 0.6, 33: 0.45, 34: 1.1, 36: 0.75, 37: 1.3, 38: 1.2}
+             30: 0.75, 31: 0.45, 32: 0.6, 33: 0.45, 34: 1.1, 36: 0.75, 37: 1.3, 38: 1.2, 40: 1.6, 41: 0.9}
 # autotune candidates 11-14 (SN_GEMM_TILE8W=0 drops them)
 _TILE8W = os.environ.get("SN_GEMM_TILE8W", "1") != "0"
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
@@ -406,7 +408,7 @@ def _side_fields(side, out, ldc, c_gstride, N, tile, epi, lds):
     launch cannot store the side output (the side is then marked incomplete)."""
     off = (out.data_ptr() - side.base.data_ptr()) // 2
     qp = side.q.data_ptr() + off
-    if ((not lds and not _SIDE_FRAG) or epi not in (EPI_BF16, EPI_BF16_DROP) or tile in (6, 7, 8, 9) or tile in PK_TILES
+    if ((not lds and not _SIDE_FRAG) or epi not in (EPI_BF16, EPI_BF16_DROP) or tile in (6, 7, 8, 9, 39, 40, 41) or tile in PK_TILES
             or N % 8 or ldc % 8
             or c_gstride % 8 or qp % 8):
         side.ok = False

@@ -236,8 +236,8 @@ def test_fp8_conv_dgrad(gpu, case, fmt, tile, monkeypatch):
 # 4-wave tiles (19, 20: dense only): every operand
 # layout, ragged edges, short and long K (the phased DMA pipeline issues zero-page DMAs past
 # the last K-step), split-K, the bias-gradient column and the implicit-GEMM convolutions
-BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20]
-MC_B = {6, 7, 11, 12, 13}  # tiles with MC (k-strided) A and B operand instances
+BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 40, 41]
+MC_B = {6, 7, 11, 12, 13, 40, 41}  # tiles with MC (k-strided) A and B operand instances
 
 
 @pytest.mark.parametrize("tile", BIG_TILES)
@@ -289,7 +289,8 @@ def _pad(t):
 @pytest.mark.parametrize("tile", BIG_TILES)
 @pytest.mark.parametrize("case", [(2, 13, 13, 64, 384, 3, 3, 1, 1, 1), (2, 27, 27, 96, 256, 5, 5, 1, 2, 2),
                                   (4, 14, 14, 32, 128, 1, 1, 1, 0, 1), (3, 9, 9, 64, 40, 3, 3, 1, 1, 2),
-                                  (2, 7, 7, 192, 96, 3, 3, 1, 1, 2)])
+                                  (2, 7, 7, 192, 96, 3, 3, 1, 1, 2), (2, 9, 9, 24, 32, 2, 2, 1, 0, 1),
+                                  (2, 11, 11, 40, 48, 3, 3, 1, 1, 1)])
 def test_gemm256_conv(gpu, tile, case, monkeypatch):
     from sparknet_amd.ops import gemm as G, hip, ref
     from sparknet_amd.ops.spec import ConvSpec
@@ -438,7 +439,7 @@ def test_db_tiles_edges_and_k_tail(gpu, tile, shape, monkeypatch):
 
 
 @pytest.mark.parametrize("tile", [21, 22])
-@pytest.mark.parametrize("M,N,K", [(64, 576, 64 * 40), (48, 1200, 333 * 8), (17, 200, 1000), (64, 4096, 256)])
+@pytest.mark.parametrize("M,N,K", [(64, 576, 64 * 40), (48, 1200, 333 * 8), (24, 200, 1000), (64, 4096, 256)])
 def test_thin_tiles(gpu, tile, M, N, K, monkeypatch):
     """64-row tiles (gemm_tiles_c.hip): NT / NN / TN dense products, split-K, the bias column."""
     from sparknet_amd.ops import gemm as G
@@ -474,5 +475,33 @@ def test_thin_tiles_conv(gpu, tile, case, monkeypatch):
     dw_r, db_r = torch.zeros_like(dw), torch.zeros_like(db)
     hip.conv_backward(dy, x, w, s, False, dw, db)
     ref.conv_backward(dy, x, w, s, False, dw_r, db_r)
+    _close(dw, dw_r)
+    _close(db, db_r, 1e-3)
+
+
+@pytest.mark.parametrize("tile", [0, 4, 5, 16])
+@pytest.mark.parametrize("case", [(2, 9, 9, 24, 32, 2, 2, 1, 0, 1), (2, 11, 11, 40, 48, 3, 3, 1, 1, 1),
+                                  (2, 13, 13, 96, 64, 5, 5, 1, 2, 2), (3, 10, 10, 56, 24, 3, 3, 2, 1, 1)])
+def test_small_cg_im2col(gpu, tile, case, monkeypatch):
+    """Implicit im2col with 16 < Cg < 64 channels per group: a 64-wide K-step straddles up
+    to three filter taps (the branch-free carry of GStager.issue); fwd, dgrad, wgrad + bias
+    against the fp32 reference."""
+    from sparknet_amd.ops import gemm as G, hip, ref
+    from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    N, H, W, Cc, K, R, S, st, pd, g = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    x = _bf(N, H, W, Cc, device=gpu)
+    w = (torch.randn(K, R, S, Cc // g, device=gpu) * 0.1).to(torch.bfloat16)
+    bias = torch.randn(K, device=gpu)
+    _close(hip.conv_forward(x, w, bias, s, relu=True), ref.conv_forward(x, w, bias, s, relu=True))
+    if tile != 0:  # 4 / 16: K-contiguous B only (forward products); 5: 48-wide outputs
+        return
+    dy = _bf(N, s.P, s.Q, K, device=gpu)
+    dw, db = torch.zeros(K, R, S, Cc // g, device=gpu), torch.zeros(K, device=gpu)
+    dw_r, db_r = torch.zeros_like(dw), torch.zeros_like(db)
+    dx = hip.conv_backward(dy, x, w, s, True, dw, db)
+    dx_r = ref.conv_backward(dy, x, w, s, True, dw_r, db_r)
+    _close(dx, dx_r)
     _close(dw, dw_r)
     _close(db, db_r, 1e-3)
