@@ -119,6 +119,10 @@ def main():
         return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.model == "vgg16":
+        # VGG-16 at per-GPU batch 2048 fills ~170 GB with tensors of 6-13 GB; growable segments
+        # keep the caching allocator from fragmenting the 288 GB (set before the first HIP call)
+        os.environ.setdefault("PYTORCH_ALLOC_CONF", "expandable_segments:True")
     import torch
     if args.cpu:
         dev = torch.device("cpu")

@@ -47,6 +47,16 @@ SN_DEV uint4 pack8(const float* f) {
   return r;
 }
 
+// XCD-aware bijective block remap: the hardware deals consecutive block ids round-robin over
+// the 8 XCDs (each with its own L2); after the remap the blocks that share an XCD hold a
+// contiguous range of logical ids, so neighbouring tiles (stencil halos, shared input rows)
+// meet in one L2 instead of being fetched by several.
+SN_DEV int xcd_block(int bid, int nwg) {
+  if (nwg < 16) return bid;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 // Fast division by a runtime-invariant divisor for 0 <= n < 2^24 (pixel / tap indices):
 // fp32 reciprocal estimate + one correction step replaces the ~40-instruction integer
 // division sequence in the implicit-GEMM address generators.

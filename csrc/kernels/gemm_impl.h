@@ -91,7 +91,7 @@ struct SnGemmArgs {
   // bf16 epilogues of unsplit 4-wave tiles: stage the finished tile through the idle LDS
   // stages and store it as whole 16-B row chunks (host: ldc % 8 == 0, 16-B aligned C)
   int lds_store;
-  int addr_legacy;  // 1: general per-lane address decode only (A/B probe of the fast DMA paths)
+  int addr_legacy;  // 1: general per-lane address decode only; 2: only the MC im2col path general (A/B probes)
   // bf16 epilogues of gemm_kernel, unsplit: also store the finished (bf16-rounded) output as
   // fp8 bytes q_out[grp * q_gstride + m * q_ld + n] = sat(v * q_slot[0]) and fold its |max|
   // into q_slot[1] — the quantisation pass of the fp8 product that consumes this output
@@ -113,11 +113,10 @@ struct SnGemmArgs {
 namespace {
 
 // a * b + c on the full-rate 24-bit multiplier (a, b < 2^24; the low 32 bits of the sum).
-// Inline asm: the compiler otherwise forms quarter-rate v_mad_u64_u32 from __umul24 + add,
-// and sinks the address arithmetic of an LDS-DMA into a branch on the lane's validity.
+// Inline asm: the compiler otherwise forms quarter-rate v_mad_u64_u32 from __umul24 + add.
 SN_DEV unsigned mad24(unsigned a, unsigned b, unsigned c) {
   unsigned d;
-  asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
 }
 
@@ -205,7 +204,8 @@ struct GStager {
   // per-instruction column terms, and whether this wave holds a ones-column lane (then it
   // stages through global loads and the ones page; otherwise through the buffer resource)
   int sn_, sp_, sq_;
-  int cdh[MC ? NI : 1], cdw[MC ? NI : 1], ccol[MC ? NI : 1];
+  int cdh[MC ? NI : 1], cdw[MC ? NI : 1], colo[MC ? NI : 1], ccol[MC ? NI : 1];
+  bool mc_lean;  // MC+IM2COL: the select / 24-bit address path (SnGemmArgs.addr_legacy != 2)
   bool wave_has_one;
   // Low-VALU address paths (all decisions wave-uniform, taken once at init):
   //  KC+IM2COL: kcmode 1 = every K-step lies inside ONE filter tap (Cg % (8*EPC) == 0), so
@@ -233,6 +233,7 @@ struct GStager {
     ld = op.ld;
     g = op.g;
     ones_col = ones;
+    mc_lean = legacy == 0;
     if (MODE == OP_IM2COL) {
       const unsigned long long a = reinterpret_cast<unsigned long long>(op.ptr);
       const unsigned nbytes = (unsigned)((unsigned long long)g.N * g.H * g.W * g.C * ES);
@@ -285,13 +286,14 @@ struct GStager {
         cs[j] = tap - cr[j] * g.S;
         cdh[j] = cr[j] * g.dh;
         cdw[j] = cs[j] * g.dw;
+        colo[j] = (cdh[j] * g.W + cdw[j]) * g.C + coff + cc[j];
         ccol[j] = coff + cc[j];
       }
     }
     kcmode = 0;
     fast = false;
     if (MODE == OP_IM2COL && !MC) {
-      kcmode = __builtin_amdgcn_readfirstlane(legacy ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
+      kcmode = __builtin_amdgcn_readfirstlane(legacy == 1 ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
       if (kcmode == 1 && (g.R > 16 || g.S > 16)) kcmode = 2;  // the tap masks hold 16 rows / cols
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -309,7 +311,7 @@ struct GStager {
     if (MODE == OP_DENSE) {
       // element extent of the operand for this group: KC rows x ld, MC (k rows) x ld
       const long long extent = MC ? (long long)k_lim_hint * ld : (long long)rows_lim * ld;
-      fast = __builtin_amdgcn_readfirstlane((int)(!legacy && extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
+      fast = __builtin_amdgcn_readfirstlane((int)(legacy != 1 && extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
       // built unconditionally from wave-uniform values so it stays in SGPRs
       const unsigned long long a = reinterpret_cast<unsigned long long>(base);
       rsrc[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
@@ -559,13 +561,16 @@ struct GStager {
         // Q >= RPI (every conv but a tiny spatial extent): a step of RPI pixels wraps q at most
         // once and p at most once — selects, not per-lane (divergent) carry loops
         const bool wrap1 = g.Q >= RPI;
-        if (wrap1 && !wave_has_one) {
+        if (wrap1 && !wave_has_one && mc_lean) {
           // the common case as its own straight-line code: buffer-resource DMAs, the K tail
           // test only in the last K-step, 24-bit address arithmetic
           // rows past the K range read zeros (relative row limit; no row is past it before the
           // last K-step)
           const int krel = k_lim - k_tile;
           const unsigned cb = (unsigned)(g.C * ES);
+          unsigned ob[NI];
+          // every offset first (NI independent chains the scheduler can interleave), then the
+          // DMAs
 #pragma unroll
           for (int j = 0; j < NI; ++j) {
             if (j > 0) {
@@ -582,21 +587,16 @@ struct GStager {
             const bool v = cv[j] & ((unsigned)h < (unsigned)g.H) & ((unsigned)w < (unsigned)g.W) & (rr[j] < krel);
             const unsigned pix = mad24(mad24((unsigned)n, (unsigned)g.H, (unsigned)h), (unsigned)g.W, (unsigned)w);
             const unsigned o = mad24(pix, cb, (unsigned)(ccol[j] * ES));
-            dma_buf(v ? o : 0xffffffffu, dst + j * 1024);
+            ob[j] = v ? o : 0xffffffffu;
           }
-        } else {
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          if (j > 0) {
-            q += RPI;
-            if (wrap1) {
-              const bool wq = q >= g.Q;
-              q -= wq ? g.Q : 0;
-              p += wq;
-              const bool wp = p >= g.P;
-              p -= wp ? g.P : 0;
-              n += wp;
-            } else {
+          for (int j = 0; j < NI; ++j) dma_buf(ob[j], dst + j * 1024);
+        } else {
+          // general path: per-lane carry loops, 32-bit offsets
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            if (j > 0) {
+              q += RPI;
               while (q >= g.Q) {
                 q -= g.Q;
                 ++p;
@@ -606,33 +606,29 @@ struct GStager {
                 ++n;
               }
             }
+            const int hrow = p * g.sh - g.ph, wrow = q * g.sw - g.pw;
+            val[j] = cv[j] && k_tile + rr[j] < k_lim && (unsigned)(hrow + cdh[j]) < (unsigned)g.H &&
+                     (unsigned)(wrow + cdw[j]) < (unsigned)g.W;
+            off[j] = ((n * g.H + hrow) * g.W + wrow) * g.C + colo[j];
           }
-          // 24-bit multiplies (full-rate v_mad_u32_u24, not the quarter-rate 32-bit ones): for
-          // a valid lane every factor is below 2^24 (host: < 2^24 pixels per launch), an
-          // invalid lane's offset is never used
-          const int h = (int)__umul24((unsigned)p, (unsigned)g.sh) - g.ph + cdh[j];
-          const int w = (int)__umul24((unsigned)q, (unsigned)g.sw) - g.pw + cdw[j];
-          val[j] = cv[j] && k_tile + rr[j] < k_lim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          const unsigned pix = __umul24(__umul24((unsigned)n, (unsigned)g.H) + (unsigned)h, (unsigned)g.W) + (unsigned)w;
-          off[j] = (int)(__umul24(pix, (unsigned)g.C) + (unsigned)ccol[j]);
-        }
-        if (!wave_has_one) {
+          if (!wave_has_one) {
 #pragma unroll
-          for (int j = 0; j < NI; ++j) dma_buf(val[j] ? (unsigned)off[j] * (unsigned)ES : 0xffffffffu, dst + j * 1024);
-        } else {
+            for (int j = 0; j < NI; ++j) dma_buf(val[j] ? (unsigned)off[j] * (unsigned)ES : 0xffffffffu, dst + j * 1024);
+          } else {
 #pragma unroll
-          for (int j = 0; j < NI; ++j)
-            dma(base + (long long)off[j] * ES, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
-        }
+            for (int j = 0; j < NI; ++j)
+              dma(base + (long long)off[j] * ES, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
+          }
         }
         // next tile: BKE pixels on
         sq_ += BKE;
-        const int dp = fdiv24(sq_, g.Q, invQ);
-        sq_ -= (int)__umul24((unsigned)dp, (unsigned)g.Q);
+        const int dp = fdiv(sq_, g.Q, invQ);
+        sq_ -= dp * g.Q;
         sp_ += dp;
-        const int dn = fdiv24(sp_, g.P, invP);
-        sp_ -= (int)__umul24((unsigned)dn, (unsigned)g.P);
-        sn_ += dn;
+        while (sp_ >= g.P) {
+          sp_ -= g.P;
+          ++sn_;
+        }
       }
     }
   }

@@ -17,7 +17,7 @@ __global__ void maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
                             PoolGeom g, int gate) {
   const int cv = VEC ? g.C / 8 : g.C;
   const long long total = (long long)g.N * g.P * g.Q * cv;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const uint32_t pix = udiv((uint32_t)i, g.fcv), pq = udiv(pix, g.fQ), n = udiv(pq, g.fP);
     const int c0 = (int)((uint32_t)i - pix * cv) * (VEC ? 8 : 1);
@@ -72,7 +72,7 @@ template <bool VEC>
 __global__ void avepool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g) {
   const int cv = VEC ? g.C / 8 : g.C;
   const long long total = (long long)g.N * g.P * g.Q * cv;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const uint32_t pix = udiv((uint32_t)i, g.fcv), pq = udiv(pix, g.fQ), n = udiv(pq, g.fP);
     const int c0 = (int)((uint32_t)i - pix * cv) * (VEC ? 8 : 1);
@@ -112,7 +112,7 @@ __global__ void pool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restric
                          PoolGeom g) {
   const int cv = VEC ? g.C / 8 : g.C;
   const long long total = (long long)g.N * g.H * g.W * cv;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const uint32_t pix = udiv((uint32_t)i, g.fcv), ph_ = udiv(pix, g.fW), n = udiv(ph_, g.fH);
     const int c0 = (int)((uint32_t)i - pix * cv) * (VEC ? 8 : 1);
@@ -221,7 +221,7 @@ __global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, bf16_t* __restrict__
   float qmax = 0.f;
   const float qsc = qs.q ? qs.slot[0] : 0.f;
   const long long total = (long long)g.N * g.P * g.Q * cv;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const uint32_t pix = udiv((uint32_t)i, g.fcv), pq = udiv(pix, g.fQ), n = udiv(pq, g.fP);
     const int c0 = (int)((uint32_t)i - pix * cv) * 8;
@@ -276,7 +276,7 @@ __global__ void pool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restr
   float qmax = 0.f;
   const float qsc = qs.q ? qs.slot[0] : 0.f;
   const long long total = (long long)g.N * g.H * g.W * cv;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const uint32_t pix = udiv((uint32_t)i, g.fcv), ph_ = udiv(pix, g.fW), n = udiv(ph_, g.fH);
     const int c0 = (int)((uint32_t)i - pix * cv) * 8;
@@ -339,7 +339,7 @@ __global__ void pool_bwd_k3s2(const bf16_t* __restrict__ dy, const uint8_t* __re
                               bf16_t* __restrict__ dx, PoolGeom g, FDiv fBW, FDiv fBH, int BW, int BH) {
   const int cv = g.C / 8;
   const long long total = (long long)g.N * BH * BW * cv;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const uint32_t blk = udiv((uint32_t)i, g.fcv), bh_ = udiv(blk, fBW), n = udiv(bh_, fBH);
     const int c0 = (int)((uint32_t)i - blk * cv) * 8;

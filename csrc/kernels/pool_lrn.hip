@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256) pool_lrn_fwd(const bf16_t* __restrict__ x
   constexpr int PRE = (SIZE - 1) / 2;
   const int cv = g.C >> 3;
   const long long npix = (long long)g.N * g.P * g.Q;
-  const long long pix0 = (long long)blockIdx.x * g.pix;
+  const long long pix0 = (long long)xcd_block(blockIdx.x, gridDim.x) * g.pix;
   const int npx = (int)min((long long)g.pix, npix - pix0);
   const int items = npx * cv;
   for (int it = threadIdx.x; it < items; it += blockDim.x) {
@@ -143,8 +143,9 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
   extern __shared__ uint4 tile[];  // (rows + 1) x Q x cg chunks of the pooled gradient
   constexpr int PRE = (SIZE - 1) / 2, POST = SIZE - PRE - 1;
   const int cg = g.cg;
-  const int wg = blockIdx.x / g.ngrp;
-  const int ch0 = (blockIdx.x - wg * g.ngrp) * cg;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int wg = bid / g.ngrp;
+  const int ch0 = (bid - wg * g.ngrp) * cg;
   const int n = wg / g.nb;
   const int bh0 = (wg - n * g.nb) * g.rows;
   const int qcg = g.Q * cg;

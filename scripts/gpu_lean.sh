@@ -2,7 +2,7 @@
 # lean DMA-issue GEMM mainloop + 8-phase 256x256 tiles (40/41) + e4m3 direct conv: numerics, dense
 # shapes, CaffeNet bench + GEMM census, VGG-16 b2048 fp8 (direct on / off) vs bf16 (gpurun)
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests/test_conv3x3_fp8_gpu.py tests/test_gemm_gpu.py tests/test_gemm_fp8_mc_gpu.py -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/lean_tests.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_conv3x3_fp8_gpu.py tests/test_pool_lrn_gpu.py tests/test_kernels_gpu.py tests/test_gemm_gpu.py tests/test_gemm_fp8_mc_gpu.py -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/lean_tests.log 2>&1
 rc=$?; tail -8 gpurun_out/lean_tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u scripts/pk_probe.py --dense --tiles 0,6,11,13,16,40,41 > gpurun_out/lean_dense.txt 2>&1 || { tail -20 gpurun_out/lean_dense.txt; exit 4; }

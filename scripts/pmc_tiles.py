@@ -19,4 +19,13 @@ for t in [int(v) for v in os.environ.get("TILES", "0,13,30,39").split(",")]:
     for _ in range(10):
         hip.conv_forward(x, w, None, s)
     torch.cuda.synchronize()
+# WGRAD_TILES: the weight gradient of the same conv (MC dense dy x MC implicit im2col of x,
+# split-K slabs + reduce), 10x per tile
+dy = (torch.rand(s.N, s.P, s.Q, s.K, device="cuda") * 2 - 1).to(torch.bfloat16)
+dw = torch.zeros(s.K, s.R, s.S, s.Cg, device="cuda")
+for t in [int(v) for v in os.environ.get("WGRAD_TILES", "").split(",") if v]:
+    gemm._FORCE_TILE = t
+    for _ in range(10):
+        hip.conv_backward(dy, x, w, s, False, dw, None)
+    torch.cuda.synchronize()
 print("done")
