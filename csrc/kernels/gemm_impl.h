@@ -91,7 +91,7 @@ struct SnGemmArgs {
   // bf16 epilogues of unsplit 4-wave tiles: stage the finished tile through the idle LDS
   // stages and store it as whole 16-B row chunks (host: ldc % 8 == 0, 16-B aligned C)
   int lds_store;
-  int addr_legacy;  // 1: general per-lane address decode only; 2: only the MC im2col path general (A/B probes)
+  int addr_legacy;  // 1: general per-lane address decode only (A/B probe of the fast DMA paths)
   // bf16 epilogues of gemm_kernel, unsplit: also store the finished (bf16-rounded) output as
   // fp8 bytes q_out[grp * q_gstride + m * q_ld + n] = sat(v * q_slot[0]) and fold its |max|
   // into q_slot[1] — the quantisation pass of the fp8 product that consumes this output
@@ -118,15 +118,6 @@ SN_DEV unsigned mad24(unsigned a, unsigned b, unsigned c) {
   unsigned d;
   asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
-}
-
-// floor(n / d) for 0 <= n < 2^23 (fp32 reciprocal estimate, one correction step), with the
-// back-multiply on the full-rate 24-bit multiplier
-SN_DEV int fdiv24(int n, int d, float inv) {
-  int q = __float2int_rz((float)n * inv);
-  const int r = n - (int)__umul24((unsigned)q, (unsigned)d);
-  q += (r >= d) - (r < 0);
-  return q;
 }
 
 // KC tile: [TILE rows][64 k] bf16, 128-B rows, 16-B chunk index XOR (row>>1)&7.
@@ -190,7 +181,7 @@ struct GStager {
   bool pv[NI];                     // element offset of the (h=ph, w=pw) corner, may be < 0
   int cr[NI], cs[NI], cc[NI];  // MC+IM2COL: column decode (cols fixed across k)
   bool cv[NI], co[NI];         //   column valid / column is the ones column
-  float invPQ, invQ, invP, invCg, invS, invKg;
+  float invPQ, invQ, invCg, invS, invKg;
   // KC+IM2COL: (tap row, tap col, channel) of the NEXT tile to issue — tiles are issued in
   // order, so the decode advances by one K-step per issue (wave-uniform, scalar) instead
   // of dividing k_tile by Cg and S every time; and a raw buffer resource over the input
@@ -204,8 +195,7 @@ struct GStager {
   // per-instruction column terms, and whether this wave holds a ones-column lane (then it
   // stages through global loads and the ones page; otherwise through the buffer resource)
   int sn_, sp_, sq_;
-  int cdh[MC ? NI : 1], cdw[MC ? NI : 1], colo[MC ? NI : 1], ccol[MC ? NI : 1];
-  bool mc_lean;  // MC+IM2COL: the select / 24-bit address path (SnGemmArgs.addr_legacy != 2)
+  int cdh[MC ? NI : 1], cdw[MC ? NI : 1], colo[MC ? NI : 1];
   bool wave_has_one;
   // Low-VALU address paths (all decisions wave-uniform, taken once at init):
   //  KC+IM2COL: kcmode 1 = every K-step lies inside ONE filter tap (Cg % (8*EPC) == 0), so
@@ -233,7 +223,6 @@ struct GStager {
     ld = op.ld;
     g = op.g;
     ones_col = ones;
-    mc_lean = legacy == 0;
     if (MODE == OP_IM2COL) {
       const unsigned long long a = reinterpret_cast<unsigned long long>(op.ptr);
       const unsigned nbytes = (unsigned)((unsigned long long)g.N * g.H * g.W * g.C * ES);
@@ -258,7 +247,6 @@ struct GStager {
     invKg = MODE == OP_FLIPW ? 1.f / (float)g.C : 0.f;
     invPQ = 1.f / (float)(g.P * g.Q);
     invQ = 1.f / (float)g.Q;
-    invP = 1.f / (float)g.P;
     invCg = 1.f / (float)g.Cg;
     invS = 1.f / (float)g.S;
 #pragma unroll
@@ -287,13 +275,12 @@ struct GStager {
         cdh[j] = cr[j] * g.dh;
         cdw[j] = cs[j] * g.dw;
         colo[j] = (cdh[j] * g.W + cdw[j]) * g.C + coff + cc[j];
-        ccol[j] = coff + cc[j];
       }
     }
     kcmode = 0;
     fast = false;
     if (MODE == OP_IM2COL && !MC) {
-      kcmode = __builtin_amdgcn_readfirstlane(legacy == 1 ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
+      kcmode = __builtin_amdgcn_readfirstlane(legacy ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
       if (kcmode == 1 && (g.R > 16 || g.S > 16)) kcmode = 2;  // the tap masks hold 16 rows / cols
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -311,7 +298,7 @@ struct GStager {
     if (MODE == OP_DENSE) {
       // element extent of the operand for this group: KC rows x ld, MC (k rows) x ld
       const long long extent = MC ? (long long)k_lim_hint * ld : (long long)rows_lim * ld;
-      fast = __builtin_amdgcn_readfirstlane((int)(legacy != 1 && extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
+      fast = __builtin_amdgcn_readfirstlane((int)(!legacy && extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
       // built unconditionally from wave-uniform values so it stays in SGPRs
       const unsigned long long a = reinterpret_cast<unsigned long long>(base);
       rsrc[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
@@ -558,67 +545,31 @@ struct GStager {
         int n = sn_, p = sp_, q = sq_;
         int off[NI];
         bool val[NI];
-        // Q >= RPI (every conv but a tiny spatial extent): a step of RPI pixels wraps q at most
-        // once and p at most once — selects, not per-lane (divergent) carry loops
-        const bool wrap1 = g.Q >= RPI;
-        if (wrap1 && !wave_has_one && mc_lean) {
-          // the common case as its own straight-line code: buffer-resource DMAs, the K tail
-          // test only in the last K-step, 24-bit address arithmetic
-          // rows past the K range read zeros (relative row limit; no row is past it before the
-          // last K-step)
-          const int krel = k_lim - k_tile;
-          const unsigned cb = (unsigned)(g.C * ES);
-          unsigned ob[NI];
-          // every offset first (NI independent chains the scheduler can interleave), then the
-          // DMAs
 #pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            if (j > 0) {
-              q += RPI;
-              const bool wq = q >= g.Q;
-              q -= wq ? g.Q : 0;
-              p += wq;
-              const bool wp = p >= g.P;
-              p -= wp ? g.P : 0;
-              n += wp;
+        for (int j = 0; j < NI; ++j) {
+          if (j > 0) {
+            q += RPI;
+            while (q >= g.Q) {
+              q -= g.Q;
+              ++p;
             }
-            const int h = (int)mad24((unsigned)p, (unsigned)g.sh, (unsigned)(cdh[j] - g.ph));
-            const int w = (int)mad24((unsigned)q, (unsigned)g.sw, (unsigned)(cdw[j] - g.pw));
-            const bool v = cv[j] & ((unsigned)h < (unsigned)g.H) & ((unsigned)w < (unsigned)g.W) & (rr[j] < krel);
-            const unsigned pix = mad24(mad24((unsigned)n, (unsigned)g.H, (unsigned)h), (unsigned)g.W, (unsigned)w);
-            const unsigned o = mad24(pix, cb, (unsigned)(ccol[j] * ES));
-            ob[j] = v ? o : 0xffffffffu;
+            while (p >= g.P) {
+              p -= g.P;
+              ++n;
+            }
           }
+          const int hrow = p * g.sh - g.ph, wrow = q * g.sw - g.pw;
+          val[j] = cv[j] && k_tile + rr[j] < k_lim && (unsigned)(hrow + cdh[j]) < (unsigned)g.H &&
+                   (unsigned)(wrow + cdw[j]) < (unsigned)g.W;
+          off[j] = ((n * g.H + hrow) * g.W + wrow) * g.C + colo[j];
+        }
+        if (!wave_has_one) {
 #pragma unroll
-          for (int j = 0; j < NI; ++j) dma_buf(ob[j], dst + j * 1024);
+          for (int j = 0; j < NI; ++j) dma_buf(val[j] ? (unsigned)off[j] * (unsigned)ES : 0xffffffffu, dst + j * 1024);
         } else {
-          // general path: per-lane carry loops, 32-bit offsets
 #pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            if (j > 0) {
-              q += RPI;
-              while (q >= g.Q) {
-                q -= g.Q;
-                ++p;
-              }
-              while (p >= g.P) {
-                p -= g.P;
-                ++n;
-              }
-            }
-            const int hrow = p * g.sh - g.ph, wrow = q * g.sw - g.pw;
-            val[j] = cv[j] && k_tile + rr[j] < k_lim && (unsigned)(hrow + cdh[j]) < (unsigned)g.H &&
-                     (unsigned)(wrow + cdw[j]) < (unsigned)g.W;
-            off[j] = ((n * g.H + hrow) * g.W + wrow) * g.C + colo[j];
-          }
-          if (!wave_has_one) {
-#pragma unroll
-            for (int j = 0; j < NI; ++j) dma_buf(val[j] ? (unsigned)off[j] * (unsigned)ES : 0xffffffffu, dst + j * 1024);
-          } else {
-#pragma unroll
-            for (int j = 0; j < NI; ++j)
-              dma(base + (long long)off[j] * ES, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
-          }
+          for (int j = 0; j < NI; ++j)
+            dma(base + (long long)off[j] * ES, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
         }
         // next tile: BKE pixels on
         sq_ += BKE;

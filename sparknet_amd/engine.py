@@ -524,8 +524,8 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
     channels are not multiples of 16 (e.g. an RGB input conv) stay bf16, and so do layers
     with fewer than ``min_macs_per_input`` forward MACs per input element (where the
     quantisation pass over a large activation costs more than the faster product saves),
-    except 64 -> 64 3x3 convs (VGG's conv1_2), which run the e4m3 direct kernel
-    (ops.hip.direct_fp8_ok; SN_CONV_DIRECT_FP8=0 returns them to bf16).
+    except, with SN_CONV_DIRECT_FP8=1, 64 -> 64 3x3 convs (VGG's conv1_2), which then run the
+    e4m3 direct kernel (ops.hip.direct_fp8_ok).
 
     ``dgrad``: also run the data gradients of stride-1 Convolutions in e4m3 (the output
     gradient and the flip-transposed weights quantised per tensor; weight gradients stay
@@ -832,6 +832,46 @@ class OverlappedUpdate:
         torch.cuda.current_stream(self.solver.device).wait_stream(self.side)
 
 
+def release_activations(net) -> int:
+    """Drop the net's references to its per-iteration tensors — the data / diff of every blob
+    a layer with bottoms produces, and the layers' forward-to-backward workspaces — so the
+    eager warm-up's buffers return to the caching allocator.  A graph capture allocates every
+    activation afresh in its private pool; without this the warm-up's copies stay referenced
+    until the capture overwrites them one layer at a time, and a net that fills most of the
+    288 GB (VGG-16 at per-GPU batch 2048) holds both sets at once.  The tops of data layers
+    (written in place by the feeders) and the parameters are kept.  Returns the blobs dropped."""
+    keep = set()
+    for li in range(len(net.layers)):
+        if not net.bottom_ids[li]:
+            keep.update(net.top_ids[li])
+    n = 0
+    for bi, blob in enumerate(net.blobs):
+        if bi in keep:
+            continue
+        blob._data = None
+        blob._diff = None
+        n += 1
+    for layer in net.layers:
+        for d in getattr(layer, "_ws", None) or ():
+            if isinstance(d, dict):
+                d.clear()
+    gc.collect()
+    torch.cuda.empty_cache()
+    return n
+
+
+def _release_before_capture(dev) -> bool:
+    """release_activations before a capture when the warm-up holds over 45 % of the device
+    (SN_GRAPH_RELEASE=1 / 0 forces it on / off)."""
+    env = os.environ.get("SN_GRAPH_RELEASE", "")
+    if env in ("0", "1"):
+        return env == "1"
+    if dev.type != "cuda":
+        return False
+    total = torch.cuda.get_device_properties(dev).total_memory
+    return torch.cuda.memory_reserved(dev) > 0.45 * total
+
+
 class GraphStep:
     """One captured solver iteration (iter_size = 1)."""
 
@@ -912,6 +952,8 @@ class GraphStep:
                 s.iter += 1
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
+        if _release_before_capture(dev):
+            release_activations(s.net)
         self.graph = torch.cuda.CUDAGraph()
         self._use_branches = True
         if self.pre:

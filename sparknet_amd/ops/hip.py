@@ -276,8 +276,11 @@ def direct_conv_ok(s: ConvSpec) -> bool:
 
 
 # the e4m3 direct kernel (csrc/kernels/conv3x3_fp8.hip) for the same 64 -> 64 products under
-# engine.enable_fp8 (forward, and the data gradient with an e4m3 output gradient)
-_DIRECT_FP8 = os.environ.get("SN_CONV_DIRECT_FP8", "1") != "0"
+# engine.enable_fp8 (forward, and the data gradient with an e4m3 output gradient).  Opt-in
+# (SN_CONV_DIRECT_FP8=1): at VGG conv1_2's shape it runs the forward 1.37x faster than the bf16
+# direct kernel but the data gradient only ~1.2x (with dy's fp8 copy free), and the layer's
+# extra fp8 buffers push VGG-16 b2048 past the 288 GB (profiles/r4_direct8_probe.txt)
+_DIRECT_FP8 = os.environ.get("SN_CONV_DIRECT_FP8", "0") == "1"
 
 
 def direct_fp8_ok(s: ConvSpec) -> bool:

@@ -24,8 +24,9 @@ def _close(a, b, tol):
 
 @pytest.mark.parametrize("N,H,W", [(1, 16, 16), (2, 13, 29), (3, 33, 17), (40, 56, 56), (2, 224, 224)])
 @pytest.mark.parametrize("relu,bias", [(False, False), (True, True)])
-def test_direct_fp8_forward(gpu, N, H, W, relu, bias):
+def test_direct_fp8_forward(gpu, N, H, W, relu, bias, monkeypatch):
     from sparknet_amd.ops import hip
+    monkeypatch.setattr(hip, "_DIRECT_FP8", True)
     from sparknet_amd.ops.spec import ConvSpec
     s = ConvSpec(N, H, W, 64, 64, 3, 3, 1, 1, 1, 1, 1, 1, 1)
     assert hip.direct_fp8_ok(s)
@@ -47,6 +48,7 @@ def test_direct_fp8_matches_gemm_path(gpu, monkeypatch):
     """The direct kernel and the implicit-GEMM fp8 path read the same bytes and scales."""
     from sparknet_amd.ops import hip
     from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(hip, "_DIRECT_FP8", True)
     s = ConvSpec(4, 40, 40, 64, 64, 3, 3, 1, 1, 1, 1, 1, 1, 1)
     xq, _ = _f8(torch.randn(4, 40, 40, 64, device=gpu) * 4)
     wq, _ = _f8(torch.randn(64, 3, 3, 64, device=gpu) * 4)
@@ -59,12 +61,13 @@ def test_direct_fp8_matches_gemm_path(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("N,H,W,gated", [(2, 20, 37, True), (24, 56, 56, False), (2, 224, 224, True)])
-def test_direct_fp8_dgrad(gpu, N, H, W, gated):
+def test_direct_fp8_dgrad(gpu, N, H, W, gated, monkeypatch):
     """ops.hip._conv_dgrad_fp8 on a 64 -> 64 conv takes the direct kernel (e4m3 dy x e4m3
     flip-transposed weights), gate fused; error vs the fp32 transposed conv of the bf16
     inputs within e4m3 rounding, like the GEMM path's test (test_gemm_gpu.test_fp8_conv_dgrad)."""
     from sparknet_amd.ops import hip
     from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(hip, "_DIRECT_FP8", True)
     s = ConvSpec(N, H, W, 64, 64, 3, 3, 1, 1, 1, 1, 1, 1, 1)
     gen = torch.Generator(device=gpu).manual_seed(7)
     x = torch.randn(N, H, W, 64, device=gpu, generator=gen).to(torch.bfloat16)

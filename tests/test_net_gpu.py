@@ -224,6 +224,38 @@ def test_fp8_fused_quant_is_bitwise_equal(gpu, monkeypatch):
     assert torch.equal(res["1"][1], res["0"][1])
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+def test_release_activations_before_capture_is_bitwise_equal(gpu, monkeypatch, fp8):
+    """engine.release_activations (run before a capture when the warm-up holds most of the
+    device, forced here with SN_GRAPH_RELEASE=1): the captured iteration re-creates every
+    activation, gradient, workspace and fp8 side output it dropped, so training is bitwise equal
+    to a capture that kept the warm-up's buffers."""
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.engine import GraphStep, enable_fp8, fuse_relu
+    net_p = models.vgg16(train_batch=4, test_batch=4, crop=32, classes=10)
+    res = {}
+    for rel in ("1", "0"):
+        monkeypatch.setenv("SN_GRAPH_RELEASE", rel)
+        sp = models.zoo.vgg16_solver(net_p)
+        sp.base_lr = 0.002
+        solver = Solver(sp, device=torch.device("cuda:0"), seed=5, build_test_nets=False)
+        fuse_relu(solver.net)
+        if fp8:
+            enable_fp8(solver.net, 0.0, dgrad=True, wgrad=True)
+        g = torch.Generator().manual_seed(2)
+        x = torch.randn(4, 3, 32, 32, generator=g) * 0.5
+        y = torch.tensor([[1.0], [3.0], [5.0], [7.0]])
+
+        def pre():
+            solver.net.blob_by_name("data").set_nchw(x)
+            solver.net.blob_by_name("label").set_nchw(y)
+        st = GraphStep(solver, warmup=2, pre=pre, overlap=False)
+        losses = [float(st.step()) for _ in range(6)]
+        res[rel] = (losses, solver.net.flat_data.clone())
+    assert res["1"][0] == res["0"][0], (res["1"][0], res["0"][0])
+    assert torch.equal(res["1"][1], res["0"][1])
+
+
 def test_fused_fold_weight_gradient_with_image_chunks(gpu, monkeypatch):
     """A conv whose S2D-folded input comes from the fused augment (the data blob itself is
     never written) and whose batch is split into image chunks (VGG-16 conv1_1 at batch
