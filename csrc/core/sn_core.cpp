@@ -725,13 +725,14 @@ int sn_solver_step(void* s, int iters) {
     g_err = "null state";
     return 1;
   }
-  // steps (eager Python iterations, or the step graph's capture / replays) rebind or
-  // rewrite the train net's blobs: a forward plan's buffers are no longer what the net
-  // (sn_backward, sn_blob_get) sees
-  invalidate(s, P_FWD_TRAIN);
   NativeState& st = native_state(s);
   NativeStep* ns = st.step.get();
   if (!ns) {
+    // steps through Python (eager iterations, or the step graph's capture) rebind the train
+    // net's blobs: a forward plan's buffers are no longer what the net (sn_backward,
+    // sn_blob_get) sees.  Native replays of the step graph write only the step graph's own
+    // buffers and update the weights in place, so a forward plan stays valid across them.
+    invalidate(s, P_FWD_TRAIN);
     Gil g;
     if (native_enabled() && !st.step_failed && iters > 3) {
       PyObject* ok = call_quiet(s, "native_eligible", nullptr);

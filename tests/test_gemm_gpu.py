@@ -505,3 +505,25 @@ def test_small_cg_im2col(gpu, tile, case, monkeypatch):
     _close(dx, dx_r)
     _close(dw, dw_r)
     _close(db, db_r, 1e-3)
+
+
+@pytest.mark.parametrize("tile,splits", [(22, 229), (22, 1), (21, 229), (0, 229)])
+def test_thin_tiles_small_c(gpu, tile, splits, monkeypatch):
+    """cifar10_quick's conv1 weight gradient (C 8 after channel padding, 5x5 pad 2, M = 32
+    filters, N = 201 with the bias column, reduction over 100 x 32 x 32 pixels) at the
+    split-K the first-call tuner picked: against the fp32 reference."""
+    from sparknet_amd.ops import gemm as G, hip, ref
+    from sparknet_amd.ops.spec import ConvSpec
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    s = ConvSpec(100, 32, 32, 8, 32, 5, 5, 1, 1, 2, 2, 1, 1, 1)
+    kchunk = -(-(-(-102400 // splits)) // 64) * 64
+    monkeypatch.setattr(G, "choose_splits", lambda *a, **k: (-(-102400 // kchunk), kchunk))
+    x = _bf(100, 32, 32, 8, device=gpu)
+    w = (torch.randn(32, 5, 5, 8, device=gpu) * 0.1).to(torch.bfloat16)
+    dy = _bf(100, 32, 32, 32, device=gpu)
+    dw, db = torch.zeros(32, 5, 5, 8, device=gpu), torch.zeros(32, device=gpu)
+    dw_r, db_r = torch.zeros_like(dw), torch.zeros_like(db)
+    hip.conv_backward(dy, x, w, s, False, dw, db)
+    ref.conv_backward(dy, x, w, s, False, dw_r, db_r)
+    _close(dw, dw_r)
+    _close(db, db_r, 1e-3)

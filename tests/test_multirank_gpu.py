@@ -106,7 +106,9 @@ def _sync_worker(rank, world, port, q, steps, batch, seed):
             s.net.layer_by_name("label").feed(y[lo:lo + batch])
             s.step(1)
         torch.cuda.synchronize()
-        q.put((rank, s.net.flat_data.detach().cpu().clone(), None))
+        # numpy, pickled by value: a torch tensor would travel as a shared-memory fd that the
+        # parent cannot open once this process has exited
+        q.put((rank, s.net.flat_data.detach().float().cpu().numpy().copy(), None))
         if comm is not None:
             comm.close()
     except BaseException as e:  # noqa: BLE001
@@ -169,7 +171,7 @@ def test_sync_sgd_share_gpu_matches_single_rank_large_batch(gpu, world):
             p.join(timeout=60)
         for _, _, err in res:
             assert err is None, err
-        return [w for _, w, _ in sorted(res, key=lambda t: t[0])]
+        return [torch.from_numpy(w) for _, w, _ in sorted(res, key=lambda t: t[0])]
 
     multi = launch(world, batch)
     single = launch(1, world * batch)[0]
