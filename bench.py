@@ -120,9 +120,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.model == "vgg16":
-        # VGG-16 at per-GPU batch 2048 fills ~170 GB with tensors of 6-13 GB; growable segments
-        # keep the caching allocator from fragmenting the 288 GB (set before the first HIP call)
-        os.environ.setdefault("PYTORCH_ALLOC_CONF", "expandable_segments:True")
+        # VGG-16 at per-GPU batch 2048 fills ~170 GB with tensors of 6-13 GB: cached blocks above
+        # 1 GB are not split for smaller requests, so the caching allocator cannot fragment the
+        # 288 GB into partly used giant segments (expandable segments are not supported on
+        # ROCm here); set before the first HIP call
+        os.environ.setdefault("PYTORCH_ALLOC_CONF", "max_split_size_mb:1024")
     import torch
     if args.cpu:
         dev = torch.device("cpu")

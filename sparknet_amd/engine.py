@@ -524,8 +524,8 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
     channels are not multiples of 16 (e.g. an RGB input conv) stay bf16, and so do layers
     with fewer than ``min_macs_per_input`` forward MACs per input element (where the
     quantisation pass over a large activation costs more than the faster product saves),
-    except, with SN_CONV_DIRECT_FP8=1, 64 -> 64 3x3 convs (VGG's conv1_2), which then run the
-    e4m3 direct kernel (ops.hip.direct_fp8_ok).
+    except 64 -> 64 3x3 convs (VGG's conv1_2), which run the e4m3 direct kernel
+    (ops.hip.direct_fp8_ok; SN_CONV_DIRECT_FP8=0 returns them to bf16).
 
     ``dgrad``: also run the data gradients of stride-1 Convolutions in e4m3 (the output
     gradient and the flip-transposed weights quantised per tensor; weight gradients stay

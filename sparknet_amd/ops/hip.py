@@ -276,11 +276,12 @@ def direct_conv_ok(s: ConvSpec) -> bool:
 
 
 # the e4m3 direct kernel (csrc/kernels/conv3x3_fp8.hip) for the same 64 -> 64 products under
-# engine.enable_fp8 (forward, and the data gradient with an e4m3 output gradient).  Opt-in
-# (SN_CONV_DIRECT_FP8=1): at VGG conv1_2's shape it runs the forward 1.37x faster than the bf16
-# direct kernel but the data gradient only ~1.2x (with dy's fp8 copy free), and the layer's
-# extra fp8 buffers push VGG-16 b2048 past the 288 GB (profiles/r4_direct8_probe.txt)
-_DIRECT_FP8 = os.environ.get("SN_CONV_DIRECT_FP8", "0") == "1"
+# engine.enable_fp8 (forward, and the data gradient with an e4m3 output gradient; the layer's
+# weight gradient then runs fp8 too): forward 1.37x the bf16 direct kernel at VGG conv1_2's
+# shape (profiles/r4_direct8_probe.txt), VGG-16 b2048 fp8 step 186 -> 181 ms with the thin tiles
+# and 192 -> 182 ms without (profiles/r4_vgg16_fp8_variants.jsonl).  SN_CONV_DIRECT_FP8=0 keeps
+# these layers bf16.
+_DIRECT_FP8 = os.environ.get("SN_CONV_DIRECT_FP8", "1") != "0"
 
 
 def direct_fp8_ok(s: ConvSpec) -> bool:

@@ -399,13 +399,17 @@ def test_googlenet_zero_copy_concat_bitwise(gpu, monkeypatch):
         assert torch.equal(ga, gb)
 
 
-def test_fp8_layer_selection_threshold(gpu):
-    """enable_fp8's default cost-model threshold keeps VGG's conv1_2 (576 MACs per input
-    element) and a 10-way fc8 in bf16, everything else eligible in e4m3."""
+@pytest.mark.parametrize("direct", [True, False])
+def test_fp8_layer_selection_threshold(gpu, direct, monkeypatch):
+    """enable_fp8's default cost-model threshold keeps a 10-way fc8 in bf16 and everything
+    else eligible in e4m3; VGG's conv1_2 (576 MACs per input element, below the threshold)
+    is chosen only for the e4m3 direct kernel (SN_CONV_DIRECT_FP8, default on)."""
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.engine import enable_fp8
+    from sparknet_amd.ops import hip
+    monkeypatch.setattr(hip, "_DIRECT_FP8", direct)
     net_p = models.vgg16(train_batch=2, test_batch=2, crop=32, classes=10)
     solver = Solver(models.zoo.vgg16_solver(net_p), device=torch.device("cuda:0"), seed=5, build_test_nets=False)
-    assert enable_fp8(solver.net) == 13
+    assert enable_fp8(solver.net) == (14 if direct else 13)
     chosen = {layer.name for layer in solver.net.layers if getattr(layer, "fp8_slots", None) is not None}
-    assert "conv1_2" not in chosen and "fc8" not in chosen and "conv2_1" in chosen and "fc6" in chosen
+    assert ("conv1_2" in chosen) == direct and "fc8" not in chosen and "conv2_1" in chosen and "fc6" in chosen
