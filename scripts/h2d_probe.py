@@ -1,34 +1,38 @@
-#!/usr/bin/env python3
-"""Pinned host -> device copy bandwidth of one CaffeNet minibatch (50 MB uint8): one copy
-on one stream vs the batch split over 2 / 4 streams (several SDMA engines), with and
-without binding this process to the GPU's NUMA node."""
+"""H2D feed bandwidth on the box: one CaffeNet minibatch of uint8 256x256x3 images (50.3 MB)
+from pinned host memory, as one copy, split over 2 / 4 copy streams, and (run under
+HSA_ENABLE_SDMA=0 by the caller) through the blit-kernel path."""
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch  # noqa: E402
+import torch
 
-from sparknet_amd.parallel.topology import bind_to_gpu_numa, gpu_numa_node  # noqa: E402
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+n = B * 256 * 256 * 3
+src = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+src.random_(0, 255)
+dst = torch.empty(n, dtype=torch.uint8, device="cuda")
+streams = [torch.cuda.Stream() for _ in range(4)]
 
-node = bind_to_gpu_numa(0) if os.environ.get("BIND") else -1
-print("gpu numa node", gpu_numa_node(0), "bound", node, flush=True)
-x = torch.randint(0, 256, (256, 3, 256, 256), dtype=torch.uint8).pin_memory()
-d = torch.empty_like(x, device="cuda")
-for ns in (1, 2, 4, 8):
-    streams = [torch.cuda.Stream() for _ in range(ns)]
-    parts = x.chunk(ns)
-    dparts = d.chunk(ns)
+
+def run(k, reps=20):
+    chunk = -(-n // k)
     for _ in range(3):
-        for s, p, q in zip(streams, parts, dparts):
-            with torch.cuda.stream(s):
-                q.copy_(p, non_blocking=True)
+        for i in range(k):
+            with torch.cuda.stream(streams[i]):
+                dst[i * chunk:(i + 1) * chunk].copy_(src[i * chunk:(i + 1) * chunk], non_blocking=True)
     torch.cuda.synchronize()
     t = time.perf_counter()
-    for _ in range(20):
-        for s, p, q in zip(streams, parts, dparts):
-            with torch.cuda.stream(s):
-                q.copy_(p, non_blocking=True)
+    for _ in range(reps):
+        for i in range(k):
+            with torch.cuda.stream(streams[i]):
+                dst[i * chunk:(i + 1) * chunk].copy_(src[i * chunk:(i + 1) * chunk], non_blocking=True)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t) / 20
-    print(f"{ns} stream(s): {dt * 1e3:.2f} ms per 50 MB batch = {x.numel() / dt / 1e9:.1f} GB/s", flush=True)
+    dt = (time.perf_counter() - t) / reps
+    return dt
+
+
+for k in (1, 2, 4):
+    dt = run(k)
+    print(f"SDMA={os.environ.get('HSA_ENABLE_SDMA', '1')} streams={k}: {n / 1e6:.1f} MB in {dt * 1e3:.3f} ms = "
+          f"{n / dt / 1e9:.1f} GB/s", flush=True)

@@ -231,7 +231,11 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
         y, ldy = out, chan_stride(out)
     else:
         y, ldy = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device), s.K
-    if direct_conv_ok(s) and ldx == s.C and ldy == s.K and x.is_contiguous() and not _side_covers(y):
+    direct_io = ldx == s.C and ldy == s.K and x.is_contiguous() and not _side_covers(y)
+    if direct_io and packed_conv_ok(s):
+        call("conv_packed3x3", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu))
+        return y
+    if direct_io and direct_conv_ok(s):
         call("conv3x3_direct", x, _c(w), b, None, y, s.N, s.H, s.W, s.C, s.K, s.ph, int(relu))
         return y
     if _implicit_ok(s):
@@ -273,6 +277,20 @@ def direct_conv_ok(s: ConvSpec) -> bool:
         return True
     return (_DIRECT_K96 and s.C == 48 and s.K == 96 and s.groups == 1 and s.R == 3 and s.S == 3 and s.sh == 1
             and s.sw == 1 and s.ph == 0 and s.pw == 0 and s.dh == 1 and s.dw == 1)
+
+
+# CaffeNet / AlexNet conv1 after the fold (48 -> 96, 3x3, pad 0) on the tap-packed direct kernel
+# (csrc/kernels/conv_packed.hip: 14 instead of 18 K steps, 192-pixel row-major tiles instead of
+# 16 x 16 ones); SN_CONV_PACKED=0 returns it to the 64-channel direct kernel
+_PACKED = os.environ.get("SN_CONV_PACKED", "1") != "0"
+
+
+def packed_conv_ok(s: ConvSpec) -> bool:
+    if not (_PACKED and s.K == 96 and 0 < s.C <= 48 and s.C % 8 == 0 and s.groups == 1 and s.R == 3 and s.S == 3
+            and s.sh == 1 and s.sw == 1 and s.ph == 0 and s.pw == 0 and s.dh == 1 and s.dw == 1 and s.Q > 0):
+        return False
+    rows = min(s.H, (191 + s.Q - 1) // s.Q + 3)  # input rows one 192-pixel tile touches
+    return rows * s.W * s.C * 2 <= 38400 and s.P * s.Q * 96 < 2 ** 31
 
 
 # the e4m3 direct kernel (csrc/kernels/conv3x3_fp8.hip) for the same 64 -> 64 products under

@@ -265,14 +265,16 @@ def test_conv3x3_c64_direct(gpu, shape, monkeypatch):
 
 @pytest.mark.parametrize("shape", [(2, 57, 57), (1, 20, 35)])
 def test_conv3x3_k96_direct(gpu, shape, monkeypatch):
-    """The direct 3x3 conv for 48 -> 96 channels, pad 0 (CaffeNet conv1 after the
-    space-to-depth fold) with bias + ReLU, against the fp32 reference and the GEMM path."""
+    """The 64-channel direct 3x3 kernel's 48 -> 96-channel, pad-0 instance (CaffeNet conv1
+    after the space-to-depth fold, SN_CONV_PACKED=0) with bias + ReLU, against the fp32
+    reference and the GEMM path."""
     from sparknet_amd.ops import hip
     import torch.nn.functional as F
     N, H, W = shape
     s = ConvSpec(N, H, W, 48, 96, 3, 3, 1, 1, 0, 0, 1, 1, 1)
     monkeypatch.setattr(hip, "_DIRECT_K96", True)
-    assert hip.direct_conv_ok(s)
+    monkeypatch.setattr(hip, "_PACKED", False)
+    assert hip.direct_conv_ok(s) and not hip.packed_conv_ok(s)
     x = rnd(N, H, W, 48)
     w = rnd(96, 3, 3, 48, scale=0.1)
     b = torch.randn(96, device="cuda")
@@ -281,6 +283,50 @@ def test_conv3x3_k96_direct(gpu, shape, monkeypatch):
     close(y, ref.permute(0, 2, 3, 1), 1e-2)
     monkeypatch.setattr(hip, "_DIRECT_K96", False)
     close(y, hip.conv_forward(x, w, b, s, relu=True), 1e-2)
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 57, 57, 48), (1, 20, 35, 48), (3, 9, 200, 16), (2, 3, 3, 8), (1, 4, 70, 40),
+                                     (260, 57, 57, 48)])
+@pytest.mark.parametrize("relu,bias", [(True, True), (False, False)])
+def test_conv_packed_direct(gpu, N, H, W, C, relu, bias, monkeypatch):
+    """The tap-packed direct conv (csrc/kernels/conv_packed.hip: k = tap * C + c, 192-pixel
+    row-major tiles; CaffeNet conv1 after the fold is (N, 57, 57, 48)): ragged last tiles,
+    a tile spanning many short rows (W = 3), wide rows (W = 200), C < 48 (zero-weight K tail),
+    more tiles than CUs (N = 260: the persistent loop's cross-tile patch prefetch), against
+    the fp32 reference and, at C = 48, the 64-channel direct kernel."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    monkeypatch.setattr(hip, "_PACKED", True)
+    s = ConvSpec(N, H, W, C, 96, 3, 3, 1, 1, 0, 0, 1, 1, 1)
+    assert hip.packed_conv_ok(s)
+    x = rnd(N, H, W, C)
+    w = rnd(96, 3, 3, C, scale=0.1)
+    b = torch.randn(96, device="cuda") if bias else None
+    y = hip.conv_forward(x, w, b, s, relu=relu)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b)
+    if relu:
+        ref = torch.relu(ref)
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+    if C == 48:
+        monkeypatch.setattr(hip, "_PACKED", False)
+        close(y, hip.conv_forward(x, w, b, s, relu=relu), 1e-2)
+
+
+def test_conv_packed_caffenet_conv1(gpu, monkeypatch):
+    """CaffeNet conv1 (227 x 227 x 3, 11 x 11 / 4) through conv_forward: the space-to-depth
+    fold feeds the packed kernel; against the fp32 reference of the unfolded conv."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    monkeypatch.setattr(hip, "_PACKED", True)
+    s = ConvSpec(4, 227, 227, 3, 96, 11, 11, 4, 4, 0, 0, 1, 1, 1)
+    plan = hip.s2d_plan(s)
+    assert plan is not None and hip.packed_conv_ok(plan[4])
+    x = rnd(4, 227, 227, 3)
+    w = rnd(96, 11, 11, 3, scale=0.05)
+    b = torch.randn(96, device="cuda")
+    y = hip.conv_forward(x, w, b, s, relu=True)
+    ref = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=4))
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
 
 
 def test_softmax_loss_and_accuracy(gpu):
