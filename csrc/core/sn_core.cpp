@@ -15,6 +15,7 @@
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -357,14 +358,26 @@ struct NativeForward {
   }
 };
 
+// One layer parameter inside the flat buffers, for the native sn_blob_* verbs (layer >= 0).
+struct ParamDesc {
+  long long off = 0, count = 0;
+  int layout = 0;  // 0: internal order = Caffe's; 1: internal [K][R][S][C], Caffe [K][C][R][S]
+  int ndim = 0;
+  int cs[6] = {1, 1, 1, 1, 1, 1};  // Caffe shape
+  int is[4] = {1, 1, 1, 1};        // internal shape
+};
+
 struct NativeWeights {
   float* data = nullptr;  // flat fp32 masters (device or host memory)
+  float* diff = nullptr;  // flat fp32 gradients, same offsets
   long long count = 0;
   bool cuda = false;
   void* compute = nullptr;  // bf16 compute shadow (GPU) or null
   long long compute_count = 0;
   hipStream_t stream = nullptr;
   cast_fn_t cast = nullptr;
+  std::map<std::pair<int, int>, ParamDesc> params;  // (layer, index)
+  std::vector<float> stage;                         // host staging for layout conversion
 };
 
 // Per-state native plans.  A plan that could not be built (CPU state, data layers fed
@@ -591,6 +604,31 @@ NativeWeights* native_weights(void* s) {
   w->compute = (void*)(uintptr_t)dict_ll(d, "compute");
   w->compute_count = dict_ll(d, "compute_count");
   w->stream = (hipStream_t)(uintptr_t)dict_ll(d, "stream");
+  w->diff = (float*)(uintptr_t)dict_ll(d, "diff");
+  if (PyObject* rows = PyDict_GetItemString(d, "params")) {  // borrowed
+    const Py_ssize_t nr = PySequence_Size(rows);
+    for (Py_ssize_t i = 0; i < nr && !PyErr_Occurred(); ++i) {
+      PyObject* row = PySequence_GetItem(rows, i);
+      long long v[16];
+      bool ok = row && PySequence_Size(row) == 16;
+      for (int j = 0; ok && j < 16; ++j) {
+        PyObject* x = PySequence_GetItem(row, j);
+        v[j] = x ? PyLong_AsLongLong(x) : -1;
+        Py_XDECREF(x);
+        ok = x != nullptr && !PyErr_Occurred();
+      }
+      Py_XDECREF(row);
+      if (!ok) break;
+      ParamDesc p;
+      p.off = v[2];
+      p.count = v[3];
+      p.layout = (int)v[4];
+      p.ndim = (int)v[5];
+      for (int j = 0; j < 6; ++j) p.cs[j] = (int)v[6 + j];
+      for (int j = 0; j < 4; ++j) p.is[j] = (int)v[12 + j];
+      w->params[{(int)v[0], (int)v[1]}] = p;
+    }
+  }
   Py_DECREF(d);
   if (PyErr_Occurred()) {
     fetch_error("weights_plan");
@@ -616,6 +654,80 @@ void invalidate(void* s, unsigned what) {
   if (what & P_FWD_TEST) st->fwd[1].reset(), st->fwd_failed[1] = false;
   if (what & P_WEIGHTS) st->weights.reset(), st->weights_failed = false;
   if (what & P_SCORES) st->scores_native = st->scores_pending = false;
+}
+
+// The native weights plan's descriptor of parameter `index` of layer `layer`, or null
+// (activation blobs, params outside the flat buffers, no plan: the Python path).
+const ParamDesc* native_param(void* s, int layer, int index, NativeWeights** wo) {
+  if (layer < 0) return nullptr;
+  NativeWeights* w = native_weights(s);
+  if (!w) return nullptr;
+  auto it = w->params.find({layer, index});
+  if (it == w->params.end()) return nullptr;
+  *wo = w;
+  return &it->second;
+}
+
+// internal [K][R][S][C] <-> Caffe [K][C][R][S]
+void krsc_to_kcrs(const float* src, float* dst, const int* is, bool to_caffe) {
+  const long long K = is[0], R = is[1], S = is[2], Cc = is[3];
+  for (long long k = 0; k < K; ++k)
+    for (long long r = 0; r < R; ++r)
+      for (long long q = 0; q < S; ++q)
+        for (long long c = 0; c < Cc; ++c) {
+          const long long a = ((k * R + r) * S + q) * Cc + c, b = ((k * Cc + c) * R + r) * S + q;
+          if (to_caffe) dst[b] = src[a];
+          else dst[a] = src[b];
+        }
+}
+
+bool param_buffer_ok(const ParamDesc& p, long long n, const void* buf) {
+  if (n < p.count || (p.count > 0 && !buf)) {
+    g_err = "buffer holds " + std::to_string(n) + " floats, blob has " + std::to_string(p.count);
+    return false;
+  }
+  return true;
+}
+
+int param_get(NativeWeights* w, const ParamDesc& p, int diff, float* out, long long n) {
+  if (!param_buffer_ok(p, n, out)) return 1;
+  const float* src = (diff ? w->diff : w->data) + p.off;
+  float* dst = out;
+  if (p.layout) {
+    w->stage.resize((size_t)p.count);
+    dst = w->stage.data();
+  }
+  if (w->cuda) {
+    HIPOK(hipMemcpyAsync(dst, src, sizeof(float) * p.count, hipMemcpyDeviceToHost, w->stream));
+    HIPOK(hipStreamSynchronize(w->stream));
+  } else {
+    std::memcpy(dst, src, sizeof(float) * p.count);
+  }
+  if (p.layout) krsc_to_kcrs(dst, out, p.is, true);
+  return 0;
+}
+
+int param_set(NativeWeights* w, const ParamDesc& p, int diff, const float* in, long long n) {
+  if (!param_buffer_ok(p, n, in)) return 1;
+  float* dst = (diff ? w->diff : w->data) + p.off;
+  const float* src = in;
+  if (p.layout) {
+    w->stage.resize((size_t)p.count);
+    krsc_to_kcrs(in, w->stage.data(), p.is, false);
+    src = w->stage.data();
+  }
+  if (!w->cuda) {
+    std::memcpy(dst, src, sizeof(float) * p.count);
+    return 0;
+  }
+  HIPOK(hipMemcpyAsync(dst, src, sizeof(float) * p.count, hipMemcpyHostToDevice, w->stream));
+  // the master changed: refresh its slice of the bf16 compute shadow (Net.sync_compute)
+  if (!diff && w->compute && w->cast(dst, static_cast<char*>(w->compute) + 2 * p.off, p.count, w->stream)) {
+    g_err = "sn_blob_set: sn_cast_f32_bf16 launch failed";
+    return 1;
+  }
+  HIPOK(hipStreamSynchronize(w->stream));  // `in` may be reused as soon as this returns
+  return 0;
 }
 
 }  // namespace
@@ -1076,21 +1188,30 @@ int sn_num_test_scores(void* s) {
 }
 
 int sn_blob_num_axes(void* s, int layer, int index) {
+  NativeWeights* w = nullptr;
+  if (const ParamDesc* p = native_param(s, layer, index, &w)) return p->ndim;
   Gil g;
   return (int)int_call(s, "blob_num_axes", "(ii)", layer, index);
 }
 
 int sn_blob_axis_shape(void* s, int layer, int index, int axis) {
+  NativeWeights* w = nullptr;
+  if (const ParamDesc* p = native_param(s, layer, index, &w))
+    if (axis >= 0 && axis < p->ndim) return p->cs[axis];
   Gil g;
   return (int)int_call(s, "blob_axis_shape", "(iii)", layer, index, axis);
 }
 
 int sn_blob_get(void* s, int layer, int index, int diff, float* out, long long n) {
+  NativeWeights* w = nullptr;
+  if (const ParamDesc* p = native_param(s, layer, index, &w)) return param_get(w, *p, diff, out, n);
   Gil g;
   return status(call(s, "blob_get", "(iiiKL)", layer, index, diff, (unsigned long long)(uintptr_t)out, n));
 }
 
 int sn_blob_set(void* s, int layer, int index, int diff, const float* in, long long n) {
+  NativeWeights* w = nullptr;
+  if (const ParamDesc* p = native_param(s, layer, index, &w)) return param_set(w, *p, diff, in, n);
   Gil g;
   return status(call(s, "blob_set", "(iiiKL)", layer, index, diff, (unsigned long long)(uintptr_t)in, n));
 }

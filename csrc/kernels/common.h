@@ -137,6 +137,18 @@ SN_DEV bool dropout_keep(const long long* rng, int stream, unsigned thr, unsigne
 
 #define SN_CHECK_LAUNCH() (hipGetLastError() == hipSuccess ? 0 : 1)
 
+// CUs of the current device (persistent kernels launch one block per CU); cached per process
+// (one process per GPU), 256 if the query fails.
+static inline int sn_cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
 static inline int sn_blocks(long long n, int per_block, int cap = 65535 * 8) {
   long long b = (n + per_block - 1) / per_block;
   if (b < 1) b = 1;

@@ -178,16 +178,6 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const
 
 }  // namespace
 
-static int cu_count() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  return cus;
-}
-
 // y[N][P][Q][K] = conv3x3(x[N][H][W][C], w[K][3][3][C]) (+ bias, ReLU, gate), stride 1, pad
 // 0 or 1 (P = H + 2 pad - 2) — a forward conv, or a data gradient with flip-transposed
 // weights.  K = 64 (VGG-16 conv1_2: C = 64, pad 1) or 96 (CaffeNet / AlexNet conv1 after the
@@ -205,7 +195,7 @@ extern "C" int sn_conv3x3_direct(const bf16_t* x, const bf16_t* w, const float* 
   g.th = (g.P + TILE - 1) / TILE;
   g.tw = (g.Q + TILE - 1) / TILE;
   g.tiles = N * g.th * g.tw;
-  const int cus = cu_count();
+  const int cus = sn_cu_count();
   const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
   static int nw = 0;
   if (!nw) {

@@ -179,16 +179,6 @@ conv3x3_fp8_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ w,
   }
 }
 
-int cu_count8() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  return cus;
-}
-
 }  // namespace
 
 // y[N][H][W][64] (bf16) = deq_x * deq_w * conv3x3(x[N][H][W][64] e4m3, w[64][3][3][64] e4m3)
@@ -205,7 +195,7 @@ extern "C" int sn_conv3x3_fp8(const uint8_t* x, const uint8_t* w, const float* d
   g.th = (g.H + TILE - 1) / TILE;
   g.tw = (g.W + TILE - 1) / TILE;
   g.tiles = N * g.th * g.tw;
-  const int cus = cu_count8();
+  const int cus = sn_cu_count();
   const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
   hipLaunchKernelGGL(conv3x3_fp8_kernel, dim3((unsigned)grid), dim3(512), 0, st, x, w, deq_x, deq_w, bias, gate, y, g,
                      (int)relu);

@@ -170,16 +170,6 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
   }
 }
 
-int cu_count_p() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  return cus;
-}
-
 }  // namespace
 
 // y[N][H-2][W-2][96] = conv3x3(x[N][H][W][C], w[96][3][3][C]) (+ bias, ReLU), stride 1, pad 0;
@@ -198,7 +188,7 @@ extern "C" int sn_conv_packed3x3(const bf16_t* x, const bf16_t* w, const float* 
   if ((long long)g.P * g.Q >= (1LL << 31) / KOUT) return 3;
   g.tpi = (g.P * g.Q + TP - 1) / TP;
   g.tiles = N * g.tpi;
-  const int cus = cu_count_p();
+  const int cus = sn_cu_count();
   const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
   hipLaunchKernelGGL(conv_packed_kernel, dim3((unsigned)grid), dim3(NT), 0, st, x, w, bias, y, g, (int)relu);
   return SN_CHECK_LAUNCH();

@@ -13,6 +13,7 @@ then copied to the device.
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 
 import numpy as np
@@ -268,7 +269,45 @@ class CoreState:
             raise RuntimeError("host nets with a separate compute copy stay on the Python path")
         return {"data": int(data.data_ptr()), "count": int(net.num_param_elems), "cuda": int(data.is_cuda),
                 "compute": int(comp.data_ptr()) if shadow else 0, "compute_count": int(comp.numel()) if shadow else 0,
-                "stream": int(torch.cuda.current_stream(self.device).cuda_stream) if data.is_cuda else 0}
+                "stream": int(torch.cuda.current_stream(self.device).cuda_stream) if data.is_cuda else 0,
+                "diff": int(net.flat_diff.data_ptr()), "params": self._param_table()}
+
+    def _param_table(self) -> list:
+        """Per-parameter rows for the native sn_blob_* verbs on layer parameters:
+        (layer, index, flat offset, count, layout, caffe ndim, caffe dims[6], internal dims[4]);
+        layout 0 = the internal order is Caffe's, 1 = internal [K][R][S][C] holding Caffe's
+        [K][C][R][S] (convolution weights).  Params with any other layout are left out and
+        stay on the Python path."""
+        net = self.net
+        base = net.flat_data.data_ptr()
+        rows = []
+        for li, layer in enumerate(net.layers):
+            for pi, prm in enumerate(layer.params):
+                off = getattr(prm, "offset", None)
+                cs = tuple(prm.caffe_shape)
+                if off is None or len(cs) > 6 or prm.data is None or prm.data.data_ptr() != base + 4 * off:
+                    continue
+                layout = 0
+                ishape = tuple(prm.shape) + (1,) * (4 - len(prm.shape)) if len(prm.shape) <= 4 else None
+                if prm._to_caffe is not None:
+                    # a 4-D [K][R][S][C] view of the internal tensor: the conv weight itself,
+                    # or an InnerProduct weight over an NHWC image bottom (layer.perm = (C, H, W))
+                    view = tuple(prm.shape) if len(prm.shape) == 4 else None
+                    perm = getattr(layer, "perm", None)
+                    if view is None and pi == 0 and perm is not None and len(prm.shape) == 2:
+                        view = (prm.shape[0], perm[1], perm[2], perm[0])
+                    if view is None or math.prod(view) != prm.count:
+                        continue
+                    probe = torch.arange(prm.count, dtype=torch.float64).reshape(prm.shape)
+                    expect = probe.reshape(view).permute(0, 3, 1, 2).reshape(cs)
+                    if not torch.equal(prm._to_caffe(probe).reshape(cs), expect):
+                        continue
+                    layout, ishape = 1, view
+                if ishape is None:
+                    continue
+                rows.append((li, pi, int(off), int(prm.count), layout, len(cs)) + tuple(int(d) for d in cs)
+                            + (1,) * (6 - len(cs)) + tuple(int(d) for d in ishape))
+        return rows
 
     def set_scores(self, scores: list) -> None:
         """Scores of a native sn_solver_test, handed over at the next Python entry."""

@@ -53,7 +53,8 @@ int main(int argc, char** argv) {
   CHECK(sn_solver_step(st, 5));
   printf("native=%lld\n", sn_native_iterations(st)); /* > 0 on a GPU: the C++ step loop ran */
   /* steady state: once each verb has run (its first call builds the native plan), step,
-   * test, forward and get / set weights never enter the interpreter on a GPU state */
+   * test, forward, get / set weights and the parameter blob verbs never enter the interpreter
+   * on a GPU state */
   CHECK(sn_set_test_data_callback(st, 0, data_cb, NULL));
   CHECK(sn_set_test_data_callback(st, 1, label_cb, NULL));
   CHECK(sn_solver_test(st, 2) != 1);
@@ -62,8 +63,17 @@ int main(int argc, char** argv) {
   long long np = sn_num_params(st);
   float* ws = (float*)malloc(sizeof(float) * np);
   CHECK(sn_get_weights(st, ws, np));
+  /* a layer parameter blob through the per-blob verbs (conv1 weights: the internal
+   * [K][R][S][C] layout converted to Caffe's [K][C][R][S] natively) */
+  long long pc = 1;
+  for (int a = 0; a < sn_blob_num_axes(st, 2, 0); ++a) pc *= sn_blob_axis_shape(st, 2, 0, a);
+  float* pb = (float*)malloc(sizeof(float) * pc);
   const long long py0 = sn_python_entries();
   CHECK(sn_solver_step(st, 3));
+  CHECK(sn_blob_num_axes(st, 2, 0) != 4);
+  CHECK(sn_blob_get(st, 2, 0, 0, pb, pc));
+  CHECK(sn_blob_set(st, 2, 0, 0, pb, pc));
+  CHECK(sn_blob_get(st, 2, 0, 1, pb, pc));
   CHECK(sn_solver_test(st, 2) != 1);
   const int nscores = sn_num_test_scores(st);
   const float score = sn_get_test_score(st, 0);
@@ -72,6 +82,7 @@ int main(int argc, char** argv) {
   CHECK(sn_forward(st, &warm));
   const long long py = sn_python_entries() - py0;
   free(ws);
+  free(pb);
   printf("steady_py=%lld scores=%d score0=%.4f fwd=%.4f\n", py, nscores, score, warm);
   CHECK(!isfinite(score) || !isfinite(warm) || nscores != 1);
   CHECK(sn_load_net_from_protobuf(st, "\xff\xff\xff", 3) == 0); /* garbage bytes must fail cleanly */

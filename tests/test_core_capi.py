@@ -105,6 +105,70 @@ def test_ctypes_inside_python(core_lib, tmp_path):
     lib.sn_destroy_state(st)
 
 
+def test_native_param_blob_verbs_match_python(core_lib, monkeypatch):
+    """sn_blob_num_axes / axis_shape / get / set on layer parameters run natively off the
+    weights plan (flat buffer offsets + the conv weights' [K][R][S][C] -> [K][C][R][S]
+    conversion) and agree with the Python path (SN_NATIVE_STEP=0) on every parameter of
+    every layer, data and diff; a native set is what the Python path reads back."""
+    lib = C.CDLL(core_lib)
+    lib.sn_create_state.restype = C.c_void_p
+    lib.sn_last_error.restype = C.c_char_p
+    lib.sn_python_entries.restype = C.c_longlong
+    st = C.c_void_p(lib.sn_create_state())
+    buf, n = C.c_char_p(), C.c_int()
+    assert lib.sn_parse_solver_prototxt(SOLVER.encode(), C.byref(buf), C.byref(n)) == 0
+    assert lib.sn_set_device(st, -1) == 0
+    assert lib.sn_load_solver_from_protobuf(st, buf, n) == 0, lib.sn_last_error()
+
+    def fill(p, batch, nd, shape, user):
+        cnt = int(np.prod([shape[i] for i in range(nd)]))
+        arr = np.ctypeslib.as_array(p, shape=(cnt,))
+        arr[:] = np.cos(0.11 * np.arange(cnt)).astype(np.float32) if nd == 4 else (np.arange(cnt) % 3)
+
+    cb = CB(fill)
+    assert lib.sn_set_train_data_callback(st, 0, cb, None) == 0
+    assert lib.sn_set_train_data_callback(st, 1, cb, None) == 0
+    assert lib.sn_solver_step(st, 2) == 0, lib.sn_last_error()
+    rng = np.random.default_rng(3)
+
+    def blob(layer, index, native):
+        monkeypatch.setenv("SN_NATIVE_STEP", "1" if native else "0")
+        axes = lib.sn_blob_num_axes(st, layer, index)
+        shape = [lib.sn_blob_axis_shape(st, layer, index, a) for a in range(axes)]
+        return axes, shape
+
+    def get(layer, index, diff, cnt, native):
+        monkeypatch.setenv("SN_NATIVE_STEP", "1" if native else "0")
+        out = (C.c_float * cnt)()
+        assert lib.sn_blob_get(st, layer, index, diff, out, C.c_longlong(cnt)) == 0, lib.sn_last_error()
+        return np.frombuffer(out, dtype=np.float32).copy()
+
+    checked = 0
+    for layer in range(lib.sn_num_layers(st)):
+        for index in range(lib.sn_num_layer_weights(st, layer)):
+            axes, shape = blob(layer, index, False)
+            assert blob(layer, index, True) == (axes, shape)
+            cnt = int(np.prod(shape))
+            for diff in (0, 1):
+                np.testing.assert_array_equal(get(layer, index, diff, cnt, True), get(layer, index, diff, cnt, False))
+            vals = rng.standard_normal(cnt).astype(np.float32)
+            monkeypatch.setenv("SN_NATIVE_STEP", "1")
+            py0 = lib.sn_python_entries()
+            assert lib.sn_blob_set(st, layer, index, 0, vals.ctypes.data_as(C.POINTER(C.c_float)),
+                                   C.c_longlong(cnt)) == 0, lib.sn_last_error()
+            assert lib.sn_python_entries() == py0  # the plan exists: no interpreter entry
+            np.testing.assert_array_equal(get(layer, index, 0, cnt, False), vals)
+            small = (C.c_float * 1)()
+            monkeypatch.setenv("SN_NATIVE_STEP", "1")
+            if cnt > 1:
+                assert lib.sn_blob_get(st, layer, index, 0, small, C.c_longlong(1)) != 0
+                assert b"buffer holds 1 floats" in lib.sn_last_error()
+            checked += 1
+    assert checked >= 4
+    lib.sn_free(buf)
+    lib.sn_destroy_state(st)
+
+
 def _ctypes_train(core_lib, device, iters, native):
     lib = C.CDLL(core_lib)
     lib.sn_create_state.restype = C.c_void_p
