@@ -75,6 +75,8 @@ extern "C" int sn_augment(const uint8_t* src, bf16_t* dst, long long N, long lon
 // One thread per folded output pixel (the Philox draw is amortised over its f*f*Cp
 // channels); F / CP are compile-time for the common RGB cases so the channel ->
 // (dy, dx, c) decode is shifts, with a runtime fallback.
+typedef uint32_t __attribute__((aligned(1))) u32_unaligned;  // gfx950 global loads allow any byte alignment
+
 template <int F, int CP, int MM>
 __global__ void __launch_bounds__(256) augment_s2d_kernel(const uint8_t* __restrict__ src, bf16_t* __restrict__ x2,
                                                           int N, int C, int Hs, int Ws, int crop_h, int crop_w,
@@ -113,27 +115,66 @@ __global__ void __launch_bounds__(256) augment_s2d_kernel(const uint8_t* __restr
         mir = 0;
       }
       uint4* out = reinterpret_cast<uint4*>(x2) + pix * cv;
+      bool done = false;
+      if constexpr (F == 4 && CP == 3) {
+        // RGB into 4 x 4 folds (CaffeNet conv1): the 4 source columns of one (row, channel)
+        // are 4 consecutive bytes (reversed under the mirror), so one unaligned 32-bit load
+        // replaces four byte loads — 12 loads per folded pixel instead of 48.  Folded columns
+        // that reach past the crop (the last one) keep the per-element path below.
+        const int w0 = j * 4 - pw;
+        if (C == 3 && w0 >= 0 && w0 + 3 < crop_w) {
+          float v48[48];
 #pragma unroll
-      for (int ch = 0; ch < cv; ++ch) {
-        float v[8];
+          for (int dy = 0; dy < 4; ++dy) {
+            const int h = r * 4 + dy - ph;
+            const bool okh = (unsigned)h < (unsigned)crop_h;
+            const int sh = min(max(h, 0), crop_h - 1) + ho;
+            const int s0 = (mir ? crop_w - 4 - w0 : w0) + wo;  // leftmost of the 4 source bytes
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int e = ch * 8 + t;
-          const int d = e / Cp, c = e - d * Cp;
-          const int h = r * f + d / f - ph, w = j * f + d % f - pw;  // crop coordinates
-          // branch-free: load from a clamped in-image address, then select (a load under a
-          // per-element condition makes hipcc wait vmcnt(0) per element)
-          const bool ok = c < C && (unsigned)h < (unsigned)crop_h && (unsigned)w < (unsigned)crop_w;
-          const int hc = min(max(h, 0), crop_h - 1), wc = min(max(w, 0), crop_w - 1), cc = min(c, C - 1);
-          const int sh = hc + ho, sw = (mir ? (crop_w - 1 - wc) : wc) + wo;
-          float x = (float)src[(((long long)n * C + cc) * Hs + sh) * Ws + sw];
-          if (MM == 1) x -= mean[cc];  // mean mode is a template parameter: no per-element branch
-          if (MM == 2) x -= mean[((long long)cc * Hs + sh) * Ws + sw];
-          x = ok ? x * scale : 0.f;
-          v[t] = x;
+            for (int c = 0; c < 3; ++c) {
+              const uint8_t* row = src + (((long long)n * C + c) * Hs + sh) * Ws;
+              const uint32_t word = *reinterpret_cast<const u32_unaligned*>(row + s0);
+#pragma unroll
+              for (int dx = 0; dx < 4; ++dx) {
+                const int b = mir ? 3 - dx : dx;
+                float x = (float)((word >> (8 * b)) & 0xffu);
+                if (MM == 1) x -= mean[c];
+                if (MM == 2) x -= mean[((long long)c * Hs + sh) * Ws + s0 + b];
+                v48[(dy * 4 + dx) * 3 + c] = okh ? x * scale : 0.f;
+              }
+            }
+          }
+#pragma unroll
+          for (int ch = 0; ch < 6; ++ch) {
+            if (staged) tile[threadIdx.x * CVS + ch] = pack8(v48 + 8 * ch);
+            else out[ch] = pack8(v48 + 8 * ch);
+          }
+          done = true;
         }
-        if (staged) tile[threadIdx.x * CVS + ch] = pack8(v);
-        else out[ch] = pack8(v);
+      }
+      if (!done) {
+#pragma unroll
+        for (int ch = 0; ch < cv; ++ch) {
+          float v[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int e = ch * 8 + t;
+            const int d = e / Cp, c = e - d * Cp;
+            const int h = r * f + d / f - ph, w = j * f + d % f - pw;  // crop coordinates
+            // branch-free: load from a clamped in-image address, then select (a load under a
+            // per-element condition makes hipcc wait vmcnt(0) per element)
+            const bool ok = c < C && (unsigned)h < (unsigned)crop_h && (unsigned)w < (unsigned)crop_w;
+            const int hc = min(max(h, 0), crop_h - 1), wc = min(max(w, 0), crop_w - 1), cc = min(c, C - 1);
+            const int sh = hc + ho, sw = (mir ? (crop_w - 1 - wc) : wc) + wo;
+            float x = (float)src[(((long long)n * C + cc) * Hs + sh) * Ws + sw];
+            if (MM == 1) x -= mean[cc];  // mean mode is a template parameter: no per-element branch
+            if (MM == 2) x -= mean[((long long)cc * Hs + sh) * Ws + sw];
+            x = ok ? x * scale : 0.f;
+            v[t] = x;
+          }
+          if (staged) tile[threadIdx.x * CVS + ch] = pack8(v);
+          else out[ch] = pack8(v);
+        }
       }
     }
     if (staged) {

@@ -18,6 +18,8 @@
 // intermediates, so the fused pair is bitwise equal to the two separate launches.
 #include "common.h"
 
+#include <cmath>
+
 #include <cstdlib>
 
 struct PLGeom {
@@ -133,7 +135,9 @@ SN_DEV void plrn_load24(const bf16_t* row, int c0, int C, float* v) {
   }
 }
 
-template <int SIZE>
+// MLDS: phase 1 also stages the argmax mask of the pooled rows in LDS (after the gradient
+// tile), so phase 2's window reads are LDS reads instead of dependent global loads.
+template <int SIZE, bool MLDS>
 __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ xp, const bf16_t* __restrict__ dyn,
                                                     const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
                                                     PLGeom g) {
@@ -161,9 +165,11 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
     const int p = bh0 - 1 + (int)r;
     if (p < 0 || p >= g.P) {
       tile[it] = make_uint4(0u, 0u, 0u, 0u);
+      if (MLDS) reinterpret_cast<uint2*>(tile + items1)[it] = make_uint2(0u, 0u);
       continue;
     }
     const long long base = (((long long)n * g.P + p) * g.Q + q) * g.C;
+    if (MLDS) reinterpret_cast<uint2*>(tile + items1)[it] = *reinterpret_cast<const uint2*>(mask + base + c0);
     float xv[24], gv[24];
     plrn_load24(xp + base, c0, g.C, xv);
     plrn_load24(dyn + base, c0, g.C, gv);
@@ -212,7 +218,10 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
         ok[t] = p >= 0 && p < g.P && q >= 0 && q < g.Q;
         const int pc = min(max(p, 0), g.P - 1), qc = min(max(q, 0), g.Q - 1);
         dv[t] = tile[((int)r + wa) * qcg + qc * cg + lc];
-        mv[t] = *reinterpret_cast<const uint2*>(mask + (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0);
+        if (MLDS)
+          mv[t] = reinterpret_cast<const uint2*>(tile + items1)[((int)r + wa) * qcg + qc * cg + lc];
+        else
+          mv[t] = *reinterpret_cast<const uint2*>(mask + (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0);
       }
     float f[4][8];
 #pragma unroll
@@ -258,27 +267,44 @@ static bool plrn_ok(long long N, long long H, long long W, long long C, long lon
 }
 
 // Workgroup shapes (host side, shared with the Python eligibility check).
-static int plrn_fwd_pix(long long C) { return (int)(512 / (C / 8) > 0 ? 512 / (C / 8) : 1); }
-// backward tile: the channel group is the whole pixel or at least 8 chunks (128 B), so
-// the gradient rows are written in full cache lines; then the most block rows (least halo
-// recomputation) whose (rows + 1) x Q x cg tile fits the LDS budget (SN_PLRN_LDS bytes,
-// default 32 KB: several workgroups per CU).  SN_PLRN_CG forces the group size.
-static bool plrn_bwd_tile(long long Q, long long C, int* rows, int* cg) {
+static int plrn_fwd_pix(long long C) {
+  // (pixel, chunk) items per workgroup: 256 (one per thread) beat 512 / 1024 / 2048 at both
+  // CaffeNet shapes (pool1/norm1 51.5 -> 47.8 us, pool2/norm2 31.1 -> 28.3 us,
+  // profiles/r4_plrn_tiles.txt); SN_PLRN_FWD_ITEMS overrides
+  const char* e = std::getenv("SN_PLRN_FWD_ITEMS");
+  const long long items = e ? std::atoll(e) : 256;
+  return (int)(items / (C / 8) > 0 ? items / (C / 8) : 1);
+}
+// backward tile: for each channel group cg (a divisor of the C / 8 chunks, at least 4 chunks =
+// 64 B of a pixel, or the whole pixel) the most block rows (<= 7, least halo recomputation)
+// whose (rows + 1) x Q x cg tile fits the LDS budget (SN_PLRN_LDS bytes, default 32 KB); of
+// those, the shape whose grid is closest to 2560 workgroups (10 per CU: enough to fill every
+// CU with short blocks, few enough that the halo rows stay a small share).  Measured on CaffeNet
+// (profiles/r4_plrn_tiles.txt): pool1/norm1 74.4 -> 63.3 us (cg 12 -> 4), pool2/norm2 45.4 ->
+// 42.4 us (cg 16 -> 8).  SN_PLRN_CG forces the group size.
+static bool plrn_bwd_tile(long long N, long long Q, long long C, long long BH, int item_bytes, int* rows, int* cg) {
   const int cv = (int)(C / 8);
   const char* e = std::getenv("SN_PLRN_LDS");
   const long long budget = e ? std::atoll(e) : 32 * 1024;
   const char* fc = std::getenv("SN_PLRN_CG");
-  for (int r = 7; r >= 1; --r)
-    for (int c = cv; c >= 1; --c) {
-      if (cv % c) continue;
-      if (fc ? c != std::atoi(fc) : (c != cv && c < 8)) continue;
-      if ((long long)(r + 1) * Q * c * 16 <= budget) {
-        *rows = r;
-        *cg = c;
-        return true;
-      }
+  double best = 1e30;
+  bool found = false;
+  for (int c = cv; c >= 1; --c) {
+    if (cv % c) continue;
+    if (fc ? c != std::atoi(fc) : (c != cv && c < 4)) continue;
+    int r = 7;
+    while (r >= 1 && (long long)(r + 1) * Q * c * item_bytes > budget) --r;
+    if (r < 1) continue;
+    const double grid = (double)N * (double)((BH + r - 1) / r) * (double)(cv / c);
+    const double d = std::fabs(std::log(grid / 2560.0));
+    if (d < best - 1e-9) {
+      best = d;
+      *rows = r;
+      *cg = c;
+      found = true;
     }
-  return false;
+  }
+  return found;
 }
 
 extern "C" int sn_pool_lrn_fwd(const bf16_t* x, bf16_t* pooled, uint8_t* mask, bf16_t* y, long long N, long long H,
@@ -305,9 +331,14 @@ extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_
                                long long pw, long long size, float alpha, float beta, float k, hipStream_t st) {
   if (!plrn_ok(N, H, W, C, P, Q, ph, pw, size)) return 4;
   PLGeom g = plgeom(N, H, W, C, P, Q, ph, pw, size, alpha, beta, k);
-  if (!plrn_bwd_tile(Q, C, &g.rows, &g.cg)) return 4;
-  g.ngrp = (int)(C / 8) / g.cg;
   g.BH = (int)((H + ph + 1) / 2);
+  // argmax mask staged in LDS by phase 1 (SN_PLRN_MASK_LDS=0: phase 2 reads it from global
+  // memory): pool1/norm1 63.5 -> 62.2 us, pool2/norm2 42.5 -> 41.3 us (profiles/r4_plrn_tiles.txt)
+  const char* me = std::getenv("SN_PLRN_MASK_LDS");
+  const int mlds = me ? std::atoi(me) != 0 : 1;
+  const int item_bytes = mlds ? 24 : 16;
+  if (!plrn_bwd_tile(N, Q, C, g.BH, item_bytes, &g.rows, &g.cg)) return 4;
+  g.ngrp = (int)(C / 8) / g.cg;
   g.BW = (int)((W + pw + 1) / 2);
   // every pooled row the blocks read exists in the tile: blocks bh read rows bh-1, bh
   if (g.BH > P + 1 || g.BW > Q + 1) return 4;
@@ -316,12 +347,18 @@ extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_
   g.fQcg = make_fdiv((uint32_t)(Q * g.cg));
   g.fBWcg = make_fdiv((uint32_t)(g.BW * g.cg));
   dim3 grid((unsigned)(N * g.nb * g.ngrp));
-  const size_t lds = (size_t)(g.rows + 1) * Q * g.cg * sizeof(uint4);
+  const size_t lds = (size_t)(g.rows + 1) * Q * g.cg * item_bytes;
+#define SN_PLRN_BWD(S)                                                                                          \
+  do {                                                                                                          \
+    if (mlds) hipLaunchKernelGGL((lrn_pool_bwd<S, true>), grid, dim3(256), lds, st, xp, dyn, mask, dx, g);   \
+    else hipLaunchKernelGGL((lrn_pool_bwd<S, false>), grid, dim3(256), lds, st, xp, dyn, mask, dx, g);       \
+  } while (0)
   switch (size) {
-    case 3: hipLaunchKernelGGL(lrn_pool_bwd<3>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
-    case 5: hipLaunchKernelGGL(lrn_pool_bwd<5>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
-    case 7: hipLaunchKernelGGL(lrn_pool_bwd<7>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
-    default: hipLaunchKernelGGL(lrn_pool_bwd<9>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
+    case 3: SN_PLRN_BWD(3); break;
+    case 5: SN_PLRN_BWD(5); break;
+    case 7: SN_PLRN_BWD(7); break;
+    default: SN_PLRN_BWD(9); break;
   }
+#undef SN_PLRN_BWD
   return SN_CHECK_LAUNCH();
 }

@@ -407,15 +407,19 @@ def test_cast_and_augment(gpu):
         close(out[n], expect, 1e-2)
 
 
-@pytest.mark.parametrize("src_hw", [(40, 44), (39, 41)])
+@pytest.mark.parametrize("src_hw", [(40, 44), (39, 41), (256, 256)])
 @pytest.mark.parametrize("mean_mode", [1, 2])
-@pytest.mark.parametrize("ksp", [(11, 4, 0), (7, 2, 3), (3, 1, 1)])
+@pytest.mark.parametrize("ksp", [(11, 4, 0), (11, 4, 2), (7, 2, 3), (3, 1, 1)])
 def test_augment_s2d_equals_augment_then_fold(gpu, mean_mode, ksp, src_hw, monkeypatch):
     """The fused augment + space-to-depth kernel (row-tiled LDS path and the per-pixel
-    path) is bitwise the two-pass result; odd source widths take the byte-load staging."""
+    path) is bitwise the two-pass result; odd source widths take the byte-load staging, and
+    the 4 x 4 RGB fold's 32-bit-load path (any byte alignment, mirrored or not, padded or
+    not) matches too — at CaffeNet's 256 -> 227 crop as well."""
     from sparknet_amd.ops import hip
     N, crop = 3, 35
     Hs, Ws = src_hw
+    if Hs == 256:
+        N, crop = 4, 227
     img = torch.randint(0, 256, (N, 3, Hs, Ws), dtype=torch.uint8, device="cuda")
     mean = (torch.rand(3, device="cuda") * 200) if mean_mode == 1 else (torch.rand(3, Hs, Ws, device="cuda") * 200)
     rng = torch.tensor([11, 5], dtype=torch.int64, device="cuda")
@@ -431,10 +435,11 @@ def test_augment_s2d_equals_augment_then_fold(gpu, mean_mode, ksp, src_hw, monke
     assert torch.equal(x2, ref2)
     monkeypatch.setenv("SN_AUGMENT_DIRECT", "1")
     x3 = torch.full_like(ref2, 7.0)
-    lab = torch.tensor([4, 0, 9], dtype=torch.int32, device="cuda")
+    labs = [4, 0, 9, 2][:N]
+    lab = torch.tensor(labs, dtype=torch.int32, device="cuda")
     lab_out = torch.full((N, 1), -1.0, device="cuda")
     hip.augment_s2d(img, x3, crop, plan, s, mean, mean_mode, 0.25, rng, True, True, lab, lab_out)
-    assert torch.equal(x3, ref2) and lab_out.flatten().tolist() == [4.0, 0.0, 9.0]
+    assert torch.equal(x3, ref2) and lab_out.flatten().tolist() == [float(v) for v in labs]
 
 
 @pytest.mark.parametrize("k", [2, 3, 8, 11])
