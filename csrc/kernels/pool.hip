@@ -7,6 +7,8 @@
 // traffic than Caffe's int mask) and the backward pass is a gather (no atomics).
 #include "common.h"
 
+#include <cstdlib>
+
 struct PoolGeom {
   int N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw;
   FDiv fcv, fW, fH, fQ, fP, fsh, fsw;  // cv = channel chunks per pixel (C/8 or C)
@@ -268,6 +270,72 @@ __global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, bf16_t* __restrict__
   if (qs.q) q_flush(qs, qmax);
 }
 
+// 3x3 / stride-1 max pooling forward, one thread per 2 x 2 block of outputs: the 4 x 4 input
+// pixels the block's windows cover are loaded once (16 loads for 4 outputs instead of 36);
+// each window is scanned in the order maxpool_fwd_k uses (first strict maximum wins), so the
+// values and the argmax mask are bitwise equal.
+__global__ void __launch_bounds__(256) maxpool_fwd_k3s1(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                        uint8_t* __restrict__ mask, PoolGeom g, int gate, QSide qs,
+                                                        FDiv fBQ, FDiv fBP, int BQ, int BP) {
+  const int cv = g.C / 8;
+  float qmax = 0.f;
+  const float qsc = qs.q ? qs.slot[0] : 0.f;
+  const long long total = (long long)g.N * BP * BQ * cv;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t blk = udiv((uint32_t)i, g.fcv), bp_ = udiv(blk, fBQ), n = udiv(bp_, fBP);
+    const int c0 = (int)((uint32_t)i - blk * cv) * 8;
+    const int bq = (int)(blk - bp_ * BQ), bp = (int)(bp_ - n * BP);
+    const int hs = 2 * bp - g.ph, ws = 2 * bq - g.pw;  // input row / column of the block's first window
+    uint4 v[16];
+    bool ok[16];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int h = hs + a, w = ws + b;
+        ok[a * 4 + b] = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+        const int hc = min(max(h, 0), g.H - 1), wc = min(max(w, 0), g.W - 1);
+        v[a * 4 + b] = *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + hc) * g.W + wc) * g.C + c0);
+      }
+#pragma unroll
+    for (int oa = 0; oa < 2; ++oa)
+#pragma unroll
+      for (int ob = 0; ob < 2; ++ob) {
+        const int p = 2 * bp + oa, q = 2 * bq + ob;
+        if (p >= g.P || q >= g.Q) continue;
+        float best[8];
+        int arg[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+#pragma unroll
+        for (int widx = 0; widx < 9; ++widx) {
+          const int t = (oa + widx / 3) * 4 + (ob + widx % 3);
+          float f[8];
+          unpack8(v[t], f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (ok[t] && f[k] > best[k]) { best[k] = f[k]; arg[k] = widx; }
+        }
+        if (gate) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (!(best[k] > 0.f)) arg[k] = 255;
+        }
+        const long long o = (((long long)n * g.P + p) * g.Q + q) * g.C + c0;
+        *reinterpret_cast<uint4*>(y + o) = pack8(best);
+        if (qs.q) *reinterpret_cast<uint2*>(qs.q + o) = q_pack8(qs, qsc, best, qmax);
+        if (mask) {
+          uint2 m;
+          m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+          m.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+          *reinterpret_cast<uint2*>(mask + o) = m;
+        }
+      }
+  }
+  if (qs.q) q_flush(qs, qmax);
+}
+
 // NH x NW = max number of windows covering one input pixel (ceil(k / stride) per axis).
 template <int NH, int NW, bool MAX>
 __global__ void pool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
@@ -399,6 +467,49 @@ __global__ void pool_bwd_k3s2(const bf16_t* __restrict__ dy, const uint8_t* __re
   }
 }
 
+// 2x2 / stride-2 max pooling (VGG-16's five pools): each input pixel lies in at most one
+// window, so one thread owns a window's 2 x 2 input block for 8 channels — one dy load and one
+// mask load feed four pixel stores (the per-pixel gather above re-reads both for each of the
+// four).  Blocks without a window (floor-mode edges) store zeros; same arithmetic as
+// pool_bwd_k<1, 1, true> (0 + dy where the argmax matches), so the results are bitwise equal.
+__global__ void __launch_bounds__(256) pool_bwd_k2s2(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+                              bf16_t* __restrict__ dx, PoolGeom g, FDiv fBW, FDiv fBH, int BW, int BH, QSide qs) {
+  const int cv = g.C / 8;
+  float qmax = 0.f;
+  const float qsc = qs.q ? qs.slot[0] : 0.f;
+  const long long total = (long long)g.N * BH * BW * cv;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t blk = udiv((uint32_t)i, g.fcv), bh_ = udiv(blk, fBW), n = udiv(bh_, fBH);
+    const int c0 = (int)((uint32_t)i - blk * cv) * 8;
+    const int bw = (int)(blk - bh_ * BW), bh = (int)(bh_ - n * BH);
+    const bool win = bh < g.P && bw < g.Q;
+    const long long o = (((long long)n * g.P + min(bh, g.P - 1)) * g.Q + min(bw, g.Q - 1)) * g.C + c0;
+    const uint4 dv = *reinterpret_cast<const uint4*>(dy + o);
+    const uint2 mv = *reinterpret_cast<const uint2*>(mask + o);
+    float f[8];
+    unpack8(dv, f);
+    const uint32_t mw[2] = {mv.x, mv.y};
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int h = 2 * bh + a - g.ph, w = 2 * bw + b - g.pw;
+        if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          acc[k] = 0.f;
+          if (win && (int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == a * 2 + b) acc[k] += f[k];
+        }
+        const long long od = (((long long)n * g.H + h) * g.W + w) * g.C + c0;
+        *reinterpret_cast<uint4*>(dx + od) = pack8(acc);
+        if (qs.q) *reinterpret_cast<uint2*>(qs.q + od) = q_pack8(qs, qsc, acc, qmax);
+      }
+  }
+  if (qs.q) q_flush(qs, qmax);
+}
+
 static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long long P, long long Q, long long kh,
                        long long kw, long long sh, long long sw, long long ph, long long pw) {
   PoolGeom g;
@@ -409,6 +520,23 @@ static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long 
   g.fQ = make_fdiv((uint32_t)Q); g.fP = make_fdiv((uint32_t)P);
   g.fsh = make_fdiv((uint32_t)sh); g.fsw = make_fdiv((uint32_t)sw);
   return g;
+}
+
+// SN_POOL_K2S2=1: 2x2 / stride-2 max-pool backward with one thread per window block.  Opt-in:
+// 6 % faster on VGG's two largest pools at b256 but slower on the small ones, VGG-16 b2048 fp8
+// unchanged (11.31 vs 11.32 k img/s, profiles/r4_pool_block_ab.txt)
+static bool k2s2_ok() {
+  const char* e = std::getenv("SN_POOL_K2S2");
+  return e && std::atoi(e) != 0;
+}
+
+// SN_POOL_K3S1=1: 3x3 / stride-1 max pooling (forward and backward) with one thread per 2 x 2
+// block.  Opt-in: fewer loads, but lower occupancy than the per-output gathers whose re-reads hit
+// L1 / L2 — 5-25 % slower at GoogLeNet's Inception shapes, GoogLeNet 20.8-21.0 vs 21.0-21.1 k
+// img/s (profiles/r4_pool_block_ab.txt)
+static bool k3s1_ok() {
+  const char* e = std::getenv("SN_POOL_K3S1");
+  return e && std::atoi(e) != 0;
 }
 
 extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long N, long long H, long long W,
@@ -425,7 +553,13 @@ extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long 
   long long total = N * P * Q * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
   if (method == 0 && vec && kh == kw && (kh == 2 || kh == 3)) {
-    if (kh == 3) hipLaunchKernelGGL((maxpool_fwd_k<3, 3>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate, qs);
+    if (kh == 3 && sh == 1 && sw == 1 && k3s1_ok()) {
+      const int BP = (int)((P + 1) / 2), BQ = (int)((Q + 1) / 2);
+      const long long nt = N * BP * BQ * (C / 8);
+      hipLaunchKernelGGL(maxpool_fwd_k3s1, dim3(sn_blocks(nt, 256, 16384)), dim3(256), 0, st, x, y, mask, g,
+                         (int)gate, qs, make_fdiv((uint32_t)BQ), make_fdiv((uint32_t)BP), BQ, BP);
+    } else if (kh == 3)
+      hipLaunchKernelGGL((maxpool_fwd_k<3, 3>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate, qs);
     else hipLaunchKernelGGL((maxpool_fwd_k<2, 2>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate, qs);
   } else if (method == 0) {
     if (vec) hipLaunchKernelGGL(maxpool_fwd<true>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
@@ -435,6 +569,63 @@ extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long 
     else hipLaunchKernelGGL(avepool_fwd<false>, grid, dim3(256), 0, st, x, y, g);
   }
   return SN_CHECK_LAUNCH();
+}
+
+// 3x3 / stride-1 max pooling (GoogLeNet's Inception pool branches): the per-pixel gather
+// loads 9 windows (dy + mask) per input pixel; one thread per 2 x 2 input block loads the 4 x 4
+// windows that cover it — 4 per pixel.  Each pixel sums its windows in ascending (p, q) order
+// starting from 0, as pool_bwd_k<3, 3, true> does, so the results are bitwise equal.
+__global__ void __launch_bounds__(256) pool_bwd_k3s1(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+                              bf16_t* __restrict__ dx, PoolGeom g, FDiv fBW, FDiv fBH, int BW, int BH, QSide qs) {
+  const int cv = g.C / 8;
+  float qmax = 0.f;
+  const float qsc = qs.q ? qs.slot[0] : 0.f;
+  const long long total = (long long)g.N * BH * BW * cv;
+  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t blk = udiv((uint32_t)i, g.fcv), bh_ = udiv(blk, fBW), n = udiv(bh_, fBH);
+    const int c0 = (int)((uint32_t)i - blk * cv) * 8;
+    const int bw = (int)(blk - bh_ * BW), bh = (int)(bh_ - n * BH);
+    // windows p0 .. p0 + 3 (q0 .. q0 + 3) cover input rows 2 bh, 2 bh + 1 (columns 2 bw, 2 bw + 1)
+    const int p0 = 2 * bh + g.ph - 2, q0 = 2 * bw + g.pw - 2;
+    uint4 dv[16];
+    uint2 mv[16];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int pc = min(max(p0 + t, 0), g.P - 1), qc = min(max(q0 + u, 0), g.Q - 1);
+        const long long o = (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0;
+        dv[t * 4 + u] = *reinterpret_cast<const uint4*>(dy + o);
+        mv[t * 4 + u] = *reinterpret_cast<const uint2*>(mask + o);
+      }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int h = 2 * bh + a, w = 2 * bw + b;
+        if (h >= g.H || w >= g.W) continue;
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const int p = p0 + a + t, q = q0 + b + u, wi = (a + t) * 4 + (b + u);
+            if (p < 0 || p >= g.P || q < 0 || q >= g.Q) continue;
+            const int widx = (2 - t) * 3 + (2 - u);  // this pixel's offset inside window (p, q)
+            float f[8];
+            unpack8(dv[wi], f);
+            const uint32_t mw[2] = {mv[wi].x, mv[wi].y};
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if ((int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == widx) acc[k] += f[k];
+          }
+        const long long od = (((long long)n * g.H + h) * g.W + w) * g.C + c0;
+        *reinterpret_cast<uint4*>(dx + od) = pack8(acc);
+        if (qs.q) *reinterpret_cast<uint2*>(qs.q + od) = q_pack8(qs, qsc, acc, qmax);
+      }
+  }
+  if (qs.q) q_flush(qs, qmax);
 }
 
 extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, long long N, long long H, long long W,
@@ -461,6 +652,19 @@ extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, lo
     else
       hipLaunchKernelGGL((pool_bwd_k3s2<false>), g2, dim3(256), 0, st, dy, mask, dx, g, make_fdiv((uint32_t)BW),
                          make_fdiv((uint32_t)BH), BW, BH);
+  } else if (vec && method == 0 && kh == 2 && kw == 2 && sh == 2 && sw == 2 && k2s2_ok()) {
+    if (q && !(qslot && qpart)) return 9;
+    // one thread per 2x2 input block over the padded extent [0, H + ph) x [0, W + pw)
+    const int BH = (int)((H + ph + 1) / 2), BW = (int)((W + pw + 1) / 2);
+    const long long nt = N * BH * BW * (C / 8);
+    hipLaunchKernelGGL(pool_bwd_k2s2, dim3(sn_blocks(nt, 256, 16384)), dim3(256), 0, st, dy, mask, dx, g,
+                       make_fdiv((uint32_t)BW), make_fdiv((uint32_t)BH), BW, BH, qs);
+  } else if (vec && method == 0 && kh == 3 && kw == 3 && sh == 1 && sw == 1 && ph <= 2 && pw <= 2 && k3s1_ok()) {
+    if (q && !(qslot && qpart)) return 9;
+    const int BH = (int)((H + 1) / 2), BW = (int)((W + 1) / 2);
+    const long long nt = N * BH * BW * (C / 8);
+    hipLaunchKernelGGL(pool_bwd_k3s1, dim3(sn_blocks(nt, 256, 16384)), dim3(256), 0, st, dy, mask, dx, g,
+                       make_fdiv((uint32_t)BW), make_fdiv((uint32_t)BH), BW, BH, qs);
   } else if (vec && nh == nw && nh >= 1 && nh <= 3) {
     if (q && !(qslot && qpart)) return 9;
 #define SN_POOL_BWD_K(NN)                                                                                  \

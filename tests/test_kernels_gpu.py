@@ -140,7 +140,8 @@ def test_linear(gpu, M, K, N):
 @pytest.mark.parametrize("method", [POOL_MAX, POOL_AVE])
 @pytest.mark.parametrize("geo", [(2, 55, 55, 96, 3, 2, 0), (2, 32, 32, 32, 3, 2, 0), (2, 8, 8, 24, 3, 2, 1),
                                  (2, 7, 7, 16, 7, 1, 0), (2, 6, 6, 3, 2, 2, 0), (2, 9, 9, 16, 3, 1, 1),
-                                 (2, 8, 8, 16, 2, 2, 0), (2, 13, 13, 32, 3, 2, 1)])
+                                 (2, 8, 8, 16, 2, 2, 0), (2, 13, 13, 32, 3, 2, 1), (2, 7, 9, 16, 2, 2, 0),
+                                 (2, 8, 8, 16, 2, 2, 1)])
 def test_pool(gpu, method, geo):
     from sparknet_amd.ops import hip
     N, H, W, Cc, k, st, pd = geo
@@ -200,6 +201,34 @@ def test_maxpool_relu_gate(gpu, geo):
     dy = rnd(N, s.P, s.Q, Cc)
     close(hip.pool_backward(dy, x, s, mask, gate=True), ref.pool_backward(dy, x, s, gate=True), 1e-2)
     close(hip.pool_backward(dy, x, s, None, gate=True), ref.pool_backward(dy, x, s, gate=True), 1e-2)
+
+
+@pytest.mark.parametrize("geo", [(4, 56, 56, 128, 2, 2, 0), (3, 7, 9, 16, 2, 2, 0), (2, 8, 8, 16, 2, 2, 1),
+                                 (2, 28, 28, 192, 3, 1, 1), (3, 7, 9, 16, 3, 1, 1), (2, 9, 8, 16, 3, 1, 0),
+                                 (2, 6, 6, 16, 3, 1, 2)])
+def test_pool_block_backward_bitwise(gpu, geo, monkeypatch):
+    """The max-pool backwards with one thread per 2 x 2 input block (pool.hip pool_bwd_k2s2:
+    VGG's 2x2 / stride-2 pools; pool_bwd_k3s1: GoogLeNet's 3x3 / stride-1 Inception pools)
+    are bitwise the per-pixel gather's result (SN_POOL_K2S2=0 / SN_POOL_K3S1=0), gated or
+    not, ragged and padded edges included; so is the 3x3 / stride-1 forward with one thread
+    per 2 x 2 output block (maxpool_fwd_k3s1), values and argmax mask."""
+    from sparknet_amd.ops import hip
+    N, H, W, Cc, k, st, pd = geo
+    knob = "SN_POOL_K2S2" if k == 2 else "SN_POOL_K3S1"
+    s = PoolSpec(N, H, W, Cc, k, k, st, st, pd, pd, POOL_MAX)
+    x = torch.relu(rnd(N, H, W, Cc).float() - 0.5).to(torch.bfloat16)
+    dy = rnd(N, s.P, s.Q, Cc)
+    for gate in (False, True):
+        monkeypatch.setenv(knob, "0")
+        y0, mask = hip.pool_forward_mask(x, s, gate=gate)
+        monkeypatch.setenv(knob, "1")
+        y1, mask1 = hip.pool_forward_mask(x, s, gate=gate)  # k = 3: maxpool_fwd_k3s1
+        assert torch.equal(y1.view(torch.int16), y0.view(torch.int16)) and torch.equal(mask1, mask)
+        a = hip.pool_backward(dy, x, s, mask, gate=gate)
+        monkeypatch.setenv(knob, "0")
+        b = hip.pool_backward(dy, x, s, mask, gate=gate)
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+        close(a, ref.pool_backward(dy, x, s, gate=gate), 1e-2)
 
 
 @pytest.mark.parametrize("e5m2", [False, True])
