@@ -85,6 +85,13 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
   __syncthreads();
 
   const char* wb = smem + lane * 16 + ni * 3 * 1024;
+  // this lane's 12 output channels are the same in every tile: their bias values stay in
+  // registers (a per-tile global load of them stalled each epilogue on an L2 round trip)
+  float bv[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bv[i][k] = bias ? bias[ni * 48 + i * 16 + (lane >> 4) * 4 + k] : 0.f;
   int cur = 0;
   for (; tile < g.tiles; tile += gridDim.x) {
     const long long next = tile + gridDim.x;
@@ -148,7 +155,7 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if (bias) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] += bias[ch + k];
+          for (int k = 0; k < 4; ++k) v[k] += bv[i][k];
         }
         if (relu) {
 #pragma unroll
