@@ -143,6 +143,17 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
 #pragma unroll
         for (int j = 0; j < 3; ++j) asm volatile("" : "+v"(acc[i][j])::"memory");
     }
+    // hand the next tile's patch to LDS before this tile's stores: its loads were issued before
+    // the MFMAs and have landed, while a wait placed after the stores would also wait for them
+    // (vmcnt counts stores); the other buffer's last reader was tile t - 1, behind the barrier
+    if (next < g.tiles) {
+      char* pn = smem + W_BYTES + (cur ^ 1) * PCAP;
+#pragma unroll
+      for (int i = 0; i < PER_T; ++i) {
+        const int q = tid + i * NT;
+        if (q < PCAP / 16) *reinterpret_cast<uint4*>(pn + q * 16) = pre[i];
+      }
+    }
     // epilogue: lane holds output channels ch .. ch + 3 of pixel m
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -162,14 +173,6 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
           for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
         }
         *reinterpret_cast<uint2*>(yo + ch) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    }
-    if (next < g.tiles) {
-      char* pn = smem + W_BYTES + (cur ^ 1) * PCAP;
-#pragma unroll
-      for (int i = 0; i < PER_T; ++i) {
-        const int q = tid + i * NT;
-        if (q < PCAP / 16) *reinterpret_cast<uint4*>(pn + q * 16) = pre[i];
       }
     }
     __syncthreads();  // next patch in LDS, and every wave is done reading this one
