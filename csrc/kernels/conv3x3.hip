@@ -65,7 +65,7 @@ SN_DEV uint4 patch_load(const bf16_t* __restrict__ x, const Geo& g, long long t,
 // 4mi..4mi+3 x channels ni*KOUT/2 .. (two waves per SIMD to hide the LDS read latency).
 // DBUF: double-buffered patch (KOUT = 64); KOUT = 96 weights (108 KB) leave room for one
 // patch, written after a barrier while the next tile's loads wait in registers.
-template <int NW, int KOUT, bool DBUF>
+template <int NW, int KOUT, bool DBUF, bool GATE>
 __global__ void __launch_bounds__(NW * 64, 1)
 conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const float* __restrict__ bias,
                const bf16_t* __restrict__ gate, bf16_t* __restrict__ y, Geo g, int relu) {
@@ -95,6 +95,13 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const
 
   int cur = 0;
   const int mrow = lane & 15, ncol = (lane >> 4) * 4;
+  // this lane's output channels are the same in every tile: bias values stay in registers (a
+  // per-tile global load of them stalled each epilogue on an L2 round trip)
+  float bv[NF][4];
+#pragma unroll
+  for (int i = 0; i < NF; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bv[i][k] = bias ? bias[n0w + 16 * i + ncol + k] : 0.f;
   for (; tile < g.tiles; tile += gridDim.x) {
     const long long next = tile + gridDim.x;
     uint4 pre[PER_T];
@@ -105,6 +112,21 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const
         pre[i] = q < CHUNKS ? patch_load(x, g, next, q) : make_uint4(0, 0, 0, 0);
       }
     }
+    int n_img, ty, tx;
+    tile_coords(g, tile, n_img, ty, tx);
+    // data gradient: this tile's ReLU-backward gate, loaded before the MFMAs so the epilogue
+    // does not wait on it
+    uint2 gpf[4][GATE ? NF : 1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < (GATE ? NF : 1); ++i) {
+        const int h = ty * TILE + 4 * mi + j, wc = tx * TILE + mrow;
+        gpf[j][i] = make_uint2(0u, 0u);
+        if (GATE && h < g.P && wc < g.Q)
+          gpf[j][i] = *reinterpret_cast<const uint2*>(
+              gate + (((long long)n_img * g.P + h) * g.Q + wc) * KOUT + n0w + 16 * i + ncol);
+      }
     f32x4 acc[NF][4];
 #pragma unroll
     for (int i = 0; i < NF; ++i)
@@ -130,9 +152,18 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const
         __builtin_amdgcn_s_setprio(0);
       }
     }
+    // DBUF: hand the next tile's patch to LDS before this tile's stores (its loads have landed;
+    // a wait after the stores would also wait for them); the other buffer's last reader was
+    // tile t - 1, behind the barrier
+    if (DBUF && next < g.tiles) {
+      char* pn = smem + WB + (cur ^ 1) * P_BYTES;
+#pragma unroll
+      for (int i = 0; i < PER_T; ++i) {
+        const int q = tid + i * NT;
+        if (q < CHUNKS) *reinterpret_cast<uint4*>(pn + kc_off(q >> 3, q & 7)) = pre[i];
+      }
+    }
     // epilogue: lane holds output channels n .. n+3 of pixel (4 mi + j, mrow)
-    int n_img, ty, tx;
-    tile_coords(g, tile, n_img, ty, tx);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int h = ty * TILE + 4 * mi + j, wc = tx * TILE + mrow;
@@ -144,14 +175,14 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if (bias) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] += bias[n + k];
+          for (int k = 0; k < 4; ++k) v[k] += bv[i][k];
         }
         if (relu) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
         }
-        if (gate) {
-          const uint2 gv = *reinterpret_cast<const uint2*>(gate + o + n);
+        if (GATE) {
+          const uint2 gv = gpf[j][GATE ? i : 0];
           const uint32_t gw[2] = {gv.x, gv.y};
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -162,13 +193,15 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const
         *reinterpret_cast<uint2*>(y + o + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
     }
-    if (!DBUF) __syncthreads();  // single patch buffer: every wave is done reading it
-    if (next < g.tiles) {
-      char* pn = smem + WB + (DBUF ? (cur ^ 1) : 0) * P_BYTES;
+    if (!DBUF) {
+      __syncthreads();  // single patch buffer: every wave is done reading it
+      if (next < g.tiles) {
+        char* pn = smem + WB;
 #pragma unroll
-      for (int i = 0; i < PER_T; ++i) {
-        const int q = tid + i * NT;
-        if (q < CHUNKS) *reinterpret_cast<uint4*>(pn + kc_off(q >> 3, q & 7)) = pre[i];
+        for (int i = 0; i < PER_T; ++i) {
+          const int q = tid + i * NT;
+          if (q < CHUNKS) *reinterpret_cast<uint4*>(pn + kc_off(q >> 3, q & 7)) = pre[i];
+        }
       }
     }
     __syncthreads();  // next patch in LDS (DBUF: and every wave is done reading this one)
@@ -202,14 +235,21 @@ extern "C" int sn_conv3x3_direct(const bf16_t* x, const bf16_t* w, const float* 
     const char* e = getenv("SN_C64_WAVES");
     nw = (e && atoi(e) == 4) ? 4 : 8;
   }
+#define SN_C3(NWV, KV, DB, NTH)                                                                             \
+  do {                                                                                                     \
+    if (gate)                                                                                              \
+      hipLaunchKernelGGL((conv3x3_kernel<NWV, KV, DB, true>), dim3((unsigned)grid), dim3(NTH), 0, st, x, w, bias, \
+                         gate, y, g, (int)relu);                                                           \
+    else                                                                                                   \
+      hipLaunchKernelGGL((conv3x3_kernel<NWV, KV, DB, false>), dim3((unsigned)grid), dim3(NTH), 0, st, x, w, bias, \
+                         gate, y, g, (int)relu);                                                           \
+  } while (0)
   if (K == 96)
-    hipLaunchKernelGGL((conv3x3_kernel<8, 96, false>), dim3((unsigned)grid), dim3(512), 0, st, x, w, bias, gate, y, g,
-                       (int)relu);
+    SN_C3(8, 96, false, 512);
   else if (nw == 4)
-    hipLaunchKernelGGL((conv3x3_kernel<4, 64, true>), dim3((unsigned)grid), dim3(256), 0, st, x, w, bias, gate, y, g,
-                       (int)relu);
+    SN_C3(4, 64, true, 256);
   else
-    hipLaunchKernelGGL((conv3x3_kernel<8, 64, true>), dim3((unsigned)grid), dim3(512), 0, st, x, w, bias, gate, y, g,
-                       (int)relu);
+    SN_C3(8, 64, true, 512);
+#undef SN_C3
   return SN_CHECK_LAUNCH();
 }

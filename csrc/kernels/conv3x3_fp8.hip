@@ -59,6 +59,7 @@ SN_DEV uint4 patch_load8(const uint8_t* __restrict__ x, const Geo8& g, long long
 
 // 8 waves: wave (mi = w & 3, ni = w >> 2) owns output rows 4 mi .. 4 mi + 3 (four 16-pixel M
 // fragments) x output channels 32 ni .. 32 ni + 31 (two N fragments).
+template <bool GATE>
 __global__ void __launch_bounds__(512, 1)
 conv3x3_fp8_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ w, const float* __restrict__ deq_x,
                    const float* __restrict__ deq_w, const float* __restrict__ bias, const bf16_t* __restrict__ gate,
@@ -89,6 +90,13 @@ conv3x3_fp8_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ w,
 
   int cur = 0;
   const int mrow = lane & 15, ncol = (lane >> 4) * 4;
+  // this lane's output channels are the same in every tile: bias values stay in registers (a
+  // per-tile global load of them stalled each epilogue on an L2 round trip)
+  float bv[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bv[i][k] = bias ? bias[n0w + 16 * i + ncol + k] : 0.f;
   for (; tile < g.tiles; tile += gridDim.x) {
     const long long next = tile + gridDim.x;
     uint4 pre[PER_T];
@@ -99,6 +107,21 @@ conv3x3_fp8_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ w,
         pre[i] = q < CHUNKS ? patch_load8(x, g, next, q) : make_uint4(0, 0, 0, 0);
       }
     }
+    int n_img, ty, tx;
+    tile_coords8(g, tile, n_img, ty, tx);
+    // data gradient: this tile's ReLU-backward gate, loaded before the MFMAs so the epilogue
+    // does not wait on it
+    uint2 gpf[4][GATE ? 2 : 1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < (GATE ? 2 : 1); ++i) {
+        const int h = ty * TILE + 4 * mi + j, wc = tx * TILE + mrow;
+        gpf[j][i] = make_uint2(0u, 0u);
+        if (GATE && h < g.H && wc < g.W)
+          gpf[j][i] = *reinterpret_cast<const uint2*>(
+              gate + (((long long)n_img * g.H + h) * g.W + wc) * 64 + n0w + 16 * i + ncol);
+      }
     f32x4 acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -134,9 +157,18 @@ conv3x3_fp8_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ w,
 #pragma unroll
         for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[i][j])::"memory");
     }
+    // hand the next tile's patch to LDS before this tile's stores (its loads have landed; a
+    // wait after the stores would also wait for them); the other buffer's last reader was tile
+    // t - 1, behind the barrier
+    if (next < g.tiles) {
+      char* pn = smem + W_BYTES + (cur ^ 1) * P_BYTES;
+#pragma unroll
+      for (int i = 0; i < PER_T; ++i) {
+        const int q = tid + i * NT;
+        if (q < CHUNKS) *reinterpret_cast<uint4*>(pn + off64(q >> 2, q & 3)) = pre[i];
+      }
+    }
     // epilogue: lane holds output channels n .. n+3 of pixel (4 mi + j, mrow)
-    int n_img, ty, tx;
-    tile_coords8(g, tile, n_img, ty, tx);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int h = ty * TILE + 4 * mi + j, wc = tx * TILE + mrow;
@@ -148,14 +180,14 @@ conv3x3_fp8_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ w,
         float v[4] = {acc[i][j][0] * dq, acc[i][j][1] * dq, acc[i][j][2] * dq, acc[i][j][3] * dq};
         if (bias) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] += bias[n + k];
+          for (int k = 0; k < 4; ++k) v[k] += bv[i][k];
         }
         if (relu) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
         }
-        if (gate) {
-          const uint2 gv = *reinterpret_cast<const uint2*>(gate + o + n);
+        if (GATE) {
+          const uint2 gv = gpf[j][GATE ? i : 0];
           const uint32_t gw[2] = {gv.x, gv.y};
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -164,14 +196,6 @@ conv3x3_fp8_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ w,
           }
         }
         *reinterpret_cast<uint2*>(y + o + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    }
-    if (next < g.tiles) {
-      char* pn = smem + W_BYTES + (cur ^ 1) * P_BYTES;
-#pragma unroll
-      for (int i = 0; i < PER_T; ++i) {
-        const int q = tid + i * NT;
-        if (q < CHUNKS) *reinterpret_cast<uint4*>(pn + off64(q >> 2, q & 3)) = pre[i];
       }
     }
     __syncthreads();  // next patch in LDS, and every wave is done reading this one
@@ -197,7 +221,11 @@ extern "C" int sn_conv3x3_fp8(const uint8_t* x, const uint8_t* w, const float* d
   g.tiles = N * g.th * g.tw;
   const int cus = sn_cu_count();
   const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
-  hipLaunchKernelGGL(conv3x3_fp8_kernel, dim3((unsigned)grid), dim3(512), 0, st, x, w, deq_x, deq_w, bias, gate, y, g,
+  if (gate)
+    hipLaunchKernelGGL(conv3x3_fp8_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, x, w, deq_x, deq_w, bias, gate, y, g,
+                     (int)relu);
+  else
+    hipLaunchKernelGGL(conv3x3_fp8_kernel<false>, dim3((unsigned)grid), dim3(512), 0, st, x, w, deq_x, deq_w, bias, gate, y, g,
                      (int)relu);
   return SN_CHECK_LAUNCH();
 }
