@@ -13,7 +13,7 @@ for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
         k = r["Kernel_Name"]
         if "gemm" not in k and "splitk" not in k:
             continue
-        k = k.split("(SnGemmArgs")[0].split("(")[0][-70:]
+        k = k.replace("(anonymous namespace)::", "").split("(SnGemmArgs")[0].split("(")[0][-70:]
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in vals.items():
     print(k)

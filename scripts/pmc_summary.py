@@ -15,8 +15,9 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 
 
 def short(name, grid=""):
+    name = re.sub(r"\(anonymous namespace\)::", "", name)
     head = name.split("(")[0] if not name.startswith("void (") else name[5:].split(")(")[0]
-    head = re.sub(r"^void ", "", re.sub(r"\(anonymous namespace\)::", "", head))
+    head = re.sub(r"^void ", "", head)
     head = head if len(head) < 90 else head[:90]
     return f"{head} grid={grid}"
 

@@ -9,6 +9,15 @@ path = sys.argv[1]
 if os.path.isdir(path):
     path = os.path.join(path, "run_kernel_trace.csv")
 rows = list(csv.DictReader(open(path)))
+
+
+def kname(n, width=60):
+    """Kernel name without 'void', the argument list or the anonymous-namespace prefix
+    (splitting at the first '(' blanked every '(anonymous namespace)::' kernel)."""
+    n = n.replace("(anonymous namespace)::", "").replace("void ", "")
+    n = n.split("(SnGemmArgs")[0] if "gemm" in n else n.split("(")[0]
+    return n[-width:]
+
 idx = [i for i, r in enumerate(rows) if 'solver_update' in r['Kernel_Name']]
 a, b = idx[-2], idx[-1]
 tot = 0
@@ -17,7 +26,7 @@ for r in rows[a + 1:b + 1]:
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     tot += d
     n = r['Kernel_Name']
-    k = (n.split("(SnGemmArgs")[0] if "gemm" in n else n.split("(")[0].replace("void ", ""))[-60:]
+    k = kname(n)
     agg[k] = agg.get(k, 0) + d
 print("per-iteration kernel time by kernel (us):")
 for k, v in sorted(agg.items(), key=lambda x: -x[1])[:25]:
@@ -28,6 +37,5 @@ if len(sys.argv) > 2:
         d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
         n = r['Kernel_Name']
         if sys.argv[2] == "all" or sys.argv[2] in n:
-            name = n.split('(SnGemmArgs')[0] if 'gemm_kernel' in n else n.split('(')[0]
             print(f"{d:8.1f}us grid=({int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])},{r['Grid_Size_Y']},"
-                  f"{r['Grid_Size_Z']}) {name[-70:]}")
+                  f"{r['Grid_Size_Z']}) {kname(n, 70)}")

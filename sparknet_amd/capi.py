@@ -221,6 +221,16 @@ class CoreState:
     # in the state of that replay (sn_backward, blob reads), and the caller reports the
     # replay's loss.  Any later Python forward of the same net rebinds the blobs again,
     # so sn_core.cpp drops the plan whenever one can run (invalidate(P_FWD_*)).
+    @staticmethod
+    def _stateful_params(net) -> list:
+        """Parameter blobs a forward pass writes: train-phase BatchNorm running statistics
+        (batch_norm_layer.cpp:104-121 updates them inside Forward)."""
+        out = []
+        for layer in net.layers:
+            if layer.type_name == "BatchNorm" and not getattr(layer, "use_global", True):
+                out += [p for p in layer.params if p.data is not None]
+        return out
+
     def forward_plan(self, test: bool) -> dict:
         """Capture one forward pass and replay it once; called right after the Python
         verb ran the same forward eagerly, so every GEMM is already autotuned."""
@@ -247,7 +257,14 @@ class CoreState:
         finally:
             for layer, src, _ in feeds:
                 layer.set_source(src)
+        # The eager forward of this call already updated the stateful layers (train-phase
+        # BatchNorm running mean / variance / factor, Caffe updates them once per Forward):
+        # the replay below must not update them a second time, so their parameter blobs are
+        # saved and put back around it.
+        saved = [(p.data, p.data.clone()) for p in self._stateful_params(net)]
         graph.replay()  # the blobs now hold a real forward of the staged batch (see above)
+        for dst, src in saved:
+            dst.copy_(src)
         torch.cuda.synchronize(dev)
         acc.zero_()
         self.__dict__.setdefault("_fwd_graphs", {})[bool(test)] = (graph, acc, loss_buf)

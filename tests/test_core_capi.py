@@ -348,3 +348,54 @@ def test_native_forward_then_backward_and_blob_reads(core_lib):
         for x, y in zip(a[1:], b[1:]):
             assert np.isfinite(y).all()
             np.testing.assert_allclose(y, x, rtol=2e-2, atol=2e-2 * (np.abs(x).max() + 1e-6))
+
+
+def _bn_stats_after_forwards(core_lib, native_verbs, forwards=3):
+    """3 Python-path steps of a net with a train-phase BatchNorm, then `forwards` sn_forward
+    calls (the first one builds the native plan when native_verbs is on): the BN running
+    mean / variance / factor after each call."""
+    lib = C.CDLL(core_lib)
+    lib.sn_create_state.restype = C.c_void_p
+    lib.sn_last_error.restype = C.c_char_p
+    os.environ["SN_NATIVE_STEP"] = "0"
+    try:
+        st = C.c_void_p(lib.sn_create_state())
+        buf, n = C.c_char_p(), C.c_int()
+        solver = os.path.join(ROOT, "tests", "native", "core_solver_bn.prototxt")
+        assert lib.sn_parse_solver_prototxt(solver.encode(), C.byref(buf), C.byref(n)) == 0
+        assert lib.sn_set_device(st, 0) == 0
+        assert lib.sn_load_solver_from_protobuf(st, buf, n) == 0, lib.sn_last_error()
+
+        def fill(p, batch, nd, shape, user):
+            cnt = int(np.prod([shape[i] for i in range(nd)]))
+            arr = np.ctypeslib.as_array(p, shape=(cnt,))
+            arr[:] = np.cos(0.23 * np.arange(cnt)).astype(np.float32) if nd == 4 else np.arange(cnt) % 3
+        cb = CB(fill)
+        assert lib.sn_set_train_data_callback(st, 0, cb, None) == 0
+        assert lib.sn_set_train_data_callback(st, 1, cb, None) == 0
+        assert lib.sn_solver_step(st, 3) == 0, lib.sn_last_error()
+        os.environ["SN_NATIVE_STEP"] = "1" if native_verbs else "0"
+        out = []
+        for _ in range(forwards):
+            loss = C.c_float()
+            assert lib.sn_forward(st, C.byref(loss)) == 0, lib.sn_last_error()
+            out.append([_blob(lib, st, 3, i, 0) for i in range(3)])  # layer 3 = bn1
+        lib.sn_free(buf)
+        lib.sn_destroy_state(st)
+        return out
+    finally:
+        os.environ.pop("SN_NATIVE_STEP", None)
+
+
+@pytest.mark.gpu
+def test_native_forward_plan_updates_batchnorm_stats_once(core_lib):
+    """building the captured forward plan replays the forward once after the
+    eager forward; a train-phase BatchNorm must still update its running statistics once
+    per sn_forward (Caffe: once per Forward, batch_norm_layer.cpp:104-121)."""
+    py = _bn_stats_after_forwards(core_lib, False)
+    nat = _bn_stats_after_forwards(core_lib, True)
+    for a, b in zip(py, nat):
+        # the moving-average factor counts the updates exactly
+        assert float(b[2][0]) == pytest.approx(float(a[2][0]), rel=1e-6), (a[2], b[2])
+        for x, y in zip(a[:2], b[:2]):
+            np.testing.assert_allclose(y, x, rtol=2e-2, atol=1e-3 * (np.abs(x).max() + 1e-6))

@@ -2,9 +2,16 @@
 
 * cifar10_quick trained through the production path (captured hipGraph, device feeder:
   pinned H2D + on-device mean subtraction, fused ReLU / FC updates) on a learnable
-  synthetic set reaches >= 90 % train accuracy in 300 steps.  Reference analogue: the
-  CifarApp accuracy check (src/test/scala/libs/CifarSpec.scala:92 brackets the accuracy of
-  an untrained net around chance; a trained one must leave that bracket).
+  synthetic set reaches >= 90 % train accuracy in 300 steps, with the loss bounded after
+  step 100, under two fp32 summation orders of conv1's weight gradient (the tuned split-K,
+  and 229-way split-K on the 64-row tile 22).  Reference analogue: the CifarApp accuracy
+  check (src/test/scala/libs/CifarSpec.scala:92 brackets the accuracy of an untrained net
+  around chance; a trained one must leave that bracket).
+  The solver runs at base_lr 0.0005, half the reference cifar10_quick rate: on this
+  trivially separable set the loss collapses to ~0 and training at lr 0.001 spikes (to
+  5-17) under EVERY summation order — the fp32 CPU engine too (scripts/
+  cifar_quick_cpu_traj.py) — so whether step 300 lands inside a spike was a coin flip on
+  the split count (round-4 'thin tile' report; profiles/r5_cifar_stability.txt).
 * A 20-step loss trajectory of a small CaffeNet (dropout 0) on the bf16 GPU engine stays
   within 5 % (relative) of the fp32 CPU engine from identical initial weights, and both
   decrease.
@@ -36,14 +43,25 @@ def _patterns(n, classes=10, seed=0):
     return imgs.clamp(0, 255).to(torch.uint8), y.int()
 
 
-def test_cifar10_quick_learns_synthetic_patterns(gpu):
+@pytest.mark.parametrize("order", ["tuned", "thin229"])
+def test_cifar10_quick_learns_synthetic_patterns(gpu, order, monkeypatch):
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.data.prefetch import DeviceFeeder, TensorSource
     from sparknet_amd.engine import LocalSGDTrainer, fuse_relu
+    from sparknet_amd.ops import gemm as G
+    if order == "thin229":
+        raw = G._tuned_config_raw
+
+        def forced(M, N, K, *a, **k):
+            if (M, N, K) == (32, 201, 102400):  # conv1 dW + bias column over 100 x 32 x 32 pixels
+                return (22, 229, 448)
+            return raw(M, N, K, *a, **k)
+        monkeypatch.setattr(G, "_tuned_config_raw", forced)
     mean = [125.0, 123.0, 114.0]
     x, y = _patterns(2000)
-    solver = Solver(models.solver_for("cifar10_quick", train_batch=100, test_batch=100), device=gpu, seed=5,
-                    build_test_nets=False)
+    sp = models.solver_for("cifar10_quick", train_batch=100, test_batch=100)
+    sp.base_lr = 0.0005
+    solver = Solver(sp, device=gpu, seed=5, build_test_nets=False)
     net = solver.net
     fuse_relu(net)
     feeder = DeviceFeeder(TensorSource(x, y, 100), net.blob_by_name("data"), net.blob_by_name("label"), crop=32,
@@ -53,6 +71,7 @@ def test_cifar10_quick_learns_synthetic_patterns(gpu):
     losses = [float(trainer.local_step()) for _ in range(300)]
     torch.cuda.synchronize()
     assert losses[-1] < 0.5 * losses[0], (losses[0], losses[-1])
+    assert max(losses[100:]) < 1.0, max(losses[100:])  # no divergence spike once learnt
     # train accuracy: eager forward of the trained net on 5 batches
     correct = total = 0
     m = torch.tensor(mean).view(1, 3, 1, 1)
