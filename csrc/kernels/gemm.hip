@@ -164,6 +164,12 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 14: return a.epi == EPI_SGD ? 4 : sn_gemm_big8(a, stream);  // gemm_big8.hip
     case 21:
     case 22: return sn_gemm_tiles_c(a, stream);  // gemm_tiles_c.hip (64-row tiles)
+    case 23:
+    case 24:
+    case 25:
+    case 26:
+    case 27:
+    case 28: return sn_gemm_mf32(a, stream);  // gemm_mf32.hip (32x32x16 MFMA twins)
     case 40:
     case 41: return a.epi == EPI_SGD ? 4 : sn_gemm_t256p8(a, stream);  // gemm_t256p8.hip (8-phase)
     case 15:

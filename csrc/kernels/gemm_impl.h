@@ -125,8 +125,12 @@ SN_DEV int kc_off(int row, int kc) { return row * 128 + ((kc ^ ((row >> 1) & 7))
 
 // MC tile: [64 k rows][TILE cols] bf16 (TILE*2-byte rows).  32-B granules XOR-swizzled
 // so the 8 rows a half-wave tr-reads land in 8 distinct granules of the 256-B bank row.
-template <int TILE>
+// SW = 1: the image read by the 32x32x16 MFMA (read_frag32): a half-wave tr-reads 4 rows
+// x 32 columns (two adjacent granules per row), so rows k..k+3 XOR the granule index by
+// 2 (k & 3) (256-B+ rows) or by 2 ((k >> 1) & 1) (128-B rows, 2 rows per bank row).
+template <int TILE, int SW = 0>
 SN_DEV int swz_mc(int k) {
+  if (SW) return TILE >= 128 ? ((k & 3) << 6) : (((k >> 1) & 1) << 6);
   if (TILE >= 128) return (((k & 3) | (((k >> 3) & 1) << 2)) << 5);
   return ((((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 5);  // 128-B rows: 2 rows per bank row
 }
@@ -156,7 +160,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // maps to that slot.  Lanes outside the matrix read a zero page.
 //   KC: [TILE rows][64 k], 8 chunks per row, 8 rows per instruction.
 //   MC: [64 k rows][TILE cols], TILE/8 chunks per row.
-template <int MC, int MODE, int TILE, int NW, int ES = 2>
+template <int MC, int MODE, int TILE, int NW, int ES = 2, int SW = 0>
 struct GStager {
   static constexpr int NI = TILE / (8 * NW);      // wave-instructions per wave per tile
   static constexpr int CPL = MC ? TILE * ES / 16 : 8;  // 16-B chunks per LDS row
@@ -253,7 +257,7 @@ struct GStager {
     for (int j = 0; j < NI; ++j) {
       const int row = (wave * NI + j) * RPI + lane / CPL, pos = lane % CPL;
       rr[j] = row;
-      ch[j] = MC ? (pos ^ (ES == 1 ? swz_mc8(row) : (swz_mc<TILE>(row) >> 4))) : (pos ^ ((row >> 1) & 7));
+      ch[j] = MC ? (pos ^ (ES == 1 ? swz_mc8(row) : (swz_mc<TILE, SW>(row) >> 4))) : (pos ^ ((row >> 1) & 7));
       if (MODE == OP_IM2COL && !MC) {
         const int PQ = g.P * g.Q;
         int pix = tile_row0 + row;
@@ -612,6 +616,33 @@ SN_DEV bf16x8_t read_frag(const char* lds, int x0, int s, int lane) {
   }
 }
 
+// Fragment of a 32-row subtile (rows x0..x0+31) for 16-deep k-substep s (0..3 of a BK = 64
+// K-step), laid out as the 32x32x16 MFMA operand: lane l holds X[x0 + (l&31)][16s + 8(l>>5) + j],
+// j = 0..7.  KC: one ds_read_b128 (conflict-free under kc_off).  MC (image swizzled with
+// swz_mc<TILE, 1>): two ds_read_b64_tr_b16 per fragment, 16-lane group g covering columns
+// x0 + 16 (g & 1) .. + 15 and k rows 16s + 8 (g >> 1) + 0..3 / 4..7.
+template <int MC, int TILE>
+SN_DEV bf16x8_t read_frag32(const char* lds, int x0, int s, int lane) {
+  if (!MC) {
+    const int row = x0 + (lane & 31);
+    const int kc = 2 * s + (lane >> 5);
+    uint4 v = *reinterpret_cast<const uint4*>(lds + kc_off(row, kc));
+    return __builtin_bit_cast(bf16x8_t, v);
+  } else {
+    const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int col_b = (x0 + 16 * (gq & 1) + 4 * p) * 2;
+    const int k0 = s * 16 + (gq >> 1) * 8 + q;
+    const int k1 = k0 + 4;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const char* a0 = lds + k0 * (TILE * 2) + (col_b ^ swz_mc<TILE, 1>(k0));
+    const char* a1 = lds + k1 * (TILE * 2) + (col_b ^ swz_mc<TILE, 1>(k1));
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, r);
+  }
+}
+
 // s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= N only.
 constexpr int waitcnt_vm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
 
@@ -855,9 +886,14 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
   }
 }
 
+// MF32 = 1: the wave tile is computed with v_mfma_f32_32x32x16_bf16 ((MFR/2) x (NFR/2) blocks
+// of 32x32, four 16-deep k-substeps per K-step) instead of the 16x16x32 form: the same LDS
+// fragment bytes per K-step, half the MFMA instructions, 24 of every 32 MFMA cycles free for
+// VALU issue instead of 8 of 16.  MC operands use the swz_mc<TILE, 1> image.
 template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, int FP8 = 0,
-          int NFR = 4, int MFR = 4>
+          int NFR = 4, int MFR = 4, int MF32 = 0>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) gemm_kernel(SnGemmArgs args) {
+  static_assert(!MF32 || (!FP8 && NFR % 2 == 0 && MFR % 2 == 0), "32x32 blocks: bf16, even fragment counts");
   // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
   constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
   // MFMA operand formats: src A of the instruction is our B fragment (cbsz), src B our A
@@ -906,8 +942,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   const int k1 = min(args.K, k0 + args.kchunk);
 
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  using SA = GStager<AMC, AMODE, BM, NW, ES>;
-  using SB = GStager<BMC, BMODE, BNL, NW, ES>;
+  using SA = GStager<AMC, AMODE, BM, NW, ES, MF32>;
+  using SB = GStager<BMC, BMODE, BNL, NW, ES, MF32>;
   SA sa;
   SB sb;
   sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, split * args.kchunk, args.K, args.addr_legacy);
@@ -915,17 +951,50 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1, split * args.kchunk, args.K, args.addr_legacy);
 
   f32x4 acc[NFR][MFR];
+  constexpr int NB32 = MF32 ? NFR / 2 : 1, MB32 = MF32 ? MFR / 2 : 1;
+  f32x16 acc32[NB32][MB32];
+  if constexpr (MF32) {
 #pragma unroll
-  for (int i = 0; i < NFR; ++i)
+    for (int i = 0; i < NB32; ++i)
 #pragma unroll
-    for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < MB32; ++j) acc32[i][j] = f32x16{};
+  } else {
+#pragma unroll
+    for (int i = 0; i < NFR; ++i)
+#pragma unroll
+      for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   const int wm0 = (wave % WM) * (16 * MFR), wn0 = (wave / WM) * (16 * NFR);
   const int nk = k1 > k0 ? (k1 - k0 + BKE - 1) / BKE : 0;
 
   auto compute = [&](const char* la) __attribute__((always_inline)) {
     const char* lb = la + A_BYTES;
-    if constexpr (FP8 && MFR * NFR > 16) {
+    if constexpr (MF32) {
+      // two 16-deep substeps per fragment batch (the 16x16 path's two 32-deep substeps: the
+      // same fragment bytes and VGPRs per batch)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8_t fa[2][MB32], fb[2][NB32];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+          for (int i = 0; i < NB32; ++i) fb[s][i] = read_frag32<BMC, BNL>(lb, wn0 + 32 * i, 2 * h + s, lane);
+#pragma unroll
+          for (int j = 0; j < MB32; ++j) fa[s][j] = read_frag32<AMC, BM>(la, wm0 + 32 * j, 2 * h + s, lane);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int i = 0; i < NB32; ++i)
+#pragma unroll
+            for (int j = 0; j < MB32; ++j)
+              acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s][i], fa[s][j], acc32[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      return;
+    } else if constexpr (FP8 && MFR * NFR > 16) {
       // large fp8 tiles (gemm_fp8big.hip): B fragments held, A fragments streamed per row
       // group, so at most NFR + 1 fragments (8 VGPRs each) live beside the accumulators
       i32x8 fb8[NFR];
@@ -1060,8 +1129,27 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   }
 
   // Epilogue.  acc[i][j] holds D[n][m] with m = lane&15 (+16j), n = 4(lane>>4)+r (+16i):
-  // each lane owns 4 consecutive output columns of one output row.
-  const int mrow_l = lane & 15, ncol_l = (lane >> 4) * 4;
+  // each lane owns 4 consecutive output columns of one output row.  MF32: the 32x32 block
+  // (I, J) holds D[n][m] with m = 32J + (lane&31), n = 32I + 8b + 4(lane>>5) + r in its
+  // registers 4b + r; its four 4-register groups become acc[2I + (b>>1)][2J + (b&1)], so the
+  // epilogue below sees the same 4-column fragments at the positions wave_m / wave_n give.
+  if constexpr (MF32) {
+#pragma unroll
+    for (int i = 0; i < NFR; ++i)
+#pragma unroll
+      for (int j = 0; j < MFR; ++j) {
+        const int b = ((i & 1) << 1) | (j & 1);
+        const f32x16& t = acc32[i >> 1][j >> 1];
+        acc[i][j] = f32x4{t[4 * b], t[4 * b + 1], t[4 * b + 2], t[4 * b + 3]};
+      }
+  }
+  // wave-relative row (m) of fragment row j, and column (n) of fragment (i, j), of this lane
+  auto wave_m = [&](int j) __attribute__((always_inline)) {
+    return MF32 ? 32 * (j >> 1) + (lane & 31) : 16 * j + (lane & 15);
+  };
+  auto wave_n = [&](int i, int j) __attribute__((always_inline)) {
+    return MF32 ? 32 * (i >> 1) + 8 * (((i & 1) << 1) | (j & 1)) + 4 * (lane >> 5) : 16 * i + 4 * (lane >> 4);
+  };
   // fp32 outputs: the bias-gradient column (when routed to bias_out) is not part of C
   const int c_cols = (!epi_bf16<EPI>() && args.bias_out) ? args.ones_col : args.N;
   if constexpr (EPI == EPI_SGD) {
@@ -1088,10 +1176,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
         char* wbuf = (wave % WM) == 0 ? smem0 : smem1;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int lr = 16 * j + mrow_l;
+          const int lr = wave_m(j);
 #pragma unroll
           for (int i = 0; i < NFR; ++i) {
-            const int ch = (wn0 + 16 * i + ncol_l) >> 2;
+            const int ch = (wn0 + wave_n(i, j)) >> 2;
             *reinterpret_cast<f32x4*>(wbuf + lr * 512 + ((ch ^ (lr & 15)) << 4)) = acc[i][j];
           }
         }
@@ -1136,8 +1224,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       for (int j = 0; j < MFR; ++j)
 #pragma unroll
         for (int i = 0; i < NFR; ++i) {
-          const long long o = grp * args.c_gstride + (long long)(m_blk + wm0 + 16 * j + mrow_l) * args.ldc +
-                              n_blk + wn0 + 16 * i + ncol_l;
+          const long long o = grp * args.c_gstride + (long long)(m_blk + wm0 + wave_m(j)) * args.ldc +
+                              n_blk + wn0 + wave_n(i, j);
           Wv[j][i] = *reinterpret_cast<const float4*>(args.sgd_w + o);
           Av[j][i] = *reinterpret_cast<const float4*>(args.sgd_h + o);
         }
@@ -1145,8 +1233,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       for (int j = 0; j < MFR; ++j)
 #pragma unroll
         for (int i = 0; i < NFR; ++i) {
-          const long long o = grp * args.c_gstride + (long long)(m_blk + wm0 + 16 * j + mrow_l) * args.ldc +
-                              n_blk + wn0 + 16 * i + ncol_l;
+          const long long o = grp * args.c_gstride + (long long)(m_blk + wm0 + wave_m(j)) * args.ldc +
+                              n_blk + wn0 + wave_n(i, j);
           float W[4] = {Wv[j][i].x, Wv[j][i].y, Wv[j][i].z, Wv[j][i].w};
           float A[4] = {Av[j][i].x, Av[j][i].y, Av[j][i].z, Av[j][i].w};
           const f32x4 v = acc[i][j];
@@ -1178,10 +1266,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       char* wbuf = wm0 < HALF ? smem0 : smem1;
 #pragma unroll
       for (int j = 0; j < MFR; ++j) {
-        const int lr = wm0 + 16 * j + mrow_l, m = m_blk + lr;
+        const int lr = wm0 + wave_m(j), m = m_blk + lr;
 #pragma unroll
         for (int i = 0; i < NFR; ++i) {
-          const int nl = wn0 + 16 * i + ncol_l, n = n_blk + nl;
+          const int nl = wn0 + wave_n(i, j), n = n_blk + nl;
           float o[4] = {0.f, 0.f, 0.f, 0.f};
           if (m < args.M && n < args.N) epi_bf16_math<EPI, (FP8 != 0)>(args, grp, m, n, acc[i][j], args.N, o);
           *reinterpret_cast<uint2*>(wbuf + (lr % HALF) * PITCH + nl * 2) =
@@ -1221,11 +1309,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   float qmax = 0.f;
 #pragma unroll
   for (int j = 0; j < MFR; ++j) {
-    const int m = m_blk + wm0 + 16 * j + mrow_l;
+    const int m = m_blk + wm0 + wave_m(j);
     if (m >= args.M) continue;
 #pragma unroll
     for (int i = 0; i < NFR; ++i) {
-      const int n = n_blk + wn0 + 16 * i + ncol_l;
+      const int n = n_blk + wn0 + wave_n(i, j);
       if (n >= args.N) continue;
       epi_store<EPI, (FP8 != 0)>(args, grp, split, m, n, acc[i][j], c_cols, epi_bf16<EPI>() ? &qmax : nullptr);
     }
@@ -1524,25 +1612,26 @@ int launch256(const SnGemmArgs& a, hipStream_t stream) {
   return 4;
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS, int NFR = 4, int MFR = 4>
+template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS, int NFR = 4, int MFR = 4,
+          int MF32 = 0>
 int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS, false, NFR, MFR>), grid,
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS, false, NFR, MFR, MF32>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_BF16_DROP:  // InnerProduct forward only (dense NT)
       if (AMC || AMODE != OP_DENSE || BMC || BMODE != OP_DENSE) return 4;
-      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, NW, NS, false, NFR, MFR>), grid,
-                         dim3(NW * 64), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, NW, NS, false, NFR, MFR, MF32>),
+                         grid, dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS, false, NFR, MFR>), grid,
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS, false, NFR, MFR, MF32>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32_ACC:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS, false, NFR, MFR>), grid,
-                         dim3(NW * 64), 0, st, a);
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS, false, NFR, MFR, MF32>),
+                         grid, dim3(NW * 64), 0, st, a);
       break;
     default:
       return 2;
@@ -1620,3 +1709,4 @@ int sn_gemm_pk_a(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_tiles_c(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_t256p8(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_pk_b(const SnGemmArgs& a, hipStream_t stream);
+int sn_gemm_mf32(const SnGemmArgs& a, hipStream_t stream);

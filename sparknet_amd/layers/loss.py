@@ -19,31 +19,54 @@ from .. import ops
 from ..core.layer import Layer, register
 
 
+def _prod(dims) -> int:
+    n = 1
+    for d in dims:
+        n *= int(d)
+    return n
+
+
 def rows_view(blob, axis, diff=False):
-    """[outer*inner, channels] view of a blob along ``axis`` (channels last physically)."""
+    """[outer*inner, channels] view of a blob along ``axis`` (Caffe's outer-major, inner-minor
+    row order: softmax_loss_layer.cpp:36-37 canonicalises any axis).  A 4-D blob's storage
+    is NHWC: axis 1 is already channels-last; any other axis goes through the logical NCHW
+    layout first."""
     t = blob.diff if diff else blob.data
     axis = blob.canonical_axis(axis)
     if blob.is_image:
-        if axis != 1:
-            raise NotImplementedError("only axis=1 is supported for 4-D blobs")
-        return t.reshape(-1, blob.shape[1])
-    if axis == len(blob.shape) - 1 or blob.count_range(axis + 1) == 1:
+        if axis == 1:
+            return t.reshape(-1, blob.shape[1])
+        t = _lh().nhwc_to_nchw(t) if t.is_cuda else t.permute(0, 3, 1, 2)
+    elif axis == len(blob.shape) - 1 or blob.count_range(axis + 1) == 1:
         return t.reshape(-1, blob.shape[axis])
     # generic: move axis last ([outer][A][inner] -> [outer][inner][A])
+    outer, A, inner = _prod(blob.shape[:axis]), blob.shape[axis], _prod(blob.shape[axis + 1:])
+    if inner == 1:
+        return t.reshape(-1, A)
     if t.is_cuda:
-        outer, A, inner = blob.count_range(0, axis), blob.shape[axis], blob.count_range(axis + 1)
-        return _lh().transpose(t, outer, A, inner).reshape(-1, A)
-    perm = [d for d in range(t.dim()) if d != axis] + [axis]
-    return t.permute(*perm).reshape(-1, blob.shape[axis])
+        return _lh().transpose(t.contiguous(), outer, A, inner).reshape(-1, A)
+    return t.reshape(outer, A, inner).permute(0, 2, 1).reshape(-1, A)
 
 
 def rows_view_back(rows, blob, axis):
     """Inverse of :func:`rows_view` for a result in the [rows, A] layout."""
     axis = blob.canonical_axis(axis)
-    if blob.is_image or axis == len(blob.shape) - 1 or blob.count_range(axis + 1) == 1:
+    if (blob.is_image and axis == 1) or (not blob.is_image and (
+            axis == len(blob.shape) - 1 or blob.count_range(axis + 1) == 1)):
         return rows.reshape(blob.data.shape)
-    outer, A, inner = blob.count_range(0, axis), blob.shape[axis], blob.count_range(axis + 1)
-    return _lh().transpose(rows.reshape(outer, inner, A), outer, inner, A).reshape(blob.data.shape)
+    outer, A, inner = _prod(blob.shape[:axis]), blob.shape[axis], _prod(blob.shape[axis + 1:])
+    if inner == 1:
+        t = rows
+    elif rows.is_cuda:
+        t = _lh().transpose(rows.contiguous().reshape(outer, inner, A), outer, inner, A)
+    else:
+        t = rows.reshape(outer, inner, A).permute(0, 2, 1)
+    if not blob.is_image:
+        return t.reshape(blob.data.shape)
+    N, C_, H, W = blob.shape
+    if rows.is_cuda:
+        return _lh().nchw_to_nhwc(t.contiguous().reshape(N, C_, H * W), N, C_, H, W)
+    return t.reshape(N, C_, H, W).permute(0, 2, 3, 1).contiguous()
 
 
 def _lh():
@@ -133,7 +156,7 @@ class SoftmaxWithLossLayer(LossLayer):
         self.prob, self.norm = prob, norm
         tops[0].data = loss.reshape(())
         if len(tops) > 1:
-            tops[1].data = prob.reshape(tops[1].data.shape).to(self.dtype)
+            tops[1].data = rows_view_back(prob, bottoms[0], self.axis).to(self.dtype)
 
     def backward(self, tops, propagate_down, bottoms):
         if len(propagate_down) > 1 and propagate_down[1]:
@@ -141,7 +164,7 @@ class SoftmaxWithLossLayer(LossLayer):
         if propagate_down[0]:
             g = ops.softmax_loss_backward(self.prob, bottoms[1].data, tops[0].diff, self.norm,
                                           self.ignore_label, bottoms[0].dtype)
-            bottoms[0].diff = g.reshape(bottoms[0].data.shape)
+            bottoms[0].diff = rows_view_back(g, bottoms[0], self.axis).to(bottoms[0].dtype)
 
 
 @register("Softmax")
@@ -157,29 +180,14 @@ class SoftmaxLayer(Layer):
 
     def forward(self, bottoms, tops):
         b = bottoms[0]
-        if b.data.is_cuda:
-            tops[0].data = rows_view_back(ops.softmax_forward(rows_view(b, self.axis)), b, self.axis)
-            return
-        y = ops.softmax_forward(rows_view(b, self.axis))
-        if b.is_image or self.axis == len(b.shape) - 1 or b.count_range(self.axis + 1) == 1:
-            tops[0].data = y.reshape(tops[0].data.shape)
-        else:
-            tops[0].data = torch.softmax(b.data.float(), dim=self.axis).to(self.dtype)
+        tops[0].data = rows_view_back(ops.softmax_forward(rows_view(b, self.axis)), b, self.axis).to(self.dtype)
 
     def backward(self, tops, propagate_down, bottoms):
         if not propagate_down[0]:
             return
         t, b = tops[0], bottoms[0]
-        if t.diff.is_cuda:
-            g = ops.softmax_backward(rows_view(t, self.axis, diff=True), rows_view(t, self.axis))
-            b.diff = rows_view_back(g, b, self.axis)
-            return
-        if b.is_image or self.axis == len(b.shape) - 1 or b.count_range(self.axis + 1) == 1:
-            g = ops.softmax_backward(rows_view(t, self.axis, diff=True), rows_view(t, self.axis))
-            b.diff = g.reshape(b.data.shape)
-        else:
-            y, d = t.data.float(), t.diff.float()
-            b.diff = (y * (d - (d * y).sum(self.axis, keepdim=True))).to(self.dtype)
+        g = ops.softmax_backward(rows_view(t, self.axis, diff=True), rows_view(t, self.axis))
+        b.diff = rows_view_back(g, b, self.axis).to(b.dtype)
 
 
 @register("Accuracy")

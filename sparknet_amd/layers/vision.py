@@ -40,6 +40,191 @@ def conv_geometry(cp):
     return int(kh), int(kw), sh, sw, ph, pw
 
 
+# --- N-d convolution (base_conv_layer.cpp:16-110: num_spatial_axes != 2, axis != 1 or
+# force_nd_im2col) --------------------------------------------------------------------------
+
+def _nd_field(cp, rep: str, h: str, w: str, nsp: int, default):
+    """A repeated kernel/stride/pad field given once or per spatial axis, or its _h/_w pair
+    (2-D only); Caffe's CHECKs become ValueErrors (base_conv_layer.cpp:26-96)."""
+    if cp.HasField(h) or cp.HasField(w):
+        if nsp != 2:
+            raise ValueError(f"{h} & {w} can only be used for 2D convolution")
+        return int(getattr(cp, h)), int(getattr(cp, w))
+    vals = [int(v) for v in getattr(cp, rep)]
+    if not vals:
+        if default is None:
+            raise ValueError("kernel_size is required")
+        return (default,) * nsp
+    if len(vals) not in (1, nsp):
+        raise ValueError(f"{rep} must be specified once, or once per spatial dimension "
+                         f"({rep} specified {len(vals)} times; {nsp} spatial dims)")
+    return tuple(vals * nsp if len(vals) == 1 else vals)
+
+
+def _canonical_axis(axis: int, nd: int) -> int:
+    a = axis + nd if axis < 0 else axis
+    if not 0 <= a < nd:
+        raise ValueError(f"axis {axis} out of range for a {nd}-axis blob")
+    return a
+
+
+def conv_nd_mode(cp, bottom) -> bool:
+    """The N-d path: a blob that is not 4-D, a channel axis other than 1, or force_nd_im2col."""
+    nd = len(bottom.shape)
+    return nd != 4 or _canonical_axis(int(cp.axis), nd) != 1 or bool(cp.force_nd_im2col)
+
+
+def _logical(blob, diff=False):
+    return blob.nchw(diff=diff)
+
+
+def _store_logical(blob, t, diff=False):
+    """Write a logical-layout tensor into a blob (a 4-D blob's storage is NHWC)."""
+    if blob.is_image:
+        blob.set_nchw(t.reshape(blob.shape), diff=diff)
+    elif diff:
+        blob.diff = t.reshape(blob.shape).to(blob.dtype)
+    else:
+        blob.data = t.reshape(blob.shape).to(blob.dtype)
+
+
+class _NdGeometry:
+    """Channel axis, batch / spatial split and kernel geometry of an N-d Convolution,
+    Deconvolution or Im2col (the same parsing as base_conv_layer.cpp:16-110)."""
+
+    def nd_setup(self, cp, bottom):
+        nd = len(bottom.shape)
+        self.axis = _canonical_axis(int(cp.axis), nd)
+        self.nsp = nd - self.axis - 1
+        if self.nsp < 1:
+            raise ValueError("convolution needs at least one spatial axis")
+        self.ks = _nd_field(cp, "kernel_size", "kernel_h", "kernel_w", self.nsp, None)
+        self.st = _nd_field(cp, "stride", "stride_h", "stride_w", self.nsp, 1)
+        self.pd = _nd_field(cp, "pad", "pad_h", "pad_w", self.nsp, 0)
+        if min(self.ks) <= 0 or min(self.st) <= 0:
+            raise ValueError("kernel and stride dimensions must be nonzero")
+        self.C = int(bottom.shape[self.axis])
+
+    def nd_split(self, shape):
+        import math
+        return int(math.prod(shape[:self.axis])), int(shape[self.axis]), tuple(int(d) for d in shape[self.axis + 1:])
+
+
+class ConvolutionNdLayer(_NdGeometry, Layer):
+    """Convolution over any number of spatial axes (and any channel axis): N-d im2col +
+    the MFMA GEMM on the GPU (ops.hip.conv_nd_*), the fp32 reference on the CPU.  Weights
+    keep Caffe's [K][C/g][k_0..k_{n-1}] layout.  Created by ConvolutionLayer.layer_setup when
+    conv_nd_mode holds; its type_name keeps the engine's 2-D fusion passes away from it."""
+    type_name = "ConvolutionND"
+
+    def layer_setup(self, bottoms, tops):
+        cp = self.lp.convolution_param
+        if len(bottoms) != len(tops):
+            raise ValueError("Convolution needs as many tops as bottoms")
+        self.nd_setup(cp, bottoms[0])
+        self.K = int(cp.num_output)
+        self.groups = int(cp.group)
+        if self.K <= 0:
+            raise ValueError("num_output must be positive")
+        if self.C % self.groups or self.K % self.groups:
+            raise ValueError("channels and num_output must be divisible by group")
+        self.weight = self.add_param((self.K, self.C // self.groups) + self.ks,
+                                     filler=cp.weight_filler if cp.HasField("weight_filler") else None)
+        self.bias = None
+        if cp.bias_term:
+            self.bias = self.add_param((self.K,), filler=cp.bias_filler if cp.HasField("bias_filler") else None)
+
+    def spec(self, b) -> ops.ConvNdSpec:
+        num, C, ins = self.nd_split(b.shape)
+        if C != self.C:
+            raise ValueError(f"{self.name}: input channels changed {self.C} -> {C}")
+        return ops.ConvNdSpec(num, C, self.K, ins, self.ks, self.st, self.pd, self.groups)
+
+    def reshape(self, bottoms, tops):
+        for b, t in zip(bottoms, tops):
+            s = self.spec(b)
+            if min(s.outs) <= 0:
+                raise ValueError(f"{self.name}: empty convolution output {s.outs}")
+            t.reshape(tuple(b.shape[:self.axis]) + (self.K,) + s.outs, self.dtype)
+
+    def forward(self, bottoms, tops):
+        w = self.weight.compute
+        bias = self.bias.data if self.bias is not None else None
+        for b, t in zip(bottoms, tops):
+            s = self.spec(b)
+            x = _logical(b).reshape((s.num, s.C) + s.ins)
+            _store_logical(t, ops.conv_nd_forward(x, w, bias, s))
+
+    def backward(self, tops, propagate_down, bottoms):
+        w = self.weight.compute
+        dw = self.weight.diff if self.param_grads_needed(0) else None
+        db = self.bias.diff if (self.bias is not None and self.param_grads_needed(1)) else None
+        for i, (t, b) in enumerate(zip(tops, bottoms)):
+            s = self.spec(b)
+            x = _logical(b).reshape((s.num, s.C) + s.ins)
+            dy = _logical(t, diff=True).reshape((s.num, s.K) + s.outs)
+            dx = ops.conv_nd_backward(dy, x, w, s, bool(propagate_down[i]), dw, db)
+            if propagate_down[i]:
+                _store_logical(b, dx, diff=True)
+
+
+class DeconvolutionNdLayer(_NdGeometry, Layer):
+    """N-d transposed convolution (deconv_layer.cpp): forward = the data gradient of the
+    convolution mapping top (num_output channels) -> bottom, backward = that convolution's
+    forward (bottom diff) and weight gradient.  Weight Caffe shape [C][K/g][k...]."""
+    type_name = "DeconvolutionND"
+
+    def layer_setup(self, bottoms, tops):
+        cp = self.lp.convolution_param
+        self.nd_setup(cp, bottoms[0])
+        self.K = int(cp.num_output)
+        self.groups = int(cp.group)
+        if self.C % self.groups or self.K % self.groups:
+            raise ValueError("channels and num_output must be divisible by group")
+        self.weight = self.add_param((self.C, self.K // self.groups) + self.ks,
+                                     filler=cp.weight_filler if cp.HasField("weight_filler") else None)
+        self.bias = None
+        if cp.bias_term:
+            self.bias = self.add_param((self.K,), filler=cp.bias_filler if cp.HasField("bias_filler") else None)
+
+    def conv_spec(self, b) -> ops.ConvNdSpec:
+        """The convolution top -> bottom whose data gradient this layer's forward is."""
+        num, C, ins = self.nd_split(b.shape)
+        outs = tuple((i - 1) * st + k - 2 * p for i, k, st, p in zip(ins, self.ks, self.st, self.pd))
+        return ops.ConvNdSpec(num, self.K, C, outs, self.ks, self.st, self.pd, self.groups)
+
+    def reshape(self, bottoms, tops):
+        for b, t in zip(bottoms, tops):
+            sc = self.conv_spec(b)
+            if min(sc.ins) <= 0:
+                raise ValueError(f"{self.name}: empty deconvolution output {sc.ins}")
+            t.reshape(tuple(b.shape[:self.axis]) + (self.K,) + sc.ins, self.dtype)
+
+    def forward(self, bottoms, tops):
+        w = self.weight.compute
+        for b, t in zip(bottoms, tops):
+            sc = self.conv_spec(b)
+            x = _logical(b).reshape((sc.num, sc.K) + sc.outs)
+            y = ops.conv_nd_backward(x, None, w, sc, True, None, None)
+            if self.bias is not None:
+                y = (y.float() + self.bias.data.float().view((1, -1) + (1,) * sc.nd)).to(y.dtype)
+            _store_logical(t, y)
+
+    def backward(self, tops, propagate_down, bottoms):
+        w = self.weight.compute
+        dw = self.weight.diff if self.param_grads_needed(0) else None
+        for i, (t, b) in enumerate(zip(tops, bottoms)):
+            sc = self.conv_spec(b)
+            dtop = _logical(t, diff=True).reshape((sc.num, sc.C) + sc.ins)
+            if self.bias is not None and self.param_grads_needed(1):
+                self.bias.diff += dtop.float().reshape(sc.num, sc.C, -1).sum((0, 2))
+            if dw is not None:
+                x = _logical(b).reshape((sc.num, sc.K) + sc.outs)
+                ops.conv_nd_backward(x, dtop, w, sc, False, dw, None)
+            if propagate_down[i]:
+                _store_logical(b, ops.conv_nd_forward(dtop, w, None, sc), diff=True)
+
+
 @register("Convolution")
 class ConvolutionLayer(Layer):
     exact_bottoms = -1
@@ -54,13 +239,12 @@ class ConvolutionLayer(Layer):
 
     def layer_setup(self, bottoms, tops):
         cp = self.lp.convolution_param
-        if cp.axis != 1:
-            raise NotImplementedError("Convolution only supports axis=1 (NCHW logical)")
+        if conv_nd_mode(cp, bottoms[0]):
+            self.__class__ = ConvolutionNdLayer  # N-d path (see conv_nd_mode)
+            return self.layer_setup(bottoms, tops)
         if len(bottoms) != len(tops):
             raise ValueError("Convolution needs as many tops as bottoms")
         b = bottoms[0]
-        if len(b.shape) != 4:
-            raise NotImplementedError("only 2-D spatial convolution is supported")
         self.R, self.S, self.sh, self.sw, self.ph, self.pw = conv_geometry(cp)
         self.K = int(cp.num_output)
         self.groups = int(cp.group)
@@ -238,6 +422,9 @@ class DeconvolutionLayer(Layer):
 
     def layer_setup(self, bottoms, tops):
         cp = self.lp.convolution_param
+        if conv_nd_mode(cp, bottoms[0]):
+            self.__class__ = DeconvolutionNdLayer  # N-d path (see conv_nd_mode)
+            return self.layer_setup(bottoms, tops)
         self.R, self.S, self.sh, self.sw, self.ph, self.pw = conv_geometry(cp)
         self.K = int(cp.num_output)
         self.groups = int(cp.group)
@@ -578,7 +765,11 @@ class Im2colLayer(Layer):
     exact_tops = 1
 
     def layer_setup(self, bottoms, tops):
-        self.R, self.S, self.sh, self.sw, self.ph, self.pw = conv_geometry(self.lp.convolution_param)
+        cp = self.lp.convolution_param
+        if conv_nd_mode(cp, bottoms[0]):
+            self.__class__ = Im2colNdLayer
+            return self.layer_setup(bottoms, tops)
+        self.R, self.S, self.sh, self.sw, self.ph, self.pw = conv_geometry(cp)
 
     def reshape(self, bottoms, tops):
         N, C, H, W = bottoms[0].shape
@@ -615,6 +806,61 @@ class Im2colLayer(Layer):
         x = torch.nn.functional.fold(d, b.shape[2:], (self.R, self.S), padding=(self.ph, self.pw),
                                      stride=(self.sh, self.sw))
         b.diff = x.permute(0, 2, 3, 1).contiguous().to(b.dtype)
+
+
+class Im2colNdLayer(_NdGeometry, Layer):
+    """N-d im2col layer (im2col_layer.cpp with num_spatial_axes != 2): top =
+    shape[:axis] + [C * prod(k)] + outs, each image's columns in (c, taps) order."""
+    type_name = "Im2colND"
+    exact_bottoms = 1
+    exact_tops = 1
+
+    def layer_setup(self, bottoms, tops):
+        self.nd_setup(self.lp.convolution_param, bottoms[0])
+
+    def spec(self, b) -> ops.ConvNdSpec:
+        num, C, ins = self.nd_split(b.shape)
+        return ops.ConvNdSpec(num, C, 1, ins, self.ks, self.st, self.pd, 1)
+
+    def reshape(self, bottoms, tops):
+        b = bottoms[0]
+        s = self.spec(b)
+        tops[0].reshape(tuple(b.shape[:self.axis]) + (s.C * s.T,) + s.outs, self.dtype)
+
+    def forward(self, bottoms, tops):
+        b = bottoms[0]
+        s = self.spec(b)
+        x = _logical(b).reshape((s.num, s.C) + s.ins)
+        CT = s.C * s.T
+        if x.is_cuda:
+            from ..ops import hip, layers_hip
+            x = x.contiguous()
+            col = torch.empty((s.num * s.P, CT), dtype=x.dtype, device=x.device)
+            hip.call("im2col_nd", x, col, s.nd, s.num, s.C, s.C, 0, CT, hip._nd_dims(s), hip._nd_dt(x),
+                     hip._nd_dt(col))
+            y = layers_hip.transpose(col, s.num, s.P, CT)
+        else:
+            y = ops.ref.im2col_nd(x.float(), s).reshape(s.num, s.P, CT).transpose(1, 2)
+        _store_logical(tops[0], y)
+
+    def backward(self, tops, propagate_down, bottoms):
+        if not propagate_down[0]:
+            return
+        b, t = bottoms[0], tops[0]
+        s = self.spec(b)
+        CT = s.C * s.T
+        dy = _logical(t, diff=True).reshape(s.num, CT, s.P)
+        if dy.is_cuda:
+            from ..ops import hip, layers_hip
+            dcol = layers_hip.transpose(dy.contiguous(), s.num, CT, s.P)
+            dx = torch.empty((s.num, s.C) + s.ins, dtype=dy.dtype, device=dy.device)
+            hip.call("col2im_nd", dcol, dx, s.nd, s.num, s.C, s.C, 0, CT, hip._nd_dims(s), hip._nd_dt(dcol),
+                     hip._nd_dt(dx), 0)
+        else:
+            x = _logical(b).reshape((s.num, s.C) + s.ins).float().detach().requires_grad_(True)
+            col = ops.ref.im2col_nd(x, s).reshape(s.num, s.P, CT).transpose(1, 2)
+            dx, = torch.autograd.grad(col, x, dy.float())
+        _store_logical(b, dx, diff=True)
 
 
 __all__ = ["ConvolutionLayer", "DeconvolutionLayer", "PoolingLayer", "LRNLayer", "InnerProductLayer",

@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 
 from . import ref
-from .spec import POOL_AVE, POOL_MAX, POOL_STOCHASTIC, ConvSpec, PoolSpec  # noqa: F401
+from .spec import POOL_AVE, POOL_MAX, POOL_STOCHASTIC, ConvNdSpec, ConvSpec, PoolSpec  # noqa: F401
 
 _hip = None
 
@@ -38,6 +38,8 @@ def _dispatch(name):
 
 conv_forward = _dispatch("conv_forward")
 conv_backward = _dispatch("conv_backward")
+conv_nd_forward = _dispatch("conv_nd_forward")
+conv_nd_backward = _dispatch("conv_nd_backward")
 linear_forward = _dispatch("linear_forward")
 linear_backward = _dispatch("linear_backward")
 pool_forward = _dispatch("pool_forward")

@@ -115,6 +115,8 @@ TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96)
          6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64),
          11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192), 15: (128, 192), 16: (192, 128),
          17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64), 21: (64, 256), 22: (64, 128),
+         # v_mfma_f32_32x32x16_bf16 twins of tiles 0, 10, 16, 13, 1, 11 (csrc/kernels/gemm_mf32.hip)
+         23: (128, 128), 24: (128, 64), 25: (192, 128), 26: (256, 128), 27: (256, 64), 28: (256, 256),
          # persistent ring-pipelined tiles (csrc/kernels/gemm_pk.h): one 512-thread block per CU
          30: (256, 128), 31: (256, 64), 32: (256, 96), 33: (128, 128), 34: (256, 192), 36: (128, 256),
          37: (192, 384), 38: (256, 256), 39: (256, 128),
@@ -124,9 +126,9 @@ PK_TILES = frozenset((30, 31, 32, 33, 34, 36, 37, 38))
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
 _SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512, 21: 512,
-          22: 768,
+          22: 768, 24: 768, 26: 256, 28: 256,
           30: 256, 31: 256, 32: 256, 33: 256, 34: 256, 36: 256, 37: 256, 38: 256, 39: 256, 40: 256, 41: 256}
-_KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55,
+_KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55, 26: 1.1, 28: 2.0,
              30: 0.75, 31: 0.45, 32: 0.6, 33: 0.45, 34: 1.1, 36: 0.75, 37: 1.3, 38: 1.2, 40: 1.6, 41: 0.9}
 # autotune candidates 11-14 (SN_GEMM_TILE8W=0 drops them)
 _TILE8W = os.environ.get("SN_GEMM_TILE8W", "1") != "0"

@@ -17,7 +17,7 @@ import torch
 from . import _lib
 from .gemm import (EPI_BF16, EPI_F32, EPI_F32_ACC, ConvGeom, Dense, FlipW, Im2col, colsum, gemm,
                    linear_dgrad, linear_fwd, linear_wgrad)
-from .spec import POOL_MAX, ConvSpec, PoolSpec
+from .spec import POOL_MAX, ConvNdSpec, ConvSpec, PoolSpec
 
 call = _lib.call
 BF16 = torch.bfloat16
@@ -669,6 +669,87 @@ def linear_backward_sgd(dy2, x2, w, need_dx, sgd, db=None, gate=None, db_acc=Tru
     with wgrad_side("fcsgd"):  # forked after the dgrad: the update overwrites w
         if not linear_wgrad_sgd(dy2, x2, sgd, db, db_acc) and db is not None:
             colsum(dy2, db, accumulate=db_acc)
+    return dx
+
+
+# --------------------------------------------------------------------------------------
+# N-d convolution (csrc/kernels/conv_nd.hip: N-d im2col / col2im) on the MFMA GEMM engine
+# --------------------------------------------------------------------------------------
+
+def _nd_dims(s: ConvNdSpec):
+    v = list(s.ins) + list(s.outs) + list(s.ks) + list(s.st) + list(s.pd)
+    return (C.c_int * len(v))(*v)
+
+
+def _nd_dt(t: torch.Tensor) -> int:
+    assert t.dtype in (BF16, torch.float32), t.dtype
+    return int(t.dtype == torch.float32)
+
+
+def _nd_col(x, s: ConvNdSpec, g: int) -> torch.Tensor:
+    """im2col of channel group g: [num * P][ld] bf16 (ld = Cg*T rounded up to 8, pad = 0)."""
+    ld = _round8(s.Cg * s.T)
+    col = torch.empty((s.num * s.P, ld), dtype=BF16, device=x.device)
+    call("im2col_nd", x, col, s.nd, s.num, s.C, s.Cg, g * s.Cg, ld, _nd_dims(s), _nd_dt(x), 0)
+    return col
+
+
+def _nd_chan_cl(t, s: ConvNdSpec, chans: int, g: int, per: int) -> torch.Tensor:
+    """[num][chans][P] channel group g (per channels) -> channels-last [num * P][per]."""
+    from . import layers_hip as lh
+    if s.groups == 1:
+        return lh.transpose(t, s.num, chans, s.P).view(s.num * s.P, chans)
+    tmp = torch.empty((s.num, per, s.P), dtype=t.dtype, device=t.device)
+    lh.axis_copy(t, tmp, s.num, chans, per, s.P, g * per, 0, per)
+    return lh.transpose(tmp, s.num, per, s.P).view(s.num * s.P, per)
+
+
+def conv_nd_forward(x, w, b, s: ConvNdSpec):
+    """x [num][C][ins] bf16, w [K][Cg][ks] bf16 (Caffe layout) -> y [num][K][outs] bf16: per
+    group an N-d im2col, one NT MFMA product with the bias epilogue, and a transpose of the
+    channels-last result into the group's channel slice."""
+    from . import layers_hip as lh
+    x = _c(x)
+    CT = s.Cg * s.T
+    y = torch.empty((s.num, s.K, s.P), dtype=BF16, device=x.device)
+    for g in range(s.groups):
+        col = _nd_col(x, s, g)
+        wg = torch.zeros((s.Kg, col.shape[1]), dtype=BF16, device=x.device)
+        wg[:, :CT] = w[g * s.Kg:(g + 1) * s.Kg].reshape(s.Kg, CT)
+        bg = b[g * s.Kg:(g + 1) * s.Kg].float().contiguous() if b is not None else None
+        yc = linear_fwd(col, wg, bg)  # [num * P][Kg]
+        if s.groups == 1:
+            y = lh.transpose(yc, s.num, s.P, s.Kg, out_shape=(s.num, s.K, s.P))
+        else:
+            lh.axis_copy(lh.transpose(yc, s.num, s.P, s.Kg), y, s.num, s.Kg, s.K, s.P, 0, g * s.Kg, s.Kg)
+    return y.view((s.num, s.K) + s.outs)
+
+
+def conv_nd_backward(dy, x, w, s: ConvNdSpec, need_dx: bool, dw=None, db=None):
+    """Weight / bias gradients (accumulated into dw [K][Cg][ks], db [K], fp32) from one TN
+    product per group over the channels-last dy and the im2col of x (bias through the
+    ones column); the data gradient from one NN product per group and the N-d col2im."""
+    dy = _c(dy).to(BF16)
+    if x is not None:
+        x = _c(x)
+    assert x is not None or dw is None, "the weight gradient needs the input"
+    CT = s.Cg * s.T
+    dx = torch.empty((s.num, s.C) + s.ins, dtype=dy.dtype, device=dy.device) if need_dx else None
+    for g in range(s.groups):
+        dyc = _nd_chan_cl(dy, s, s.K, g, s.Kg)  # [num * P][Kg]
+        if dw is not None:
+            col = _nd_col(x, s, g)
+            dwg = dw.view(s.K, CT)[g * s.Kg:(g + 1) * s.Kg]
+            dbg = db[g * s.Kg:(g + 1) * s.Kg] if db is not None else None
+            if not linear_wgrad(dyc, col[:, :CT], dwg, accumulate=True, db=dbg, db_acc=True) and dbg is not None:
+                colsum(dyc, dbg, accumulate=True)
+        elif db is not None:
+            colsum(dyc, db[g * s.Kg:(g + 1) * s.Kg], accumulate=True)
+        if need_dx:
+            wg = w[g * s.Kg:(g + 1) * s.Kg].reshape(s.Kg, CT).contiguous()
+            dcol = linear_dgrad(dyc, wg)  # [num * P][CT] (possibly a view of a padded buffer)
+            call("col2im_nd", dcol, dx, s.nd, s.num, s.C, s.Cg, g * s.Cg, dcol.stride(0), _nd_dims(s), 0,
+                 _nd_dt(dx), 0)
     return dx
 
 

@@ -13,7 +13,7 @@ import math
 import torch
 import torch.nn.functional as F
 
-from .spec import POOL_AVE, POOL_MAX, ConvSpec, PoolSpec
+from .spec import POOL_AVE, POOL_MAX, ConvNdSpec, ConvSpec, PoolSpec
 
 
 def nchw(x):
@@ -36,6 +36,56 @@ def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None):
     if relu:
         y = F.relu(y)
     return nhwc(y).to(x.dtype)
+
+
+# --- N-d convolution (base_conv_layer.cpp:16-40, im2col.cpp im2col_nd_cpu) ------------
+
+def im2col_nd(x, s: ConvNdSpec, g: int = 0):
+    """[num][C][ins] -> col [num * P][Cg * T] of channel group g (Caffe's (c, taps) order)."""
+    xp = F.pad(x[:, g * s.Cg:(g + 1) * s.Cg], [p for d in reversed(s.pd) for p in (d, d)])
+    taps = []
+    import itertools
+    for kk in itertools.product(*[range(k) for k in s.ks]):
+        idx = [slice(None), slice(None)] + [slice(k0, k0 + st * (o - 1) + 1, st)
+                                            for k0, st, o in zip(kk, s.st, s.outs)]
+        taps.append(xp[tuple(idx)])
+    col = torch.stack(taps, 2)  # [num][Cg][T][outs]
+    return col.reshape(s.num, s.Cg * s.T, s.P).transpose(1, 2).reshape(s.num * s.P, s.Cg * s.T)
+
+
+def conv_nd_forward(x, w, b, s: ConvNdSpec):
+    """x [num][C][ins], w [K][Cg][ks] (Caffe layout) -> y [num][K][outs]."""
+    x, w = x.float(), w.float()
+    ys = []
+    for g in range(s.groups):
+        col = im2col_nd(x, s, g)
+        wg = w[g * s.Kg:(g + 1) * s.Kg].reshape(s.Kg, -1)
+        ys.append((col @ wg.t()).reshape(s.num, s.P, s.Kg).transpose(1, 2))
+    y = torch.cat(ys, 1)
+    if b is not None:
+        y = y + b.float().view(1, -1, 1)
+    return y.reshape((s.num, s.K) + s.outs)
+
+
+def conv_nd_backward(dy, x, w, s: ConvNdSpec, need_dx: bool, dw=None, db=None):
+    """Gradients of conv_nd_forward by autograd on the same formula; dw / db accumulate
+    (Caffe's Backward adds into the param diffs).  x may be None when dw is None (the data
+    gradient alone: a Deconvolution forward)."""
+    if x is None:
+        assert dw is None
+        x = torch.zeros((s.num, s.C) + tuple(s.ins), dtype=dy.dtype)
+    xr = x.float().detach().requires_grad_(need_dx)
+    wr = w.float().detach().requires_grad_(dw is not None)
+    y = conv_nd_forward(xr, wr, None, s)
+    ins = [t for t in (xr, wr) if t.requires_grad]
+    grads = torch.autograd.grad(y, ins, dy.float()) if ins else ()
+    gi = iter(grads)
+    dx = next(gi) if need_dx else None
+    if dw is not None:
+        dw += next(gi).reshape(dw.shape)
+    if db is not None:
+        db += dy.float().reshape(s.num, s.K, -1).sum((0, 2))
+    return dx.to(x.dtype) if dx is not None else None
 
 
 def _gated(dx, gate):

@@ -43,6 +43,49 @@ class ConvSpec:
                         self.ph, self.pw, self.dh, self.dw, self.groups)
 
 
+@dataclass(frozen=True)
+class ConvNdSpec:
+    """N-d convolution over a logical [num][C][D_0..D_{n-1}] blob (Caffe's general path:
+    base_conv_layer.cpp:16-40 — every axis before the channel axis is batch, every axis
+    after it spatial; no dilation in this Caffe)."""
+    num: int
+    C: int
+    K: int
+    ins: tuple
+    ks: tuple
+    st: tuple
+    pd: tuple
+    groups: int = 1
+
+    @property
+    def nd(self) -> int:
+        return len(self.ins)
+
+    @property
+    def outs(self) -> tuple:
+        return tuple((i + 2 * p - k) // s + 1 for i, k, s, p in zip(self.ins, self.ks, self.st, self.pd))
+
+    @property
+    def Cg(self) -> int:
+        return self.C // self.groups
+
+    @property
+    def Kg(self) -> int:
+        return self.K // self.groups
+
+    @property
+    def T(self) -> int:
+        return math.prod(self.ks)
+
+    @property
+    def P(self) -> int:
+        return math.prod(self.outs)
+
+    @property
+    def Sin(self) -> int:
+        return math.prod(self.ins)
+
+
 POOL_MAX, POOL_AVE, POOL_STOCHASTIC = 0, 1, 2
 
 

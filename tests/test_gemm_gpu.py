@@ -236,8 +236,9 @@ def test_fp8_conv_dgrad(gpu, case, fmt, tile, monkeypatch):
 # 4-wave tiles (19, 20: dense only): every operand
 # layout, ragged edges, short and long K (the phased DMA pipeline issues zero-page DMAs past
 # the last K-step), split-K, the bias-gradient column and the implicit-GEMM convolutions
-BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 40, 41]
-MC_B = {6, 7, 11, 12, 13, 40, 41}  # tiles with MC (k-strided) A and B operand instances
+# 23-28: the v_mfma_f32_32x32x16_bf16 twins of tiles 0, 10, 16, 13, 1, 11 (gemm_mf32.hip)
+BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 40, 41, 23, 24, 25, 26, 27, 28]
+MC_B = {6, 7, 11, 12, 13, 40, 41, 23, 24, 26, 27, 28}  # tiles with MC (k-strided) A and B operand instances
 
 
 @pytest.mark.parametrize("tile", BIG_TILES)
@@ -250,7 +251,7 @@ def test_gemm256_layouts(gpu, tile, M, N, K, monkeypatch):
     _close(G.linear_fwd(x, w, b, relu=True), torch.relu(x.float() @ w.float().t() + b))
     dy = _bf(M, N, device=gpu)
     w2 = _bf(N, K, device=gpu)
-    if tile in MC_B or tile in (16, 18, 19, 20):  # NN: MC B operand (192-row tiles: MC A excluded)
+    if tile in MC_B or tile in (16, 18, 19, 20, 25):  # NN: MC B operand (192-row tiles: MC A excluded)
         _close(G.linear_dgrad(dy, w2), dy.float() @ w2.float())
     if tile not in MC_B:
         return
