@@ -326,6 +326,20 @@ extern "C" int sn_pool_lrn_fwd(const bf16_t* x, bf16_t* pooled, uint8_t* mask, b
   return SN_CHECK_LAUNCH();
 }
 
+// Host probe for the Python eligibility check (ops.hip.pool_lrn_eligible): 1 when both
+// sn_pool_lrn_fwd and sn_lrn_pool_bwd accept the shape with the current environment's
+// backward tile (the same plrn_ok / plrn_bwd_tile / row-coverage tests they apply).
+extern "C" int sn_pool_lrn_supported(long long N, long long H, long long W, long long C, long long P, long long Q,
+                                     long long ph, long long pw, long long size) {
+  if (!plrn_ok(N, H, W, C, P, Q, ph, pw, size)) return 0;
+  const char* me = std::getenv("SN_PLRN_MASK_LDS");
+  const int item_bytes = (me ? std::atoi(me) != 0 : 1) ? 24 : 16;
+  const long long BH = (H + ph + 1) / 2, BW = (W + pw + 1) / 2;
+  int rows = 0, cg = 0;
+  if (!plrn_bwd_tile(N, Q, C, BH, item_bytes, &rows, &cg)) return 0;
+  return BH <= P + 1 && BW <= Q + 1 ? 1 : 0;
+}
+
 extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_t* mask, bf16_t* dx, long long N,
                                long long H, long long W, long long C, long long P, long long Q, long long ph,
                                long long pw, long long size, float alpha, float beta, float k, hipStream_t st) {

@@ -254,18 +254,30 @@ extern "C" int sn_solver_update(long long kind, float* w, const float* g, float*
   return SN_CHECK_LAUNCH();
 }
 
-// model averaging helper: w = w * scale, shadow = bf16(w)   (after an all-reduce SUM)
-__global__ void scale_shadow(float* __restrict__ w, bf16_t* __restrict__ shadow, long long n4, float scale) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+// model averaging / gradient averaging helper: w = w * scale, shadow = bf16(w) (after an
+// all-reduce SUM; shadow may be null).  16-B vectors over the aligned body, scalars for the
+// (< 4-element) tail, so any bucket boundary works.
+__global__ void scale_shadow(float* __restrict__ w, bf16_t* __restrict__ shadow, long long n, long long n4,
+                             float scale) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 v = reinterpret_cast<float4*>(w)[i];
     v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
     reinterpret_cast<float4*>(w)[i] = v;
     if (shadow) reinterpret_cast<uint2*>(shadow)[i] = make_uint2(pack2(v.x, v.y), pack2(v.z, v.w));
   }
+  for (long long i = 4 * n4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = w[i] * scale;
+    w[i] = v;
+    if (shadow) shadow[i] = f2bf(v);
+  }
 }
 
 extern "C" int sn_scale_shadow(float* w, bf16_t* shadow, long long n, float scale, hipStream_t st) {
-  if (n % 4) return 7;
-  hipLaunchKernelGGL(scale_shadow, dim3(sn_blocks(n / 4, 256, 16384)), dim3(256), 0, st, w, shadow, n / 4, scale);
+  if (n <= 0) return 0;
+  const bool vec = (reinterpret_cast<uintptr_t>(w) & 15) == 0 && (reinterpret_cast<uintptr_t>(shadow) & 7) == 0;
+  const long long n4 = vec ? n / 4 : 0;
+  hipLaunchKernelGGL(scale_shadow, dim3(sn_blocks(n4 > 0 ? n4 : n, 256, 16384)), dim3(256), 0, st, w, shadow, n, n4,
+                     scale);
   return SN_CHECK_LAUNCH();
 }

@@ -485,7 +485,7 @@ def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, 
                     dw2[g * s.Kg:(g + 1) * s.Kg].copy_(tmp[:s.Kg, :kred])
 
 
-FP8_WGRAD_BIAS = os.environ.get("SN_FP8_WGRAD_BIAS", "1") != "0"
+FP8_WGRAD_BIAS = os.environ.get("SN_FP8_WGRAD_BIAS", "0") == "1"  # exact bias gradient by default
 
 
 def fp8_wgrad_ok(s: ConvSpec) -> bool:
@@ -517,12 +517,14 @@ def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc):
     gradient (e4m3 / e5m2, MC: [pixels][K]), B = the implicit im2col of the layer input's
     e4m3 copy kept from the forward (MC), both read transposed from LDS by
     ds_read_b64_tr_b8; fp32 accumulation, split-K slabs, dequantised epilogue.  The bias
-    gradient stays an exact bf16 column sum (reference: base_conv_layer.cpp:338-376,
-    conv_layer.cu:35-53)."""
+    gradient is, by default, an exact column sum of the bf16 dy (a separate pass); with
+    SN_FP8_WGRAD_BIAS=1 it rides on the product as an e4m3 ones column instead, i.e. the
+    column sum of the QUANTISED dy, whose small entries are rounded or flushed (reference:
+    base_conv_layer.cpp:338-376, conv_layer.cu:35-53)."""
     sc, ix, xq, idy = f8w
-    # the bias gradient rides on the product as a virtual ones column of B (an e4m3 1.0,
-    # dequantised by dy's factor only): the column sum of the QUANTISED output gradient,
-    # instead of a separate bf16 pass over dy (SN_FP8_WGRAD_BIAS=0 keeps that pass)
+    # SN_FP8_WGRAD_BIAS=1: the bias gradient rides on the product as a virtual ones column of
+    # B (an e4m3 1.0, dequantised by dy's factor only) — the column sum of the QUANTISED
+    # output gradient — instead of the exact bf16 pass over dy (the default)
     fused_db = db is not None and kred % 16 == 0 and FP8_WGRAD_BIAS
     if db is not None and not fused_db:
         colsum(dy2, db, accumulate=db_acc)
@@ -847,8 +849,11 @@ def pool_lrn_eligible(s: PoolSpec, size: int, within: bool) -> bool:
         return False
     if s.ph >= 3 or s.pw >= 3 or s.N * s.H * s.W * s.C >= 1 << 32:
         return False
-    cv = s.C // 8  # backward tile (pool_lrn.hip plrn_bwd_tile): two pooled rows of a 128-B group fit 32 KB
-    return 2 * s.Q * 16 * min(cv, 8) <= 32 * 1024 and (s.H + s.ph + 1) // 2 <= s.P + 1 and (s.W + s.pw + 1) // 2 <= s.Q + 1
+    # the kernels' own host tests (plrn_ok, the backward tile search of plrn_bwd_tile with the
+    # LDS-staged mask's 24-B items and >= 4-chunk groups, row coverage): one source of truth
+    fn = _lib.kernels().sn_pool_lrn_supported
+    fn.restype = C.c_int
+    return bool(fn(*(C.c_longlong(v) for v in (s.N, s.H, s.W, s.C, s.P, s.Q, s.ph, s.pw, size))))
 
 
 def pool_lrn_forward(x, s: PoolSpec, gate: bool, size: int, alpha: float, beta: float, k: float):

@@ -35,6 +35,18 @@ AVERAGE_BUCKET_BYTES = 64 << 20
 WATCHDOG_EXIT_CODE = 75
 
 
+
+def _scale(flat: torch.Tensor, shadow, scale: float) -> None:
+    """flat *= scale (and refresh its bf16 shadow): the HIP scale kernel on device
+    buffers (one pass, vectorised, graph-capturable), plain in-place on host buffers."""
+    if flat.is_cuda:
+        from ..ops import hip
+        hip.scale_shadow(flat, shadow, scale)
+    else:
+        flat.mul_(scale)
+        if shadow is not None:
+            shadow.copy_(flat)
+
 class Watchdog:
     """Fail-fast rank monitor (the reference fails the whole Spark job on the
     first task failure, spark.task.maxFailures=1, src/main/scala/apps/CifarApp.scala:30).
@@ -183,11 +195,7 @@ class Comm:
         for (s, e), ws in zip(ranges, works):
             for w in ws:
                 w.wait()
-            if cuda:
-                from ..ops import hip
-                hip.scale_shadow(flat[s:e], shadow[s:e] if shadow is not None else None, scale)
-            else:
-                flat[s:e].mul_(scale)
+            _scale(flat[s:e], shadow[s:e] if shadow is not None else None, scale)
         if not cuda:
             net.sync_compute()
         return t
@@ -198,7 +206,7 @@ class Comm:
             return
         self.allreduce_sum(net.flat_diff)
         if average:
-            net.flat_diff.mul_(1.0 / self.world_size)
+            _scale(net.flat_diff, None, 1.0 / self.world_size)
 
     def allreduce_scores(self, scores: list[float], device=None) -> list[float]:
         if self.world_size == 1:
@@ -322,4 +330,4 @@ class SyncSGDCallback:
         self.works = []
         for s, e in self.late:
             dist.all_reduce(self.net.flat_diff[s:e], op=dist.ReduceOp.SUM)
-        self.net.flat_diff.mul_(1.0 / self.comm.world_size)
+        _scale(self.net.flat_diff, None, 1.0 / self.comm.world_size)

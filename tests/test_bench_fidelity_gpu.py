@@ -1,0 +1,156 @@
+"""Correctness gate at the HEADLINE bench's exact configuration.
+
+bench.py's CaffeNet step: the packaged prototxt at per-GPU batch 256, crop 227, 1000 outputs,
+fused ReLU epilogues, the augment kernel writing conv1's space-to-depth-folded input, the
+InnerProduct SGD updates inside the weight-gradient GEMMs (EPI_SGD), Dropout inside the fc6 /
+fc7 epilogues, and the tuned GEMM database's tiles / split-K factors (e.g. fc6 forward split 8,
+conv1's folded weight gradient split 109) — fed a learnable uint8 set instead of noise so the
+loss moves.  The reference is the fp32 CPU engine from the same initial weights, fed the same
+batches, cropped / mirrored / dropped by the same Philox draws.
+
+* one iteration: every layer's weight and bias UPDATE (w1 - w0, i.e. -lr x gradient at zero
+  momentum history) within 2 % of the layer's largest fp32 update;
+* the production hipGraph path for 20 steps: its per-iteration losses track the fp32 engine
+  within 4 % over the iterations both ran, and the loss falls;
+* the gate has teeth: with conv1's weight-gradient product made to drop half its reduction
+  (a simulated split-K bug) the update check fails.
+
+Reference: caffe/src/caffe/test/test_gradient_based_solver.cpp:225-320 (update of one
+iteration vs a reference computed independently)."""
+import math
+
+import pytest
+import torch
+
+from sparknet_amd import models
+
+pytestmark = pytest.mark.gpu
+
+B, SRC, CLASSES = 256, 256, 10
+MEAN = [104.0, 117.0, 123.0]
+
+
+def _data(n=2 * B, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    y = torch.randint(0, CLASSES, (n,), generator=g)
+    yy, xx = torch.meshgrid(torch.arange(float(SRC)), torch.arange(float(SRC)), indexing="ij")
+    imgs = torch.empty(n, 3, SRC, SRC)
+    for c in range(CLASSES):
+        idx = (y == c).nonzero().flatten()
+        th = math.pi * c / CLASSES
+        stripes = 50.0 * torch.sin(2 * math.pi * 6 * (xx * math.cos(th) + yy * math.sin(th)) / SRC)
+        for ch in range(3):
+            imgs[idx, ch] = 128 + 60 * math.cos(2 * math.pi * c / CLASSES + 2.1 * ch) + stripes
+    imgs += torch.randn(imgs.shape, generator=g) * 12
+    return imgs.clamp(0, 255).to(torch.uint8), y.int()
+
+
+def _solver_param():
+    return models.solver_for("caffenet", train_batch=B, test_batch=50, crop=227)  # bench.py's config
+
+
+def _trainer(dev, w0, x, y, graph):
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.data.prefetch import DeviceFeeder, TensorSource
+    from sparknet_amd.engine import LocalSGDTrainer, fuse_fc_updates, fuse_input_fold, fuse_relu
+    solver = Solver(_solver_param(), device=dev, seed=1701, build_test_nets=False)
+    net = solver.net
+    net.flat_data.copy_(w0.to(net.flat_data.device))
+    net.sync_compute()
+    cuda = dev.type == "cuda"
+    if cuda:
+        fuse_relu(net)
+    feeder = DeviceFeeder(TensorSource(x, y, B, pin=cuda), net.blob_by_name("data"), net.blob_by_name("label"),
+                          crop=227, mean=MEAN, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev,
+                          group=2 if cuda else 1)
+    if cuda:
+        assert fuse_input_fold(net, feeder)
+    tr = LocalSGDTrainer(solver, None, tau=1000, feeder=feeder, use_graph=graph)
+    if cuda and not graph:
+        assert fuse_fc_updates(solver) > 0  # the eager step runs the graph's EPI_SGD kernels
+    return tr, solver
+
+
+def _initial_weights():
+    from sparknet_amd.core.solver import Solver
+    return Solver(_solver_param(), device=torch.device("cpu"), seed=1701,
+                  build_test_nets=False).net.flat_data.detach().clone()
+
+
+def _updates(solver, w0):
+    """{layer/param: w1 - w0} of every learnable parameter after the iterations run."""
+    w1 = solver.net.flat_data.detach().float().cpu()
+    out = {}
+    for li, layer in enumerate(solver.net.layers):
+        for pi, p in enumerate(layer.params):
+            if p.owner is None and p.count:
+                out[f"{layer.name}/{pi}"] = (w1[p.offset:p.offset + p.count] - w0[p.offset:p.offset + p.count])
+    return out
+
+
+def _one_step_updates(dev, w0, x, y):
+    tr, solver = _trainer(dev, w0, x, y, graph=False)
+    tr.local_step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    return _updates(solver, w0)
+
+
+def _worst(ug, uc):
+    worst = ("", 0.0)
+    for k, c in uc.items():
+        e = float((ug[k] - c).abs().max() / (c.abs().max() + 1e-12))
+        if e > worst[1]:
+            worst = (k, e)
+    return worst
+
+
+@pytest.fixture(scope="module")
+def fixture_data():
+    x, y = _data()
+    w0 = _initial_weights()
+    uc = _one_step_updates(torch.device("cpu"), w0, x, y)
+    return x, y, w0, uc
+
+
+@pytest.mark.timeout(900)
+def test_bench_config_one_step_updates_match_fp32(gpu, fixture_data):
+    x, y, w0, uc = fixture_data
+    ug = _one_step_updates(torch.device(gpu), w0, x, y)
+    assert ug.keys() == uc.keys() and len(uc) == 16  # 8 learnable layers x (weight, bias)
+    name, err = _worst(ug, uc)
+    assert err <= 0.02, (name, err)
+
+
+@pytest.mark.timeout(900)
+def test_bench_config_gate_catches_a_broken_wgrad(gpu, fixture_data, monkeypatch):
+    """Half of conv1's weight-gradient reduction dropped (split-K chunks past the middle
+    skipped) must fail the 2 % update gate."""
+    from sparknet_amd.ops import gemm as G
+    x, y, w0, uc = fixture_data
+    orig = G._launch
+
+    def broken(M, N, K, *a, **k):
+        if M == 96 and K >= 500000:  # conv1's folded weight gradient: 96 x 433 x 774400
+            K = K // 2
+        return orig(M, N, K, *a, **k)
+    monkeypatch.setattr(G, "_launch", broken)
+    ug = _one_step_updates(torch.device(gpu), w0, x, y)
+    name, err = _worst(ug, uc)
+    assert name.startswith("conv1") and err > 0.02, (name, err)
+
+
+@pytest.mark.timeout(900)
+def test_bench_config_graph_losses_track_fp32(gpu, fixture_data):
+    x, y, w0, _ = fixture_data
+    tr, solver = _trainer(torch.device(gpu), w0, x, y, graph=True)
+    assert tr.step_fn is not None
+    gl = [float(tr.local_step())]  # capture call: iterations 0..2, the loss of iteration 2
+    while solver.iter < 20:
+        gl.append(float(tr.local_step()))
+    torch.cuda.synchronize()
+    trc, sc = _trainer(torch.device("cpu"), w0, x, y, graph=False)
+    cl = [float(trc.local_step()) for _ in range(8)]
+    for i, c in enumerate(cl[2:]):  # GPU list index 0 = iteration 2
+        assert abs(gl[i] - c) <= 0.04 * max(1.0, abs(c)), (i + 2, gl[i], c, gl, cl)
+    assert sum(gl[-5:]) < sum(gl[:5]), gl

@@ -88,3 +88,25 @@ def test_caffenet_step_fused_equals_unfused(gpu):
         results.append((losses, net.flat_data.detach().clone()))
     assert results[0][0] == results[1][0]
     assert torch.equal(results[0][1], results[1][1])
+
+
+@pytest.mark.parametrize("case", [(1, 200, 200, 56, 0, 5), (1, 260, 260, 56, 0, 3), (2, 27, 27, 56, 0, 5)])
+def test_pool_lrn_eligibility_matches_kernels(gpu, case):
+    """the Python eligibility check mirrors the kernels' own host tests (prime
+    channel-chunk counts such as C = 56, cv = 7, at wide pooled rows), so every shape it
+    accepts launches, and every shape it refuses takes the unfused path without error."""
+    from sparknet_amd.ops import hip
+    N, H, W, C, pad, size = case
+    s = PoolSpec(N, H, W, C, 3, 3, 2, 2, pad, pad)
+    alpha, beta, k = 1e-4, 0.75, 1.0
+    x = _inputs(N, H, W, C, 3).to(gpu)
+    p_ref, m_ref = hip.pool_forward_mask(x, s, False)
+    dy = _inputs(N, s.P, s.Q, C, 4).to(gpu)
+    dp = hip.lrn_backward(dy, p_ref, size, alpha, beta, k)
+    dx_ref = hip.pool_backward(dp, x, s, m_ref)
+    if hip.pool_lrn_eligible(s, size, False):
+        pooled, mask, y = hip.pool_lrn_forward(x, s, False, size, alpha, beta, k)
+        assert torch.equal(hip.lrn_pool_backward(dy, pooled, mask, s, size, alpha, beta, k), dx_ref)
+    else:
+        with pytest.raises(RuntimeError):
+            hip.lrn_pool_backward(dy, p_ref, m_ref, s, size, alpha, beta, k)
