@@ -11,9 +11,14 @@ above bf16alt: a known limitation at that rate).  At lr 0.002 the trajectory is 
 (bf16alt floor 0.046 with the tuned tiles); fp8 fwd + dgrad + wgrad learns measurably slower in
 the last windows, where the loss falls fastest: max deviation 0.160 with the tuned tiles
 (0.066 with every GEMM on the cost-model tile; e5m2 gradients 0.12; lr 0.001: 0.028 / 0.046,
-profiles/r4_fp8_lr_sweep.txt).  The test runs at lr 0.002 and asserts every 20-step smoothed fp8
-loss within max(0.2, 2 x the bf16-vs-bf16alt floor) of bf16 — not the 0.15 asked for — and fp8
-ending below its starting loss.  The floor and the fp8 deviation are printed (pytest -s).
+profiles/r4_fp8_lr_sweep.txt).  Round 5 A/B'd the components one at a time on the
+test's own trajectories (profiles/r5_fp8_fidelity_ab.txt, lr 0.002, floor 0.023): fwd + dgrad
++ wgrad 0.125, without fp8 weight gradients 0.087, with the e4m3 bias column 0.112, without the
+amax history 0.114 — no single component carries the gap (e4m3's 3 mantissa bits make fp8 learn a
+little slower in the fastest-falling windows), and the production mode meets the original gate.
+The test runs at lr 0.002 and asserts every 20-step smoothed fp8 loss within
+max(0.15, 1.5 x the bf16-vs-bf16alt floor) of bf16 (the round-3 gate, restored) and fp8 ending
+below its starting loss.  The floor and the fp8 deviation are printed (pytest -s).
 
 The data is a learnable synthetic task (no datasets on the box): 10 fixed random class
 templates plus Gaussian noise (scripts/fp8_trajectory.py), so the loss falls from ln(10).
@@ -68,7 +73,7 @@ def test_fp8_vgg16_200_steps_tracks_bf16(gpu, monkeypatch):
     sb, sa, s8 = _smooth(bf), _smooth(alt), _smooth(f8)
     floor = max(abs(a - b) for a, b in zip(sb, sa))
     dev = max(abs(a - b) for a, b in zip(sb, s8))
-    bound = max(0.2, 2.0 * floor)
+    bound = max(0.15, 1.5 * floor)
     print("bf16   ", [round(v, 3) for v in sb], "\nbf16alt", [round(v, 3) for v in sa],
           "\nfp8    ", [round(v, 3) for v in s8], f"\nchaos floor {floor:.3f}  fp8 max dev {dev:.3f}  bound {bound:.3f}")
     assert all(v == v for v in f8), "fp8 loss went non-finite"
