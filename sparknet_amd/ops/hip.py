@@ -361,7 +361,18 @@ def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
 
 
 def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
-                  dw_acc=True, db_acc=True):
+                  dw_acc=True, db_acc=True, dx_out=None):
+    """``dx_out``: write the data gradient there — contiguous, or a channel slice of a wider
+    NHWC buffer (engine.fuse_siblings: the merged sibling gradient), which the stride-1
+    implicit dgrad writes in place (ldc = the slice's pixel stride)."""
+    if dx_out is not None and need_dx:
+        if chan_stride(dx_out) == s.C or (_implicit_ok(s) and s.sh == s.sw == 1 and s.dh == s.dw == 1
+                                          and s.Kg % 8 == 0 and chan_stride(dx_out) and _image_chunk(s) >= s.N
+                                          and not (ws and ("fp8_dgrad" in ws or "fp8_dx_side" in ws))):
+            return _conv_backward_chunked(dy, x, w, s, need_dx, dw, db, gate, ws, dw_acc, db_acc, dx_out)
+        dx = conv_backward(dy, x, w, s, need_dx, dw, db, gate, ws, dw_acc, db_acc)
+        dx_out.copy_(dx)
+        return dx_out
     side_req = ws.pop("fp8_dx_side", None) if ws else None
     if side_req is not None and need_dx:
         # the data-gradient GEMM epilogue also stores dx as fp8 for the layer below's fp8 data
@@ -538,7 +549,8 @@ def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc):
 def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
     ldd, ldx = ldd or s.K, ldx or s.C
     dx = dx_out if dx_out is not None else torch.empty((s.N, s.H, s.W, s.C), dtype=BF16, device=x.device)
-    if gate is not None and ldx != s.C:  # the gate (= x, a channel slice) must share dx's layout
+    ldo = chan_stride(dx)  # C, or the pitch of a channel-slice destination (conv_backward dx_out)
+    if gate is not None and chan_stride(gate) != ldo:  # the gate (= x) must share dx's layout
         gate = _c(gate)
     if s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0:
         # dgrad == forward conv of dy with flipped / transposed weights, pad' = R-1-pad.
@@ -569,8 +581,8 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
                 wt = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
                 call("flip_weights", _c(w), wt, s.groups, s.Kg, s.R, s.S, s.Cg)
             B = Dense(wt.view(s.C, kr2), kr2, True, gstride=s.Cg * kr2)
-        gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, s.C, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg,
-             gate=_c(gate) if gate is not None else None)
+        gemm(s.N * s.H * s.W, s.Cg, kr2, A, B, dx, ldo, epi=EPI_BF16, groups=s.groups, c_gstride=s.Cg,
+             gate=gate)
         return dx
     # generic: dcol = dy_g @ W_g, then col2im (gather, no atomics)
     assert ldd == s.K
@@ -1088,6 +1100,21 @@ def solver_update(kind, data, diff, history, compute, tables, hyper, l1, clip, g
     call("solver_update", int(kind), data, diff, h0, h1, compute, tables["pos"], tables["mult"], tables["n"],
          hyper, int(l1), int(clip), tables["part"], tables["part"].numel(), tables["total"], int(grid_limit),
          tables.get("src"))
+
+
+def copy_segments(segs) -> None:
+    """One launch for up to 8 (src, dst, accumulate) tensor copies (csrc/kernels/segcopy.hip):
+    contiguous bf16 / fp32 tensors of equal element counts, converting between the two and
+    optionally adding into dst."""
+    rows = []
+    for src, dst, acc in segs:
+        assert src.is_contiguous() and dst.is_contiguous() and src.numel() == dst.numel()
+        rows.append((src.data_ptr(), dst.data_ptr(), src.numel(), int(src.dtype == torch.float32),
+                     int(dst.dtype == torch.float32), int(acc)))
+    for i in range(0, len(rows), 8):
+        chunk = [v for r in rows[i:i + 8] for v in r]
+        arr = (C.c_longlong * len(chunk))(*chunk)
+        call("copy_segments", arr, len(chunk) // 6)
 
 
 def scale_shadow(flat, shadow, scale: float):

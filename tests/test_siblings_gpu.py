@@ -1,0 +1,117 @@
+"""Merged Inception sibling convolutions (engine.fuse_siblings): the 3x3_reduce / 5x5_reduce
+pair of every GoogLeNet module runs as one forward GEMM, one weight-gradient GEMM and one
+data-gradient GEMM, the 3x3 / 5x5 consumers read channel slices of the merged output and
+write their data gradients into slices of the merged gradient, and the Split drops the
+follower from its sum.  Checked against the unmerged engine from identical weights and
+batches: losses, and every parameter update of a step (eager; and the 4-stream hipGraph
+path, whose branch-stream plan must carry the group's extra dependencies)."""
+import os
+
+import pytest
+import torch
+
+from sparknet_amd import models
+
+pytestmark = pytest.mark.gpu
+
+B = 8
+
+
+def _solver(dev, w0, merged, monkeypatch):
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.engine import fuse_relu, fuse_siblings
+    monkeypatch.setenv("SN_FUSE_SIBLINGS", "1" if merged else "0")
+    sp = models.solver_for("googlenet", train_batch=B, test_batch=B, crop=224)
+    solver = Solver(sp, device=dev, seed=3, build_test_nets=False)
+    net = solver.net
+    net.flat_data.copy_(w0.to(dev))
+    net.sync_compute()
+    fuse_relu(net)
+    groups = sum(1 for l in net.layers if getattr(l, "sibling", None) is not None and l.sibling[1] == 0)
+    return solver, groups
+
+
+def _batches(n):
+    g = torch.Generator().manual_seed(7)
+    return [(torch.randn(B, 3, 224, 224, generator=g) * 40, torch.randint(0, 1000, (B, 1), generator=g).float())
+            for _ in range(n)]
+
+
+def _w0():
+    from sparknet_amd.core.solver import Solver
+    sp = models.solver_for("googlenet", train_batch=B, test_batch=B, crop=224)
+    return Solver(sp, device=torch.device("cpu"), seed=3, build_test_nets=False).net.flat_data.detach().clone()
+
+
+def _close(a, b, tol):
+    err = float((a - b).abs().max() / (b.abs().max() + 1e-12))
+    assert err < tol, err
+
+
+def _per_param(solver, delta):
+    out = {}
+    for layer in solver.net.layers:
+        for pi, p in enumerate(layer.params):
+            if p.owner is None and p.count:
+                out[f"{layer.name}/{pi}"] = delta[p.offset:p.offset + p.count]
+    return out
+
+
+def test_googlenet_siblings_merged_step_matches_unmerged(gpu, monkeypatch):
+    """One step: loss, and every parameter's update against its own largest update (the
+    merged data gradient sums the siblings in fp32 where the unmerged Split sums bf16 terms,
+    so the two are close, not bitwise)."""
+    w0 = _w0()
+    (xb, yb), = _batches(1)
+    res = {}
+    for merged in (False, True):
+        solver, groups = _solver(gpu, w0, merged, monkeypatch)
+        assert groups == (9 if merged else 0)
+        net = solver.net
+        net.blob_by_name("data").set_nchw(xb)
+        net.blob_by_name("label").set_nchw(yb)
+        solver.stage_hyper()
+        loss = float(solver.iteration())
+        torch.cuda.synchronize()
+        res[merged] = (loss, _per_param(solver, net.flat_data.detach().float().cpu() - w0))
+    assert abs(res[True][0] - res[False][0]) <= 1e-3 * max(1.0, abs(res[False][0]))
+    errs = sorted(((float((res[True][1][k] - v).abs().max() / (v.abs().max() + 1e-12)), k)
+                   for k, v in res[False][1].items()), reverse=True)
+    print("worst per-parameter update errors:", [(k, round(e, 4)) for e, k in errs[:8]])
+    assert errs[0][0] < 2e-2, errs[:8]
+
+
+def test_googlenet_siblings_graph_streams(gpu, monkeypatch):
+    """The production path (GraphStep, 4 branch streams in the star topology) with merged
+    siblings tracks the eager merged step."""
+    from sparknet_amd.engine import GraphStep
+    w0 = _w0()
+    batches = _batches(6)
+    out = {}
+    for graph in (False, True):
+        solver, groups = _solver(gpu, w0, True, monkeypatch)
+        assert groups == 9
+        net = solver.net
+        it = iter(range(10 ** 6))
+
+        def pre():
+            xb, yb = batches[next(it) % len(batches)]
+            net.blob_by_name("data").set_nchw(xb)
+            net.blob_by_name("label").set_nchw(yb)
+        if graph:
+            st = GraphStep(solver, warmup=2, pre=pre, overlap=False, streams=4)
+            losses = [float(st.step())]  # iterations 0..2
+            while solver.iter < 6:
+                losses.append(float(st.step()))
+            losses = [None, None] + losses
+        else:
+            losses = []
+            for _ in range(6):
+                pre()
+                solver.stage_hyper()
+                losses.append(float(solver.iteration()))
+                solver.iter += 1
+        torch.cuda.synchronize()
+        out[graph] = losses
+    for a, b in zip(out[True][2:], out[False][2:]):
+        assert a == a and abs(a - b) <= 2e-2 * max(1.0, abs(b)), (out[True], out[False])
