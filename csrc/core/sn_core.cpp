@@ -383,10 +383,39 @@ struct NativeWeights {
 // Per-state native plans.  A plan that could not be built (CPU state, data layers fed
 // from Python, solver features the graph cannot hold) is remembered as such until the
 // state changes, so an ineligible state costs one Python call, not one per verb.
+// Captured backward of the train net (CoreState.backward_plan): sn_backward replays it.
+struct NativeBackward {
+  hipGraphExec_t exec = nullptr;
+  hipStream_t stream = nullptr;
+};
+
+// One activation blob (CoreState.blob_table) for the native sn_blob_* verbs on layer < 0:
+// device data / gradient pointers (graph-owned memory of the forward / backward plans),
+// bf16 or fp32, 4-D image blobs stored NHWC (logical NCHW dims).
+struct BlobDesc {
+  void* data = nullptr;
+  void* diff = nullptr;
+  int f32 = 0, image = 0, ndim = 0;
+  int dims[6] = {1, 1, 1, 1, 1, 1};
+  long long count = 1;
+};
+
+// Layer / blob names and counts (CoreState.meta_plan), read once per loaded net.
+struct NativeMeta {
+  std::vector<std::string> layers, blobs;
+  std::vector<int> weights;
+  int outputs = 0;
+};
+
 struct NativeState {
   std::unique_ptr<NativeStep> step;
   std::unique_ptr<NativeForward> fwd[2];  // [0] train net (sn_forward), [1] test net
   std::unique_ptr<NativeWeights> weights;
+  std::unique_ptr<NativeBackward> bwd;
+  std::vector<BlobDesc> blobs;  // from the train forward plan; gradients from the backward plan
+  std::unique_ptr<NativeMeta> meta;
+  bool bwd_failed = false, meta_failed = false;
+  std::vector<uint16_t> blob_stage;
   bool step_failed = false, fwd_failed[2] = {false, false}, weights_failed = false;
   std::vector<float> scores;  // last native sn_solver_test
   bool scores_native = false, scores_pending = false;
@@ -557,6 +586,29 @@ int native_iteration(NativeStep& ns) {
 }
 
 // The forward executor of the train (test = 0) or test (1) net, if built.
+// Parse CoreState.blob_table rows into BlobDesc (GIL held).
+bool parse_blobs(PyObject* rows, std::vector<BlobDesc>& out) {
+  out.clear();
+  if (!rows || !PyList_Check(rows)) return false;
+  for (Py_ssize_t i = 0; i < PyList_Size(rows); ++i) {
+    PyObject* r = PyList_GetItem(rows, i);
+    if (!PyTuple_Check(r) || PyTuple_Size(r) != 11) return false;
+    auto at = [&](int k) { return PyLong_AsLongLong(PyTuple_GetItem(r, k)); };
+    BlobDesc b;
+    b.data = (void*)(uintptr_t)at(0);
+    b.diff = (void*)(uintptr_t)at(1);
+    b.f32 = (int)at(2);
+    b.image = (int)at(3);
+    b.ndim = (int)at(4);
+    for (int d = 0; d < 6; ++d) {
+      b.dims[d] = (int)at(5 + d);
+      if (d < b.ndim) b.count *= b.dims[d];
+    }
+    out.push_back(b);
+  }
+  return !PyErr_Occurred();
+}
+
 NativeForward* native_forward(void* s, int test) {
   NativeState* st = find_native(s);
   return st && native_enabled() ? st->fwd[test].get() : nullptr;
@@ -578,6 +630,11 @@ void build_forward(void* s, int test) {
   nf->acc_dev = (float*)(uintptr_t)dict_ll(d, "acc_dev");
   nf->n_out = (int)dict_ll(d, "n_out");
   const bool fed = nf->feeds.build(PyDict_GetItemString(d, "feeds"));
+  if (!test) {
+    if (!parse_blobs(PyDict_GetItemString(d, "blobs"), st.blobs)) st.blobs.clear();
+    st.bwd.reset();  // it read the blobs this capture rebound
+    st.bwd_failed = false;
+  }
   Py_DECREF(d);
   if (PyErr_Occurred()) {
     fetch_error("forward_plan");
@@ -586,6 +643,136 @@ void build_forward(void* s, int test) {
   if (!fed || hipHostMalloc((void**)&nf->out_host, sizeof(float) * (1 + nf->n_out), 0) != hipSuccess) return;
   st.fwd_failed[test] = false;
   st.fwd[test] = std::move(nf);
+}
+
+NativeBackward* native_backward(void* s) {
+  NativeState* st = find_native(s);
+  return st && native_enabled() && st->fwd[0] ? st->bwd.get() : nullptr;
+}
+
+// Build it right after the Python verb ran a backward (GIL held), on top of the train
+// forward plan whose graph memory the blobs are bound to.
+void build_backward(void* s) {
+  if (!native_enabled()) return;
+  NativeState& st = native_state(s);
+  if (!st.fwd[0] || st.bwd || st.bwd_failed) return;
+  st.bwd_failed = true;
+  PyObject* d = call_quiet(s, "backward_plan", nullptr);
+  if (!d) return;
+  auto nb = std::make_unique<NativeBackward>();
+  nb->exec = (hipGraphExec_t)(uintptr_t)dict_ll(d, "exec");
+  nb->stream = (hipStream_t)(uintptr_t)dict_ll(d, "stream");
+  std::vector<BlobDesc> blobs;
+  const bool ok = parse_blobs(PyDict_GetItemString(d, "blobs"), blobs);
+  Py_DECREF(d);
+  if (PyErr_Occurred()) {
+    fetch_error("backward_plan");
+    return;
+  }
+  if (!ok || !nb->exec) return;
+  st.blobs = std::move(blobs);
+  st.bwd_failed = false;
+  st.bwd = std::move(nb);
+}
+
+NativeMeta* native_meta(void* s) {
+  if (!native_enabled()) return nullptr;
+  NativeState& st = native_state(s);
+  if (st.meta) return st.meta.get();
+  if (st.meta_failed) return nullptr;
+  Gil g;
+  st.meta_failed = true;
+  PyObject* d = call_quiet(s, "meta_plan", nullptr);
+  if (!d) return nullptr;
+  auto m = std::make_unique<NativeMeta>();
+  auto strs = [](PyObject* l, std::vector<std::string>& out) {
+    if (!l || !PyList_Check(l)) return false;
+    for (Py_ssize_t i = 0; i < PyList_Size(l); ++i) {
+      const char* c = PyUnicode_AsUTF8(PyList_GetItem(l, i));
+      if (!c) return false;
+      out.emplace_back(c);
+    }
+    return true;
+  };
+  bool ok = strs(PyDict_GetItemString(d, "layers"), m->layers) && strs(PyDict_GetItemString(d, "blobs"), m->blobs);
+  PyObject* w = PyDict_GetItemString(d, "weights");
+  ok = ok && w && PyList_Check(w);
+  for (Py_ssize_t i = 0; ok && i < PyList_Size(w); ++i) m->weights.push_back((int)PyLong_AsLong(PyList_GetItem(w, i)));
+  m->outputs = (int)dict_ll(d, "outputs");
+  Py_DECREF(d);
+  if (PyErr_Occurred() || !ok) {
+    PyErr_Clear();
+    return nullptr;
+  }
+  st.meta_failed = false;
+  st.meta = std::move(m);
+  return st.meta.get();
+}
+
+// The activation blob `index` with a native pointer for data (diff = 0) or gradient (1).
+const BlobDesc* native_blob(void* s, int index, int diff, hipStream_t* stream) {
+  NativeState* st = find_native(s);
+  if (!st || !native_enabled() || !st->fwd[0] || index < 0 || index >= (int)st->blobs.size()) return nullptr;
+  const BlobDesc& b = st->blobs[(size_t)index];
+  if (!(diff ? b.diff : b.data)) return nullptr;
+  if (diff && !st->bwd) return nullptr;
+  *stream = st->fwd[0]->stream;
+  return &b;
+}
+
+// logical (NCHW) element index -> storage index of an NHWC image blob
+inline long long nhwc_index(const BlobDesc& b, long long i) {
+  const long long W = b.dims[3], H = b.dims[2], Cc = b.dims[1];
+  const long long w = i % W, h = (i / W) % H, c = (i / (W * H)) % Cc, n = i / (W * H * Cc);
+  return ((n * H + h) * W + w) * Cc + c;
+}
+
+int blob_get_native(NativeState& st, const BlobDesc& b, hipStream_t stream, int diff, float* out, long long n) {
+  if (!out || n < b.count) {
+    g_err = "sn_blob_get: buffer smaller than the blob";
+    return 1;
+  }
+  const void* src = diff ? b.diff : b.data;
+  const size_t es = b.f32 ? 4 : 2;
+  st.blob_stage.resize((size_t)(b.count * es + 1) / 2);
+  void* tmp = st.blob_stage.data();
+  HIPOK(hipMemcpyAsync(tmp, src, es * b.count, hipMemcpyDeviceToHost, stream));
+  HIPOK(hipStreamSynchronize(stream));
+  for (long long i = 0; i < b.count; ++i) {
+    const long long j = b.image ? nhwc_index(b, i) : i;
+    if (b.f32) {
+      out[i] = static_cast<const float*>(tmp)[j];
+    } else {
+      const uint32_t u = (uint32_t)static_cast<const uint16_t*>(tmp)[j] << 16;
+      std::memcpy(&out[i], &u, 4);
+    }
+  }
+  return 0;
+}
+
+int blob_set_native(NativeState& st, const BlobDesc& b, hipStream_t stream, int diff, const float* in, long long n) {
+  if (!in || n < b.count) {
+    g_err = "sn_blob_set: buffer smaller than the blob";
+    return 1;
+  }
+  void* dst = diff ? b.diff : b.data;
+  const size_t es = b.f32 ? 4 : 2;
+  st.blob_stage.resize((size_t)(b.count * es + 1) / 2);
+  void* tmp = st.blob_stage.data();
+  for (long long i = 0; i < b.count; ++i) {
+    const long long j = b.image ? nhwc_index(b, i) : i;
+    if (b.f32) {
+      static_cast<float*>(tmp)[j] = in[i];
+    } else {  // round to nearest even, as the device casts
+      uint32_t u;
+      std::memcpy(&u, &in[i], 4);
+      const uint32_t r = ((u >> 16) & 1u) + 0x7fffu;
+      static_cast<uint16_t*>(tmp)[j] = (uint16_t)((u + r) >> 16);
+    }
+  }
+  HIPOK(hipMemcpyAsync(dst, tmp, es * b.count, hipMemcpyHostToDevice, stream));
+  HIPOK(hipStreamSynchronize(stream));
+  return 0;
 }
 
 NativeWeights* native_weights(void* s) {
@@ -644,13 +831,18 @@ NativeWeights* native_weights(void* s) {
 }
 
 // Forget the plans that depend on what a verb is about to change.
-enum : unsigned { P_STEP = 1, P_FWD_TRAIN = 2, P_FWD_TEST = 4, P_WEIGHTS = 8, P_SCORES = 16 };
+enum : unsigned { P_STEP = 1, P_FWD_TRAIN = 2, P_FWD_TEST = 4, P_WEIGHTS = 8, P_SCORES = 16, P_META = 32 };
 
 void invalidate(void* s, unsigned what) {
   NativeState* st = find_native(s);
   if (!st) return;
   if (what & P_STEP) st->step.reset(), st->step_failed = false;
-  if (what & P_FWD_TRAIN) st->fwd[0].reset(), st->fwd_failed[0] = false;
+  if (what & P_FWD_TRAIN) {  // the backward plan and the blob table hang off the forward plan
+    st->fwd[0].reset(), st->fwd_failed[0] = false;
+    st->bwd.reset(), st->bwd_failed = false;
+    st->blobs.clear();
+  }
+  if (what & P_META) st->meta.reset(), st->meta_failed = false;
   if (what & P_FWD_TEST) st->fwd[1].reset(), st->fwd_failed[1] = false;
   if (what & P_WEIGHTS) st->weights.reset(), st->weights_failed = false;
   if (what & P_SCORES) st->scores_native = st->scores_pending = false;
@@ -776,7 +968,7 @@ int sn_load_solver_from_protobuf(void* s, const char* bytes, int len) {
 int sn_load_net_from_protobuf(void* s, const char* bytes, int len) {
   Gil g;
   sync_python(s);
-  invalidate(s, P_FWD_TRAIN | P_FWD_TEST | P_WEIGHTS | P_SCORES);
+  invalidate(s, P_FWD_TRAIN | P_FWD_TEST | P_WEIGHTS | P_SCORES | P_META);
   return status(call(s, "load_net", "(y#)", bytes, (Py_ssize_t)len));
 }
 
@@ -827,8 +1019,19 @@ int sn_forward(void* s, float* loss) {
 }
 
 int sn_backward(void* s) {
+  if (!s) {
+    g_err = "null state";
+    return 1;
+  }
+  if (NativeBackward* nb = native_backward(s)) {
+    HIPOK(hipGraphLaunch(nb->exec, nb->stream));
+    HIPOK(hipStreamSynchronize(nb->stream));
+    return 0;
+  }
   Gil g;
-  return status(call(s, "backward", nullptr));
+  const int rc = status(call(s, "backward", nullptr));
+  if (rc == 0) build_backward(s);
+  return rc;
 }
 
 int sn_solver_step(void* s, int iters) {
@@ -1025,6 +1228,7 @@ int sn_restore_solver_from_file(void* s, const char* path) {
 }
 
 int sn_num_layers(void* s) {
+  if (NativeMeta* m = native_meta(s)) return (int)m->layers.size();
   Gil g;
   PyObject* r = call(s, "layer_names", nullptr);
   if (!r) return -1;
@@ -1033,7 +1237,16 @@ int sn_num_layers(void* s) {
   return n;
 }
 
+int copy_name(const std::string& v, char* buf, int buflen) {
+  if (!buf || buflen <= 0) return 1;
+  std::strncpy(buf, v.c_str(), (size_t)buflen - 1);
+  buf[buflen - 1] = 0;
+  return 0;
+}
+
 int sn_layer_name(void* s, int index, char* buf, int buflen) {
+  if (NativeMeta* m = native_meta(s))
+    return index >= 0 && index < (int)m->layers.size() ? copy_name(m->layers[(size_t)index], buf, buflen) : 1;
   Gil g;
   PyObject* r = call(s, "layer_names", nullptr);
   if (!r) return 1;
@@ -1151,16 +1364,21 @@ static long long int_call(void* s, const char* method, const char* fmt, ...) {
 }
 
 int sn_num_layer_weights(void* s, int layer) {
+  if (NativeMeta* m = native_meta(s))
+    if (layer >= 0 && layer < (int)m->weights.size()) return m->weights[(size_t)layer];
   Gil g;
   return (int)int_call(s, "num_layer_weights", "(i)", layer);
 }
 
 int sn_num_data_blobs(void* s) {
+  if (NativeMeta* m = native_meta(s)) return (int)m->blobs.size();
   Gil g;
   return (int)int_call(s, "num_data_blobs", "()");
 }
 
 int sn_data_blob_name(void* s, int index, char* buf, int buflen) {
+  if (NativeMeta* m = native_meta(s))
+    return index >= 0 && index < (int)m->blobs.size() ? copy_name(m->blobs[(size_t)index], buf, buflen) : 1;
   Gil g;
   PyObject* r = call(s, "data_blob_name", "(i)", index);
   if (!r) return 1;
@@ -1176,6 +1394,7 @@ int sn_data_blob_name(void* s, int index, char* buf, int buflen) {
 }
 
 int sn_num_output_blobs(void* s) {
+  if (NativeMeta* m = native_meta(s)) return m->outputs;
   Gil g;
   return (int)int_call(s, "num_output_blobs", "()");
 }
@@ -1190,6 +1409,9 @@ int sn_num_test_scores(void* s) {
 int sn_blob_num_axes(void* s, int layer, int index) {
   NativeWeights* w = nullptr;
   if (const ParamDesc* p = native_param(s, layer, index, &w)) return p->ndim;
+  hipStream_t bs;
+  if (layer < 0)
+    if (const BlobDesc* b = native_blob(s, index, 0, &bs)) return b->ndim;
   Gil g;
   return (int)int_call(s, "blob_num_axes", "(ii)", layer, index);
 }
@@ -1198,6 +1420,10 @@ int sn_blob_axis_shape(void* s, int layer, int index, int axis) {
   NativeWeights* w = nullptr;
   if (const ParamDesc* p = native_param(s, layer, index, &w))
     if (axis >= 0 && axis < p->ndim) return p->cs[axis];
+  hipStream_t bs;
+  if (layer < 0)
+    if (const BlobDesc* b = native_blob(s, index, 0, &bs))
+      if (axis >= 0 && axis < b->ndim) return b->dims[axis];
   Gil g;
   return (int)int_call(s, "blob_axis_shape", "(iii)", layer, index, axis);
 }
@@ -1205,6 +1431,9 @@ int sn_blob_axis_shape(void* s, int layer, int index, int axis) {
 int sn_blob_get(void* s, int layer, int index, int diff, float* out, long long n) {
   NativeWeights* w = nullptr;
   if (const ParamDesc* p = native_param(s, layer, index, &w)) return param_get(w, *p, diff, out, n);
+  hipStream_t bs;
+  if (layer < 0)
+    if (const BlobDesc* b = native_blob(s, index, diff, &bs)) return blob_get_native(native_state(s), *b, bs, diff, out, n);
   Gil g;
   return status(call(s, "blob_get", "(iiiKL)", layer, index, diff, (unsigned long long)(uintptr_t)out, n));
 }
@@ -1212,6 +1441,9 @@ int sn_blob_get(void* s, int layer, int index, int diff, float* out, long long n
 int sn_blob_set(void* s, int layer, int index, int diff, const float* in, long long n) {
   NativeWeights* w = nullptr;
   if (const ParamDesc* p = native_param(s, layer, index, &w)) return param_set(w, *p, diff, in, n);
+  hipStream_t bs;
+  if (layer < 0)
+    if (const BlobDesc* b = native_blob(s, index, diff, &bs)) return blob_set_native(native_state(s), *b, bs, diff, in, n);
   Gil g;
   return status(call(s, "blob_set", "(iiiKL)", layer, index, diff, (unsigned long long)(uintptr_t)in, n));
 }

@@ -1,0 +1,11 @@
+#!/bin/bash
+# CaffeNet: weight gradients on a side stream (with / without stream priorities) vs inline
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
+: > gpurun_out/wgs_ab.jsonl
+for i in 1 2; do
+  for cfg in "base" "SN_WGRAD_STREAM=1" "SN_WGRAD_STREAM=1 SN_MAIN_PRIO=-1" "SN_WGRAD_STREAM=1 SN_WGRAD_KINDS=conv SN_MAIN_PRIO=-1"; do
+    if [ "$cfg" = base ]; then e=""; else e="$cfg"; fi
+    env $e timeout -k 10 300 python -u bench.py >> gpurun_out/wgs_ab.jsonl 2> gpurun_out/wgs_ab.err || { tail -20 gpurun_out/wgs_ab.err; exit 5; }
+    echo "$cfg: $(tail -1 gpurun_out/wgs_ab.jsonl | cut -c70-130)"
+  done
+done

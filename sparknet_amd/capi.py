@@ -26,6 +26,31 @@ from .core.solver import Solver
 CALLBACK = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_void_p)
 
 
+class _plain_backward:
+    """The net's backward as Caffe's Net::Backward: gradients into the parameter diffs, no
+    solver work.  The native step path (engine.GraphStep) fuses the InnerProduct SGD update
+    into the weight-gradient GEMM (engine.fuse_fc_updates) and may route conv weight
+    gradients to split-K slabs the solver consumes (engine.fuse_splitk_updates); both are
+    switched off for an sn_backward / backward-plan capture and restored afterwards."""
+
+    def __init__(self, net):
+        self.net = net
+
+    def __enter__(self):
+        self.saved = []
+        for layer in self.net.layers:
+            for attr in ("fused_update", "slab_grad"):
+                if getattr(layer, attr, None) is not None:
+                    self.saved.append((layer, attr, getattr(layer, attr)))
+                    setattr(layer, attr, None)
+        return self
+
+    def __exit__(self, *exc):
+        for layer, attr, val in self.saved:
+            setattr(layer, attr, val)
+        return False
+
+
 class CoreState:
     """caffenet_state (ccaffe.cpp:22-31): a solver with its train net, a test net, the
     device, callbacks and the last test scores."""
@@ -93,7 +118,8 @@ class CoreState:
         return float(self.net.forward())
 
     def backward(self) -> None:
-        self.net.backward()
+        with _plain_backward(self.net):
+            self.net.backward()
 
     def step(self, n: int) -> None:
         self.solver.step(n)
@@ -268,10 +294,62 @@ class CoreState:
         torch.cuda.synchronize(dev)
         acc.zero_()
         self.__dict__.setdefault("_fwd_graphs", {})[bool(test)] = (graph, acc, loss_buf)
+        if not test:
+            self.__dict__.pop("_bwd_graph", None)  # it read the blobs this capture rebound
         return {"exec": int(graph.raw_cuda_graph_exec()),
                 "stream": int(torch.cuda.current_stream(dev).cuda_stream),
                 "loss_dev": int(loss_buf.data_ptr()), "acc_dev": int(acc.data_ptr()), "n_out": n_out,
-                "feeds": [f for _, _, f in feeds]}
+                "feeds": [f for _, _, f in feeds], "blobs": [] if test else self.blob_table()}
+
+    # -- native backward and activation blobs (sn_core.cpp NativeBackward, BlobDesc) -------------
+    # sn_backward replays a captured backward of the train net: built right after the Python
+    # verb ran a backward (on the blobs the train forward plan left bound to its graph
+    # memory), replayed once (so the blob gradients hold a real backward of the staged batch)
+    # with the flat gradient buffer restored afterwards (the eager call already accumulated
+    # this pass: Caffe's Backward adds into the parameter diffs once per call).  The blob
+    # table gives the native sn_blob_* verbs on activation blobs (layer < 0) each blob's
+    # device data / gradient pointer, dtype and layout, read with hipMemcpy.
+    def backward_plan(self) -> dict:
+        net = self.net
+        if self.device.type != "cuda" or False not in self.__dict__.get("_fwd_graphs", {}):
+            raise RuntimeError("native backward needs the train forward plan")
+        if net.ctx.stale_diffs:
+            net.finish_param_diffs()
+        dev = self.device
+        torch.cuda.synchronize(dev)
+        saved = net.flat_diff.clone()
+        graph = torch.cuda.CUDAGraph()
+        with _plain_backward(net):
+            with torch.cuda.graph(graph):
+                net.backward()
+        graph.replay()
+        net.flat_diff.copy_(saved)
+        torch.cuda.synchronize(dev)
+        self.__dict__["_bwd_graph"] = graph
+        return {"exec": int(graph.raw_cuda_graph_exec()),
+                "stream": int(torch.cuda.current_stream(dev).cuda_stream), "blobs": self.blob_table()}
+
+    def blob_table(self) -> list:
+        """(data ptr, diff ptr or 0, dtype (0 bf16, 1 fp32), NHWC image, ndim, dims[6]) per
+        net blob, in blob order; blobs whose storage is not a plain contiguous bf16 / fp32
+        device tensor get a null data pointer (they stay on the Python path)."""
+        rows = []
+        for b in self.net.blobs:
+            d = b._data
+            g = b._diff
+            ok = d is not None and d.is_cuda and d.is_contiguous() and d.dtype in (torch.bfloat16, torch.float32)
+            gok = ok and g is not None and g.is_cuda and g.is_contiguous() and g.dtype == d.dtype
+            shape = tuple(int(x) for x in b.shape)
+            rows.append((int(d.data_ptr()) if ok and len(shape) <= 6 else 0, int(g.data_ptr()) if gok else 0,
+                         int(d.dtype == torch.float32) if ok else 0, int(b.is_image), len(shape))
+                        + shape + (1,) * (6 - len(shape)))
+        return rows
+
+    def meta_plan(self) -> dict:
+        """Names and counts the metadata verbs return (read once per loaded net)."""
+        net = self.net
+        return {"layers": list(net.layer_names), "weights": [len(l.params) for l in net.layers],
+                "blobs": list(net.blob_names), "outputs": len(net.output_blobs)}
 
     def weights_plan(self) -> dict:
         """Flat fp32 master buffer (device or host memory) and its compute shadow for the

@@ -1090,7 +1090,9 @@ class GraphStep:
         if side_wgrad:
             from .ops import hip
             if self.wgrad_stream is None:
-                self.wgrad_stream = torch.cuda.Stream(s.device)
+                # SN_WGRAD_PRIO: HIP stream priority of the side stream (0 = normal; the
+                # capture stream's is SN_MAIN_PRIO): the data-gradient chain is the critical path
+                self.wgrad_stream = torch.cuda.Stream(s.device, priority=int(os.environ.get("SN_WGRAD_PRIO", "0")))
             hip.WgradStream.begin(self.wgrad_stream)
         try:
             loss = (self.branches.forward_backward() if self._use_branches and self.branches
@@ -1112,7 +1114,7 @@ class GraphStep:
     def capture(self) -> None:
         s = self.solver
         dev = s.device
-        side = torch.cuda.Stream(dev)
+        side = torch.cuda.Stream(dev, priority=int(os.environ.get("SN_MAIN_PRIO", "0")))
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for w in range(self.warmup):

@@ -68,6 +68,17 @@ int main(int argc, char** argv) {
   long long pc = 1;
   for (int a = 0; a < sn_blob_num_axes(st, 2, 0); ++a) pc *= sn_blob_axis_shape(st, 2, 0, a);
   float* pb = (float*)malloc(sizeof(float) * pc);
+  /* backward, activation blobs (data and gradient) and the name / count verbs: their first
+   * calls build the native backward plan, blob table and metadata */
+  CHECK(sn_backward(st));
+  long long ac = 1;
+  const int nb_axes = sn_blob_num_axes(st, -1, 2);
+  for (int a = 0; a < nb_axes; ++a) ac *= sn_blob_axis_shape(st, -1, 2, a);
+  float* ab = (float*)malloc(sizeof(float) * ac);
+  CHECK(sn_blob_get(st, -1, 2, 0, ab, ac));
+  CHECK(sn_blob_get(st, -1, 2, 1, ab, ac));
+  char nm[64];
+  CHECK(sn_num_layers(st) <= 0 || sn_layer_name(st, 2, nm, sizeof nm) || sn_num_data_blobs(st) <= 0);
   const long long py0 = sn_python_entries();
   CHECK(sn_solver_step(st, 3));
   CHECK(sn_blob_num_axes(st, 2, 0) != 4);
@@ -80,9 +91,17 @@ int main(int argc, char** argv) {
   CHECK(sn_get_weights(st, ws, np));
   CHECK(sn_set_weights(st, ws, np));
   CHECK(sn_forward(st, &warm));
+  CHECK(sn_backward(st));
+  CHECK(sn_blob_num_axes(st, -1, 2) != nb_axes);
+  CHECK(sn_blob_get(st, -1, 2, 0, ab, ac));
+  CHECK(sn_blob_get(st, -1, 2, 1, ab, ac));
+  CHECK(sn_blob_set(st, -1, 2, 1, ab, ac));
+  CHECK(sn_num_layers(st) <= 0 || sn_layer_name(st, 2, nm, sizeof nm) || sn_num_data_blobs(st) <= 0 ||
+        sn_data_blob_name(st, 0, nm, sizeof nm) || sn_num_output_blobs(st) < 0 || sn_num_layer_weights(st, 2) != 2);
   const long long py = sn_python_entries() - py0;
   free(ws);
   free(pb);
+  free(ab);
   printf("steady_py=%lld scores=%d score0=%.4f fwd=%.4f\n", py, nscores, score, warm);
   CHECK(!isfinite(score) || !isfinite(warm) || nscores != 1);
   CHECK(sn_load_net_from_protobuf(st, "\xff\xff\xff", 3) == 0); /* garbage bytes must fail cleanly */
