@@ -16,6 +16,7 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 typedef uint16_t bf16_t;  // raw storage type of a bf16 element
 
 #define SN_DEV __device__ __forceinline__

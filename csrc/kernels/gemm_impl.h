@@ -91,7 +91,8 @@ struct SnGemmArgs {
   // bf16 epilogues of unsplit 4-wave tiles: stage the finished tile through the idle LDS
   // stages and store it as whole 16-B row chunks (host: ldc % 8 == 0, 16-B aligned C)
   int lds_store;
-  int addr_legacy;  // 1: general per-lane address decode only (A/B probe of the fast DMA paths)
+  int addr_legacy;  // bit 0: general per-lane address decode only (A/B probe of the fast DMA paths);
+                    // bit 1: the MC im2col row table (opt-in A/B: slower, docs/PERF_NOTES.md)
   // bf16 epilogues of gemm_kernel, unsplit: also store the finished (bf16-rounded) output as
   // fp8 bytes q_out[grp * q_gstride + m * q_ld + n] = sat(v * q_slot[0]) and fold its |max|
   // into q_slot[1] — the quantisation pass of the fp8 product that consumes this output
@@ -106,6 +107,13 @@ struct SnGemmArgs {
   // a single address serialises ~10^5 block atomics), folded into q_slot[1] afterwards by
   // sn_fp8_fold_amax
   float* q_part;
+  // In-launch split-K combine (gemm_kernel tiles, splits > 1, not EPI_SGD): fp32 slabs
+  // fix_ws[(grp * splits + split) * fix_sstride + m * fix_ld + n] and one zero-initialised
+  // counter per (group, output tile) at fix_cnt[grp * tiles + tile]; null = the separate
+  // splitk_reduce launch.  C / ldc / bias / gate / ... then describe the FINAL output.
+  float* fix_ws;
+  long long fix_ld, fix_sstride;
+  int* fix_cnt;
 };
 
 }  // extern "C"
@@ -201,6 +209,20 @@ struct GStager {
   int sn_, sp_, sq_;
   int cdh[MC ? NI : 1], cdw[MC ? NI : 1], colo[MC ? NI : 1];
   bool wave_has_one;
+  // MC+IM2COL row table (waves without the ones column, bf16; opt-in, addr_legacy == 2): the
+  // wave's RW = 64/NW pixel rows of a K-step are decoded lane-parallel, RW rows x KS = NW
+  // K-steps per decode (one division chain per KS K-steps instead of a per-instruction walk),
+  // and each instruction fetches its rows' (pixel offset, packed h / w) by ds_bpermute; the
+  // next issue's pair is fetched at the end of an issue.  It cuts the stager's VALU from ~55
+  // to ~22 per K-step (tile 10), yet the CaffeNet weight gradients run 8-10 % SLOWER with it
+  // (profiles/r5_wgrad_rowtab_ab.txt): the MC weight-gradient loop is not VALU-bound.
+  static constexpr int RW = 64 / NW, KS = 64 / RW;
+  bool rowtab;
+  int bstep;                           // K-step index inside the current decode batch
+  int tb_off, tb_hw;                   // this lane's decode: byte offset of the pixel corner,
+                                       // (h & 0xffff) | (w << 16), h = -16384 past k_lim
+  int nx_off[MC ? NI : 1], nx_hw[MC ? NI : 1];  // the next issue's rows, per instruction
+  int colb[MC ? NI : 1];               // colo in bytes
   // Low-VALU address paths (all decisions wave-uniform, taken once at init):
   //  KC+IM2COL: kcmode 1 = every K-step lies inside ONE filter tap (Cg % (8*EPC) == 0), so
   //   the tap offset and its (dh, dw) shift are scalars and a lane's DMA offset is
@@ -284,7 +306,7 @@ struct GStager {
     kcmode = 0;
     fast = false;
     if (MODE == OP_IM2COL && !MC) {
-      kcmode = __builtin_amdgcn_readfirstlane(legacy ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
+      kcmode = __builtin_amdgcn_readfirstlane((legacy & 1) ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
       if (kcmode == 1 && (g.R > 16 || g.S > 16)) kcmode = 2;  // the tap masks hold 16 rows / cols
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -302,7 +324,7 @@ struct GStager {
     if (MODE == OP_DENSE) {
       // element extent of the operand for this group: KC rows x ld, MC (k rows) x ld
       const long long extent = MC ? (long long)k_lim_hint * ld : (long long)rows_lim * ld;
-      fast = __builtin_amdgcn_readfirstlane((int)(!legacy && extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
+      fast = __builtin_amdgcn_readfirstlane((int)(!(legacy & 1) && extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
       // built unconditionally from wave-uniform values so it stays in SGPRs
       const unsigned long long a = reinterpret_cast<unsigned long long>(base);
       rsrc[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
@@ -334,6 +356,30 @@ struct GStager {
 #pragma unroll
       for (int j = 0; j < NI; ++j) any = any || co[j];
       wave_has_one = __ballot(any) != 0ull;
+      rowtab = __builtin_amdgcn_readfirstlane((int)(ES == 2 && legacy == 2 && !wave_has_one)) != 0;
+      bstep = -1;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) colb[j] = colo[j] * ES;
+    }
+  }
+
+  // Row table: lane L decodes pixel row wave*RW + L%RW of K-step (k_first + BKE * (L/RW)).
+  SN_DEV void rt_decode(int wave, int lane, int k_first, int k_lim) {
+    const int pix = k_first + BKE * (lane / RW) + wave * RW + lane % RW;
+    const int PQ = g.P * g.Q;
+    const int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
+    const int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
+    const int h = p * g.sh - g.ph, w = q * g.sw - g.pw;
+    tb_off = (int)(((unsigned)((n * g.H + h) * g.W + w) * (unsigned)g.C) * (unsigned)ES);  // modular, as colb
+    tb_hw = pix < k_lim ? ((h & 0xffff) | (w << 16)) : (int)0xc000;  // h = -16384: never inside
+  }
+  // the (offset, h/w) pairs of K-step u of the batch for this lane's NI instructions
+  SN_DEV void rt_fetch(int u, int lane) {
+    const int a = (u * RW + lane / CPL) * 4;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      nx_off[j] = __builtin_amdgcn_ds_bpermute(a + j * RPI * 4, tb_off);
+      nx_hw[j] = __builtin_amdgcn_ds_bpermute(a + j * RPI * 4, tb_hw);
     }
   }
 
@@ -543,6 +589,24 @@ struct GStager {
           long long off = v ? (long long)kout * rowlen + (long long)(RS - 1 - tap) * g.Cg + col : 0;
           dma(base + off * 2, v, dst + j * 1024);
         }
+      } else if (rowtab) {
+        const int lane = threadIdx.x & 63;
+        if (bstep < 0) {  // first issue of the block: decode the first batch
+          rt_decode(wave, lane, k_tile, k_lim);
+          rt_fetch(0, lane);
+          bstep = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int h = ((nx_hw[j] << 16) >> 16) + cdh[j], w = (nx_hw[j] >> 16) + cdw[j];
+          const bool v = cv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          dma_buf(v ? (unsigned)(nx_off[j] + colb[j]) : 0xffffffffu, dst + j * 1024);
+        }
+        if (++bstep == KS) {
+          bstep = 0;
+          rt_decode(wave, lane, k_tile + BKE, k_lim);
+        }
+        rt_fetch(bstep, lane);
       } else {
         // rows = pixels: walk the lane's pixel (n, p, q) by RPI per instruction instead of
         // two divisions per instruction; offsets are 32-bit (host: < 2^31 elements)
@@ -1150,6 +1214,77 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   auto wave_n = [&](int i, int j) __attribute__((always_inline)) {
     return MF32 ? 32 * (i >> 1) + 8 * (((i & 1) << 1) | (j & 1)) + 4 * (lane >> 5) : 16 * i + 4 * (lane >> 4);
   };
+  int esplit = split;  // the fp32 slab the epilogue stores into (split-K without fix_cnt)
+  if constexpr (EPI != EPI_SGD) {
+    if (args.fix_cnt) {
+      // In-launch deterministic split-K combine (host: splits > 1): every K-slice block stores
+      // its fp32 partial tile in its slab WRITE-THROUGH (sc1 16-B buffer stores: visible to every
+      // XCD once drained, so no release fence — an agent-scope release per block, i.e. an L2
+      // write-back in each of hundreds of blocks, cost CaffeNet 9 %), drains them, and takes a
+      // relaxed agent-scope ticket on the tile's counter; the block that draws ticket splits-1
+      // acquires (agent scope), sums ALL slices in split order 0..S-1 (its own from registers:
+      // the same fp32 values, so the sum is bitwise independent of which block arrives last, and
+      // equal to splitk_reduce_kernel's sequential order) and runs the product's real epilogue;
+      // it resets the counter for the next launch (the host zeroes the counter pool once).
+      // cdna_hip_programming.md, "In-launch split-K reduction" and Guideline 16 R1.
+      const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(args.fix_ws, (short)0, 0x7fffffff, 0x00020000);
+      const unsigned sbase = (unsigned)(((long long)grp * args.splits + split) * args.fix_sstride);  // host: < 2^29 floats
+#pragma unroll
+      for (int j = 0; j < MFR; ++j) {
+        const int m = m_blk + wm0 + wave_m(j);
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) {
+          const int n = n_blk + wn0 + wave_n(i, j);
+          if (m < args.M && n < args.N)  // host: fix_ld % 4 == 0 and fix_ld >= N rounded up to 4
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), wsr,
+                                                   (int)((sbase + (unsigned)m * (unsigned)args.fix_ld + n) * 4u), 0, 16);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* cnt = args.fix_cnt + (long long)grp * tiles + tile;
+      int* flag = reinterpret_cast<int*>(smem0);
+      if (tid == 0) {
+        const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = ticket == args.splits - 1;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *flag = last;
+      }
+      __syncthreads();
+      if (!*flag) return;
+      const float* ws0 = args.fix_ws + (long long)grp * args.splits * args.fix_sstride;
+      f32x4 sum[NFR][MFR];
+#pragma unroll
+      for (int i = 0; i < NFR; ++i)
+#pragma unroll
+        for (int j = 0; j < MFR; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < args.splits; ++q) {
+        const float* sq = ws0 + (long long)q * args.fix_sstride;
+#pragma unroll
+        for (int j = 0; j < MFR; ++j) {
+          const int m = m_blk + wm0 + wave_m(j);
+#pragma unroll
+          for (int i = 0; i < NFR; ++i) {
+            const int n = n_blk + wn0 + wave_n(i, j);
+            f32x4 v = acc[i][j];
+            if (q != split && m < args.M && n < args.N)
+              v = *reinterpret_cast<const f32x4*>(sq + (long long)m * args.fix_ld + n);
+            sum[i][j] += v;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NFR; ++i)
+#pragma unroll
+        for (int j = 0; j < MFR; ++j) acc[i][j] = sum[i][j];
+      esplit = 0;
+      __syncthreads();  // the flag word is LDS the staged epilogue below may reuse
+    }
+  }
   // fp32 outputs: the bias-gradient column (when routed to bias_out) is not part of C
   const int c_cols = (!epi_bf16<EPI>() && args.bias_out) ? args.ones_col : args.N;
   if constexpr (EPI == EPI_SGD) {
@@ -1315,7 +1450,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     for (int i = 0; i < NFR; ++i) {
       const int n = n_blk + wn0 + wave_n(i, j);
       if (n >= args.N) continue;
-      epi_store<EPI, (FP8 != 0)>(args, grp, split, m, n, acc[i][j], c_cols, epi_bf16<EPI>() ? &qmax : nullptr);
+      epi_store<EPI, (FP8 != 0)>(args, grp, esplit, m, n, acc[i][j], c_cols, epi_bf16<EPI>() ? &qmax : nullptr);
     }
   }
   if (epi_bf16<EPI>() && args.q_out) q_amax_flush(args, qmax, smem0);

@@ -28,6 +28,9 @@ int launch_tile64(const SnGemmArgs& a, hipStream_t stream) {
 // (one block per CU); 128x64 x 3 stages = 72 KB (two per CU).
 int launch_tile_ns3(const SnGemmArgs& a, hipStream_t stream) {
   const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
+  // 128x64: also the weight-gradient forms (MC x MC dense / im2col), whose NS = 2 tile 10
+  // waits for each K-step's DMA (one K-step in flight per block, three blocks per CU)
+  if (a.tile == 20 && (key == 0b1010 || key == 0b1011)) return launch_tile64<3>(a, stream);
   if (key != 0b0000 && key != 0b0010) return 4;  // dense NT / NN
   if (a.tile == 20) return launch_tile64<3>(a, stream);
   const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
@@ -39,7 +42,7 @@ int launch_tile_ns3(const SnGemmArgs& a, hipStream_t stream) {
 }  // namespace
 
 // 256x64 (skinny N), 256x128 / 128x256 (8 waves, 3 stages), 128x64 (three blocks per CU),
-// 128x128 / 128x64 with 3 stages (19, 20)
+// 128x128 / 128x64 with 3 stages (19: dense; 20: dense and the weight-gradient forms)
 int sn_gemm_tiles_b(const SnGemmArgs& a, hipStream_t stream) {
   switch (a.tile) {
     case 1: return launch_tile<256, 64, 4, 2>(a, stream);

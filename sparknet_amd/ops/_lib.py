@@ -50,7 +50,9 @@ class SnGemmArgs(C.Structure):
                 ("drop_scale", C.c_float), ("gate_scale", C.c_float), ("lds_store", C.c_int),
                 ("addr_legacy", C.c_int),
                 ("q_out", C.c_void_p), ("q_ld", C.c_longlong), ("q_gstride", C.c_longlong), ("q_slot", C.c_void_p),
-                ("q_e5m2", C.c_int), ("q_part", C.c_void_p)]
+                ("q_e5m2", C.c_int), ("q_part", C.c_void_p),
+                ("fix_ws", C.c_void_p), ("fix_ld", C.c_longlong), ("fix_sstride", C.c_longlong),
+                ("fix_cnt", C.c_void_p)]
 
 
 def lib_path(name: str = "libsn_kernels.so") -> Path:

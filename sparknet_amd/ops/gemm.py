@@ -263,7 +263,9 @@ _NO_XTRA = (0, 0, 0.0, 1.0)
 _LDS_EPI = os.environ.get("SN_GEMM_LDS_EPI", "1") != "0"
 _LDS_EPI_TILES = frozenset(int(t) for t in os.environ.get("SN_GEMM_LDS_EPI_TILES", "0,1,4,5,10,12,13,14,15,16,17,18,19,20").split(","))
 # SnGemmArgs.addr_legacy: 1 = the general per-lane DMA address decode only (A/B probes of
-# the scalar-offset fast paths; SN_GEMM_LEGACY_ADDR=1)
+# the scalar-offset fast paths; SN_GEMM_LEGACY_ADDR=1); 2 = the lane-parallel row table of MC
+# im2col operands instead of the per-instruction pixel walk (SN_GEMM_LEGACY_ADDR=2: an A/B
+# only, 8-10 % slower on the CaffeNet weight gradients, profiles/r5_wgrad_rowtab_ab.txt)
 _ADDR_LEGACY = int(os.environ.get("SN_GEMM_LEGACY_ADDR", "0"))
 
 
@@ -273,6 +275,49 @@ def _drop_fields(xtra):
     if not rng:
         return (0, 0, 0, 1.0, gscale)
     return (rng, dstream, int(4294967295 * ratio) & 0xffffffff, 1.0 / (1.0 - ratio), gscale)
+
+
+# In-launch deterministic split-K combine (SN_GEMM_FIXUP=1): the gemm_kernel tile family
+# (not the gemm256 / persistent tiles) reduces its own slabs in the last-arriving block of each
+# output tile.  Counters: one zeroed pool per device, handed out round-robin (each launch's
+# counters return to zero when it completes; the pool is far larger than the counters of all
+# launches one step keeps in flight, so concurrent branch-stream launches never share one).
+# SN_GEMM_FIXUP: 0 = always the reduce launch (default), 1 = the combine where _fixup_pays,
+# 2 = always.  Measured SLOWER on every CaffeNet split-K product it can replace (fc6 forward
+# 35 -> 60 us, conv5 weight gradient 65 -> 82 us; bench.py -4 % CaffeNet, -1 % GoogLeNet:
+# profiles/r5_splitk_combine_ab.txt): one block reading (splits - 1) 32-64 KB fp32 tiles is
+# latency-bound at ~18 GB/s, where the reduce launch reads every slab chip-wide.
+_FIXUP = int(os.environ.get("SN_GEMM_FIXUP", "0"))
+FIX_READ_BW = 18e9     # bytes/s one last-arriving block reads the other slices' slabs at (measured)
+REDUCE_RATE = 2.5e12   # bytes/s of the splitk_reduce launches (CaffeNet step trace, r5)
+REDUCE_LAUNCH = 2e-6   # s: the extra kernel boundary of a reduce launch
+
+
+def _fixup_pays(M, N, groups, splits, bm, bn) -> bool:
+    """The combine serialises (splits-1) fp32 tiles of reading on each tile's last block; the
+    reduce launch reads every slab chip-wide plus one kernel boundary.  At the measured rates
+    only small tiles split a few ways combine (e.g. 128x64 in 2 slices)."""
+    t_fix = (splits - 1) * bm * bn * 4 / FIX_READ_BW
+    t_red = splits * M * (-(-N // 4) * 4) * groups * 4 / REDUCE_RATE + REDUCE_LAUNCH
+    return t_fix < t_red
+_FIX_TILES = frozenset((0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
+                        23, 24, 25, 26, 27, 28))
+_FIX_POOL: dict = {}
+_FIX_POOL_INTS = 1 << 20
+
+
+def _fix_counters(n: int, device) -> int:
+    pool = _FIX_POOL.get(device)
+    if pool is None:
+        assert not torch.cuda.is_current_stream_capturing(), "split-K counter pool created during capture"
+        pool = [torch.zeros(_FIX_POOL_INTS, dtype=torch.int32, device=device), 0]
+        _FIX_POOL[device] = pool
+    assert n <= _FIX_POOL_INTS, n
+    if pool[1] + n > _FIX_POOL_INTS:
+        pool[1] = 0
+    off = pool[1]
+    pool[1] += -(-n // 32) * 32  # 128-B aligned slices
+    return pool[0].data_ptr() + 4 * off
 
 
 def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc, ones, sg,
@@ -313,6 +358,26 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     sink = _DEFER_SINK
     deferred = (sink is not None and epi == EPI_F32 and not fp8 and (bias_grad is None or not bias_acc)
                 and sink.accepts(out, bias_grad))
+    if (_FIXUP and not deferred and not fp8 and tile in _FIX_TILES and epi != EPI_SGD
+            and (_FIXUP == 2 or _fixup_pays(M, N, groups, splits, bm, bn))):
+        # in-launch combine: the last K-slice block of each tile sums the slabs (split order)
+        # and runs the real epilogue — no splitk_reduce launch (gemm_kernel fix_cnt)
+        assert groups * splits * M * ldw * 4 < (1 << 31), "split-K combine: slab offsets are 31-bit"
+        ws = torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device)
+        e = EPI_BF16_DROP if (epi == EPI_BF16 and xtra[0]) else epi
+        lds = int(_LDS_EPI and epi == EPI_BF16 and tile in _LDS_EPI_TILES and ldc % 8 == 0 and c_gstride % 8 == 0
+                  and out.data_ptr() % 16 == 0)
+        args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, e,
+                               sa, sb, out.data_ptr(), ldc, c_gstride, 0,
+                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, f8, *dq, raster,
+                               ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), lds)
+        args.addr_legacy = _ADDR_LEGACY
+        args.fix_ws, args.fix_ld, args.fix_sstride = ws.data_ptr(), ldw, M * ldw
+        args.fix_cnt = _fix_counters(groups * tm_ * tn_, out.device)
+        _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
+        if _lib.DEBUG_SYNC:
+            _lib.debug_sync("gemm")
+        return
     ws = (sink.slab(groups * splits * M * ldw, out.device).view(groups, splits, M, ldw) if deferred
           else torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device))
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
@@ -541,7 +606,7 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
         if b_kc_dense and N % 96 == 0:
             tiles.append(17)
     if epi != EPI_SGD and N >= 64:
-        tiles.append(20)  # 3-stage 128x64, dense NT / NN only (InnerProduct forward / data gradient)
+        tiles.append(20)  # 3-stage 128x64: dense NT / NN (InnerProduct fwd / dgrad), MC x MC (weight gradients)
     if M <= 64 and _THIN:  # 64-row tiles: thin weight gradients (64-channel convs, Inception reduce layers)
         tiles += [21, 22]
     if epi != EPI_SGD:

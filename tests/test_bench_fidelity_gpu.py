@@ -9,11 +9,18 @@ loss moves.  The reference is the fp32 CPU engine from the same initial weights,
 batches, cropped / mirrored / dropped by the same Philox draws.
 
 * one iteration: every layer's weight and bias UPDATE (w1 - w0, i.e. -lr x gradient at zero
-  momentum history) within 2 % of the layer's largest fp32 update;
+  momentum history) against the fp32 engine's, as the largest deviation relative to the
+  layer's largest fp32 update AND as the relative L2 norm of the deviation, each within
+  max(2 %, 1.5 x the bf16 floor of that layer).  The floor is measured in the fixture: the
+  CPU engine run with bf16 storage (the GPU's activation / gradient / weight-copy rounding
+  points, on the fp32 CPU kernels) against the fp32 engine.  At this initialisation the
+  input layers' gradients are sums of nearly cancelling terms, so bf16 storage alone moves
+  conv1's update by ~15 % (max) / ~11 % (L2) and conv2's by ~7 %; the fc layers' L2 floors
+  are < 1 %, so there the 2 % bound applies;
 * the production hipGraph path for 20 steps: its per-iteration losses track the fp32 engine
   within 4 % over the iterations both ran, and the loss falls;
 * the gate has teeth: with conv1's weight-gradient product made to drop half its reduction
-  (a simulated split-K bug) the update check fails.
+  (a simulated split-K bug) the update check fails on conv1 and only there.
 
 Reference: caffe/src/caffe/test/test_gradient_based_solver.cpp:225-320 (update of one
 iteration vs a reference computed independently)."""
@@ -49,11 +56,11 @@ def _solver_param():
     return models.solver_for("caffenet", train_batch=B, test_batch=50, crop=227)  # bench.py's config
 
 
-def _trainer(dev, w0, x, y, graph):
+def _trainer(dev, w0, x, y, graph, dtype=None):
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.data.prefetch import DeviceFeeder, TensorSource
     from sparknet_amd.engine import LocalSGDTrainer, fuse_fc_updates, fuse_input_fold, fuse_relu
-    solver = Solver(_solver_param(), device=dev, seed=1701, build_test_nets=False)
+    solver = Solver(_solver_param(), device=dev, seed=1701, build_test_nets=False, dtype=dtype)
     net = solver.net
     net.flat_data.copy_(w0.to(net.flat_data.device))
     net.sync_compute()
@@ -88,21 +95,28 @@ def _updates(solver, w0):
     return out
 
 
-def _one_step_updates(dev, w0, x, y):
-    tr, solver = _trainer(dev, w0, x, y, graph=False)
+def _one_step_updates(dev, w0, x, y, dtype=None):
+    tr, solver = _trainer(dev, w0, x, y, graph=False, dtype=dtype)
     tr.local_step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     return _updates(solver, w0)
 
 
-def _worst(ug, uc):
-    worst = ("", 0.0)
-    for k, c in uc.items():
-        e = float((ug[k] - c).abs().max() / (c.abs().max() + 1e-12))
-        if e > worst[1]:
-            worst = (k, e)
-    return worst
+def _errs(u, uc):
+    """{param: (max deviation / max |fp32 update|, ||deviation|| / ||fp32 update||)}"""
+    return {k: (float((u[k] - c).abs().max() / (c.abs().max() + 1e-12)),
+                float((u[k] - c).norm() / (c.norm() + 1e-12))) for k, c in uc.items()}
+
+
+def _violations(ug, uc, floor):
+    """Parameters whose GPU deviation exceeds max(2 %, 1.5 x the bf16 floor), per metric."""
+    bad = []
+    for k, (emax, el2) in _errs(ug, uc).items():
+        fmax, fl2 = floor[k]
+        if emax > max(0.02, 1.5 * fmax) or el2 > max(0.02, 1.5 * fl2):
+            bad.append((k, round(emax, 4), round(el2, 4), round(fmax, 4), round(fl2, 4)))
+    return bad
 
 
 @pytest.fixture(scope="module")
@@ -110,24 +124,27 @@ def fixture_data():
     x, y = _data()
     w0 = _initial_weights()
     uc = _one_step_updates(torch.device("cpu"), w0, x, y)
-    return x, y, w0, uc
+    floor = _errs(_one_step_updates(torch.device("cpu"), w0, x, y, dtype=torch.bfloat16), uc)
+    return x, y, w0, uc, floor
 
 
 @pytest.mark.timeout(900)
 def test_bench_config_one_step_updates_match_fp32(gpu, fixture_data):
-    x, y, w0, uc = fixture_data
+    x, y, w0, uc, floor = fixture_data
     ug = _one_step_updates(torch.device(gpu), w0, x, y)
     assert ug.keys() == uc.keys() and len(uc) == 16  # 8 learnable layers x (weight, bias)
-    name, err = _worst(ug, uc)
-    assert err <= 0.02, (name, err)
+    print("per-parameter (max, L2) deviation vs fp32 / bf16 floor:",
+          {k: (round(a, 4), round(b, 4), round(floor[k][0], 4), round(floor[k][1], 4))
+           for k, (a, b) in _errs(ug, uc).items()})
+    assert not _violations(ug, uc, floor)
 
 
 @pytest.mark.timeout(900)
 def test_bench_config_gate_catches_a_broken_wgrad(gpu, fixture_data, monkeypatch):
     """Half of conv1's weight-gradient reduction dropped (split-K chunks past the middle
-    skipped) must fail the 2 % update gate."""
+    skipped) must fail the update gate."""
     from sparknet_amd.ops import gemm as G
-    x, y, w0, uc = fixture_data
+    x, y, w0, uc, floor = fixture_data
     orig = G._launch
 
     def broken(M, N, K, *a, **k):
@@ -136,13 +153,13 @@ def test_bench_config_gate_catches_a_broken_wgrad(gpu, fixture_data, monkeypatch
         return orig(M, N, K, *a, **k)
     monkeypatch.setattr(G, "_launch", broken)
     ug = _one_step_updates(torch.device(gpu), w0, x, y)
-    name, err = _worst(ug, uc)
-    assert name.startswith("conv1") and err > 0.02, (name, err)
+    bad = _violations(ug, uc, floor)
+    assert bad and all(b[0].startswith("conv1/") for b in bad), bad
 
 
 @pytest.mark.timeout(900)
 def test_bench_config_graph_losses_track_fp32(gpu, fixture_data):
-    x, y, w0, _ = fixture_data
+    x, y, w0, _, _ = fixture_data
     tr, solver = _trainer(torch.device(gpu), w0, x, y, graph=True)
     assert tr.step_fn is not None
     gl = [float(tr.local_step())]  # capture call: iterations 0..2, the loss of iteration 2
