@@ -1,54 +1,96 @@
-"""Batch-256 InnerProduct GEMMs (CaffeNet fc6 / fc7 / fc8 forward and data gradient) by
-tile and split-K factor, against torch.matmul (hipBLASLt).  Times include the split-K
-reduce (the whole gemm() call)."""
+#!/usr/bin/env python3
+"""InnerProduct products of CaffeNet at batch 256 (fc6 / fc7 / fc8 forward with bias + ReLU,
+data gradient with the ReLU gate): every gemm_kernel-family tile x split-K factor, timed as
+the whole product (GEMM + reduce launch), against the tuned-database choice.  Prints the best
+configurations so the database can be updated where a better one exists.
+
+    python scripts/fc_probe.py [--tiles 0,1,2,...] [--splits 1,2,3,...]
+"""
+from __future__ import annotations
+
+import argparse
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
 import torch  # noqa: E402
 
-from sparknet_amd.ops import _lib, gemm  # noqa: E402
-from sparknet_amd.ops.gemm import EPI_BF16, Dense  # noqa: E402
 
-_lib.kernels()
-
-
-def timeit(fn, reps=20):
+def timed(fn, reps=20, passes=5):
     fn()
     torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda._sleep(1 << 18)
-    a.record()
-    for _ in range(reps):
-        fn()
-    b.record()
-    torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps * 1e3
+    best = []
+    for _ in range(passes):
+        torch.cuda._sleep(1 << 18)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        best.append(e0.elapsed_time(e1) * 1e3 / reps)
+    best.sort()
+    return best[len(best) // 2]
 
 
-B = 256
-for name, N, K in [("fc6", 4096, 9216), ("fc7", 4096, 4096), ("fc8", 1000, 4096)]:
-    x = (torch.randn(B, K, device="cuda") * 0.1).to(torch.bfloat16)
-    w = (torch.randn(N, K, device="cuda") * 0.1).to(torch.bfloat16)
-    dy = (torch.randn(B, N, device="cuda") * 0.1).to(torch.bfloat16)
-    y = torch.empty(B, N, dtype=torch.bfloat16, device="cuda")
-    dx = torch.empty(B, K, dtype=torch.bfloat16, device="cuda")
-    t_bf = timeit(lambda: torch.matmul(x, w.t()))
-    t_bd = timeit(lambda: torch.matmul(dy, w))
-    t_of = timeit(lambda: gemm.linear_fwd(x, w, out=y))
-    t_od = timeit(lambda: gemm.linear_dgrad(dy, w, out=dx))
-    print(f"{name}: fwd blas {t_bf:.1f} us, ours(tuned) {t_of:.1f} | dgrad blas {t_bd:.1f}, ours(tuned) {t_od:.1f}")
-    for t in (0, 10, 19, 20, 21, 22):
-        rf, rd = [], []
-        for s in (1, 2, 4, 8, 16):
-            gemm._FORCE_TILE = t
-            try:
-                rf.append(f"s{s}:{timeit(lambda: gemm.gemm(B, N, K, Dense(x, K, True), Dense(w, K, True), y, N, epi=EPI_BF16, splits=s)):.1f}")
-            except Exception:  # noqa: BLE001
-                rf.append(f"s{s}:-")
-            try:
-                rd.append(f"s{s}:{timeit(lambda: gemm.gemm(B, K, N, Dense(dy, N, True), Dense(w, K, False), dx, K, epi=EPI_BF16, splits=s)):.1f}")
-            except Exception:  # noqa: BLE001
-                rd.append(f"s{s}:-")
-        gemm._FORCE_TILE = -1
-        print(f"  tile {t:2d} fwd " + " ".join(rf) + " | dgrad " + " ".join(rd))
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", default="0,1,2,3,4,5,10,12,13,16,17,18,19,20,23,24,26,27")
+    ap.add_argument("--splits", default="1,2,3,4,6,8,12,16")
+    args = ap.parse_args()
+    from sparknet_amd.ops import gemm as G
+    dev = torch.device("cuda", 0)
+    tiles = [int(t) for t in args.tiles.split(",")]
+    splits = [int(s) for s in args.splits.split(",")]
+    B = 256
+    shapes = [("fc6", 9216, 4096), ("fc7", 4096, 4096), ("fc8", 4096, 1000)]
+    for name, I, O in shapes:
+        x = torch.randn(B, I, device=dev).to(torch.bfloat16)
+        w = (torch.randn(O, I, device=dev) * 0.02).to(torch.bfloat16)
+        b = torch.randn(O, device=dev)
+        dy = torch.randn(B, O, device=dev).to(torch.bfloat16)
+        gate = torch.randn(B, I, device=dev).to(torch.bfloat16)
+        y = torch.empty(B, O, device=dev, dtype=torch.bfloat16)
+        dx = torch.empty(B, I, device=dev, dtype=torch.bfloat16)
+        ref_y = torch.relu(x.float() @ w.float().t() + b)
+        ref_dx = (dy.float() @ w.float()) * (gate.float() > 0)
+        for kind, M, N, K in (("fwd", B, O, I), ("dgrad", B, I, O)):
+            if kind == "fwd":
+                def prod(s=None):
+                    G.gemm(M, N, K, G.Dense(x, K, True), G.Dense(w, K, True), y, N, epi=G.EPI_BF16, bias=b,
+                           relu=True, splits=s)
+                    return y, ref_y
+            else:
+                def prod(s=None):
+                    G.gemm(M, N, K, G.Dense(dy, K, True), G.Dense(w, N, False), dx, N, epi=G.EPI_BF16, splits=s,
+                           gate=gate)
+                    return dx, ref_dx
+            G._FORCE_TILE = -1
+            t_db = timed(lambda: prod())
+            fl = 2.0 * M * N * K
+            res = []
+            best = (t_db, "db")
+            for t in tiles:
+                G._FORCE_TILE = t
+                for s in splits:
+                    try:
+                        out, ref = prod(s)
+                        torch.cuda.synchronize()
+                    except (RuntimeError, AssertionError):
+                        continue
+                    err = float((out.float() - ref).abs().max() / (ref.abs().max() + 1e-6))
+                    if err > 2e-2:
+                        res.append(f"{t}/{s}:ERR{err:.2g}")
+                        continue
+                    us = timed(lambda: prod(s))
+                    res.append(f"{t}/{s}:{us:.1f}")
+                    if us < best[0]:
+                        best = (us, f"{t}/{s}")
+            G._FORCE_TILE = -1
+            print(f"{name} {kind:5s} M={M} N={N} K={K}: db {t_db:.1f} us ({fl / t_db / 1e6:.0f} TF/s)  best {best[1]} "
+                  f"{best[0]:.1f} us ({fl / best[0] / 1e6:.0f} TF/s) | " + " ".join(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

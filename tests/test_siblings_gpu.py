@@ -58,13 +58,21 @@ def _per_param(solver, delta):
 
 
 def test_googlenet_siblings_merged_step_matches_unmerged(gpu, monkeypatch):
-    """One step: loss, and every parameter's update against its own largest update (the
-    merged data gradient sums the siblings in fp32 where the unmerged Split sums bf16 terms,
-    so the two are close, not bitwise)."""
+    """One step: loss, and every parameter's update against its own largest update.  The
+    merged data gradient sums the siblings in fp32 where the unmerged Split sums bf16 terms
+    and the merged products reduce in another order, so the two are close, not bitwise; how
+    close is set by bf16 summation-order noise, which at this initialisation reaches several
+    per cent on a few parameters (the auxiliary classifiers' convs, whose gradients are sums
+    of nearly cancelling terms).  That noise floor is measured here: the unmerged step again
+    with every split-K product capped at one slice (another summation order).  Tile choices
+    come from the cost model (no first-call timing), so every box runs the same products."""
+    from sparknet_amd.ops import gemm as G
+    monkeypatch.setattr(G, "_AUTOTUNE", False)
     w0 = _w0()
     (xb, yb), = _batches(1)
     res = {}
-    for merged in (False, True):
+    for key, merged, cap in (("base", False, 0), ("order", False, 1), ("merged", True, 0)):
+        monkeypatch.setattr(G, "_MAX_SPLITS", cap)
         solver, groups = _solver(gpu, w0, merged, monkeypatch)
         assert groups == (9 if merged else 0)
         net = solver.net
@@ -73,12 +81,19 @@ def test_googlenet_siblings_merged_step_matches_unmerged(gpu, monkeypatch):
         solver.stage_hyper()
         loss = float(solver.iteration())
         torch.cuda.synchronize()
-        res[merged] = (loss, _per_param(solver, net.flat_data.detach().float().cpu() - w0))
-    assert abs(res[True][0] - res[False][0]) <= 1e-3 * max(1.0, abs(res[False][0]))
-    errs = sorted(((float((res[True][1][k] - v).abs().max() / (v.abs().max() + 1e-12)), k)
-                   for k, v in res[False][1].items()), reverse=True)
-    print("worst per-parameter update errors:", [(k, round(e, 4)) for e, k in errs[:8]])
-    assert errs[0][0] < 2e-2, errs[:8]
+        res[key] = (loss, _per_param(solver, net.flat_data.detach().float().cpu() - w0))
+    assert abs(res["merged"][0] - res["base"][0]) <= 1e-3 * max(1.0, abs(res["base"][0]))
+
+    def rel(a, b):
+        return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+    bad = []
+    for k, v in res["base"][1].items():
+        e, floor = rel(res["merged"][1][k], v), rel(res["order"][1][k], v)
+        if e > max(2e-2, 3.0 * floor):
+            bad.append((k, round(e, 4), round(floor, 4)))
+    worst = sorted(((rel(res["merged"][1][k], v), k) for k, v in res["base"][1].items()), reverse=True)[:8]
+    print("worst per-parameter update errors (merged vs unmerged):", [(k, round(e, 4)) for e, k in worst])
+    assert not bad, bad
 
 
 def test_googlenet_siblings_graph_streams(gpu, monkeypatch):
