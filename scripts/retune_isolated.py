@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""Re-time a model's GEMM products one at a time, on an idle GPU, against every tuner
+candidate (ops.gemm._candidates: tile x split-K), and write the winners into a tuning
+database.
+
+Why: the first-call tuner times its candidates inside the warm-up steps, and on a model whose
+Inception towers run on four branch streams the other streams' kernels share the CUs while a
+candidate is timed — GoogLeNet's database held choices up to 1.6x slower than the best tile in
+isolation (conv2/3x3 forward: tile 15 at 340 TF/s vs tile 17 at 522, scripts/conv_probe.py).
+Every product here is timed with the real operands and epilogue (the launch recorded from one
+eager step), median of 5 passes; a candidate must beat the current choice by 3 % to replace it
+and must reproduce the current choice's output (max relative error 1e-2).  fp8 and EPI_SGD
+products keep their entries.
+
+    python scripts/retune_isolated.py --model googlenet --out gpurun_out/gemm_tuned_gn.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def timed(fn, reps, passes=5):
+    fn()
+    torch.cuda.synchronize()
+    best = []
+    for _ in range(passes):
+        torch.cuda._sleep(1 << 18)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        best.append(e0.elapsed_time(e1) * 1e3 / reps)
+    best.sort()
+    return best[len(best) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="googlenet")
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--margin", type=float, default=0.97)
+    args = ap.parse_args()
+    import bench
+    from sparknet_amd import models
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.data.prefetch import DeviceFeeder, SyntheticSource
+    from sparknet_amd.engine import LocalSGDTrainer, fuse_input_fold, fuse_relu
+    from sparknet_amd.ops import gemm as G
+
+    dev = torch.device("cuda", 0)
+    B, C, HW, crop, classes, mean, in_scale = bench.DEFAULTS[args.model]
+    B = args.batch or B
+    kw = dict(train_batch=B, test_batch=max(1, min(B, 50)))
+    if args.model in ("caffenet", "alexnet", "googlenet", "vgg16"):
+        kw["crop"] = crop
+    solver = Solver(models.solver_for(args.model, **kw), device=dev, seed=1701, build_test_nets=False)
+    net = solver.net
+    fuse_relu(net)
+    src = SyntheticSource(B, C, HW, HW, classes=classes, pool=3, seed=0)
+    feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
+                          scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev)
+    fuse_input_fold(net, feeder)
+    trainer = LocalSGDTrainer(solver, None, tau=50, feeder=feeder, use_graph=False)
+    trainer.local_step()
+    torch.cuda.synchronize()
+
+    where = ["?"]
+    for layer in net.layers:
+        f, b = layer.forward, layer.backward
+
+        def fw(*a, _f=f, _n=layer.name):
+            where[0] = _n + ":fwd"
+            return _f(*a)
+
+        def bw(*a, _b=b, _n=layer.name):
+            where[0] = _n + ":bwd"
+            return _b(*a)
+        layer.forward, layer.backward = fw, bw
+    rec = []
+    orig = G._launch
+
+    def spy(*a, **k):
+        rec.append((where[0], a, k))
+        return orig(*a, **k)
+    G._launch = spy
+    trainer.local_step()
+    torch.cuda.synchronize()
+    G._launch = orig
+
+    updates = {}
+    tot_old = tot_new = 0.0
+    seen = set()
+    for name, a, k in rec:
+        a = list(a)
+        M, N, K, groups, ops, epi, out = a[0], a[1], a[2], a[3], a[4], a[5], a[6]
+        gate, bias_grad, tile, splits, kchunk = a[11], a[12], a[16], a[17], a[18]
+        deq = a[19] if len(a) > 19 else k.get("deq")
+        xtra = a[20] if len(a) > 20 else k.get("xtra", G._NO_XTRA)
+        if deq is not None or epi == G.EPI_SGD:
+            continue
+        sa, a_mc, a_mode, sb, b_mc, b_mode = ops
+        key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None,
+               bool(xtra[0]), G._geom_key(sa), G._geom_key(sb)) + (out.dtype,)
+        if key in seen:
+            continue
+        seen.add(key)
+        fl = 2.0 * M * N * K * groups
+        reps = max(2, min(40, int(2e12 / fl)))
+        saved = out.clone()
+        bsaved = bias_grad.clone() if bias_grad is not None else None
+
+        def restore():
+            out.copy_(saved)
+            if bias_grad is not None:
+                bias_grad.copy_(bsaved)
+
+        def run(t, s, kc):
+            b = list(a)
+            b[16], b[17], b[18] = t, s, kc
+            orig(*b, **k)
+        restore()
+        run(tile, splits, kchunk)
+        ref = out.float().clone()
+        scale = ref.abs().max().item() + 1e-6
+        t_old = timed(lambda: run(tile, splits, kchunk), reps)
+        best = (t_old, tile, splits, kchunk)
+        b_kc_dense = b_mc == 0 and b_mode == G.OP_DENSE
+        for t, s, kc in G._candidates(M, N, K, groups, b_kc_dense, epi):
+            if (t, s) == (tile, splits):
+                continue
+            try:
+                restore()
+                run(t, s, kc)
+            except RuntimeError:
+                continue
+            err = (out.float() - ref).abs().max().item() / scale
+            if err > 1e-2:
+                continue
+            us = timed(lambda: run(t, s, kc), reps)
+            if us < best[0]:
+                best = (us, t, s, kc)
+        restore()
+        tot_old += t_old
+        chosen = best if best[0] < args.margin * t_old else (t_old, tile, splits, kchunk)
+        tot_new += chosen[0]
+        if (chosen[1], chosen[2]) != (tile, splits):
+            updates[G._key_to_str(key)] = [chosen[1], chosen[2], chosen[3]]
+        print(f"{name:30s} {M:7d} {N:5d} {K:6d} {groups}  {tile:3d}/{splits:<3d} {t_old:8.1f} -> "
+              f"{chosen[1]:3d}/{chosen[2]:<3d} {chosen[0]:8.1f}", flush=True)
+    db = {}
+    if os.path.exists(args.out):
+        with open(args.out) as f:
+            db = json.load(f)
+    db.update(updates)
+    with open(args.out, "w") as f:
+        json.dump(dict(sorted(db.items())), f, indent=0)
+    print(f"total GEMM (distinct products): {tot_old:.1f} -> {tot_new:.1f} us; {len(updates)} entries changed -> {args.out}")
+
+
+if __name__ == "__main__":
+    main()
