@@ -722,6 +722,11 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     # interleaved passes; the minimum per candidate counts.  A candidate must beat the cost
     # model's pick by 3% to replace it, so timing noise cannot flip a choice.
     times = {c: float("inf") for c, _ in runs}
+    # Drain every stream of the device first: inside a warm-up step with branch streams the
+    # other towers' kernels would otherwise share the CUs with the candidates being timed —
+    # GoogLeNet's database held choices up to 1.6x off the isolated best that way
+    # (profiles/r5_retune_isolated_googlenet.txt).
+    torch.cuda.synchronize(out.device)
     # enough back-to-back launches per timed window that it spans >= ~150 us
     est = _cost(-(-M // TILES[tile][0]) * -(-N // TILES[tile][1]) * groups, -(-K // BK), splits, M * N * groups, tile)
     reps = max(4, min(32, int(150.0 / max(est, 1.0))))
