@@ -60,10 +60,11 @@ def parse():
                    help="run large layers' solver updates on a side stream during backward")
     p.add_argument("--no-fuse-fc", action="store_true",
                    help="store InnerProduct weight gradients and update them in the solver kernel")
-    p.add_argument("--streams", type=int, default=4,
+    p.add_argument("--streams", type=int, default=3,
                    help="HIP streams for parallel branches (Inception towers) inside the graph; 1 = sequential "
-                        "(>= 3 uses the star topology, see engine.BranchStreams; 4 measured 1-2%% faster than 2 "
-                        "on GoogLeNet)")
+                        "(>= 3 uses the star topology, see engine.BranchStreams); GoogLeNet b128 with the "
+                        "round-5 database: 1 / 2 / 3 / 4 / 6 streams = 18.1 / 20.2 / 21.4 / 20.7-20.8 / 20.1 k img/s "
+                        "(profiles/r5_googlenet_streams.txt)")
     p.add_argument("--feed-group", type=int, default=2,
                    help="H2D minibatch copies issued in groups of this many steps under one copy/compute "
                         "fence pair (DeviceFeeder group; 1 = one fence pair per step: 97k vs 102-105k img/s "
