@@ -216,13 +216,16 @@ struct GStager {
   // next issue's pair is fetched at the end of an issue.  It cuts the stager's VALU from ~55
   // to ~22 per K-step (tile 10), yet the CaffeNet weight gradients run 8-10 % SLOWER with it
   // (profiles/r5_wgrad_rowtab_ab.txt): the MC weight-gradient loop is not VALU-bound.
+  // Compiled only into the 4-wave bf16 stagers of up to 128 columns (tiles 0 / 10 and kin):
+  // in the 8-wave 256-wide tiles its registers alone pushed the K-loop into scratch spills.
   static constexpr int RW = 64 / NW, KS = 64 / RW;
+  static constexpr bool RT = MC && MODE == OP_IM2COL && ES == 2 && NW == 4 && TILE <= 128;
   bool rowtab;
   int bstep;                           // K-step index inside the current decode batch
   int tb_off, tb_hw;                   // this lane's decode: byte offset of the pixel corner,
                                        // (h & 0xffff) | (w << 16), h = -16384 past k_lim
-  int nx_off[MC ? NI : 1], nx_hw[MC ? NI : 1];  // the next issue's rows, per instruction
-  int colb[MC ? NI : 1];               // colo in bytes
+  int nx_off[RT ? NI : 1], nx_hw[RT ? NI : 1];  // the next issue's rows, per instruction
+  int colb[RT ? NI : 1];               // colo in bytes
   // Low-VALU address paths (all decisions wave-uniform, taken once at init):
   //  KC+IM2COL: kcmode 1 = every K-step lies inside ONE filter tap (Cg % (8*EPC) == 0), so
   //   the tap offset and its (dh, dw) shift are scalars and a lane's DMA offset is
@@ -356,10 +359,12 @@ struct GStager {
 #pragma unroll
       for (int j = 0; j < NI; ++j) any = any || co[j];
       wave_has_one = __ballot(any) != 0ull;
-      rowtab = __builtin_amdgcn_readfirstlane((int)(ES == 2 && legacy == 2 && !wave_has_one)) != 0;
+      rowtab = RT && __builtin_amdgcn_readfirstlane((int)(legacy == 2 && !wave_has_one)) != 0;
       bstep = -1;
+      if constexpr (RT) {
 #pragma unroll
-      for (int j = 0; j < NI; ++j) colb[j] = colo[j] * ES;
+        for (int j = 0; j < NI; ++j) colb[j] = colo[j] * ES;
+      }
     }
   }
 
@@ -377,7 +382,7 @@ struct GStager {
   SN_DEV void rt_fetch(int u, int lane) {
     const int a = (u * RW + lane / CPL) * 4;
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
+    for (int j = 0; j < (RT ? NI : 0); ++j) {
       nx_off[j] = __builtin_amdgcn_ds_bpermute(a + j * RPI * 4, tb_off);
       nx_hw[j] = __builtin_amdgcn_ds_bpermute(a + j * RPI * 4, tb_hw);
     }
@@ -589,7 +594,7 @@ struct GStager {
           long long off = v ? (long long)kout * rowlen + (long long)(RS - 1 - tap) * g.Cg + col : 0;
           dma(base + off * 2, v, dst + j * 1024);
         }
-      } else if (rowtab) {
+      } else if (RT && rowtab) {
         const int lane = threadIdx.x & 63;
         if (bstep < 0) {  // first issue of the block: decode the first batch
           rt_decode(wave, lane, k_tile, k_lim);
@@ -597,7 +602,7 @@ struct GStager {
           bstep = 0;
         }
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
+        for (int j = 0; j < (RT ? NI : 0); ++j) {
           const int h = ((nx_hw[j] << 16) >> 16) + cdh[j], w = (nx_hw[j] >> 16) + cdw[j];
           const bool v = cv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
           dma_buf(v ? (unsigned)(nx_off[j] + colb[j]) : 0xffffffffu, dst + j * 1024);
@@ -1215,16 +1220,18 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
     return MF32 ? 32 * (i >> 1) + 8 * (((i & 1) << 1) | (j & 1)) + 4 * (lane >> 5) : 16 * i + 4 * (lane >> 4);
   };
   int esplit = split;  // the fp32 slab the epilogue stores into (split-K without fix_cnt)
-  if constexpr (EPI != EPI_SGD) {
+  // (only in wave tiles of <= 16 fragments: larger ones would spill the K-loop to scratch;
+  // the host keeps _FIX_TILES to the tiles that have it)
+  if constexpr (EPI != EPI_SGD && NFR * MFR <= 16) {
     if (args.fix_cnt) {
       // In-launch deterministic split-K combine (host: splits > 1): every K-slice block stores
       // its fp32 partial tile in its slab WRITE-THROUGH (sc1 16-B buffer stores: visible to every
       // XCD once drained, so no release fence — an agent-scope release per block, i.e. an L2
       // write-back in each of hundreds of blocks, cost CaffeNet 9 %), drains them, and takes a
       // relaxed agent-scope ticket on the tile's counter; the block that draws ticket splits-1
-      // acquires (agent scope), sums ALL slices in split order 0..S-1 (its own from registers:
-      // the same fp32 values, so the sum is bitwise independent of which block arrives last, and
-      // equal to splitk_reduce_kernel's sequential order) and runs the product's real epilogue;
+      // acquires (agent scope), sums ALL slices in split order 0..S-1 from the slabs (so the sum
+      // is bitwise independent of which block arrives last, and equal to splitk_reduce_kernel's
+      // sequential order) and runs the product's real epilogue;
       // it resets the counter for the next launch (the host zeroes the counter pool once).
       // cdna_hip_programming.md, "In-launch split-K reduction" and Guideline 16 R1.
       const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(args.fix_ws, (short)0, 0x7fffffff, 0x00020000);
@@ -1256,12 +1263,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
       }
       __syncthreads();
       if (!*flag) return;
+      // every slice from its slab (this block's own included: the same fp32 values it stored),
+      // summed in place in split order — no second register tile
       const float* ws0 = args.fix_ws + (long long)grp * args.splits * args.fix_sstride;
-      f32x4 sum[NFR][MFR];
 #pragma unroll
       for (int i = 0; i < NFR; ++i)
 #pragma unroll
-        for (int j = 0; j < MFR; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int q = 0; q < args.splits; ++q) {
         const float* sq = ws0 + (long long)q * args.fix_sstride;
 #pragma unroll
@@ -1270,17 +1278,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
 #pragma unroll
           for (int i = 0; i < NFR; ++i) {
             const int n = n_blk + wn0 + wave_n(i, j);
-            f32x4 v = acc[i][j];
-            if (q != split && m < args.M && n < args.N)
-              v = *reinterpret_cast<const f32x4*>(sq + (long long)m * args.fix_ld + n);
-            sum[i][j] += v;
+            if (m < args.M && n < args.N) acc[i][j] += *reinterpret_cast<const f32x4*>(sq + (long long)m * args.fix_ld + n);
           }
         }
       }
-#pragma unroll
-      for (int i = 0; i < NFR; ++i)
-#pragma unroll
-        for (int j = 0; j < MFR; ++j) acc[i][j] = sum[i][j];
       esplit = 0;
       __syncthreads();  // the flag word is LDS the staged epilogue below may reuse
     }

@@ -27,31 +27,36 @@ struct ReduceOut {
   float drop_scale, gate_scale;
 };
 
-SN_DEV void reduce_store(const ReduceOut& o, int g, int r, int c, const float* acc) {
+// acc is taken by value and every index below is a compile-time constant (unrolled, guarded
+// instead of `break`): a pointer to the caller's array with a runtime index put the four
+// accumulators in scratch memory (32 B per lane, kernel-resource-usage report)
+SN_DEV void reduce_store(const ReduceOut& o, int g, int r, int c, float4 a) {
+  const float acc[4] = {a.x, a.y, a.z, a.w};
   if (o.extra && c <= o.extra_col && o.extra_col < c + 4) {
     float* e = o.extra + g * o.extra_gstride + r;
     const int q = o.extra_col - c;
-    const float v = q == 0 ? acc[0] : (q == 1 ? acc[1] : (q == 2 ? acc[2] : acc[3]));
+    const float v = q == 0 ? a.x : (q == 1 ? a.y : (q == 2 ? a.z : a.w));
     *e = o.extra_acc ? *e + v : v;
   }
   if (o.mode == 0) {
     const long long base = g * o.out_gstride + (long long)r * o.ldo + c;
     bf16_t* p = reinterpret_cast<bf16_t*>(o.out) + base;
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (c + k >= o.cols) break;
-      float v = acc[k] + (o.bias ? o.bias[(long long)g * o.cols + c + k] : 0.f);
-      if (o.relu) v = fmaxf(v, 0.f);
-      if (o.gate) v = bf2f(o.gate[base + k]) > 0.f ? v * o.gate_scale : 0.f;
-      if (o.drop_rng) v = dropout_keep(o.drop_rng, o.drop_stream, o.drop_thr, base + k) ? v * o.drop_scale : 0.f;
-      p[k] = f2bf(v);
+      if (c + k < o.cols) {
+        float v = acc[k] + (o.bias ? o.bias[(long long)g * o.cols + c + k] : 0.f);
+        if (o.relu) v = fmaxf(v, 0.f);
+        if (o.gate) v = bf2f(o.gate[base + k]) > 0.f ? v * o.gate_scale : 0.f;
+        if (o.drop_rng) v = dropout_keep(o.drop_rng, o.drop_stream, o.drop_thr, base + k) ? v * o.drop_scale : 0.f;
+        p[k] = f2bf(v);
+      }
     }
   } else {
     float* p = reinterpret_cast<float*>(o.out) + g * o.out_gstride + (long long)r * o.ldo + c;
     const int cols = o.extra ? o.extra_col : o.cols;
-    for (int k = 0; k < 4; ++k) {
-      if (c + k >= cols) break;
-      p[k] = (o.mode == 2 ? p[k] : 0.f) + acc[k];
-    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + k < cols) p[k] = (o.mode == 2 ? p[k] : 0.f) + acc[k];
   }
 }
 
@@ -87,10 +92,11 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, l
       }
     } else {
       for (int s = 0; s < splits; ++s)
+#pragma unroll
         for (int k = 0; k < 4; ++k)
           if (c + k < cols) acc[k] += p0[s * sstride + k];
     }
-    reduce_store(o, g, r, c, acc);
+    reduce_store(o, g, r, c, make_float4(acc[0], acc[1], acc[2], acc[3]));
   }
 }
 
@@ -136,7 +142,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_wide(const float* __restric
       float4 v = red[q][it];
       a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
     }
-    reduce_store(o, g, r, c, a);
+    reduce_store(o, g, r, c, make_float4(a[0], a[1], a[2], a[3]));
   }
 }
 

@@ -50,6 +50,30 @@ def main():
             occ[min(cur, 3)] = occ.get(min(cur, 3), 0) + (t - last)
         cur += d
         last = t
+    # idle intervals (no kernel of the iteration in flight) and the launches on either side
+    spans = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get(qkey, "?") if qkey else "?",
+                    r["Kernel_Name"]) for r in it)
+    gaps = []
+    reach, reach_k = spans[0][1], spans[0]
+    for sp in spans[1:]:
+        if sp[0] > reach:
+            gaps.append((sp[0] - reach, reach_k, sp))
+        if sp[1] > reach:
+            reach, reach_k = sp[1], sp
+
+    def short(n):
+        n = n.replace("(anonymous namespace)::", "").replace("void ", "")
+        return (n.split("(SnGemmArgs")[0] if "gemm" in n else n.split("(")[0])[-48:]
+    gaps.sort(reverse=True)
+    print(f"idle gaps: {len(gaps)}, total {sum(g[0] for g in gaps) / 1e3:.1f} us; largest:")
+    for g, a_, b_ in gaps[:12]:
+        print(f"  {g / 1e3:7.1f} us  after q{a_[2]} {short(a_[3])}  ->  q{b_[2]} {short(b_[3])}")
+    hist = {}
+    for g, _, _ in gaps:
+        k = 0 if g < 2000 else (1 if g < 5000 else (2 if g < 20000 else 3))
+        hist[k] = hist.get(k, 0) + 1
+    print("  gap sizes: " + ", ".join(f"{lbl}: {hist.get(i, 0)}" for i, lbl in
+                                       enumerate(("<2us", "2-5us", "5-20us", ">=20us"))))
     print(f"iteration wall {wall:.1f} us, {len(it)} launches, queue column {qkey!r}")
     print("in flight: " + "  ".join(f"{k}{'+' if k == 3 else ''}: {100.0 * v / 1e3 / wall:.1f} %"
                                     for k, v in sorted(occ.items())))

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import os
+import json
 import subprocess
 import sys
 from pathlib import Path
@@ -73,10 +74,35 @@ def _stale(obj: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def _run(cmd: list[str]) -> None:
+def _run(cmd: list[str]) -> subprocess.CompletedProcess:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def _resources(stderr: str) -> dict:
+    """{kernel symbol: {"vgpr", "agpr", "scratch", "vgpr_spill", "occupancy"}} from the
+    compiler's kernel-resource-usage remarks (scratch > 0 = the kernel spills or keeps a
+    private array in scratch memory — a register-pressure regression in a K-loop)."""
+    out, cur = {}, None
+    fields = {"VGPRs": "vgpr", "AGPRs": "agpr", "ScratchSize [bytes/lane]": "scratch", "VGPRs Spill": "vgpr_spill",
+              "Occupancy [waves/SIMD]": "occupancy"}
+    for line in stderr.splitlines():
+        if "remark:" not in line or "kernel-resource-usage" not in line:
+            continue
+        body = line.split("remark:", 1)[1].rsplit("[-Rpass", 1)[0].strip()
+        if body.startswith("Function Name:"):
+            cur = body.split(":", 1)[1].strip()
+            out[cur] = {}
+        elif cur is not None and ":" in body:
+            k, v = body.rsplit(":", 1)
+            if k.strip() in fields:
+                try:
+                    out[cur][fields[k.strip()]] = int(v.strip())
+                except ValueError:
+                    pass
+    return out
 
 
 def _compile(src: Path, hip: bool, extra: list[str] | None = None) -> Path:
@@ -84,10 +110,12 @@ def _compile(src: Path, hip: bool, extra: list[str] | None = None) -> Path:
     if _stale(obj, _deps(src)):
         obj.parent.mkdir(parents=True, exist_ok=True)
         if hip:
-            cmd = [HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)]
+            cmd = [HIPCC, *HIP_FLAGS, "-Rpass-analysis=kernel-resource-usage", "-c", str(src), "-o", str(obj)]
         else:
             cmd = ["g++", *CXX_FLAGS, *(extra or []), "-c", str(src), "-o", str(obj)]
-        _run(cmd)
+        r = _run(cmd)
+        if hip:  # per-kernel register / scratch report (tests/test_kernel_resources.py)
+            obj.with_suffix(".resources.json").write_text(json.dumps(_resources(r.stderr), indent=0, sort_keys=True))
     return obj
 
 

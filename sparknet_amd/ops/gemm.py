@@ -300,8 +300,9 @@ def _fixup_pays(M, N, groups, splits, bm, bn) -> bool:
     t_fix = (splits - 1) * bm * bn * 4 / FIX_READ_BW
     t_red = splits * M * (-(-N // 4) * 4) * groups * 4 / REDUCE_RATE + REDUCE_LAUNCH
     return t_fix < t_red
-_FIX_TILES = frozenset((0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
-                        23, 24, 25, 26, 27, 28))
+# (the tiles whose waves hold <= 16 accumulator fragments: the kernel compiles the combine
+# only there, larger register tiles would spill)
+_FIX_TILES = frozenset((0, 1, 2, 3, 4, 5, 10, 12, 13, 18, 19, 20, 21, 22, 23, 24, 27))
 _FIX_POOL: dict = {}
 _FIX_POOL_INTS = 1 << 20
 
