@@ -496,7 +496,14 @@ def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, 
                     dw2[g * s.Kg:(g + 1) * s.Kg].copy_(tmp[:s.Kg, :kred])
 
 
-FP8_WGRAD_BIAS = os.environ.get("SN_FP8_WGRAD_BIAS", "0") == "1"  # exact bias gradient by default
+# Bias gradient of the fp8 weight-gradient products.  1 (default): a virtual e4m3 ones column
+# of the product, i.e. the column sum of the QUANTISED output gradient (e4m3 / e5m2 with the
+# tensor's delayed scale: small entries are rounded or flushed); 0: an exact column sum of the
+# bf16 output gradient in a separate pass.  Measured on VGG-16 b2048 fp8, one box
+# (profiles/r5_fp8_bias_ab.txt): the separate pass reads every dy once more (6.3 ms / step,
+# 11.27-11.31k vs 11.51-11.55k img/s) and tests/test_fp8_fidelity_gpu.py passes both ways
+# (max deviation 0.071 exact vs 0.093 quantised, bound 0.234).
+FP8_WGRAD_BIAS = os.environ.get("SN_FP8_WGRAD_BIAS", "1") == "1"
 
 
 def fp8_wgrad_ok(s: ConvSpec) -> bool:
@@ -528,14 +535,12 @@ def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc):
     gradient (e4m3 / e5m2, MC: [pixels][K]), B = the implicit im2col of the layer input's
     e4m3 copy kept from the forward (MC), both read transposed from LDS by
     ds_read_b64_tr_b8; fp32 accumulation, split-K slabs, dequantised epilogue.  The bias
-    gradient is, by default, an exact column sum of the bf16 dy (a separate pass); with
-    SN_FP8_WGRAD_BIAS=1 it rides on the product as an e4m3 ones column instead, i.e. the
-    column sum of the QUANTISED dy, whose small entries are rounded or flushed (reference:
-    base_conv_layer.cpp:338-376, conv_layer.cu:35-53)."""
+    gradient, by default, rides on the product as an e4m3 ones column, i.e. it is the column
+    sum of the QUANTISED dy, whose small entries are rounded or flushed; SN_FP8_WGRAD_BIAS=0
+    computes the exact column sum of the bf16 dy in a separate pass instead (FP8_WGRAD_BIAS;
+    reference: base_conv_layer.cpp:338-376, conv_layer.cu:35-53)."""
     sc, ix, xq, idy = f8w
-    # SN_FP8_WGRAD_BIAS=1: the bias gradient rides on the product as a virtual ones column of
-    # B (an e4m3 1.0, dequantised by dy's factor only) — the column sum of the QUANTISED
-    # output gradient — instead of the exact bf16 pass over dy (the default)
+    # the ones column of B is an e4m3 1.0 dequantised by dy's factor only
     fused_db = db is not None and kred % 16 == 0 and FP8_WGRAD_BIAS
     if db is not None and not fused_db:
         colsum(dy2, db, accumulate=db_acc)
