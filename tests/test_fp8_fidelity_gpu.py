@@ -16,23 +16,37 @@ test's own trajectories (profiles/r5_fp8_fidelity_ab.txt, lr 0.002, floor 0.023)
 + wgrad 0.125, without fp8 weight gradients 0.087, with the e4m3 bias column 0.112, without the
 amax history 0.114 — no single component carries the gap (e4m3's 3 mantissa bits make fp8 learn a
 little slower in the fastest-falling windows), and the production mode meets the original gate.
-The test runs at lr 0.002 and asserts every 20-step smoothed fp8 loss within
-max(0.15, 1.5 x the bf16-vs-bf16alt floor) of bf16 (the round-3 gate, restored) and fp8 ending
-below its starting loss.  The floor and the fp8 deviation are printed (pytest -s).
+Round 5, after the register-spill fix and with the weight-gradient bias back on the e4m3
+ones column (profiles/r5_fp8_bias_ab.txt, profiles/r5_fp8_fidelity_lr.txt): lr 0.002 floor
+0.156 / fp8 0.093; lr 0.005 floor 0.206 / fp8 0.122 — inside 1.5x the floor at the production
+rate (with the exact bf16 bias pass 0.362, outside).  The VERDICT's 0.1 at lr 0.002 holds on
+that box (0.093) but is not asserted: the trajectories depend on the first-call tuner's tile
+choices for these small shapes, and with every product on its cost-model tile instead (same
+run, SN_GEMM_AUTOTUNE off) fp8 deviates 0.234 at lr 0.002 against a 0.064 floor, and 0.108 at
+lr 0.005 against 0.303.  At lr 0.005 the outcome also varies between two processes on ONE box
+(the first-call timing picks other tiles): floor 0.063 / fp8 0.375 in one run, 0.206 / 0.122 in
+the next (profiles/r5_fp8_fidelity_lr.txt) — chaotic, so it is measured (SN_FP8_FID_LR=0.005:
+within 1.5 x the floor, fp8 learning) but not part of the default suite.  By default the test
+runs lr 0.002: every 20-step smoothed fp8 loss within max(0.15, 1.5 x the bf16-vs-bf16alt floor)
+of bf16 and fp8 ending below its start.  Floors and deviations are printed (pytest -s).
 
 The data is a learnable synthetic task (no datasets on the box): 10 fixed random class
 templates plus Gaussian noise (scripts/fp8_trajectory.py), so the loss falls from ln(10).
 The reference trains in fp32 only (libccaffe/ccaffe.h:3); parity with it is unpinned —
 the bf16 run is the yardstick."""
+import os
+
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
-STEPS, BATCH, CROP, CLASSES, LR, NOISE, WINDOW = 200, 64, 64, 10, 0.002, 0.8, 20
+STEPS, BATCH, CROP, CLASSES, NOISE, WINDOW = 200, 64, 64, 10, 0.8, 20
+# learning rates under test; SN_FP8_FID_LR overrides (sweeps: scripts/gpu_r5ad.sh, e.g. "0.002,0.005")
+LRS = [float(v) for v in os.environ.get("SN_FP8_FID_LR", "0.002").split(",")]
 
 
-def _trajectory(mode, dev, monkeypatch):
+def _trajectory(mode, dev, monkeypatch, lr):
     from sparknet_amd import models
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.engine import GraphStep, enable_fp8, fuse_relu
@@ -44,7 +58,7 @@ def _trajectory(mode, dev, monkeypatch):
     templates = torch.randn(CLASSES, 3, CROP, CROP, generator=g0)
     net_p = models.vgg16(train_batch=BATCH, test_batch=BATCH, crop=CROP, classes=CLASSES)
     sp = models.zoo.vgg16_solver(net_p)
-    sp.base_lr = LR
+    sp.base_lr = lr
     solver = Solver(sp, device=dev, seed=5, build_test_nets=False)
     fuse_relu(solver.net)
     n8 = enable_fp8(solver.net, 0.0, dgrad=True, wgrad=True) if mode == "fp8" else 0
@@ -65,17 +79,26 @@ def _smooth(v):
 
 
 @pytest.mark.timeout(900)
-def test_fp8_vgg16_200_steps_tracks_bf16(gpu, monkeypatch):
-    bf, _ = _trajectory("bf16", gpu, monkeypatch)
-    alt, _ = _trajectory("bf16alt", gpu, monkeypatch)
-    f8, n8 = _trajectory("fp8", gpu, monkeypatch)
+@pytest.mark.parametrize("lr", LRS)
+def test_fp8_vgg16_200_steps_tracks_bf16(gpu, monkeypatch, lr):
+    """lr 0.002 (stable): every window within max(0.15, 1.5 x floor) and fp8 ends below its start.
+    lr 0.005 (the production rate; bf16 itself spikes near the end and can end above its
+    start): every window within 1.5 x the bf16-vs-bf16alt floor, and fp8 learns (some window
+    below the first)."""
+    bf, _ = _trajectory("bf16", gpu, monkeypatch, lr)
+    alt, _ = _trajectory("bf16alt", gpu, monkeypatch, lr)
+    f8, n8 = _trajectory("fp8", gpu, monkeypatch, lr)
     assert n8 >= 30, n8  # forward, data-gradient and weight-gradient products run fp8
     sb, sa, s8 = _smooth(bf), _smooth(alt), _smooth(f8)
     floor = max(abs(a - b) for a, b in zip(sb, sa))
     dev = max(abs(a - b) for a, b in zip(sb, s8))
-    bound = max(0.15, 1.5 * floor)
-    print("bf16   ", [round(v, 3) for v in sb], "\nbf16alt", [round(v, 3) for v in sa],
+    stable = lr <= 0.002
+    bound = max(0.15, 1.5 * floor) if stable else 1.5 * floor
+    print(f"lr {lr}\nbf16   ", [round(v, 3) for v in sb], "\nbf16alt", [round(v, 3) for v in sa],
           "\nfp8    ", [round(v, 3) for v in s8], f"\nchaos floor {floor:.3f}  fp8 max dev {dev:.3f}  bound {bound:.3f}")
     assert all(v == v for v in f8), "fp8 loss went non-finite"
     assert dev <= bound, (dev, floor, sb, sa, s8)
-    assert s8[-1] < s8[0], (s8[0], s8[-1])
+    if stable:
+        assert s8[-1] < s8[0], (s8[0], s8[-1])
+    else:
+        assert min(s8[1:]) < s8[0], s8
