@@ -1,6 +1,7 @@
-// Direct 3x3 / stride-1 / pad-0 convolution with the reduction packed across taps: CaffeNet /
+// Direct stride-1 / pad-0 convolution with the reduction packed across taps: CaffeNet /
 // AlexNet conv1 after the space-to-depth fold (227 x 227 x 3, 11 x 11 / 4 -> 57 x 57 x 48,
-// 3 x 3 / 1, 96 outputs, 55 x 55).
+// 3 x 3 / 1, 96 outputs, 55 x 55), and GoogLeNet conv1 after its fold (224 x 224 x 3, 7 x 7 / 2,
+// pad 3 -> 115 x 115 x 16, 4 x 4 / 1, 64 outputs, 112 x 112) on a <4, 64> instance.
 //
 // The 64-channel direct kernel (conv3x3.hip, K = 96 instance) ran this product at 837 TF/s
 // of issued MFMA work but only 389 TF/s of useful work (profiles/r4_step_kernels_caffenet.txt:
@@ -24,45 +25,53 @@
 
 namespace {
 
-constexpr int TP = 192;                  // output pixels per tile (12 M fragments)
-constexpr int KOUT = 96;                 // output channels (6 N fragments)
-constexpr int KS = 14;                   // 32-wide K steps: up to 56 16-B chunks = 9 taps x 48 channels
-constexpr int W_BYTES = KS * 6 * 1024;   // 86016 B of fragment-ordered weights
-constexpr int PCAP = 38400;              // patch bytes per buffer (7 rows x 57 px x 96 B = 38304)
-constexpr int NT = 512, PER_T = (PCAP / 16 + NT - 1) / NT;
+constexpr int TP = 192;  // output pixels per tile (12 M fragments)
+constexpr int NT = 512;
 
 struct GeoP {
   int N, H, W, C;  // folded input (pad 0)
-  int P, Q;        // output = H - 2, W - 2
+  int P, Q;        // output = H - TAPS + 1, W - TAPS + 1
   int PR;          // input rows staged per tile
   int tpi;         // tiles per image
   long long tiles;
 };
 
+// TAPS x TAPS taps, KOUT output channels, KS 32-wide K steps (covering TAPS^2 x the largest C),
+// PCAP patch bytes per buffer.  Instances:
+//   <3, 96, 14, 38400>: CaffeNet / AlexNet conv1 after the 4x4 fold (57 x 57 x 48 -> 55 x 55 x 96;
+//                       up to 56 16-B chunks = 9 taps x 48 channels; 7 rows x 57 px x 96 B)
+//   <4, 64,  8, 22528>: GoogLeNet conv1 after the 2x2 fold (115 x 115 x 16 -> 112 x 112 x 64;
+//                       32 chunks = 16 taps x 16 channels; 6 rows x 115 px x 32 B)
+// 8 waves: wave (mi, ni) owns 48 pixels x KOUT / 2 channels (3 x KOUT / 32 MFMA fragments).
+template <int TAPS, int KOUT, int KS, int PCAP>
 __global__ void __launch_bounds__(NT, 1)
 conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const float* __restrict__ bias,
                    bf16_t* __restrict__ y, GeoP g, int relu) {
+  constexpr int NF = KOUT / 16, NFW = NF / 2;     // N fragments: all, per wave
+  constexpr int W_BYTES = KS * NF * 1024;         // fragment-ordered weights
+  constexpr int PER_T = (PCAP / 16 + NT - 1) / NT;
+  static_assert(NF % 2 == 0 && PCAP % 16 == 0, "two N halves, whole 16-B chunks");
   __shared__ __attribute__((aligned(16))) char smem[W_BYTES + 2 * PCAP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mi = wave & 3, ni = wave >> 2;
-  const int CB = g.C * 2, CH = g.C >> 3, KC = 9 * CH;  // pixel bytes, chunks per pixel, real chunks
+  const int CB = g.C * 2, CH = g.C >> 3, KC = TAPS * TAPS * CH;  // pixel bytes, chunks per pixel, real chunks
 
-  // weights w[96][3][3][C]: row n is the packed reduction k = tap * C + c; LDS chunk q =
-  // ((ks * 6 + nf) * 64 + lane) holds row nf * 16 + (lane & 15), chunk 4 ks + (lane >> 4)
-  for (int q = tid; q < KS * 6 * 64; q += NT) {
-    const int ks = q / 384, rem = q - ks * 384, nf = rem >> 6, l = rem & 63;
+  // weights w[KOUT][TAPS][TAPS][C]: row n is the packed reduction k = tap * C + c; LDS chunk q =
+  // ((ks * NF + nf) * 64 + lane) holds row nf * 16 + (lane & 15), chunk 4 ks + (lane >> 4)
+  for (int q = tid; q < KS * NF * 64; q += NT) {
+    const int ks = q / (NF * 64), rem = q - ks * (NF * 64), nf = rem >> 6, l = rem & 63;
     const int n = nf * 16 + (l & 15), kc = ks * 4 + (l >> 4);
-    const uint4 v = kc < KC ? *reinterpret_cast<const uint4*>(w + (long long)n * 9 * g.C + kc * 8)
+    const uint4 v = kc < KC ? *reinterpret_cast<const uint4*>(w + (long long)n * TAPS * TAPS * g.C + kc * 8)
                             : make_uint4(0, 0, 0, 0);
     *reinterpret_cast<uint4*>(smem + q * 16) = v;
   }
-  // this lane's patch offset of K step ks: tap t = kc / CH at row t / 3, column t % 3, chunk
-  // kc % CH; the zero-weight tail chunks read tap 0's (finite) data
+  // this lane's patch offset of K step ks: tap t = kc / CH at row t / TAPS, column t % TAPS,
+  // chunk kc % CH; the zero-weight tail chunks read tap 0's (finite) data
   int koff[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int kc = ks * 4 + (lane >> 4);
-    const int t = kc / CH, cc = kc - t * CH, r = t / 3, s = t - r * 3;
+    const int t = kc / CH, cc = kc - t * CH, r = t / TAPS, s = t - r * TAPS;
     koff[ks] = kc < KC ? (r * g.W + s) * CB + cc * 16 : 0;
   }
   const int PQ = g.P * g.Q;
@@ -75,7 +84,7 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
     return reinterpret_cast<const char*>(x) + (((long long)n * g.H + r0) * g.W) * CB;
   };
 
-  long long tile = blockIdx.x;
+long long tile = blockIdx.x;
   if (tile < g.tiles) {
     int nch;
     const char* src = patch_src(tile, nch);
@@ -84,14 +93,14 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
   }
   __syncthreads();
 
-  const char* wb = smem + lane * 16 + ni * 3 * 1024;
-  // this lane's 12 output channels are the same in every tile: their bias values stay in
+  const char* wb = smem + lane * 16 + ni * NFW * 1024;
+  // this lane's 4 x NFW output channels are the same in every tile: their bias values stay in
   // registers (a per-tile global load of them stalled each epilogue on an L2 round trip)
-  float bv[3][4];
+  float bv[NFW][4];
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < NFW; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) bv[i][k] = bias ? bias[ni * 48 + i * 16 + (lane >> 4) * 4 + k] : 0.f;
+    for (int k = 0; k < 4; ++k) bv[i][k] = bias ? bias[ni * (KOUT / 2) + i * 16 + (lane >> 4) * 4 + k] : 0.f;
   int cur = 0;
   for (; tile < g.tiles; tile += gridDim.x) {
     const long long next = tile + gridDim.x;
@@ -114,15 +123,15 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
       pixb[j] = ((oh - r0) * g.W + ow) * CB;
     }
     const char* p = smem + W_BYTES + cur * PCAP;
-    f32x4 acc[3][3];
+    f32x4 acc[NFW][3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < NFW; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8_t fb[2][3], fa[2][3];
+    bf16x8_t fb[2][NFW], fa[2][3];
     auto load = [&](int ks, bf16x8_t* b, bf16x8_t* a) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) b[i] = *reinterpret_cast<const bf16x8_t*>(wb + (ks * 6 + i) * 1024);
+      for (int i = 0; i < NFW; ++i) b[i] = *reinterpret_cast<const bf16x8_t*>(wb + (ks * NF + i) * 1024);
 #pragma unroll
       for (int j = 0; j < 3; ++j) a[j] = *reinterpret_cast<const bf16x8_t*>(p + pixb[j] + koff[ks]);
     };
@@ -132,14 +141,14 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
       if (ks + 1 < KS) load(ks + 1, fb[(ks + 1) & 1], fa[(ks + 1) & 1]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < NFW; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks & 1][i], fa[ks & 1][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       // pin step ks's MFMAs before step ks + 2's reads: one step of fragments in flight
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < NFW; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) asm volatile("" : "+v"(acc[i][j])::"memory");
     }
@@ -161,8 +170,8 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
       if (m >= PQ) continue;
       bf16_t* yo = y + ((long long)n_img * PQ + m) * KOUT;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int ch = ni * 48 + i * 16 + (lane >> 4) * 4;
+      for (int i = 0; i < NFW; ++i) {
+        const int ch = ni * (KOUT / 2) + i * 16 + (lane >> 4) * 4;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if (bias) {
 #pragma unroll
@@ -180,19 +189,18 @@ conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, c
   }
 }
 
-}  // namespace
-
-// y[N][H-2][W-2][96] = conv3x3(x[N][H][W][C], w[96][3][3][C]) (+ bias, ReLU), stride 1, pad 0;
-// C a multiple of 8, at most 48.  Returns 3 for shapes outside the kernel.
-extern "C" int sn_conv_packed3x3(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N,
-                                 long long H, long long W, long long C, long long K, long long relu, hipStream_t st) {
+template <int TAPS, int KOUT, int KS, int PCAP>
+int launch_packed(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N, long long H,
+                  long long W, long long C, long long K, long long relu, hipStream_t st) {
   if (N <= 0 || H <= 0 || W <= 0) return 0;
-  if (K != KOUT || C <= 0 || C > 48 || C % 8 || H < 3 || W < 3 || W > 4096) return 3;
+  if (K != KOUT || C <= 0 || C % 8 || (long long)TAPS * TAPS * (C / 8) > 4LL * KS || H < TAPS || W < TAPS ||
+      W > 4096)
+    return 3;
   GeoP g;
   g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C;
-  g.P = g.H - 2; g.Q = g.W - 2;
-  // output rows a run of TP pixels can touch, + the two extra input rows of the 3 x 3 window
-  g.PR = (TP - 1 + g.Q - 1) / g.Q + 1 + 2;
+  g.P = g.H - TAPS + 1; g.Q = g.W - TAPS + 1;
+  // output rows a run of TP pixels can touch, + the TAPS - 1 extra input rows of the window
+  g.PR = (TP - 1 + g.Q - 1) / g.Q + 1 + (TAPS - 1);
   if (g.PR > g.H) g.PR = g.H;
   if ((long long)g.PR * g.W * g.C * 2 > PCAP) return 3;
   if ((long long)g.P * g.Q >= (1LL << 31) / KOUT) return 3;
@@ -200,6 +208,23 @@ extern "C" int sn_conv_packed3x3(const bf16_t* x, const bf16_t* w, const float* 
   g.tiles = N * g.tpi;
   const int cus = sn_cu_count();
   const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
-  hipLaunchKernelGGL(conv_packed_kernel, dim3((unsigned)grid), dim3(NT), 0, st, x, w, bias, y, g, (int)relu);
+  hipLaunchKernelGGL((conv_packed_kernel<TAPS, KOUT, KS, PCAP>), dim3((unsigned)grid), dim3(NT), 0, st, x, w, bias, y,
+                     g, (int)relu);
   return SN_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+// y[N][H-2][W-2][96] = conv3x3(x[N][H][W][C], w[96][3][3][C]) (+ bias, ReLU), stride 1, pad 0;
+// C a multiple of 8, at most 48.  Returns 3 for shapes outside the kernel.
+extern "C" int sn_conv_packed3x3(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N,
+                                 long long H, long long W, long long C, long long K, long long relu, hipStream_t st) {
+  return launch_packed<3, 96, 14, 38400>(x, w, bias, y, N, H, W, C, K, relu, st);
+}
+
+// y[N][H-3][W-3][64] = conv4x4(x[N][H][W][C], w[64][4][4][C]) (+ bias, ReLU), stride 1, pad 0;
+// C a multiple of 8, at most 16 (GoogLeNet conv1 after the 2x2 space-to-depth fold).
+extern "C" int sn_conv_packed4x4(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N,
+                                 long long H, long long W, long long C, long long K, long long relu, hipStream_t st) {
+  return launch_packed<4, 64, 8, 22528>(x, w, bias, y, N, H, W, C, K, relu, st);
 }

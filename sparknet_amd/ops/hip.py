@@ -235,6 +235,9 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
     if direct_io and packed_conv_ok(s):
         call("conv_packed3x3", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu))
         return y
+    if direct_io and packed44_conv_ok(s):
+        call("conv_packed4x4", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu))
+        return y
     if direct_io and direct_conv_ok(s):
         call("conv3x3_direct", x, _c(w), b, None, y, s.N, s.H, s.W, s.C, s.K, s.ph, int(relu))
         return y
@@ -291,6 +294,21 @@ def packed_conv_ok(s: ConvSpec) -> bool:
         return False
     rows = min(s.H, (191 + s.Q - 1) // s.Q + 3)  # input rows one 192-pixel tile touches
     return rows * s.W * s.C * 2 <= 38400 and s.P * s.Q * 96 < 2 ** 31
+
+
+# GoogLeNet conv1 after the 2x2 fold (115 x 115 x 16 -> 112 x 112 x 64, 4x4 taps, pad 0) on the
+# same tap-packed direct kernel's <4, 64> instance: the input rows of a 192-pixel tile staged
+# once in LDS instead of the implicit GEMM's per-tap re-reads of its 256x64 tiles;
+# SN_CONV_PACKED44=0 returns it to the GEMM
+_PACKED44 = os.environ.get("SN_CONV_PACKED44", "1") != "0"
+
+
+def packed44_conv_ok(s: ConvSpec) -> bool:
+    if not (_PACKED44 and s.K == 64 and s.C in (8, 16) and s.groups == 1 and s.R == 4 and s.S == 4
+            and s.sh == 1 and s.sw == 1 and s.ph == 0 and s.pw == 0 and s.dh == 1 and s.dw == 1 and s.Q > 0):
+        return False
+    rows = min(s.H, (191 + s.Q - 1) // s.Q + 4)  # input rows one 192-pixel tile touches
+    return rows * s.W * s.C * 2 <= 22528 and s.P * s.Q * 64 < 2 ** 31
 
 
 # the e4m3 direct kernel (csrc/kernels/conv3x3_fp8.hip) for the same 64 -> 64 products under

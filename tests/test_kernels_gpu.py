@@ -358,6 +358,48 @@ def test_conv_packed_caffenet_conv1(gpu, monkeypatch):
     close(y, ref.permute(0, 2, 3, 1), 1e-2)
 
 
+@pytest.mark.parametrize("N,H,W,C", [(2, 115, 115, 16), (1, 20, 35, 16), (3, 9, 200, 8), (2, 4, 4, 16),
+                                     (8, 115, 115, 16)])
+@pytest.mark.parametrize("relu,bias", [(True, True), (False, False)])
+def test_conv_packed44_direct(gpu, N, H, W, C, relu, bias, monkeypatch):
+    """The tap-packed direct conv's <4 taps, 64 outputs> instance (GoogLeNet conv1 after the
+    2x2 fold is (N, 115, 115, 16)): ragged last tiles, a 4 x 4 image (one output pixel), wide rows,
+    C = 8 (zero-weight K tail), more tiles than CUs (N = 8: 528 tiles), against the fp32
+    reference and the implicit-GEMM path."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    monkeypatch.setattr(hip, "_PACKED44", True)
+    s = ConvSpec(N, H, W, C, 64, 4, 4, 1, 1, 0, 0, 1, 1, 1)
+    assert hip.packed44_conv_ok(s)
+    x = rnd(N, H, W, C)
+    w = rnd(64, 4, 4, C, scale=0.1)
+    b = torch.randn(64, device="cuda") if bias else None
+    y = hip.conv_forward(x, w, b, s, relu=relu)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b)
+    if relu:
+        ref = torch.relu(ref)
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+    monkeypatch.setattr(hip, "_PACKED44", False)
+    close(y, hip.conv_forward(x, w, b, s, relu=relu), 1e-2)
+
+
+def test_conv_packed44_googlenet_conv1(gpu, monkeypatch):
+    """GoogLeNet conv1 (224 x 224 x 3, 7 x 7 / 2, pad 3) through conv_forward: the 2x2
+    space-to-depth fold feeds the packed 4x4 kernel; against the fp32 reference."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    monkeypatch.setattr(hip, "_PACKED44", True)
+    s = ConvSpec(2, 224, 224, 3, 64, 7, 7, 2, 2, 3, 3, 1, 1, 1)
+    plan = hip.s2d_plan(s)
+    assert plan is not None and hip.packed44_conv_ok(plan[4])
+    x = rnd(2, 224, 224, 3)
+    w = rnd(64, 7, 7, 3, scale=0.05)
+    b = torch.randn(64, device="cuda")
+    y = hip.conv_forward(x, w, b, s, relu=True)
+    ref = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=2, padding=3))
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+
+
 def test_softmax_loss_and_accuracy(gpu):
     from sparknet_amd.ops import hip
     x = rnd(256, 1000, scale=2.0)
