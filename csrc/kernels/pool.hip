@@ -84,18 +84,37 @@ __global__ void avepool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
     const float inv = 1.f / (float)((he - hs) * (we - ws));
     hs = max(hs, 0); ws = max(ws, 0); he = min(he, g.H); we = min(we, g.W);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int h = hs; h < he; ++h)
-      for (int w = ws; w < we; ++w) {
-        const bf16_t* src = x + (((long long)n * g.H + h) * g.W + w) * g.C + c0;
-        if (VEC) {
-          float f[8];
-          unpack8(*reinterpret_cast<const uint4*>(src), f);
+    if (VEC) {
+      // the window in row-major order, 8 loads issued before any is summed (a load inside the
+      // data-dependent window loop waited for each one: GoogLeNet's 7 x 7 global average pool
+      // took 49 dependent L2 / HBM round trips per thread); same summation order as before
+      const int ww = we - ws, win = (he - hs) * ww;
+      int hh = hs, wq = ws;  // window position of the next load
+      for (int base = 0; base < win; base += 8) {
+        uint4 v[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) acc[k] += f[k];
-        } else {
-          acc[0] += bf2f(src[0]);
+        for (int u = 0; u < 8; ++u) {
+          const bool ok = base + u < win;
+          v[u] = *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + (ok ? hh : hs)) * g.W + (ok ? wq : ws)) * g.C + c0);
+          if (ok && ++wq == we) {
+            wq = ws;
+            ++hh;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (base + u < win) {
+            float f[8];
+            unpack8(v[u], f);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += f[k];
+          }
         }
       }
+    } else {
+      for (int h = hs; h < he; ++h)
+        for (int w = ws; w < we; ++w) acc[0] += bf2f(x[(((long long)n * g.H + h) * g.W + w) * g.C + c0]);
+    }
     const long long o = (long long)pix * g.C + c0;
     if (VEC) {
 #pragma unroll
@@ -522,6 +541,170 @@ static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long 
   return g;
 }
 
+// 3x3 / stride-1 max pooling through an LDS row band (GoogLeNet's Inception pool branches).
+// The per-output gathers (maxpool_fwd_k<3, 3>, pool_bwd_k<3, 3, true>) issue 9 global loads per
+// 16-byte output; each input row is fetched from L2 by the three rows of windows that use it, and
+// both ran at ~2.9 TB/s effective in isolation at GoogLeNet b128 (profiles/r5_pool_band.txt).  Tried
+// here (opt-in, slower — see band_shape):
+// one workgroup owns (image, run of R output rows, group of cg channel chunks): it stages the R + 2
+// input rows (all columns, its channel chunks) in LDS with one coalesced load each, then every
+// output reads its 9 window taps from LDS.  The windows are scanned (forward) and summed
+// (backward) in the order of the gathers, so the results are bitwise equal.
+struct BandGeom {
+  int R, cg, ngrp, nb;
+  FDiv fWcg, fQcg, fcg;
+};
+
+__global__ void __launch_bounds__(256) maxpool3s1_band(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                       uint8_t* __restrict__ mask, PoolGeom g, int gate, BandGeom b) {
+  extern __shared__ uint4 band[];  // (R + 2) x W x cg input chunks
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int wg = bid / b.ngrp, ch0 = (bid - wg * b.ngrp) * b.cg;
+  const int n = wg / b.nb, p0 = (wg - n * b.nb) * b.R;
+  const int rows = min(b.R, g.P - p0);
+  const int h0 = p0 - g.ph;  // input row of band row 0
+  const int wcg = g.W * b.cg;
+  const int items1 = (rows + 2) * wcg;
+  for (int it = threadIdx.x; it < items1; it += blockDim.x) {
+    const uint32_t r = udiv((uint32_t)it, b.fWcg);
+    const int rem = it - (int)r * wcg;
+    const uint32_t w = udiv((uint32_t)rem, b.fcg);
+    const int lc = rem - (int)w * b.cg;
+    const int h = h0 + (int)r;
+    if ((unsigned)h < (unsigned)g.H)
+      band[it] = *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + h) * g.W + w) * g.C + (ch0 + lc) * 8);
+  }
+  __syncthreads();
+  const int qcg = g.Q * b.cg;
+  const int items2 = rows * qcg;
+  for (int it = threadIdx.x; it < items2; it += blockDim.x) {
+    const uint32_t r = udiv((uint32_t)it, b.fQcg);
+    const int rem = it - (int)r * qcg;
+    const uint32_t q = udiv((uint32_t)rem, b.fcg);
+    const int lc = rem - (int)q * b.cg;
+    const int ws = (int)q - g.pw;
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const int h = h0 + (int)r + a;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int w = ws + c;
+        if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
+        float f[8];
+        unpack8(band[((int)r + a) * wcg + w * b.cg + lc], f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (f[k] > best[k]) { best[k] = f[k]; arg[k] = a * 3 + c; }
+      }
+    }
+    if (gate) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (!(best[k] > 0.f)) arg[k] = 255;
+    }
+    const long long o = (((long long)n * g.P + p0 + (int)r) * g.Q + q) * g.C + (ch0 + lc) * 8;
+    *reinterpret_cast<uint4*>(y + o) = pack8(best);
+    if (mask) {
+      uint2 m;
+      m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+      m.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+      *reinterpret_cast<uint2*>(mask + o) = m;
+    }
+  }
+}
+
+// backward: the workgroup owns R input rows; the windows covering them are pooled rows
+// hp0 - 2 .. hp0 + R - 1 (hp0 = first row + ph), staged with their argmax masks
+__global__ void __launch_bounds__(256) pool3s1_band_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                        bf16_t* __restrict__ dx, PoolGeom g, BandGeom b) {
+  extern __shared__ uint4 band[];  // (R + 2) x Q x cg gradient chunks, then as many uint2 masks
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int wg = bid / b.ngrp, ch0 = (bid - wg * b.ngrp) * b.cg;
+  const int n = wg / b.nb, h0 = (wg - n * b.nb) * b.R;
+  const int rows = min(b.R, g.H - h0);
+  const int pr0 = h0 + g.ph - 2;  // pooled row of band row 0
+  const int qcg = g.Q * b.cg;
+  const int items1 = (rows + 2) * qcg;
+  uint2* mband = reinterpret_cast<uint2*>(band + items1);
+  for (int it = threadIdx.x; it < items1; it += blockDim.x) {
+    const uint32_t r = udiv((uint32_t)it, b.fQcg);
+    const int rem = it - (int)r * qcg;
+    const uint32_t q = udiv((uint32_t)rem, b.fcg);
+    const int lc = rem - (int)q * b.cg;
+    const int p = pr0 + (int)r;
+    if ((unsigned)p < (unsigned)g.P) {
+      const long long o = (((long long)n * g.P + p) * g.Q + q) * g.C + (ch0 + lc) * 8;
+      band[it] = *reinterpret_cast<const uint4*>(dy + o);
+      mband[it] = *reinterpret_cast<const uint2*>(mask + o);
+    }
+  }
+  __syncthreads();
+  const int wcg = g.W * b.cg;
+  const int items2 = rows * wcg;
+  for (int it = threadIdx.x; it < items2; it += blockDim.x) {
+    const uint32_t r = udiv((uint32_t)it, b.fWcg);
+    const int rem = it - (int)r * wcg;
+    const uint32_t w = udiv((uint32_t)rem, b.fcg);
+    const int lc = rem - (int)w * b.cg;
+    const int h = h0 + (int)r;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // windows p = h + ph - 2 .. h + ph (band rows r .. r + 2), q = w + pw - 2 .. w + pw, ascending
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int p = pr0 + (int)r + t;
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int q = (int)w + g.pw - 2 + u;
+        if ((unsigned)p >= (unsigned)g.P || (unsigned)q >= (unsigned)g.Q) continue;
+        const int widx = (2 - t) * 3 + (2 - u);  // this pixel's offset inside window (p, q)
+        const int li = ((int)r + t) * qcg + q * b.cg + lc;
+        float f[8];
+        unpack8(band[li], f);
+        const uint2 mv = mband[li];
+        const uint32_t mw[2] = {mv.x, mv.y};
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if ((int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == widx) acc[k] += f[k];
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + (((long long)n * g.H + h) * g.W + w) * g.C + (ch0 + lc) * 8) = pack8(acc);
+  }
+}
+
+// Band shape: cg = the largest divisor of the C / 8 chunks that is <= 8 (128-byte runs), then the
+// most rows whose (R + 2)-row tile fits SN_POOL_BAND_LDS bytes (default 40 KB).  Opt-in
+// (SN_POOL_BAND=1): 10-20 % SLOWER than the gathers at every GoogLeNet shape (3a forward 38.3 vs
+// 33.5 us, backward 41.1 vs 33.8; GoogLeNet 22.09-22.16 vs 22.25-22.30 k img/s,
+// profiles/r5_pool_band.txt) — the gathers' re-reads hit L2 and the band's load / barrier /
+// compute phases serialise within a workgroup.
+static bool band_shape(long long rows_total, long long width, long long C, int item_bytes, BandGeom* b) {
+  const char* e = std::getenv("SN_POOL_BAND");
+  if (!e || std::atoi(e) == 0) return false;
+  const char* lb = std::getenv("SN_POOL_BAND_LDS");
+  const long long budget = lb ? std::atoll(lb) : 40 * 1024;
+  const int cv = (int)(C / 8);
+  int cg = 1;
+  for (int c = 8; c >= 1; --c)
+    if (cv % c == 0) { cg = c; break; }
+  const long long per_row = width * cg * item_bytes;
+  long long R = budget / per_row - 2;
+  if (R < 2) return false;
+  if (R > rows_total) R = rows_total;
+  // balance the bands: the fewest bands of this height, then the shortest height giving as many
+  const long long nbands = (rows_total + R - 1) / R;
+  R = (rows_total + nbands - 1) / nbands;
+  b->R = (int)R;
+  b->cg = cg;
+  b->ngrp = cv / cg;
+  b->nb = (int)nbands;
+  b->fcg = make_fdiv((uint32_t)cg);
+  return true;
+}
+
 // SN_POOL_K2S2=1: 2x2 / stride-2 max-pool backward with one thread per window block.  Opt-in:
 // 6 % faster on VGG's two largest pools at b256 but slower on the small ones, VGG-16 b2048 fp8
 // unchanged (11.31 vs 11.32 k img/s, profiles/r4_pool_block_ab.txt)
@@ -552,7 +735,15 @@ extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long 
   const bool vec = (C % 8) == 0;
   long long total = N * P * Q * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
-  if (method == 0 && vec && kh == kw && (kh == 2 || kh == 3)) {
+  BandGeom bg{};
+  if (method == 0 && vec && !q && kh == 3 && kw == 3 && sh == 1 && sw == 1 && P == H + 2 * ph - 2 &&
+      Q == W + 2 * pw - 2 && band_shape(P, W, C, 16, &bg)) {
+    bg.fWcg = make_fdiv((uint32_t)(W * bg.cg));
+    bg.fQcg = make_fdiv((uint32_t)(Q * bg.cg));
+    const size_t lds = (size_t)(bg.R + 2) * W * bg.cg * 16;
+    hipLaunchKernelGGL(maxpool3s1_band, dim3((unsigned)(N * bg.nb * bg.ngrp)), dim3(256), lds, st, x, y, mask, g,
+                       (int)gate, bg);
+  } else if (method == 0 && vec && kh == kw && (kh == 2 || kh == 3)) {
     if (kh == 3 && sh == 1 && sw == 1 && k3s1_ok()) {
       const int BP = (int)((P + 1) / 2), BQ = (int)((Q + 1) / 2);
       const long long nt = N * BP * BQ * (C / 8);
@@ -565,8 +756,12 @@ extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long 
     if (vec) hipLaunchKernelGGL(maxpool_fwd<true>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
     else hipLaunchKernelGGL(maxpool_fwd<false>, grid, dim3(256), 0, st, x, y, mask, g, (int)gate);
   } else {
-    if (vec) hipLaunchKernelGGL(avepool_fwd<true>, grid, dim3(256), 0, st, x, y, g);
-    else hipLaunchKernelGGL(avepool_fwd<false>, grid, dim3(256), 0, st, x, y, g);
+    // one-wave blocks when the output is small: GoogLeNet's global 7 x 7 pool has 16384 threads
+    // (64 blocks of 256 left 3/4 of the CUs idle)
+    const int bs = total < 256 * 1024 ? 64 : 256;
+    const dim3 ag(sn_blocks(total, bs, 16384));
+    if (vec) hipLaunchKernelGGL(avepool_fwd<true>, ag, dim3(bs), 0, st, x, y, g);
+    else hipLaunchKernelGGL(avepool_fwd<false>, ag, dim3(bs), 0, st, x, y, g);
   }
   return SN_CHECK_LAUNCH();
 }
@@ -659,6 +854,13 @@ extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, lo
     const long long nt = N * BH * BW * (C / 8);
     hipLaunchKernelGGL(pool_bwd_k2s2, dim3(sn_blocks(nt, 256, 16384)), dim3(256), 0, st, dy, mask, dx, g,
                        make_fdiv((uint32_t)BW), make_fdiv((uint32_t)BH), BW, BH, qs);
+  } else if (BandGeom bg{}; vec && method == 0 && !q && kh == 3 && kw == 3 && sh == 1 && sw == 1 &&
+             P == H + 2 * ph - 2 && Q == W + 2 * pw - 2 && band_shape(H, Q, C, 24, &bg)) {
+    bg.fWcg = make_fdiv((uint32_t)(W * bg.cg));
+    bg.fQcg = make_fdiv((uint32_t)(Q * bg.cg));
+    const size_t lds = (size_t)(bg.R + 2) * Q * bg.cg * 24;
+    hipLaunchKernelGGL(pool3s1_band_bwd, dim3((unsigned)(N * bg.nb * bg.ngrp)), dim3(256), lds, st, dy, mask, dx, g,
+                       bg);
   } else if (vec && method == 0 && kh == 3 && kw == 3 && sh == 1 && sw == 1 && ph <= 2 && pw <= 2 && k3s1_ok()) {
     if (q && !(qslot && qpart)) return 9;
     const int BH = (int)((H + 1) / 2), BW = (int)((W + 1) / 2);

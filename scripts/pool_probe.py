@@ -36,6 +36,8 @@ def timed(fn, reps=10, passes=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--only", default="", help="comma-separated substrings of the shape names to run")
+    ap.add_argument("--reps", type=int, default=10)
     args = ap.parse_args()
     from sparknet_amd.ops import _lib
     from sparknet_amd.ops import hip  # noqa: F401
@@ -44,7 +46,11 @@ def main():
     B = args.batch
     shapes = [("vgg pool1", 224, 64, 2, 2, 0), ("vgg pool2", 112, 128, 2, 2, 0), ("vgg pool3", 56, 256, 2, 2, 0),
               ("vgg pool4", 28, 512, 2, 2, 0), ("vgg pool5", 14, 512, 2, 2, 0),
-              ("gn 3a pool 3x3/1", 28, 192, 3, 1, 1), ("gn pool3 3x3/2", 28, 480, 3, 2, 0)]
+              ("gn 3a pool 3x3/1", 28, 192, 3, 1, 1), ("gn 3b pool 3x3/1", 28, 256, 3, 1, 1),
+              ("gn 4a pool 3x3/1", 14, 480, 3, 1, 1), ("gn 5a pool 3x3/1", 7, 832, 3, 1, 1),
+              ("gn pool3 3x3/2", 28, 480, 3, 2, 0)]
+    if args.only:
+        shapes = [sh for sh in shapes if any(o in sh[0] for o in args.only.split(","))]
     for name, H, C, k, s, pad in shapes:
         P = (H + 2 * pad - k + s - 1) // s + 1
         if (P - 1) * s >= H + pad:
@@ -65,7 +71,7 @@ def main():
             _lib.check(lib.sn_pool_bwd(*[_lib.C.c_void_p(t.data_ptr()) for t in (dy, mask, dx)],
                                        *[_lib.C.c_longlong(v) for v in (B, H, H, C, P, P, k, k, s, s, pad, pad, 0)],
                                        None, None, None, _lib.C.c_longlong(0), _lib.C.c_void_p(st)), "pool_bwd")
-        tf, tb = timed(fwd), timed(bwd)
+        tf, tb = timed(fwd, args.reps), timed(bwd, args.reps)
         bf = x.numel() * 2 + y.numel() * 3
         bb = dy.numel() * 3 + dx.numel() * 2
         print(f"{name:18s} B={B} {H}x{H}x{C} -> {P}x{P}: fwd {tf:8.1f} us {bf / tf / 1e6:5.2f} TB/s | "

@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--out", required=True)
     ap.add_argument("--margin", type=float, default=0.97)
+    ap.add_argument("--wide", action="store_true", help="also try split-K 1-256 (powers of 2 and x1.5) on every tile")
     args = ap.parse_args()
     import bench
     from sparknet_amd import models
@@ -135,7 +136,18 @@ def main():
         t_old = timed(lambda: run(tile, splits, kchunk), reps)
         best = (t_old, tile, splits, kchunk)
         b_kc_dense = b_mc == 0 and b_mode == G.OP_DENSE
-        for t, s, kc in G._candidates(M, N, K, groups, b_kc_dense, epi):
+        cands = G._candidates(M, N, K, groups, b_kc_dense, epi)
+        if args.wide:
+            extra = []
+            for t in dict.fromkeys(c[0] for c in cands):
+                for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256):
+                    kc = -(-(-(-K // s)) // G.BK) * G.BK
+                    s2 = max(1, -(-K // kc))
+                    if s2 > 1 and s2 * M * N * groups * 4 > (256 << 20):
+                        continue
+                    extra.append((t, s2, kc))
+            cands = list(dict.fromkeys(cands + extra))
+        for t, s, kc in cands:
             if (t, s) == (tile, splits):
                 continue
             try:

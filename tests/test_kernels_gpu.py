@@ -141,7 +141,9 @@ def test_linear(gpu, M, K, N):
 @pytest.mark.parametrize("geo", [(2, 55, 55, 96, 3, 2, 0), (2, 32, 32, 32, 3, 2, 0), (2, 8, 8, 24, 3, 2, 1),
                                  (2, 7, 7, 16, 7, 1, 0), (2, 6, 6, 3, 2, 2, 0), (2, 9, 9, 16, 3, 1, 1),
                                  (2, 8, 8, 16, 2, 2, 0), (2, 13, 13, 32, 3, 2, 1), (2, 7, 9, 16, 2, 2, 0),
-                                 (2, 8, 8, 16, 2, 2, 1)])
+                                 (2, 8, 8, 16, 2, 2, 1), (2, 14, 14, 64, 5, 3, 0),
+                                 (2, 14, 14, 480, 3, 1, 1), (3, 7, 7, 832, 3, 1, 1), (2, 28, 28, 40, 3, 1, 1),
+                                 (2, 11, 13, 24, 3, 1, 0), (2, 6, 6, 8, 3, 1, 2)])
 def test_pool(gpu, method, geo):
     from sparknet_amd.ops import hip
     N, H, W, Cc, k, st, pd = geo
@@ -151,6 +153,26 @@ def test_pool(gpu, method, geo):
     close(y, ref.pool_forward(x, s), 1e-2)
     dy = rnd(N, s.P, s.Q, Cc)
     close(hip.pool_backward(dy, x, s, mask), ref.pool_backward(dy, x, s), 1e-2)
+
+
+@pytest.mark.parametrize("geo", [(2, 28, 28, 192, 1), (2, 14, 14, 480, 1), (4, 7, 7, 832, 1), (2, 9, 11, 24, 0),
+                                 (2, 5, 5, 16, 2)])
+def test_pool3s1_band_bitwise(gpu, geo, monkeypatch):
+    """The opt-in LDS-band 3x3 / stride-1 max pool (SN_POOL_BAND=1, forward + backward) is bitwise
+    equal to the default per-output gathers, ties included."""
+    from sparknet_amd.ops import hip
+    N, H, W, Cc, pd = geo
+    s = PoolSpec(N, H, W, Cc, 3, 3, 1, 1, pd, pd, POOL_MAX)
+    x = rnd(N, H, W, Cc)
+    x[0, 0, :2] = 0.0  # ties
+    dy = rnd(N, s.P, s.Q, Cc)
+    out = {}
+    for band in ("1", "0"):
+        monkeypatch.setenv("SN_POOL_BAND", band)
+        y, mask = hip.pool_forward_mask(x, s)
+        out[band] = (y, mask, hip.pool_backward(dy, x, s, mask))
+    for a, b in zip(out["1"], out["0"]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("within", [False, True])
