@@ -23,6 +23,11 @@ typedef uint16_t bf16_t;  // raw storage type of a bf16 element
 
 SN_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
+// s^-beta for the LRN scales (s >= k > 0, never denormal): v_log_f32 (log2) and v_exp_f32 (2^x)
+// directly.  __expf(-beta * __logf(s)) expanded to ~16 VALU ops (denormal range scaling, an
+// extended-precision ln 2 product) and made the LRN kernels VALU-bound (profiles/r5_lrn_pow.txt).
+SN_DEV float sn_powneg(float s, float beta) { return __builtin_amdgcn_exp2f(-beta * __builtin_amdgcn_logf(s)); }
+
 // Round-to-nearest-even f32 -> bf16 (hipcc lowers the __bf16 cast to v_cvt_pk_bf16_f32,
 // which keeps NaNs NaN — see MI355X_MICROARCH "Correctness boundaries").
 SN_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }

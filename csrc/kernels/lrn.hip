@@ -24,7 +24,7 @@ struct LrnP {
   int gate;  // backward: zero dx where x <= 0 (the in-place ReLU that produced x, fused)
 };
 
-SN_DEV float powneg(float s, float beta) { return __expf(-beta * __logf(s)); }
+SN_DEV float powneg(float s, float beta) { return sn_powneg(s, beta); }
 
 // Load the 24 channels [c0-8, c0+16) of a pixel as fp32 (zeros outside [0, C)).  The
 // three 16-B loads are unconditional (clamped chunk index) and masked afterwards, so
@@ -95,7 +95,6 @@ __global__ void lrn_across_bwd(const bf16_t* __restrict__ x, const bf16_t* __res
     float r[24];
 #pragma unroll
     for (int j = 8 - POST; j < 16 + PRE; ++j) {
-      const int c = c0 - 8 + j;
       float s = 0.f;
 #pragma unroll
       for (int d = 0; d < SIZE; ++d) {
@@ -103,7 +102,8 @@ __global__ void lrn_across_bwd(const bf16_t* __restrict__ x, const bf16_t* __res
         s += e * e;
       }
       float sc = p.k + a * s;
-      r[j] = (c >= 0 && c < p.C) ? gv[j] * xv[j] * powneg(sc, p.beta + 1.f) : 0.f;
+      // channels outside [0, C) have x = dy = 0 (load24), so r is 0 there without a branch
+      r[j] = gv[j] * xv[j] * powneg(sc, p.beta + 1.f);
       if (j >= 8 && j < 16) gv[j] = gv[j] * powneg(sc, p.beta);  // reuse: dy * scale^-beta
     }
     float o[8];

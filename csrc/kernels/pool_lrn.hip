@@ -34,7 +34,7 @@ struct PLGeom {
   FDiv fcv, fQ, fP, fcg, fQcg, fBWcg;
 };
 
-SN_DEV float plrn_pow(float s, float beta) { return __expf(-beta * __logf(s)); }
+SN_DEV float plrn_pow(float s, float beta) { return sn_powneg(s, beta); }
 
 template <int SIZE>
 __global__ void __launch_bounds__(256) pool_lrn_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ pooled,
@@ -176,7 +176,6 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
     float rr[24];
 #pragma unroll
     for (int j = 8 - POST; j < 16 + PRE; ++j) {
-      const int c = c0 - 8 + j;
       float s = 0.f;
 #pragma unroll
       for (int d = 0; d < SIZE; ++d) {
@@ -184,7 +183,8 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
         s += e * e;
       }
       float sc = g.k + a * s;
-      rr[j] = (c >= 0 && c < g.C) ? gv[j] * xv[j] * plrn_pow(sc, g.beta + 1.f) : 0.f;
+      // channels outside [0, C) have x = dy = 0 (plrn_load24): rr is 0 there without a branch
+      rr[j] = gv[j] * xv[j] * plrn_pow(sc, g.beta + 1.f);
       if (j >= 8 && j < 16) gv[j] = gv[j] * plrn_pow(sc, g.beta);
     }
     float o[8];

@@ -16,6 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--iters", action="store_true", help="also list every iteration's wall, idle total and largest gap")
     args = ap.parse_args()
     path = args.path
     if os.path.isdir(path):
@@ -29,6 +30,22 @@ def main():
     if len(idx) < 2:
         print("fewer than two solver-update launches in the trace")
         return 1
+    if args.iters:
+        for j in range(len(idx) - 1):
+            its = rows[idx[j] + 1:idx[j + 1] + 1]
+            sp = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in its)
+            reach, rk, tot, big = sp[0][1], sp[0], 0, (0, None, None)
+            for x in sp[1:]:
+                if x[0] > reach:
+                    tot += x[0] - reach
+                    if x[0] - reach > big[0]:
+                        big = (x[0] - reach, rk, x)
+                if x[1] > reach:
+                    reach, rk = x[1], x
+            nm = (lambda k: k.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][-40:])
+            where = f"{nm(big[1][2])} -> {nm(big[2][2])}" if big[1] else ""
+            print(f"iter {j}: wall {(sp[-1][1] - sp[0][0]) / 1e3:8.1f} us, {len(its)} launches, idle {tot / 1e3:7.1f} us, "
+                  f"largest gap {big[0] / 1e3:7.1f} us {where}")
     a, b = idx[-2], idx[-1]
     it = rows[a + 1:b + 1]
     t0 = min(int(r["Start_Timestamp"]) for r in it)
