@@ -150,12 +150,15 @@ def main():
 
     from sparknet_amd.parallel import diag
     rccl_log = None
-    if world > 1 and dev.type == "cuda" and not args.share_gpu:
+    # SN_COMM_FORCE=1 under torch.distributed.run --nproc-per-node 1: the process group, the
+    # initial broadcast and every window's averaging all-reduce run over RCCL at world 1
+    force_comm = os.environ.get("SN_COMM_FORCE", "0") == "1" and "MASTER_ADDR" in os.environ
+    if (world > 1 or force_comm) and dev.type == "cuda" and not args.share_gpu:
         rccl_log = diag.rccl_debug_env()  # channels / transports for the JSON (RCCL debug log)
     if dev.type == "cuda":
         _lib.kernels()
     comm = (Comm(backend="gloo" if args.share_gpu else None, device=dev if dev.type == "cuda" else None,
-                 watchdog=True, timeout_s=600.0) if world > 1 else None)
+                 watchdog=True, timeout_s=600.0) if world > 1 or force_comm else None)
     bad = diag.check_placement(comm, args.gpus, args.share_gpu or dev.type != "cuda",
                                torch.cuda.current_device() if dev.type == "cuda" else local_rank, local_rank)
     if bad is not None:

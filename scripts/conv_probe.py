@@ -43,6 +43,9 @@ def timed(fn, reps=10, passes=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="gn_conv2,cn_conv3")
+    ap.add_argument("--tiles", default="-1,0,1,2,4,11,12,13,15,16,17,18,19")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--no-dense", action="store_true")
     args = ap.parse_args()
     from sparknet_amd.ops import gemm as G, hip
     from sparknet_amd.ops.spec import ConvSpec
@@ -58,13 +61,15 @@ def main():
         a = torch.randn(M, Kr, device=dev).to(torch.bfloat16)
         wf = w.reshape(K, Kr)
         res = []
-        for t in (-1, 0, 1, 2, 4, 11, 12, 13, 15, 16, 17, 18, 19):
+        for t in [int(v) for v in args.tiles.split(",")]:
             G._FORCE_TILE = t
             try:
-                tc = timed(lambda: hip.conv_forward(x, w, b, s, relu=True))
+                tc = timed(lambda: hip.conv_forward(x, w, b, s, relu=True), args.reps)
             except (RuntimeError, AssertionError, TypeError):
                 tc = None
             try:
+                if args.no_dense:
+                    raise RuntimeError("skipped")
                 y = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
                 td = timed(lambda: G.gemm(M, K, Kr, G.Dense(a, Kr, True), G.Dense(wf, Kr, True), y, K,
                                           epi=G.EPI_BF16, bias=b, relu=True, splits=None if t < 0 else 1))

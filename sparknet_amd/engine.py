@@ -1203,7 +1203,7 @@ class LocalSGDTrainer:
 
     def broadcast_initial(self) -> None:
         """All ranks start from rank 0's initial weights (CifarApp.scala:92)."""
-        if self.comm is not None and self.comm.world_size > 1:
+        if self.comm is not None and getattr(self.comm, "active", self.comm.world_size > 1):
             self.comm.broadcast_params(self.solver.net)
 
     def local_step(self):
@@ -1216,7 +1216,7 @@ class LocalSGDTrainer:
             return loss
 
     def average(self) -> None:
-        if self.comm is not None and self.comm.world_size > 1:
+        if self.comm is not None and getattr(self.comm, "active", self.comm.world_size > 1):
             with trace_range("allreduce"):
                 self.comm.average_params(self.solver.net)
 

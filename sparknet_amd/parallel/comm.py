@@ -125,9 +125,13 @@ class Comm:
         self.bucket_bytes = bucket_bytes
         self.average_bucket_bytes = AVERAGE_BUCKET_BYTES
         self.watchdog = None
+        # SN_COMM_FORCE=1: set up the process group and run every collective even at world 1
+        # (one GPU under torch.distributed.run --nproc-per-node 1): an RCCL rehearsal of the
+        # scaling path's exact call pattern on a single-GPU box (scripts/gpu_r5ap.sh)
+        force = os.environ.get("SN_COMM_FORCE", "0") == "1" and "MASTER_ADDR" in os.environ
         if dist.is_available() and dist.is_initialized():
             self.owns = False
-        elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        elif int(os.environ.get("WORLD_SIZE", "1")) > 1 or force:
             if backend is None:
                 backend = "nccl" if torch.cuda.is_available() else "gloo"
             kw = {}
@@ -140,6 +144,8 @@ class Comm:
         self.world_size = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.backend = dist.get_backend() if dist.is_initialized() else None
+        # collectives run when there is more than one rank, or when forced at world 1
+        self.active = self.world_size > 1 or (force and dist.is_initialized())
         if watchdog and self.world_size > 1 and "MASTER_PORT" in os.environ:
             self.watchdog = Watchdog(self.rank, self.world_size)
 
@@ -151,12 +157,12 @@ class Comm:
             yield flat[s:s + per]
 
     def barrier(self) -> None:
-        if self.world_size > 1:
+        if self.active:
             dist.barrier()
 
     # -- parameter sync -------------------------------------------------------------------
     def broadcast_params(self, net, src: int = 0) -> None:
-        if self.world_size == 1:
+        if not self.active:
             return
         for b in self._buckets(net.flat_data):
             dist.broadcast(b, src)
@@ -179,7 +185,7 @@ class Comm:
         scaling of bucket i runs on the compute stream while bucket i+1 is still on the
         wire.  Returns the host-side issue time per bucket (ms; GPU timing is the
         caller's, e.g. bench.py's events)."""
-        if self.world_size == 1:
+        if not self.active:
             return []
         import time
         flat = net.flat_data
@@ -202,14 +208,14 @@ class Comm:
 
     def allreduce_grads(self, net, average: bool = True) -> None:
         """Synchronous data-parallel SGD: sum (or average) the flat gradient buffer."""
-        if self.world_size == 1:
+        if not self.active:
             return
         self.allreduce_sum(net.flat_diff)
         if average:
             _scale(net.flat_diff, None, 1.0 / self.world_size)
 
     def allreduce_scores(self, scores: list[float], device=None) -> list[float]:
-        if self.world_size == 1:
+        if not self.active:
             return list(scores)
         t = torch.tensor(list(scores), dtype=torch.float64 if device is None else torch.float32,
                          device=device or "cpu")
@@ -219,7 +225,7 @@ class Comm:
         return t.cpu().tolist()
 
     def allgather_int(self, v: int) -> list[int]:
-        if self.world_size == 1:
+        if not self.active:
             return [v]
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
         t = torch.tensor([v], dtype=torch.int64, device=dev)
@@ -228,7 +234,7 @@ class Comm:
         return [int(x.item()) for x in out]
 
     def allgather_float(self, v: float) -> list[float]:
-        if self.world_size == 1:
+        if not self.active:
             return [v]
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
         t = torch.tensor([v], dtype=torch.float64, device=dev)
@@ -237,7 +243,7 @@ class Comm:
         return [float(x.item()) for x in out]
 
     def max_over_ranks(self, v: float) -> float:
-        if self.world_size == 1:
+        if not self.active:
             return v
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
         t = torch.tensor([v], dtype=torch.float64 if dev == "cpu" else torch.float32, device=dev)
@@ -310,7 +316,7 @@ class SyncSGDCallback:
         self.comm, self.net = comm, net
         self.works = []
         self.plan = None
-        if overlap and comm.world_size > 1:
+        if overlap and comm.active:
             self.plan, self.late = grad_buckets(net, bucket_bytes)
             net.backward_hooks.append(self._hook)
 

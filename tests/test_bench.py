@@ -70,3 +70,33 @@ def test_bench_under_torchrun_like_the_driver():
     assert len(lines) == 1, r.stdout  # rank 0 prints the job line
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["config"]["parallelism"] == "dp2"
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def test_bench_forced_comm_at_world_one():
+    """SN_COMM_FORCE=1 under a one-process torch.distributed.run: the process group, the
+    initial broadcast, every averaging all-reduce and the post-window diagnostics run at world
+    1 (on a GPU box this is the RCCL rehearsal of the scaling path, scripts/gpu_r5ap.sh)."""
+    env = _clean_env()
+    env["SN_COMM_FORCE"] = "1"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1",
+                        "--verify-average", *ARGS], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["n_gpus"] == 1 and out["rccl_world"] == 1 and out["comm_backend"] == "gloo"
+    assert out["averages_in_window"] >= 1 and out["average_buckets"] >= 1
+    assert out["avg_check"]["masters_equal_across_ranks"] and out["avg_check"]["shadow_is_bf16_master"]
+    assert set(out["comm_bench"]) == {"bucket_256MB", "bucket_64MB", "bucket_16MB"}
+
+
+def test_comm_inactive_at_world_one_without_force():
+    from sparknet_amd.parallel.comm import Comm
+    c = Comm()
+    assert c.world_size == 1 and not c.active
