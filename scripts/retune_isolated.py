@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--margin", type=float, default=0.97)
     ap.add_argument("--wide", action="store_true", help="also try split-K 1-256 (powers of 2 and x1.5) on every tile")
+    ap.add_argument("--tiles", default="", help="only try these candidate tiles (comma-separated), e.g. 21,22")
     args = ap.parse_args()
     import bench
     from sparknet_amd import models
@@ -147,6 +148,9 @@ def main():
                         continue
                     extra.append((t, s2, kc))
             cands = list(dict.fromkeys(cands + extra))
+        if args.tiles:
+            only = {int(v) for v in args.tiles.split(",")}
+            cands = [c for c in cands if c[0] in only]
         for t, s, kc in cands:
             if (t, s) == (tile, splits):
                 continue

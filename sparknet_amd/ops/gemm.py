@@ -521,7 +521,8 @@ _AUTOTUNE = os.environ.get("SN_GEMM_AUTOTUNE", "1") != "0"
 _TUNED: dict = {}
 _TUNE_LOG = os.environ.get("SN_GEMM_TUNE_LOG", "0") == "1"
 _TUNE_PASSES = int(os.environ.get("SN_GEMM_TUNE_PASSES", "3"))
-# The 64-row tiles (21, 22) are autotune candidates for products with M <= 64 (SN_GEMM_THIN=0
+# The 64-row tiles (21, 22) are autotune candidates for products with M <= 64, or whose M they
+# pad less than 128-row tiles do (SN_GEMM_THIN=0
 # drops them).  SN_GEMM_THIN_RETUNE=1 also re-times such products' database choice against
 # them on first use (off by default: database entries stay authoritative and reproducible).
 # Round 4 made the tiles opt-in after cifar10_quick stopped learning when its conv1 weight
@@ -608,7 +609,11 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
             tiles.append(17)
     if epi != EPI_SGD and N >= 64:
         tiles.append(20)  # 3-stage 128x64: dense NT / NN (InnerProduct fwd / dgrad), MC x MC (weight gradients)
-    if M <= 64 and _THIN:  # 64-row tiles: thin weight gradients (64-channel convs, Inception reduce layers)
+    if _THIN and (M <= 64 or -(-M // 64) * 64 < -(-M // 128) * 128):
+        # 64-row tiles: thin weight gradients (64-channel convs, Inception reduce layers), and
+        # any M that 64-row tiles pad less than 128-row ones (M = 192: 3 x 64 rows instead of
+        # 2 x 128, a quarter of every MFMA idle — AlexNet conv4's grouped weight gradient,
+        # GoogLeNet's 192-, 160-, 320-channel convs)
         tiles += [21, 22]
     if epi != EPI_SGD:
         if _TILE64:
