@@ -278,18 +278,16 @@ static int plrn_fwd_pix(long long C) {
 // backward tile: for each channel group cg (a divisor of the C / 8 chunks, at least 4 chunks =
 // 64 B of a pixel, or the whole pixel) the most block rows (<= 7, least halo recomputation)
 // whose (rows + 1) x Q x cg tile fits the LDS budget (SN_PLRN_LDS bytes, default 32 KB); of
-// those, the most block rows (the fewest recomputed halo rows), then the grid closest to 2560
-// workgroups (10 per CU).  Measured on CaffeNet b256 (profiles/r4_plrn_tiles.txt,
-// profiles/r5_plrn_sweep.txt): pool1/norm1 74.4 -> 63.3 us (cg 12 -> 4), then 62.0 -> 56.5 us
-// once rows outrank the grid target (cg 12 x 3 rows at exactly 2560 workgroups lost to cg 4-6 x
-// 7 rows); pool2/norm2 45.4 -> 42.4 us (cg 16 -> 8).  SN_PLRN_CG forces the group size.
+// those, the shape whose grid is closest to 2560 workgroups (10 per CU: enough to fill every
+// CU with short blocks, few enough that the halo rows stay a small share).  Measured on CaffeNet
+// (profiles/r4_plrn_tiles.txt): pool1/norm1 74.4 -> 63.3 us (cg 12 -> 4), pool2/norm2 45.4 ->
+// 42.4 us (cg 16 -> 8).  SN_PLRN_CG forces the group size.
 static bool plrn_bwd_tile(long long N, long long Q, long long C, long long BH, int item_bytes, int* rows, int* cg) {
   const int cv = (int)(C / 8);
   const char* e = std::getenv("SN_PLRN_LDS");
   const long long budget = e ? std::atoll(e) : 32 * 1024;
   const char* fc = std::getenv("SN_PLRN_CG");
   double best = 1e30;
-  int best_rows = 0;
   bool found = false;
   for (int c = cv; c >= 1; --c) {
     if (cv % c) continue;
@@ -297,11 +295,9 @@ static bool plrn_bwd_tile(long long N, long long Q, long long C, long long BH, i
     int r = 7;
     while (r >= 1 && (long long)(r + 1) * Q * c * item_bytes > budget) --r;
     if (r < 1) continue;
-    const int rr = r < BH ? r : (int)BH;  // rows beyond the image do not reduce the halo share
     const double grid = (double)N * (double)((BH + r - 1) / r) * (double)(cv / c);
     const double d = std::fabs(std::log(grid / 2560.0));
-    if (rr > best_rows || (rr == best_rows && d < best - 1e-9)) {
-      best_rows = rr;
+    if (d < best - 1e-9) {
       best = d;
       *rows = r;
       *cg = c;
