@@ -22,6 +22,7 @@ class FakeComm:
         from sparknet_amd.parallel.comm import Comm
         self.other = other
         self.world_size, self.rank = 2, 0
+        self.active = True  # Comm.active: collectives run (world > 1)
         self.bucket_bytes = self.average_bucket_bytes = bucket_bytes
         self.bucket_ranges = Comm.bucket_ranges.__get__(self)
         self._avg = Comm.average_params.__get__(self)
