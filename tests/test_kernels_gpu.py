@@ -108,6 +108,27 @@ def test_flip_batch_matches_single_flips(gpu):
     assert torch.equal(items[0][1], r0)
 
 
+def test_flip_batch_vector_and_scalar_paths(gpu):
+    """The 16-byte form of flip_weights_multi (Kg, Cg multiples of 8, aligned tensors; partial
+    64 x 64 tiles) and its 2-byte fallback (odd channel counts, a weight view 2 bytes off
+    alignment) both equal the per-layer flip_weights kernel."""
+    from sparknet_amd.ops import _lib, hip
+    shapes = [(1, 72, 3, 3, 40), (2, 8, 5, 5, 136), (1, 20, 3, 3, 12), (1, 64, 3, 3, 64)]
+    items, refs = [], []
+    for i, (G, Kg, R, S, Cg) in enumerate(shapes):
+        n = G * Kg * R * S * Cg
+        base = rnd(n + 8)
+        w = base[1:n + 1] if i == 3 else base[:n]  # shape 3: misaligned view
+        wt = torch.empty((G, Cg, R, S, Kg), dtype=torch.bfloat16, device="cuda")
+        r = torch.empty_like(wt)
+        _lib.call("flip_weights", w.contiguous(), r, G, Kg, R, S, Cg)
+        items.append((w, wt, G, Kg, R, S, Cg))
+        refs.append(r)
+    hip.FlipBatch(items, "cuda").run()
+    for (_, wt, *_), r in zip(items, refs):
+        assert torch.equal(wt, r)
+
+
 @pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[8]])
 def test_conv_dgrad_inplace_weights(gpu, case, monkeypatch):
     """dgrad reading W through the FLIPW operand (no flip pass) == the reference."""
