@@ -815,6 +815,9 @@ def fp8_step(net) -> None:
         net.ctx.fp8.update()
 
 
+_DEPFREE_LRU = os.environ.get("SN_BRANCH_DEPFREE", "1") == "1"
+
+
 class BranchStreams:
     """Run independent branches of a DAG net on parallel HIP streams.
 
@@ -877,9 +880,14 @@ class BranchStreams:
             follow = [stream_of[d] for d in sorted(deps, reverse=True) if tail[stream_of[d]] == d]
             if follow:
                 sid = follow[0]
-            elif not deps:
+            elif not deps and (pos == 0 or not _DEPFREE_LRU):
                 sid = 0
             else:
+                # a node with no dependency (a loss head's backward: its
+                # top diff is the constant loss weight) takes the least recently used stream
+                # too, instead of queueing on the main stream behind the towers (GoogLeNet
+                # 22.36-22.42 -> 22.46-22.56 k img/s, profiles/r5_branch_depfree.txt;
+                # SN_BRANCH_DEPFREE=0: the main stream)
                 sid = min(range(self.n), key=lambda s: tail[s])
             if self.star and sid != 0 and any(stream_of[d] not in (0, sid) for d in deps):
                 sid = 0  # star topology: side streams only ever wait on the main stream
