@@ -828,8 +828,9 @@ class BranchStreams:
     from blob reads / writes (forward: bottoms -> tops; backward: top diffs + blob data ->
     bottom diffs + param diffs; read-after-write, write-after-read and write-after-write
     hazards), assigns every layer to one of ``n_streams`` streams (a layer continues the
-    stream of a producer it directly follows, otherwise takes the least recently used
-    stream) and joins streams with events.  Inside a hipGraph capture the events become
+    stream of a producer it directly follows, otherwise — also when it depends on nothing,
+    like an auxiliary loss head's backward — takes the least recently used stream) and
+    joins streams with events.  ``scripts/branch_sim.py`` simulates the plans on the CPU.  Inside a hipGraph capture the events become
     graph edges, so the towers of one Inception module run concurrently with no host
     involvement.  Every blob and gradient keeps its single producer, so results are
     bitwise identical to the sequential order.  Nets with backward hooks keep a
