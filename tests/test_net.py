@@ -337,26 +337,34 @@ def test_stochastic_pooling_train_samples_proportionally():
     assert torch.allclose(test.blobs[test.blob_names.index("y")].nchw(), torch.full((n, 1, 1, 1), 2.5))
 
 
-def test_branch_stream_plan_respects_dependencies():
+@pytest.mark.parametrize("aux, n_streams, star", [(False, 4, False), (True, 3, True), (True, 4, True)])
+def test_branch_stream_plan_respects_dependencies(aux, n_streams, star):
     """engine.BranchStreams: GoogLeNet's Inception towers are spread over several streams,
     and replaying the plan in stream order (each stream serial, cross-stream waits
     honoured) never runs a layer before the producers of what it reads or before the
-    readers / writers of what it overwrites."""
+    readers / writers of what it overwrites — also with the auxiliary loss heads, whose
+    backward depends on nothing and is placed on the least recently used stream, and in
+    the star topology (side streams wait on the main stream only)."""
     from sparknet_amd import models, proto
     from sparknet_amd.core.net import Net
     from sparknet_amd.engine import BranchStreams
-    n = models.googlenet(train_batch=1, test_batch=1, crop=67, classes=7, aux=False)
+    n = models.googlenet(train_batch=1, test_batch=1, crop=67 if not aux else 227, classes=7, aux=aux)
     for l in n.layer:
         if l.name == "pool5/7x7_s1":
             for f in ("kernel_h", "kernel_w", "stride_h", "stride_w", "kernel_size", "stride"):
                 l.pooling_param.ClearField(f)
             l.pooling_param.global_pooling = True
     net = Net(n, phase=proto.TRAIN, seed=1, device="cpu")
-    bs = BranchStreams(net, 4)
-    assert bs.streams_used() == 4 and bs.streams_used(backward=True) == 4
+    bs = BranchStreams(net, n_streams, star=star)
+    assert bs.streams_used() == n_streams and bs.streams_used(backward=True) == n_streams
+    if star:
+        for plan in (bs.fwd_plan, bs.bwd_plan):
+            sid_of = [sid for _, sid, _, _ in plan]
+            for _, sid, waits, _ in plan:
+                assert sid == 0 or all(sid_of[d] == 0 for d in waits)
     for plan in (bs.fwd_plan, bs.bwd_plan):
         # the earliest time each node may run when streams proceed in parallel (unit cost)
-        finish, stream_t = {}, [0] * 4
+        finish, stream_t = {}, [0] * n_streams
         for pos, (li, sid, waits, _) in enumerate(plan):
             start = max([stream_t[sid]] + [finish[d] for d in waits])
             finish[pos] = start + 1
