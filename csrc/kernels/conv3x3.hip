@@ -38,6 +38,7 @@ struct Geo {
   int P, Q;      // output (P = H + 2 pad - 2)
   int C, pad;    // input channels (<= 64, multiple of 8: stored as 128-B rows, zero-filled), padding
   int th, tw;    // output tiles per image
+  int ldy;       // output pixel stride in elements (K, or wider: a channel slice of a K-wide output)
   long long tiles;
 };
 
@@ -168,7 +169,7 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const
     for (int j = 0; j < 4; ++j) {
       const int h = ty * TILE + 4 * mi + j, wc = tx * TILE + mrow;
       if (h >= g.P || wc >= g.Q) continue;
-      const long long o = (((long long)n_img * g.P + h) * g.Q + wc) * KOUT;
+      const long long o = (((long long)n_img * g.P + h) * g.Q + wc) * g.ldy;
 #pragma unroll
       for (int i = 0; i < NF; ++i) {
         const int n = n0w + 16 * i + ncol;
@@ -215,13 +216,19 @@ conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const
 // 0 or 1 (P = H + 2 pad - 2) — a forward conv, or a data gradient with flip-transposed
 // weights.  K = 64 (VGG-16 conv1_2: C = 64, pad 1) or 96 (CaffeNet / AlexNet conv1 after the
 // space-to-depth fold: C = 48, pad 0); C <= 64, multiple of 8.
+// ldy: pixel stride of y in elements (0 = K): GoogLeNet's conv2/3x3 (64 -> 192) runs as two
+// 96-output launches into the channel halves of one 192-wide output (64.6 us each vs 155 us for
+// the implicit GEMM, scripts/direct96_probe.py).  A gated launch (data gradient) keeps ldy = K.
 extern "C" int sn_conv3x3_direct(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* gate, bf16_t* y,
                                  long long N, long long H, long long W, long long C, long long K, long long pad,
-                                 long long relu, hipStream_t st) {
+                                 long long relu, long long ldy, hipStream_t st) {
   if (N <= 0 || H <= 0 || W <= 0) return 0;
   if (C <= 0 || C > 64 || C % 8 || (K != 64 && K != 96) || (pad != 0 && pad != 1)) return 3;
+  if (ldy == 0) ldy = K;
+  if (ldy < K || ldy % 4 || (gate && ldy != K)) return 3;
   Geo g;
   g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C; g.pad = (int)pad;
+  g.ldy = (int)ldy;
   g.P = (int)(H + 2 * pad - 2);
   g.Q = (int)(W + 2 * pad - 2);
   if (g.P <= 0 || g.Q <= 0) return 3;

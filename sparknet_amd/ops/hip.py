@@ -239,7 +239,14 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
         call("conv_packed4x4", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu))
         return y
     if direct_io and direct_conv_ok(s):
-        call("conv3x3_direct", x, _c(w), b, None, y, s.N, s.H, s.W, s.C, s.K, s.ph, int(relu))
+        call("conv3x3_direct", x, _c(w), b, None, y, s.N, s.H, s.W, s.C, s.K, s.ph, int(relu), 0)
+        return y
+    if direct_io and direct96_split_ok(s):
+        # K / 96 launches of the 96-output direct kernel, each into its channel slice of y
+        wc = _c(w)
+        for j in range(0, s.K, 96):
+            call("conv3x3_direct", x, wc[j:j + 96], b[j:j + 96] if b is not None else None, None, y[..., j:],
+                 s.N, s.H, s.W, s.C, 96, s.ph, int(relu), s.K)
         return y
     if _implicit_ok(s):
         kred = s.R * s.S * s.Cg
@@ -280,6 +287,20 @@ def direct_conv_ok(s: ConvSpec) -> bool:
         return True
     return (_DIRECT_K96 and s.C == 48 and s.K == 96 and s.groups == 1 and s.R == 3 and s.S == 3 and s.sh == 1
             and s.sw == 1 and s.ph == 0 and s.pw == 0 and s.dh == 1 and s.dw == 1)
+
+
+# 3x3 / stride-1 / pad-1 convolutions with <= 64 input channels and a multiple of 96 (> 96)
+# outputs — GoogLeNet's conv2/3x3, 64 -> 192 — as 96-output direct launches writing channel
+# slices of the output: 2 x 64.6 us vs 155 us for the implicit GEMM at b128 (the GEMM re-reads
+# its 9x im2col A operand and the whole weight panel per 128-row tile; scripts/direct96_probe.py).
+# SN_CONV_DIRECT96=0 keeps the GEMM.
+_DIRECT96 = os.environ.get("SN_CONV_DIRECT96", "1") != "0"
+
+
+def direct96_split_ok(s: ConvSpec) -> bool:
+    return (_DIRECT96 and 0 < s.C <= 64 and s.C % 8 == 0 and s.K > 96 and s.K % 96 == 0 and s.groups == 1
+            and s.R == 3 and s.S == 3 and s.sh == 1 and s.sw == 1 and s.ph == 1 and s.pw == 1 and s.dh == 1
+            and s.dw == 1)
 
 
 # CaffeNet / AlexNet conv1 after the fold (48 -> 96, 3x3, pad 0) on the tap-packed direct kernel
@@ -592,7 +613,7 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
                 pre = torch.empty((s.groups, s.Cg, s.R, s.S, s.Kg), dtype=BF16, device=x.device)
                 call("flip_weights", _c(w), pre, s.groups, s.Kg, s.R, s.S, s.Cg)
             call("conv3x3_direct", dy, pre, None, _c(gate) if gate is not None else None, dx, s.N, s.H, s.W, 64, 64, 1,
-                 0)
+                 0, 0)
             return dx
         A = Im2col(dy, g2, kcontig=True, gstride=s.Kg)
         if DGRAD_INPLACE_WEIGHTS:

@@ -426,6 +426,30 @@ def test_conv_packed44_direct(gpu, N, H, W, C, relu, bias, monkeypatch):
     close(y, hip.conv_forward(x, w, b, s, relu=relu), 1e-2)
 
 
+@pytest.mark.parametrize("N,H,W,C,K", [(2, 20, 20, 64, 192), (1, 9, 37, 48, 288), (2, 56, 56, 64, 192),
+                                       (3, 5, 5, 16, 192)])
+@pytest.mark.parametrize("relu,bias", [(True, True), (False, False)])
+def test_conv_direct96_split(gpu, N, H, W, C, K, relu, bias, monkeypatch):
+    """3x3 / pad-1 convolutions with <= 64 inputs and a multiple of 96 outputs (GoogLeNet's
+    conv2/3x3, 64 -> 192) run as 96-output direct launches into channel slices of the output:
+    against the fp32 reference and the implicit-GEMM path."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    monkeypatch.setattr(hip, "_DIRECT96", True)
+    s = ConvSpec(N, H, W, C, K, 3, 3, 1, 1, 1, 1, 1, 1, 1)
+    assert hip.direct96_split_ok(s)
+    x = rnd(N, H, W, C)
+    w = rnd(K, 3, 3, C, scale=0.1)
+    b = torch.randn(K, device="cuda") if bias else None
+    y = hip.conv_forward(x, w, b, s, relu=relu)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1)
+    if relu:
+        ref = torch.relu(ref)
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+    monkeypatch.setattr(hip, "_DIRECT96", False)
+    close(y, hip.conv_forward(x, w, b, s, relu=relu), 1e-2)
+
+
 def test_conv_packed44_googlenet_conv1(gpu, monkeypatch):
     """GoogLeNet conv1 (224 x 224 x 3, 7 x 7 / 2, pad 3) through conv_forward: the 2x2
     space-to-depth fold feeds the packed 4x4 kernel; against the fp32 reference."""
