@@ -224,6 +224,14 @@ extern "C" int sn_conv_packed3x3(const bf16_t* x, const bf16_t* w, const float* 
 
 // y[N][H-3][W-3][64] = conv4x4(x[N][H][W][C], w[64][4][4][C]) (+ bias, ReLU), stride 1, pad 0;
 // C a multiple of 8, at most 16 (GoogLeNet conv1 after the 2x2 space-to-depth fold).
+// <1, 64, 2, 36864>: a 1x1 convolution with <= 64 input and 64 output channels (GoogLeNet's
+// conv2/3x3_reduce, 56 x 56 x 64 -> 64: 5 input rows x 56 px x 128 B per 192-pixel tile) —
+// the implicit GEMM runs it as one K step per 128-row tile
+extern "C" int sn_conv_packed1x1(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N,
+                                 long long H, long long W, long long C, long long K, long long relu, hipStream_t st) {
+  return launch_packed<1, 64, 2, 36864>(x, w, bias, y, N, H, W, C, K, relu, st);
+}
+
 extern "C" int sn_conv_packed4x4(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N,
                                  long long H, long long W, long long C, long long K, long long relu, hipStream_t st) {
   return launch_packed<4, 64, 8, 22528>(x, w, bias, y, N, H, W, C, K, relu, st);

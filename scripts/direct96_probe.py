@@ -43,3 +43,13 @@ for K in (192, 96, 64):
     fl = 2.0 * N * H * W * K * 9 * C
     print(f"K={K}: implicit GEMM {tg:7.1f} us ({fl / tg / 1e6:.0f} TF/s), dispatched {ts:7.1f} us" +
           (f" | direct {td:7.1f} us ({fl / td / 1e6:.0f} TF/s)" if td else ""), flush=True)
+
+# 1x1, 64 -> 64 (GoogLeNet conv2/3x3_reduce) on the packed direct kernel's <1, 64> instance
+s = ConvSpec(N, H, W, C, 64, 1, 1, 1, 1, 0, 0, 1, 1, 1)
+w = (torch.randn(64, 1, 1, C, device="cuda") * 0.05).to(torch.bfloat16)
+b = torch.randn(64, device="cuda")
+hip._PACKED11 = False
+tg = timed(lambda: hip.conv_forward(x, w, b, s, relu=True))
+hip._PACKED11 = True
+tp = timed(lambda: hip.conv_forward(x, w, b, s, relu=True))
+print(f"1x1 64->64: implicit GEMM {tg:7.1f} us | packed <1, 64> {tp:7.1f} us", flush=True)

@@ -235,6 +235,9 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
     if direct_io and packed_conv_ok(s):
         call("conv_packed3x3", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu))
         return y
+    if direct_io and packed11_conv_ok(s):
+        call("conv_packed1x1", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu))
+        return y
     if direct_io and packed44_conv_ok(s):
         call("conv_packed4x4", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu))
         return y
@@ -295,6 +298,18 @@ def direct_conv_ok(s: ConvSpec) -> bool:
 # its 9x im2col A operand and the whole weight panel per 128-row tile; scripts/direct96_probe.py).
 # SN_CONV_DIRECT96=0 keeps the GEMM.
 _DIRECT96 = os.environ.get("SN_CONV_DIRECT96", "1") != "0"
+
+
+# 1x1 convolutions with <= 64 inputs and 64 outputs (GoogLeNet's conv2/3x3_reduce) on the
+# tap-packed direct kernel's <1, 64> instance (SN_CONV_PACKED11=1; measured in
+# profiles/r5_packed11.txt)
+_PACKED11 = os.environ.get("SN_CONV_PACKED11", "0") == "1"
+
+
+def packed11_conv_ok(s: ConvSpec) -> bool:
+    return (_PACKED11 and 0 < s.C <= 64 and s.C % 8 == 0 and s.K == 64 and s.groups == 1 and s.R == 1
+            and s.S == 1 and s.sh == 1 and s.sw == 1 and s.ph == 0 and s.pw == 0 and s.dh == 1 and s.dw == 1
+            and s.W * s.C * 2 * min(s.H, (191 + s.W - 1) // s.W + 1) <= 36864)
 
 
 def direct96_split_ok(s: ConvSpec) -> bool:

@@ -450,6 +450,28 @@ def test_conv_direct96_split(gpu, N, H, W, C, K, relu, bias, monkeypatch):
     close(y, hip.conv_forward(x, w, b, s, relu=relu), 1e-2)
 
 
+@pytest.mark.parametrize("N,H,W,C", [(2, 56, 56, 64), (1, 7, 57, 64), (3, 9, 5, 16), (2, 1, 1, 64)])
+@pytest.mark.parametrize("relu,bias", [(True, True), (False, False)])
+def test_conv_packed11(gpu, N, H, W, C, relu, bias, monkeypatch):
+    """The tap-packed direct kernel's <1 tap, 64 outputs> instance (GoogLeNet conv2/3x3_reduce)
+    against the fp32 reference and the implicit GEMM."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    monkeypatch.setattr(hip, "_PACKED11", True)
+    s = ConvSpec(N, H, W, C, 64, 1, 1, 1, 1, 0, 0, 1, 1, 1)
+    assert hip.packed11_conv_ok(s)
+    x = rnd(N, H, W, C)
+    w = rnd(64, 1, 1, C, scale=0.1)
+    b = torch.randn(64, device="cuda") if bias else None
+    y = hip.conv_forward(x, w, b, s, relu=relu)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b)
+    if relu:
+        ref = torch.relu(ref)
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+    monkeypatch.setattr(hip, "_PACKED11", False)
+    close(y, hip.conv_forward(x, w, b, s, relu=relu), 1e-2)
+
+
 def test_conv_packed44_googlenet_conv1(gpu, monkeypatch):
     """GoogLeNet conv1 (224 x 224 x 3, 7 x 7 / 2, pad 3) through conv_forward: the 2x2
     space-to-depth fold feeds the packed 4x4 kernel; against the fp32 reference."""
