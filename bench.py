@@ -362,7 +362,19 @@ def host_profile(trainer, dev, n=200):
     import torch
     g, s = trainer.step_fn, trainer.solver
     parts = {"feeder": 0.0, "hyper": 0.0, "replay": 0.0}
+    # replay() cost on an idle device vs back to back: a launch that waits for the previous
+    # instance of the same graph shows up as ~one GPU step only in the back-to-back calls
     torch.cuda.synchronize(dev)
+    idle = []
+    for _ in range(3):
+        g.pre()
+        s.stage_hyper()
+        a = time.perf_counter()
+        g.graph.replay()
+        idle.append(1e6 * (time.perf_counter() - a))
+        s.iter += 1
+        torch.cuda.synchronize(dev)
+    print("replay us on an idle device: " + " ".join(f"{v:.0f}" for v in idle), file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     for _ in range(n):
         a = time.perf_counter()
