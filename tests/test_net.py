@@ -425,3 +425,17 @@ def test_fp8_dgrad_cost_model_and_eligibility():
     assert got["conv2"] == 48 * 5 * 5 and got["conv3"] == 256 * 9 and got["conv4"] == 192 * 9
     assert not ok["conv1"]  # 11x11 stride 4: the data gradient is not a stride-1 forward conv
     assert ok["conv2"] and ok["conv3"] and ok["conv4"] and ok["conv5"]
+
+
+def test_branch_sim_script_runs():
+    """scripts/branch_sim.py (CPU schedule simulation of the branch-stream plans) runs and
+    reports a span for 2 / 3 / 4 streams."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "scripts/branch_sim.py", "--batch", "8"], cwd=root, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if "streams:" in l]
+    assert len(lines) == 3 and all("forward" in l and "backward" in l for l in lines)
