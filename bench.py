@@ -41,8 +41,10 @@ def parse():
     p.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the model's train batch)")
     p.add_argument("--tau", type=int, default=50)
     p.add_argument("--no-graph", action="store_true")
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                   help="fp8: e4m3 forward and data-gradient products with per-tensor delayed scaling (bf16 weight gradients)")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
+                   help="fp8: e4m3 forward and data-gradient products with per-tensor delayed scaling; fp32: the "
+                        "reference's numerics (fp32 activations, im2col + exact-f32 MFMA products, ops/f32dev.py; "
+                        "eager, no fusions) for a precision-matched comparison with the fp32 K40 number")
     p.add_argument("--fp8-min-work", type=float, default=1000.0,
                    help="--dtype fp8: only layers with at least this many forward MACs per input element "
                         "run e4m3 (engine.enable_fp8 min_macs_per_input; VGG-16 b512: 0 -> 7.3k, 1000 -> 8.0k, "
@@ -85,6 +87,12 @@ def parse():
                    help="after the timed run, report the host time per step part (stderr)")
     p.add_argument("--save-tuned", default="",
                    help="merge this run's GEMM tile / split-K choices into a tuning database (JSON)")
+    p.add_argument("--loss-trace", action="store_true",
+                   help="print every timed step's loss (full precision) to stderr after the window")
+    p.add_argument("--autotune", action="store_true",
+                   help="time GEMM products the tuning database lacks on first use (off by default: the "
+                        "committed database + cost model give every process and rank the same kernels; with "
+                        "N > 1 ranks rank 0's choices are adopted by all before graph capture)")
     return p.parse_args()
 
 
@@ -157,6 +165,8 @@ def main():
         rccl_log = diag.rccl_debug_env()  # channels / transports for the JSON (RCCL debug log)
     if dev.type == "cuda":
         _lib.kernels()
+        from sparknet_amd.ops import gemm as G
+        G.set_autotune(args.autotune)
     comm = (Comm(backend="gloo" if args.share_gpu else None, device=dev if dev.type == "cuda" else None,
                  watchdog=True, timeout_s=600.0) if world > 1 or force_comm else None)
     bad = diag.check_placement(comm, args.gpus, args.share_gpu or dev.type != "cuda",
@@ -172,10 +182,12 @@ def main():
     if args.model in ("caffenet", "alexnet", "googlenet", "vgg16"):
         kw["crop"] = crop
     solver_param = models.solver_for(args.model, **kw)
-    solver = Solver(solver_param, device=dev, seed=1701 + rank, build_test_nets=False)
+    fp32 = args.dtype == "fp32"
+    solver = Solver(solver_param, device=dev, seed=1701 + rank, build_test_nets=False,
+                    dtype=torch.float32 if fp32 else None)
     net = solver.net
     if dev.type == "cuda":
-        fuse_relu(net)
+        fuse_relu(net)  # (a no-op on fp32 nets: the fp32 device mode runs the plain layer graph)
     src = SyntheticSource(B, C, HW, HW, classes=classes, pool=3, seed=rank)
     feeder = DeviceFeeder(src, net.blob_by_name("data"), net.blob_by_name("label"), crop=crop, mean=mean,
                           scale=in_scale, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev,
@@ -183,7 +195,8 @@ def main():
     fused_fold = fuse_input_fold(net, feeder)  # augment writes conv1's S2D-folded input directly
     n_fp8 = (enable_fp8(net, args.fp8_min_work, dgrad=args.fp8_dgrad, dgrad_format=args.fp8_dgrad_format,
                         wgrad=args.fp8_dgrad and args.fp8_wgrad) if args.dtype == "fp8" else 0)
-    trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder, use_graph=not args.no_graph and not args.cpu,
+    trainer = LocalSGDTrainer(solver, comm, tau=args.tau, feeder=feeder,
+                              use_graph=not args.no_graph and not args.cpu and not fp32,
                               overlap_update=args.overlap_update, fuse_fc=not args.no_fuse_fc,
                               streams=args.streams)
     trainer.broadcast_initial()
@@ -206,8 +219,11 @@ def main():
     t0 = time.perf_counter()
     loss = None
     averaged = False
+    trace = []
     for k in range(args.steps):
         loss = trainer.local_step()
+        if args.loss_trace:
+            trace.append(loss.detach().clone() if hasattr(loss, "detach") else loss)
         if step_evs:
             step_evs.append(torch.cuda.Event(enable_timing=True))
             step_evs[-1].record()
@@ -232,6 +248,8 @@ def main():
     if step_evs:
         ms = [step_evs[i].elapsed_time(step_evs[i + 1]) for i in range(len(step_evs) - 1)]
         print(f"rank {rank} step ms: " + " ".join(f"{v:.2f}" for v in ms), file=sys.stderr, flush=True)
+    if trace:
+        print(f"rank {rank} losses: " + " ".join(repr(float(v)) for v in trace), file=sys.stderr, flush=True)
     per_rank_ms = [round(1000.0 * elapsed_rank / args.steps, 3)]
     avg_ms = [e[0].elapsed_time(e[1]) for e in avg_events if e is not None]
     comm_info = avg_check = bucket_ms = numa_all = None
@@ -262,7 +280,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / BASELINE_IMG_S, 2) if args.model in HEADLINE else None,
-            "dtype": "fp8" if n_fp8 else ("fp32-cpu" if dev.type == "cpu" else "bf16"),
+            "dtype": "fp8" if n_fp8 else ("fp32-cpu" if dev.type == "cpu" else ("fp32" if fp32 else "bf16")),
             "data": f"synthetic (uint8 {HW}x{HW} -> on-device random crop/mirror/mean), random-init weights",
             "config": {
                 "model": f"{args.model} (bvlc_reference_caffenet / AlexNet)" if args.model == "caffenet"
@@ -286,6 +304,10 @@ def main():
             "avg_payload_mb": round(net.flat_data.numel() * 4 / 1e6, 1),
             "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2) if dev.type == "cuda" else None,
             "numa_node_rank0": numa,
+            # GEMM products run on the cost model's choice (no tuning-database entry); 0 on the
+            # zoo models' bench configurations (tests/test_tune_db_gpu.py)
+            "tune_misses": len(G.tune_misses()) if dev.type == "cuda" else None,
+            "autotune": bool(args.autotune),
         }
         if comm is not None:
             out["diag"] = {

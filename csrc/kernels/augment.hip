@@ -11,7 +11,12 @@
 
 #include <cstdlib>
 
-__global__ void augment_kernel(const uint8_t* __restrict__ src, bf16_t* __restrict__ dst, int N, int C, int Hs, int Ws,
+// OUT = bf16_t (the bf16 engine) or float (the fp32 device mode, ops.f32dev)
+SN_DEV void store_px(bf16_t* o, float v) { *o = f2bf(v); }
+SN_DEV void store_px(float* o, float v) { *o = v; }
+
+template <typename OUT>
+__global__ void augment_kernel(const uint8_t* __restrict__ src, OUT* __restrict__ dst, int N, int C, int Hs, int Ws,
                                int crop_h, int crop_w, const float* __restrict__ mean, int mean_mode, float scale,
                                const long long* __restrict__ rng, int train, int mirror, int* __restrict__ offs_out,
                                const int* __restrict__ labels, float* __restrict__ labels_out) {
@@ -44,13 +49,13 @@ __global__ void augment_kernel(const uint8_t* __restrict__ src, bf16_t* __restri
     }
     const int sh = h + ho;
     const int sw = (mir ? (crop_w - 1 - w) : w) + wo;
-    bf16_t* o = dst + i * C;
+    OUT* o = dst + i * C;
     for (int c = 0; c < C; ++c) {
       const long long si = (((long long)n * C + c) * Hs + sh) * Ws + sw;
       float v = (float)src[si];
       if (mean_mode == 1) v -= mean[c];
       else if (mean_mode == 2) v -= mean[((long long)c * Hs + sh) * Ws + sw];
-      o[c] = f2bf(v * scale);
+      store_px(o + c, v * scale);
     }
   }
 }
@@ -61,8 +66,20 @@ extern "C" int sn_augment(const uint8_t* src, bf16_t* dst, long long N, long lon
                           const int* labels, float* labels_out, hipStream_t st) {
   if (crop_h > Hs || crop_w > Ws) return 9;
   long long total = N * crop_h * crop_w;
-  hipLaunchKernelGGL(augment_kernel, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, src, dst, (int)N, (int)C,
-                     (int)Hs, (int)Ws, (int)crop_h, (int)crop_w, mean, (int)mean_mode, scale, rng, (int)train,
+  hipLaunchKernelGGL(augment_kernel<bf16_t>, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, src, dst, (int)N,
+                     (int)C, (int)Hs, (int)Ws, (int)crop_h, (int)crop_w, mean, (int)mean_mode, scale, rng, (int)train,
+                     (int)mirror, offs_out, labels, labels_out);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_augment_f32(const uint8_t* src, float* dst, long long N, long long C, long long Hs, long long Ws,
+                              long long crop_h, long long crop_w, const float* mean, long long mean_mode, float scale,
+                              const long long* rng, long long train, long long mirror, int* offs_out,
+                              const int* labels, float* labels_out, hipStream_t st) {
+  if (crop_h > Hs || crop_w > Ws) return 9;
+  long long total = N * crop_h * crop_w;
+  hipLaunchKernelGGL(augment_kernel<float>, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, src, dst, (int)N,
+                     (int)C, (int)Hs, (int)Ws, (int)crop_h, (int)crop_w, mean, (int)mean_mode, scale, rng, (int)train,
                      (int)mirror, offs_out, labels, labels_out);
   return SN_CHECK_LAUNCH();
 }
@@ -195,7 +212,7 @@ extern "C" int sn_augment_s2d(const uint8_t* src, bf16_t* x2, long long N, long 
   if (crop_h > Hs || crop_w > Ws || (f * f * Cp) % 8 || Cp < C) return 9;
   long long total = N * H2 * W2;
   dim3 grid(sn_blocks(total, 256, 16384));
-  const int direct = std::getenv("SN_AUGMENT_DIRECT") != nullptr;  // A/B: per-thread pixel stores
+  const int direct = 0;  // per-thread pixel stores (slower than the block-staged stores, round 3)
 #define SN_AUG_S2D_MM(FF, CC, MM)                                                                               \
   hipLaunchKernelGGL((augment_s2d_kernel<FF, CC, MM>), grid, dim3(256), 0, st, src, x2, (int)N, (int)C, (int)Hs, (int)Ws, \
                      (int)crop_h, (int)crop_w, mean, (int)mean_mode, scale, rng, (int)train, (int)mirror, (int)H2,     \

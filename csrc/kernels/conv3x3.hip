@@ -237,11 +237,7 @@ extern "C" int sn_conv3x3_direct(const bf16_t* x, const bf16_t* w, const float* 
   g.tiles = N * g.th * g.tw;
   const int cus = sn_cu_count();
   const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
-  static int nw = 0;
-  if (!nw) {
-    const char* e = getenv("SN_C64_WAVES");
-    nw = (e && atoi(e) == 4) ? 4 : 8;
-  }
+  const int nw = 8;  // 8 waves (2 per SIMD) beat 4 (docs/PERF_NOTES.md round 3)
 #define SN_C3(NWV, KV, DB, NTH)                                                                             \
   do {                                                                                                     \
     if (gate)                                                                                              \

@@ -464,8 +464,7 @@ extern "C" int sn_flip_desc(void* out, const bf16_t* w, bf16_t* wt, long long G,
   d.fS = make_fdiv((uint32_t)S);
   d.fR = make_fdiv((uint32_t)R);
   d.fCg = make_fdiv((uint32_t)Cg);
-  const char* e = std::getenv("SN_FLIP_VEC");
-  d.vec = (!e || std::atoi(e) != 0) && Kg % 8 == 0 && Cg % 8 == 0 &&
+  d.vec = Kg % 8 == 0 && Cg % 8 == 0 &&
           (reinterpret_cast<uintptr_t>(w) % 16) == 0 && (reinterpret_cast<uintptr_t>(wt) % 16) == 0;
   memcpy(out, &d, sizeof d);
   return 0;

@@ -117,8 +117,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
   if (a.bias_out && (a.ones_col < 0 || a.epi == EPI_BF16 || a.epi == EPI_BF16_DROP)) return 5;
   // fused fp8 side output: unsplit bf16 epilogues of gemm_kernel (not gemm256_kernel, tiles
   // 6-9), whole 8-byte chunks
-  if (a.q_out && (a.splits != 1 || (a.epi != EPI_BF16 && a.epi != EPI_BF16_DROP) || (a.tile >= 6 && a.tile <= 9) ||
-                  a.tile >= 30 ||
+  if (a.q_out && (a.splits != 1 || (a.epi != EPI_BF16 && a.epi != EPI_BF16_DROP) || (a.tile >= 6 && a.tile <= 7) ||
                   (a.N % 8) || (a.q_ld % 8) || (a.q_gstride % 8) || !a.q_slot || !a.q_part ||
                   (reinterpret_cast<unsigned long long>(a.q_out) & 7)))
     return 6;
@@ -155,36 +154,17 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 4: return launch_tile96(a, stream);
     case 5: return launch_tile48(a, stream);
     case 6:
-    case 7:
-    case 8:
-    case 9: return a.epi == EPI_SGD ? 4 : sn_gemm_t256(a, stream);  // gemm_t256.hip
+    case 7: return a.epi == EPI_SGD ? 4 : sn_gemm_t256(a, stream);  // gemm_t256.hip
     case 11:
     case 12:
     case 13:
     case 14: return a.epi == EPI_SGD ? 4 : sn_gemm_big8(a, stream);  // gemm_big8.hip
     case 21:
     case 22: return sn_gemm_tiles_c(a, stream);  // gemm_tiles_c.hip (64-row tiles)
-    case 23:
-    case 24:
-    case 25:
-    case 26:
-    case 27:
-    case 28: return sn_gemm_mf32(a, stream);  // gemm_mf32.hip (32x32x16 MFMA twins)
-    case 40:
-    case 41: return a.epi == EPI_SGD ? 4 : sn_gemm_t256p8(a, stream);  // gemm_t256p8.hip (8-phase)
     case 15:
     case 16:
     case 17:
     case 18: return a.epi == EPI_SGD ? 4 : sn_gemm_big4(a, stream);  // gemm_big4.hip
-    case 30:
-    case 31:
-    case 32:
-    case 39: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_a(a, stream);  // gemm_pk.hip (persistent ring)
-    case 33:
-    case 34:
-    case 36:
-    case 37:
-    case 38: return a.epi == EPI_SGD ? 4 : sn_gemm_pk_b(a, stream);  // gemm_pk2.hip
     default: return launch_tile<128, 128, 4, 2>(a, stream);
   }
 }

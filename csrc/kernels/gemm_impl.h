@@ -91,8 +91,6 @@ struct SnGemmArgs {
   // bf16 epilogues of unsplit 4-wave tiles: stage the finished tile through the idle LDS
   // stages and store it as whole 16-B row chunks (host: ldc % 8 == 0, 16-B aligned C)
   int lds_store;
-  int addr_legacy;  // bit 0: general per-lane address decode only (A/B probe of the fast DMA paths);
-                    // bit 1: the MC im2col row table (opt-in A/B: slower, docs/PERF_NOTES.md)
   // bf16 epilogues of gemm_kernel, unsplit: also store the finished (bf16-rounded) output as
   // fp8 bytes q_out[grp * q_gstride + m * q_ld + n] = sat(v * q_slot[0]) and fold its |max|
   // into q_slot[1] — the quantisation pass of the fp8 product that consumes this output
@@ -107,13 +105,6 @@ struct SnGemmArgs {
   // a single address serialises ~10^5 block atomics), folded into q_slot[1] afterwards by
   // sn_fp8_fold_amax
   float* q_part;
-  // In-launch split-K combine (gemm_kernel tiles, splits > 1, not EPI_SGD): fp32 slabs
-  // fix_ws[(grp * splits + split) * fix_sstride + m * fix_ld + n] and one zero-initialised
-  // counter per (group, output tile) at fix_cnt[grp * tiles + tile]; null = the separate
-  // splitk_reduce launch.  C / ldc / bias / gate / ... then describe the FINAL output.
-  float* fix_ws;
-  long long fix_ld, fix_sstride;
-  int* fix_cnt;
 };
 
 }  // extern "C"
@@ -133,12 +124,8 @@ SN_DEV int kc_off(int row, int kc) { return row * 128 + ((kc ^ ((row >> 1) & 7))
 
 // MC tile: [64 k rows][TILE cols] bf16 (TILE*2-byte rows).  32-B granules XOR-swizzled
 // so the 8 rows a half-wave tr-reads land in 8 distinct granules of the 256-B bank row.
-// SW = 1: the image read by the 32x32x16 MFMA (read_frag32): a half-wave tr-reads 4 rows
-// x 32 columns (two adjacent granules per row), so rows k..k+3 XOR the granule index by
-// 2 (k & 3) (256-B+ rows) or by 2 ((k >> 1) & 1) (128-B rows, 2 rows per bank row).
-template <int TILE, int SW = 0>
+template <int TILE>
 SN_DEV int swz_mc(int k) {
-  if (SW) return TILE >= 128 ? ((k & 3) << 6) : (((k >> 1) & 1) << 6);
   if (TILE >= 128) return (((k & 3) | (((k >> 3) & 1) << 2)) << 5);
   return ((((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 5);  // 128-B rows: 2 rows per bank row
 }
@@ -168,7 +155,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // maps to that slot.  Lanes outside the matrix read a zero page.
 //   KC: [TILE rows][64 k], 8 chunks per row, 8 rows per instruction.
 //   MC: [64 k rows][TILE cols], TILE/8 chunks per row.
-template <int MC, int MODE, int TILE, int NW, int ES = 2, int SW = 0>
+template <int MC, int MODE, int TILE, int NW, int ES = 2>
 struct GStager {
   static constexpr int NI = TILE / (8 * NW);      // wave-instructions per wave per tile
   static constexpr int CPL = MC ? TILE * ES / 16 : 8;  // 16-B chunks per LDS row
@@ -202,30 +189,23 @@ struct GStager {
   // no 64-bit address arithmetic per lane).
   int nr, ns, nc;
   i32x4 rsrc;
-  // MC+IM2COL: decode (n, p, q) of this lane's instruction-0 row pixel for the NEXT tile
-  // (advanced by BK pixels per issue; rows of instruction j are RPI pixels further on),
-  // per-instruction column terms, and whether this wave holds a ones-column lane (then it
-  // stages through global loads and the ones page; otherwise through the buffer resource)
-  int sn_, sp_, sq_;
-  int cdh[MC ? NI : 1], cdw[MC ? NI : 1], colo[MC ? NI : 1];
-  bool wave_has_one;
-  // MC+IM2COL row table (waves without the ones column, bf16; opt-in, addr_legacy == 2): the
-  // wave's RW = 64/NW pixel rows of a K-step are decoded lane-parallel, RW rows x KS = NW
-  // K-steps per decode (one division chain per KS K-steps instead of a per-instruction walk),
-  // and each instruction fetches its rows' (pixel offset, packed h / w) by ds_bpermute; the
-  // next issue's pair is fetched at the end of an issue.  It cuts the stager's VALU from ~55
-  // to ~22 per K-step (tile 10), yet the CaffeNet weight gradients run 8-10 % SLOWER with it
-  // (profiles/r5_wgrad_rowtab_ab.txt): the MC weight-gradient loop is not VALU-bound.
-  // Compiled only into the 4-wave bf16 stagers of up to 128 columns (tiles 0 / 10 and kin):
-  // in the 8-wave 256-wide tiles its registers alone pushed the K-loop into scratch spills.
-  static constexpr int RW = 64 / NW, KS = 64 / RW;
-  static constexpr bool RT = MC && MODE == OP_IM2COL && ES == 2 && NW == 4 && TILE <= 128;
-  bool rowtab;
-  int bstep;                           // K-step index inside the current decode batch
-  int tb_off, tb_hw;                   // this lane's decode: byte offset of the pixel corner,
-                                       // (h & 0xffff) | (w << 16), h = -16384 past k_lim
-  int nx_off[RT ? NI : 1], nx_hw[RT ? NI : 1];  // the next issue's rows, per instruction
-  int colb[RT ? NI : 1];               // colo in bytes
+  // MC+IM2COL (weight gradients: rows = output pixels, the reduction): every lane keeps, per
+  // instruction j, the state of ITS pixel row for the NEXT tile to issue — hc / wc = the input
+  // row / column its tap reads (p*sh - ph + r*dh, q*sw - pw + s*dw) and mofs = the byte offset
+  // of its 16-B source chunk — and advances it by BKE pixels per issue with at most one carry
+  // into p and one into n (BKE % (P*Q) < P*Q): ~14 full-rate VALU per instruction, where the
+  // former per-instruction (n, p, q) walk ran divergent carry loops and quarter-rate
+  // 64-bit multiply-adds (~28 VALU cycles per MFMA on the 128x128 tile, more than the
+  // MFMA's free issue slots: the implicit weight gradient ran 1.4-1.75x the dense product
+  // of an explicit im2col matrix, scripts/wgrad_probe.py, profiles/r6_wgrad_stager.txt).
+  // A column outside the matrix gets hc = -2^29: never inside the image, never carries.
+  static constexpr int NJ = (MC && MODE == OP_IM2COL) ? NI : 1;
+  int cdh[NJ], cdw[NJ], colo[NJ];  // the column's tap shift and source offset (init only)
+  int hc[NJ], wc[NJ], hlim[NJ], wlim[NJ];
+  unsigned mofs[NJ];
+  int s_dq, s_qsw, s_dp, s_sh, s_psh;  // per-issue advance (scalars)
+  unsigned s_d0, s_d1, s_d2;           // byte offset advance: none / q carry / p carry
+  bool wave_has_one;  // a ones-column lane in this wave: stage through global loads
   // Low-VALU address paths (all decisions wave-uniform, taken once at init):
   //  KC+IM2COL: kcmode 1 = every K-step lies inside ONE filter tap (Cg % (8*EPC) == 0), so
   //   the tap offset and its (dh, dw) shift are scalars and a lane's DMA offset is
@@ -247,8 +227,7 @@ struct GStager {
   unsigned vrs[NI];
 
   SN_DEV void init(const SnOperand& op, int grp, int wave, int lane, int tile_row0, int rows_lim,
-                   int tile_col0, int cols_lim, int ones = -1, int k_start = 0, int k_lim_hint = 0,
-                   int legacy = 0) {
+                   int tile_col0, int cols_lim, int ones = -1, int k_start = 0, int k_lim_hint = 0) {
     ld = op.ld;
     g = op.g;
     ones_col = ones;
@@ -282,7 +261,7 @@ struct GStager {
     for (int j = 0; j < NI; ++j) {
       const int row = (wave * NI + j) * RPI + lane / CPL, pos = lane % CPL;
       rr[j] = row;
-      ch[j] = MC ? (pos ^ (ES == 1 ? swz_mc8(row) : (swz_mc<TILE, SW>(row) >> 4))) : (pos ^ ((row >> 1) & 7));
+      ch[j] = MC ? (pos ^ (ES == 1 ? swz_mc8(row) : (swz_mc<TILE>(row) >> 4))) : (pos ^ ((row >> 1) & 7));
       if (MODE == OP_IM2COL && !MC) {
         const int PQ = g.P * g.Q;
         int pix = tile_row0 + row;
@@ -309,7 +288,7 @@ struct GStager {
     kcmode = 0;
     fast = false;
     if (MODE == OP_IM2COL && !MC) {
-      kcmode = __builtin_amdgcn_readfirstlane((legacy & 1) ? 0 : ((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0)));
+      kcmode = __builtin_amdgcn_readfirstlane((g.Cg % (8 * EPC)) == 0 ? 1 : (g.Cg >= 8 * EPC ? 2 : 0));
       if (kcmode == 1 && (g.R > 16 || g.S > 16)) kcmode = 2;  // the tap masks hold 16 rows / cols
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -327,7 +306,7 @@ struct GStager {
     if (MODE == OP_DENSE) {
       // element extent of the operand for this group: KC rows x ld, MC (k rows) x ld
       const long long extent = MC ? (long long)k_lim_hint * ld : (long long)rows_lim * ld;
-      fast = __builtin_amdgcn_readfirstlane((int)(!(legacy & 1) && extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
+      fast = __builtin_amdgcn_readfirstlane((int)(extent * ES < (1ll << 31) && (!MC || ones_col < 0))) != 0;
       // built unconditionally from wave-uniform values so it stays in SGPRs
       const unsigned long long a = reinterpret_cast<unsigned long long>(base);
       rsrc[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
@@ -350,41 +329,33 @@ struct GStager {
       }
     }
     if (MODE == OP_IM2COL && MC) {
-      const int PQ = g.P * g.Q, pix = k_start + rr[0];
-      sn_ = fdiv(pix, PQ, invPQ);
-      const int pq = pix - sn_ * PQ;
-      sp_ = fdiv(pq, g.Q, invQ);
-      sq_ = pq - sp_ * g.Q;
+      const int PQ = g.P * g.Q;
       bool any = false;
 #pragma unroll
-      for (int j = 0; j < NI; ++j) any = any || co[j];
-      wave_has_one = __ballot(any) != 0ull;
-      rowtab = RT && __builtin_amdgcn_readfirstlane((int)(legacy == 2 && !wave_has_one)) != 0;
-      bstep = -1;
-      if constexpr (RT) {
-#pragma unroll
-        for (int j = 0; j < NI; ++j) colb[j] = colo[j] * ES;
+      for (int j = 0; j < NI; ++j) {
+        const int pix = k_start + rr[j];
+        const int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
+        const int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
+        const int hrow = p * g.sh - g.ph, wrow = q * g.sw - g.pw;
+        hc[j] = cv[j] ? hrow + cdh[j] : -(1 << 29);
+        wc[j] = wrow + cdw[j];
+        hlim[j] = g.P * g.sh - g.ph + cdh[j];
+        wlim[j] = g.Q * g.sw - g.pw + cdw[j];
+        mofs[j] = (unsigned)((n * g.H + hrow) * g.W + wrow) * (unsigned)g.C * (unsigned)ES +
+                  (unsigned)colo[j] * (unsigned)ES;  // modular: < 2^32 where valid (host)
+        any = any || co[j];
       }
-    }
-  }
-
-  // Row table: lane L decodes pixel row wave*RW + L%RW of K-step (k_first + BKE * (L/RW)).
-  SN_DEV void rt_decode(int wave, int lane, int k_first, int k_lim) {
-    const int pix = k_first + BKE * (lane / RW) + wave * RW + lane % RW;
-    const int PQ = g.P * g.Q;
-    const int n = fdiv(pix, PQ, invPQ), pq = pix - n * PQ;
-    const int p = fdiv(pq, g.Q, invQ), q = pq - p * g.Q;
-    const int h = p * g.sh - g.ph, w = q * g.sw - g.pw;
-    tb_off = (int)(((unsigned)((n * g.H + h) * g.W + w) * (unsigned)g.C) * (unsigned)ES);  // modular, as colb
-    tb_hw = pix < k_lim ? ((h & 0xffff) | (w << 16)) : (int)0xc000;  // h = -16384: never inside
-  }
-  // the (offset, h/w) pairs of K-step u of the batch for this lane's NI instructions
-  SN_DEV void rt_fetch(int u, int lane) {
-    const int a = (u * RW + lane / CPL) * 4;
-#pragma unroll
-    for (int j = 0; j < (RT ? NI : 0); ++j) {
-      nx_off[j] = __builtin_amdgcn_ds_bpermute(a + j * RPI * 4, tb_off);
-      nx_hw[j] = __builtin_amdgcn_ds_bpermute(a + j * RPI * 4, tb_hw);
+      wave_has_one = __ballot(any) != 0ull;
+      const int dn = BKE / PQ, rem = BKE - dn * PQ, dp = rem / g.Q, dq = rem - dp * g.Q;
+      s_dq = __builtin_amdgcn_readfirstlane(dq * g.sw);
+      s_qsw = __builtin_amdgcn_readfirstlane(g.Q * g.sw);
+      s_dp = __builtin_amdgcn_readfirstlane(dp * g.sh);
+      s_sh = __builtin_amdgcn_readfirstlane(g.sh);
+      s_psh = __builtin_amdgcn_readfirstlane(g.P * g.sh);
+      const unsigned cb = (unsigned)g.C * (unsigned)ES;
+      s_d0 = __builtin_amdgcn_readfirstlane((unsigned)((dn * g.H + dp * g.sh) * g.W + dq * g.sw) * cb);
+      s_d1 = __builtin_amdgcn_readfirstlane((unsigned)(g.sh * g.W - g.Q * g.sw) * cb);
+      s_d2 = __builtin_amdgcn_readfirstlane((unsigned)((g.H - g.P * g.sh) * g.W) * cb);
     }
   }
 
@@ -594,64 +565,36 @@ struct GStager {
           long long off = v ? (long long)kout * rowlen + (long long)(RS - 1 - tap) * g.Cg + col : 0;
           dma(base + off * 2, v, dst + j * 1024);
         }
-      } else if (RT && rowtab) {
-        const int lane = threadIdx.x & 63;
-        if (bstep < 0) {  // first issue of the block: decode the first batch
-          rt_decode(wave, lane, k_tile, k_lim);
-          rt_fetch(0, lane);
-          bstep = 0;
-        }
-#pragma unroll
-        for (int j = 0; j < (RT ? NI : 0); ++j) {
-          const int h = ((nx_hw[j] << 16) >> 16) + cdh[j], w = (nx_hw[j] >> 16) + cdw[j];
-          const bool v = cv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          dma_buf(v ? (unsigned)(nx_off[j] + colb[j]) : 0xffffffffu, dst + j * 1024);
-        }
-        if (++bstep == KS) {
-          bstep = 0;
-          rt_decode(wave, lane, k_tile + BKE, k_lim);
-        }
-        rt_fetch(bstep, lane);
       } else {
-        // rows = pixels: walk the lane's pixel (n, p, q) by RPI per instruction instead of
-        // two divisions per instruction; offsets are 32-bit (host: < 2^31 elements)
-        int n = sn_, p = sp_, q = sq_;
-        int off[NI];
-        bool val[NI];
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          if (j > 0) {
-            q += RPI;
-            while (q >= g.Q) {
-              q -= g.Q;
-              ++p;
-            }
-            while (p >= g.P) {
-              p -= g.P;
-              ++n;
-            }
-          }
-          const int hrow = p * g.sh - g.ph, wrow = q * g.sw - g.pw;
-          val[j] = cv[j] && k_tile + rr[j] < k_lim && (unsigned)(hrow + cdh[j]) < (unsigned)g.H &&
-                   (unsigned)(wrow + cdw[j]) < (unsigned)g.W;
-          off[j] = ((n * g.H + hrow) * g.W + wrow) * g.C + colo[j];
-        }
+        // rows = pixels, incremental per-lane state (see the members); rows at or past k_lim
+        // (the split's / the product's end) read zeros: one compare against a scalar
+        const int krem = __builtin_amdgcn_readfirstlane(k_lim - k_tile);
         if (!wave_has_one) {
 #pragma unroll
-          for (int j = 0; j < NI; ++j) dma_buf(val[j] ? (unsigned)off[j] * (unsigned)ES : 0xffffffffu, dst + j * 1024);
+          for (int j = 0; j < NI; ++j) {
+            const bool v = ((unsigned)hc[j] < (unsigned)g.H) & ((unsigned)wc[j] < (unsigned)g.W) & (rr[j] < krem);
+            dma_buf(v ? mofs[j] : 0xffffffffu, dst + j * 1024);
+          }
         } else {
 #pragma unroll
-          for (int j = 0; j < NI; ++j)
-            dma(base + (long long)off[j] * ES, val[j], dst + j * 1024, co[j] && k_tile + rr[j] < k_lim);
+          for (int j = 0; j < NI; ++j) {
+            const bool kin = rr[j] < krem;
+            const bool v = kin && (unsigned)hc[j] < (unsigned)g.H && (unsigned)wc[j] < (unsigned)g.W;
+            dma(base + mofs[j], v, dst + j * 1024, co[j] && kin);
+          }
         }
-        // next tile: BKE pixels on
-        sq_ += BKE;
-        const int dp = fdiv(sq_, g.Q, invQ);
-        sq_ -= dp * g.Q;
-        sp_ += dp;
-        while (sp_ >= g.P) {
-          sp_ -= g.P;
-          ++sn_;
+        // next tile: BKE pixels on (q carry c1, then p carry c2)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          int w = wc[j] + s_dq;
+          const bool c1 = w >= wlim[j];
+          w -= c1 ? s_qsw : 0;
+          int h = hc[j] + s_dp + (c1 ? s_sh : 0);
+          const bool c2 = h >= hlim[j];
+          h -= c2 ? s_psh : 0;
+          mofs[j] += s_d0 + (c1 ? s_d1 : 0u) + (c2 ? s_d2 : 0u);
+          wc[j] = w;
+          hc[j] = h;
         }
       }
     }
@@ -678,33 +621,6 @@ SN_DEV bf16x8_t read_frag(const char* lds, int x0, int s, int lane) {
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
     const char* a0 = lds + k0 * (TILE * 2) + (col_b ^ swz_mc<TILE>(k0));
     const char* a1 = lds + k1 * (TILE * 2) + (col_b ^ swz_mc<TILE>(k1));
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
-    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, r);
-  }
-}
-
-// Fragment of a 32-row subtile (rows x0..x0+31) for 16-deep k-substep s (0..3 of a BK = 64
-// K-step), laid out as the 32x32x16 MFMA operand: lane l holds X[x0 + (l&31)][16s + 8(l>>5) + j],
-// j = 0..7.  KC: one ds_read_b128 (conflict-free under kc_off).  MC (image swizzled with
-// swz_mc<TILE, 1>): two ds_read_b64_tr_b16 per fragment, 16-lane group g covering columns
-// x0 + 16 (g & 1) .. + 15 and k rows 16s + 8 (g >> 1) + 0..3 / 4..7.
-template <int MC, int TILE>
-SN_DEV bf16x8_t read_frag32(const char* lds, int x0, int s, int lane) {
-  if (!MC) {
-    const int row = x0 + (lane & 31);
-    const int kc = 2 * s + (lane >> 5);
-    uint4 v = *reinterpret_cast<const uint4*>(lds + kc_off(row, kc));
-    return __builtin_bit_cast(bf16x8_t, v);
-  } else {
-    const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-    const int col_b = (x0 + 16 * (gq & 1) + 4 * p) * 2;
-    const int k0 = s * 16 + (gq >> 1) * 8 + q;
-    const int k1 = k0 + 4;
-    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-    const char* a0 = lds + k0 * (TILE * 2) + (col_b ^ swz_mc<TILE, 1>(k0));
-    const char* a1 = lds + k1 * (TILE * 2) + (col_b ^ swz_mc<TILE, 1>(k1));
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
     s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -955,14 +871,11 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
   }
 }
 
-// MF32 = 1: the wave tile is computed with v_mfma_f32_32x32x16_bf16 ((MFR/2) x (NFR/2) blocks
-// of 32x32, four 16-deep k-substeps per K-step) instead of the 16x16x32 form: the same LDS
-// fragment bytes per K-step, half the MFMA instructions, 24 of every 32 MFMA cycles free for
-// VALU issue instead of 8 of 16.  MC operands use the swz_mc<TILE, 1> image.
+// (v_mfma_f32_32x32x16_bf16 twins of these tiles measured slower on every conv product,
+// docs/PERF_NOTES.md round 5, and were removed in round 6)
 template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, int FP8 = 0,
-          int NFR = 4, int MFR = 4, int MF32 = 0>
+          int NFR = 4, int MFR = 4>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) gemm_kernel(SnGemmArgs args) {
-  static_assert(!MF32 || (!FP8 && NFR % 2 == 0 && MFR % 2 == 0), "32x32 blocks: bf16, even fragment counts");
   // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
   constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
   // MFMA operand formats: src A of the instruction is our B fragment (cbsz), src B our A
@@ -1011,59 +924,26 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   const int k1 = min(args.K, k0 + args.kchunk);
 
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  using SA = GStager<AMC, AMODE, BM, NW, ES, MF32>;
-  using SB = GStager<BMC, BMODE, BNL, NW, ES, MF32>;
+  using SA = GStager<AMC, AMODE, BM, NW, ES>;
+  using SB = GStager<BMC, BMODE, BNL, NW, ES>;
   SA sa;
   SB sb;
-  sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, split * args.kchunk, args.K, args.addr_legacy);
+  sa.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, split * args.kchunk, args.K);
   const int n_lim = min(args.N, n_blk + BN);
-  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1, split * args.kchunk, args.K, args.addr_legacy);
+  sb.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, BMC ? args.ones_col : -1, split * args.kchunk, args.K);
 
   f32x4 acc[NFR][MFR];
-  constexpr int NB32 = MF32 ? NFR / 2 : 1, MB32 = MF32 ? MFR / 2 : 1;
-  f32x16 acc32[NB32][MB32];
-  if constexpr (MF32) {
 #pragma unroll
-    for (int i = 0; i < NB32; ++i)
+  for (int i = 0; i < NFR; ++i)
 #pragma unroll
-      for (int j = 0; j < MB32; ++j) acc32[i][j] = f32x16{};
-  } else {
-#pragma unroll
-    for (int i = 0; i < NFR; ++i)
-#pragma unroll
-      for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+    for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int wm0 = (wave % WM) * (16 * MFR), wn0 = (wave / WM) * (16 * NFR);
   const int nk = k1 > k0 ? (k1 - k0 + BKE - 1) / BKE : 0;
 
   auto compute = [&](const char* la) __attribute__((always_inline)) {
     const char* lb = la + A_BYTES;
-    if constexpr (MF32) {
-      // two 16-deep substeps per fragment batch (the 16x16 path's two 32-deep substeps: the
-      // same fragment bytes and VGPRs per batch)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bf16x8_t fa[2][MB32], fb[2][NB32];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-#pragma unroll
-          for (int i = 0; i < NB32; ++i) fb[s][i] = read_frag32<BMC, BNL>(lb, wn0 + 32 * i, 2 * h + s, lane);
-#pragma unroll
-          for (int j = 0; j < MB32; ++j) fa[s][j] = read_frag32<AMC, BM>(la, wm0 + 32 * j, 2 * h + s, lane);
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int i = 0; i < NB32; ++i)
-#pragma unroll
-            for (int j = 0; j < MB32; ++j)
-              acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s][i], fa[s][j], acc32[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-      return;
-    } else if constexpr (FP8 && MFR * NFR > 16) {
+    if constexpr (FP8 && MFR * NFR > 16) {    } else if constexpr (FP8 && MFR * NFR > 16) {
       // large fp8 tiles (gemm_fp8big.hip): B fragments held, A fragments streamed per row
       // group, so at most NFR + 1 fragments (8 VGPRs each) live beside the accumulators
       i32x8 fb8[NFR];
@@ -1198,94 +1078,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
   }
 
   // Epilogue.  acc[i][j] holds D[n][m] with m = lane&15 (+16j), n = 4(lane>>4)+r (+16i):
-  // each lane owns 4 consecutive output columns of one output row.  MF32: the 32x32 block
-  // (I, J) holds D[n][m] with m = 32J + (lane&31), n = 32I + 8b + 4(lane>>5) + r in its
-  // registers 4b + r; its four 4-register groups become acc[2I + (b>>1)][2J + (b&1)], so the
-  // epilogue below sees the same 4-column fragments at the positions wave_m / wave_n give.
-  if constexpr (MF32) {
-#pragma unroll
-    for (int i = 0; i < NFR; ++i)
-#pragma unroll
-      for (int j = 0; j < MFR; ++j) {
-        const int b = ((i & 1) << 1) | (j & 1);
-        const f32x16& t = acc32[i >> 1][j >> 1];
-        acc[i][j] = f32x4{t[4 * b], t[4 * b + 1], t[4 * b + 2], t[4 * b + 3]};
-      }
-  }
+  // each lane owns 4 consecutive output columns of one output row.
   // wave-relative row (m) of fragment row j, and column (n) of fragment (i, j), of this lane
-  auto wave_m = [&](int j) __attribute__((always_inline)) {
-    return MF32 ? 32 * (j >> 1) + (lane & 31) : 16 * j + (lane & 15);
-  };
-  auto wave_n = [&](int i, int j) __attribute__((always_inline)) {
-    return MF32 ? 32 * (i >> 1) + 8 * (((i & 1) << 1) | (j & 1)) + 4 * (lane >> 5) : 16 * i + 4 * (lane >> 4);
-  };
-  int esplit = split;  // the fp32 slab the epilogue stores into (split-K without fix_cnt)
-  // (only in wave tiles of <= 16 fragments: larger ones would spill the K-loop to scratch;
-  // the host keeps _FIX_TILES to the tiles that have it)
-  if constexpr (EPI != EPI_SGD && NFR * MFR <= 16) {
-    if (args.fix_cnt) {
-      // In-launch deterministic split-K combine (host: splits > 1): every K-slice block stores
-      // its fp32 partial tile in its slab WRITE-THROUGH (sc1 16-B buffer stores: visible to every
-      // XCD once drained, so no release fence — an agent-scope release per block, i.e. an L2
-      // write-back in each of hundreds of blocks, cost CaffeNet 9 %), drains them, and takes a
-      // relaxed agent-scope ticket on the tile's counter; the block that draws ticket splits-1
-      // acquires (agent scope), sums ALL slices in split order 0..S-1 from the slabs (so the sum
-      // is bitwise independent of which block arrives last, and equal to splitk_reduce_kernel's
-      // sequential order) and runs the product's real epilogue;
-      // it resets the counter for the next launch (the host zeroes the counter pool once).
-      // cdna_hip_programming.md, "In-launch split-K reduction" and Guideline 16 R1.
-      const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(args.fix_ws, (short)0, 0x7fffffff, 0x00020000);
-      const unsigned sbase = (unsigned)(((long long)grp * args.splits + split) * args.fix_sstride);  // host: < 2^29 floats
-#pragma unroll
-      for (int j = 0; j < MFR; ++j) {
-        const int m = m_blk + wm0 + wave_m(j);
-#pragma unroll
-        for (int i = 0; i < NFR; ++i) {
-          const int n = n_blk + wn0 + wave_n(i, j);
-          if (m < args.M && n < args.N)  // host: fix_ld % 4 == 0 and fix_ld >= N rounded up to 4
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), wsr,
-                                                   (int)((sbase + (unsigned)m * (unsigned)args.fix_ld + n) * 4u), 0, 16);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      int* cnt = args.fix_cnt + (long long)grp * tiles + tile;
-      int* flag = reinterpret_cast<int*>(smem0);
-      if (tid == 0) {
-        const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = ticket == args.splits - 1;
-        if (last) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        *flag = last;
-      }
-      __syncthreads();
-      if (!*flag) return;
-      // every slice from its slab (this block's own included: the same fp32 values it stored),
-      // summed in place in split order — no second register tile
-      const float* ws0 = args.fix_ws + (long long)grp * args.splits * args.fix_sstride;
-#pragma unroll
-      for (int i = 0; i < NFR; ++i)
-#pragma unroll
-        for (int j = 0; j < MFR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int q = 0; q < args.splits; ++q) {
-        const float* sq = ws0 + (long long)q * args.fix_sstride;
-#pragma unroll
-        for (int j = 0; j < MFR; ++j) {
-          const int m = m_blk + wm0 + wave_m(j);
-#pragma unroll
-          for (int i = 0; i < NFR; ++i) {
-            const int n = n_blk + wn0 + wave_n(i, j);
-            if (m < args.M && n < args.N) acc[i][j] += *reinterpret_cast<const f32x4*>(sq + (long long)m * args.fix_ld + n);
-          }
-        }
-      }
-      esplit = 0;
-      __syncthreads();  // the flag word is LDS the staged epilogue below may reuse
-    }
-  }
+  auto wave_m = [&](int j) __attribute__((always_inline)) { return 16 * j + (lane & 15); };
+  auto wave_n = [&](int i, int j) __attribute__((always_inline)) { return 16 * i + 4 * (lane >> 4); };
+  const int esplit = split;  // the fp32 slab the epilogue stores into (split-K)
   // fp32 outputs: the bias-gradient column (when routed to bias_out) is not part of C
   const int c_cols = (!epi_bf16<EPI>() && args.bias_out) ? args.ones_col : args.N;
   if constexpr (EPI == EPI_SGD) {
@@ -1476,10 +1273,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
 // 256² template of §5).  Phase 4 reads nothing new and needs no barrier.  DMAs past the
 // last K-step read the zero page, which keeps the vmcnt arithmetic uniform.
 // ---------------------------------------------------------------------------------------
-// PH = 2 merges the phases pairwise: X = (lo,lo)+(lo,hi) reading A_lo, B_lo, B_hi and
+// The four phases are merged pairwise: X = (lo,lo)+(lo,hi) reading A_lo, B_lo, B_hi and
 // Y = (hi,hi)+(hi,lo) reading A_hi; DMA stream X(t): A_hi(t+1), Y(t): A_lo, B_lo, B_hi of
-// t+2 — two barriers per K-step and twice the MFMAs behind each read burst.
-template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BN, int PH = 2>
+// t+2 — two barriers per K-step and twice the MFMAs behind each read burst.  (The unmerged
+// 4-phase form and the 8-phase template schedule measured slower on every shape, round 4;
+// removed in round 6.)
+template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BN>
 __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
   constexpr int BM = 256, HA = 128, HB = BN / 2, NW = 8;
   constexpr int WM = BN == 256 ? 2 : 4, WN = NW / WM;
@@ -1489,7 +1288,6 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
   using SA = GStager<AMC, AMODE, HA, NW>;
   using SB = GStager<BMC, BMODE, HB, NW>;
   constexpr int H_A = SA::NI, H_B = SB::NI;  // DMA instructions per wave per half
-  constexpr int VM1 = 2 * H_A + 3 * H_B, VM23 = 3 * H_A + 2 * H_B;
   static_assert(MF >= 1 && NF >= 1 && MF * 16 * WM == HA && NF * 16 * WN == HB, "wave layout");
   static_assert(2 * STAGE <= 160 * 1024, "LDS");
 
@@ -1518,10 +1316,10 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
 
   SA sa_lo, sa_hi;
   SB sb_lo, sb_hi;
-  sa_lo.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, k0, args.K, args.addr_legacy);
-  sa_hi.init(args.A, grp, wv, lane, m_blk + HA, args.M, m_blk + HA, args.M, -1, k0, args.K, args.addr_legacy);
-  sb_lo.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, ones, k0, args.K, args.addr_legacy);
-  sb_hi.init(args.B, grp, wv, lane, n_blk + HB, n_lim, n_blk + HB, n_lim, ones, k0, args.K, args.addr_legacy);
+  sa_lo.init(args.A, grp, wv, lane, m_blk, args.M, m_blk, args.M, -1, k0, args.K);
+  sa_hi.init(args.A, grp, wv, lane, m_blk + HA, args.M, m_blk + HA, args.M, -1, k0, args.K);
+  sb_lo.init(args.B, grp, wv, lane, n_blk, n_lim, n_blk, n_lim, ones, k0, args.K);
+  sb_hi.init(args.B, grp, wv, lane, n_blk + HB, n_lim, n_blk + HB, n_lim, ones, k0, args.K);
 
   auto A_lo = [&](int b) { return smem + b * STAGE; };
   auto A_hi = [&](int b) { return smem + b * STAGE + A_HALF; };
@@ -1567,66 +1365,6 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  if constexpr (PH == 8) {
-    // The 8-phase schedule (cdna_hip_programming "The 256^2 8-phase template"): four phases
-    // per K-tile, one C-quadrant of 16 (BN 256) MFMAs per phase, two barriers per phase; each
-    // phase issues its fragment reads and ONE half-tile LDS-DMA before its first barrier and
-    // its MFMAs after it.  Half-tile stream: phase q of K-tile t stages
-    //   q0: B_lo(t+1)   q1: A_lo(t+2)   q2: B_hi(t+2)   q3: A_hi(t+2)
-    // each into a region whose last read was the phase before (WAR: the previous phase's
-    // second barrier); q3 waits vmcnt(A_lo + B_hi + A_hi loads) before its first barrier, which
-    // retires every half of K-tile t+1 (read from the next phase on).  DMAs past the K range
-    // read zeros (same instruction count, so the counted waits hold).
-    constexpr int VM3 = 2 * H_A + H_B;
-    if (nk > 0) {
-      dma_a_lo(0);
-      dma_b_hi(0);
-      dma_a_hi(0);
-      dma_b_lo(0);
-      dma_a_lo(1);
-      dma_b_hi(1);
-      dma_a_hi(1);
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM3));
-      __builtin_amdgcn_s_barrier();
-      auto ktile = [&](int t, int b) __attribute__((always_inline)) {
-        // q0: (A_lo, B_lo)
-        read_a(A_lo(b));
-        read_b(fbl, B_lo(b));
-        dma_b_lo(t + 1);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        mma(acc[0][0], fbl);
-        __builtin_amdgcn_s_barrier();
-        // q1: (A_lo, B_hi)
-        read_b(fbh, B_hi(b));
-        dma_a_lo(t + 2);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        mma(acc[0][1], fbh);
-        __builtin_amdgcn_s_barrier();
-        // q2: (A_hi, B_hi)
-        read_a(A_hi(b));
-        dma_b_hi(t + 2);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        mma(acc[1][1], fbh);
-        __builtin_amdgcn_s_barrier();
-        // q3: (A_hi, B_lo)
-        read_b(fbl, B_lo(b));
-        dma_a_hi(t + 2);
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM3));
-        __builtin_amdgcn_s_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        mma(acc[1][0], fbl);
-        __builtin_amdgcn_s_barrier();
-      };
-      for (int t = 0; t < nk; t += 2) {
-        ktile(t, 0);
-        if (t + 1 < nk) ktile(t + 1, 1);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  } else
   if (nk > 0) {
     // prologue: K-step 0 whole, K-step 1 without A_hi (issued in P1(0))
     dma_a_lo(0);
@@ -1636,7 +1374,7 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
     dma_a_lo(1);
     dma_b_lo(1);
     dma_b_hi(1);
-    if constexpr (PH == 2) {
+    {
       constexpr int VMX = 2 * H_A + 2 * H_B;
       // prologue above also issued B_hi(1) and A_hi(0): the stream matches X/Y's
       for (int t = 0; t < nk; ++t) {
@@ -1662,34 +1400,6 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
         mma(acc[1][1], fbh);
         mma(acc[1][0], fbl);
       }
-    } else
-    for (int t = 0; t < nk; ++t) {
-      const int b = t & 1;
-      // P1: needs A_lo(t), B_lo(t)
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM1));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      dma_a_hi(t + 1);
-      read_a(A_lo(b));
-      read_b(fbl, B_lo(b));
-      mma(acc[0][0], fbl);
-      // P2: needs B_hi(t)
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM23));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      dma_a_lo(t + 2);
-      read_b(fbh, B_hi(b));
-      mma(acc[0][1], fbh);
-      // P3: needs A_hi(t)
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(VM23));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      dma_b_lo(t + 2);
-      read_a(A_hi(b));
-      mma(acc[1][1], fbh);
-      // P4: B_hi(b) was last read in P2, every wave is past P3's barrier
-      dma_b_hi(t + 2);
-      mma(acc[1][0], fbl);
     }
     // no LDS-DMA may still be landing when the workgroup retires
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1714,17 +1424,17 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(SnGemmArgs args) {
     }
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int BN, int PH>
+template <int AMC, int AMODE, int BMC, int BMODE, int BN>
 int launch256_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BN, PH>), grid, dim3(512), 0, st, a);
+      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BN>), grid, dim3(512), 0, st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BN, PH>), grid, dim3(512), 0, st, a);
+      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BN>), grid, dim3(512), 0, st, a);
       break;
     case EPI_F32_ACC:
-      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BN, PH>), grid, dim3(512), 0, st, a);
+      hipLaunchKernelGGL((gemm256_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BN>), grid, dim3(512), 0, st, a);
       break;
     default:
       return 2;
@@ -1732,41 +1442,40 @@ int launch256_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   return SN_CHECK_LAUNCH();
 }
 
-template <int BN, int PH = 2>
+template <int BN>
 int launch256(const SnGemmArgs& a, hipStream_t stream) {
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles * a.splits * a.groups);
   const int key = (a.a_mc << 3) | (a.a_mode << 2) | (a.b_mc << 1) | a.b_mode;
   switch (key) {
-    case 0b0000: return launch256_epi<0, OP_DENSE, 0, OP_DENSE, BN, PH>(a, grid, stream);   // NT dense
-    case 0b0100: return launch256_epi<0, OP_IM2COL, 0, OP_DENSE, BN, PH>(a, grid, stream);  // conv fwd / dgrad
-    case 0b0010: return launch256_epi<0, OP_DENSE, 1, OP_DENSE, BN, PH>(a, grid, stream);   // NN dense
-    case 0b1010: return launch256_epi<1, OP_DENSE, 1, OP_DENSE, BN, PH>(a, grid, stream);   // TN dense
-    case 0b1011: return launch256_epi<1, OP_DENSE, 1, OP_IM2COL, BN, PH>(a, grid, stream);  // conv wgrad
+    case 0b0000: return launch256_epi<0, OP_DENSE, 0, OP_DENSE, BN>(a, grid, stream);   // NT dense
+    case 0b0100: return launch256_epi<0, OP_IM2COL, 0, OP_DENSE, BN>(a, grid, stream);  // conv fwd / dgrad
+    case 0b0010: return launch256_epi<0, OP_DENSE, 1, OP_DENSE, BN>(a, grid, stream);   // NN dense
+    case 0b1010: return launch256_epi<1, OP_DENSE, 1, OP_DENSE, BN>(a, grid, stream);   // TN dense
+    case 0b1011: return launch256_epi<1, OP_DENSE, 1, OP_IM2COL, BN>(a, grid, stream);  // conv wgrad
     default: break;
   }
   return 4;
 }
 
-template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS, int NFR = 4, int MFR = 4,
-          int MF32 = 0>
+template <int AMC, int AMODE, int BMC, int BMODE, int BM, int BN, int NW, int NS, int NFR = 4, int MFR = 4>
 int launch_epi(const SnGemmArgs& a, dim3 grid, hipStream_t st) {
   switch (a.epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS, false, NFR, MFR, MF32>), grid,
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_BF16, BM, BN, NW, NS, false, NFR, MFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_BF16_DROP:  // InnerProduct forward only (dense NT)
       if (AMC || AMODE != OP_DENSE || BMC || BMODE != OP_DENSE) return 4;
-      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, NW, NS, false, NFR, MFR, MF32>),
+      hipLaunchKernelGGL((gemm_kernel<0, OP_DENSE, 0, OP_DENSE, EPI_BF16_DROP, BM, BN, NW, NS, false, NFR, MFR>),
                          grid, dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS, false, NFR, MFR, MF32>), grid,
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32, BM, BN, NW, NS, false, NFR, MFR>), grid,
                          dim3(NW * 64), 0, st, a);
       break;
     case EPI_F32_ACC:
-      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS, false, NFR, MFR, MF32>),
+      hipLaunchKernelGGL((gemm_kernel<AMC, AMODE, BMC, BMODE, EPI_F32_ACC, BM, BN, NW, NS, false, NFR, MFR>),
                          grid, dim3(NW * 64), 0, st, a);
       break;
     default:
@@ -1841,8 +1550,4 @@ int sn_gemm_t256(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big8(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_big4(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_fp8_big(const SnGemmArgs& a, hipStream_t stream);
-int sn_gemm_pk_a(const SnGemmArgs& a, hipStream_t stream);
 int sn_gemm_tiles_c(const SnGemmArgs& a, hipStream_t stream);
-int sn_gemm_t256p8(const SnGemmArgs& a, hipStream_t stream);
-int sn_gemm_pk_b(const SnGemmArgs& a, hipStream_t stream);
-int sn_gemm_mf32(const SnGemmArgs& a, hipStream_t stream);

@@ -289,72 +289,6 @@ __global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, bf16_t* __restrict__
   if (qs.q) q_flush(qs, qmax);
 }
 
-// 3x3 / stride-1 max pooling forward, one thread per 2 x 2 block of outputs: the 4 x 4 input
-// pixels the block's windows cover are loaded once (16 loads for 4 outputs instead of 36);
-// each window is scanned in the order maxpool_fwd_k uses (first strict maximum wins), so the
-// values and the argmax mask are bitwise equal.
-__global__ void __launch_bounds__(256) maxpool_fwd_k3s1(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                        uint8_t* __restrict__ mask, PoolGeom g, int gate, QSide qs,
-                                                        FDiv fBQ, FDiv fBP, int BQ, int BP) {
-  const int cv = g.C / 8;
-  float qmax = 0.f;
-  const float qsc = qs.q ? qs.slot[0] : 0.f;
-  const long long total = (long long)g.N * BP * BQ * cv;
-  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const uint32_t blk = udiv((uint32_t)i, g.fcv), bp_ = udiv(blk, fBQ), n = udiv(bp_, fBP);
-    const int c0 = (int)((uint32_t)i - blk * cv) * 8;
-    const int bq = (int)(blk - bp_ * BQ), bp = (int)(bp_ - n * BP);
-    const int hs = 2 * bp - g.ph, ws = 2 * bq - g.pw;  // input row / column of the block's first window
-    uint4 v[16];
-    bool ok[16];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int h = hs + a, w = ws + b;
-        ok[a * 4 + b] = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-        const int hc = min(max(h, 0), g.H - 1), wc = min(max(w, 0), g.W - 1);
-        v[a * 4 + b] = *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + hc) * g.W + wc) * g.C + c0);
-      }
-#pragma unroll
-    for (int oa = 0; oa < 2; ++oa)
-#pragma unroll
-      for (int ob = 0; ob < 2; ++ob) {
-        const int p = 2 * bp + oa, q = 2 * bq + ob;
-        if (p >= g.P || q >= g.Q) continue;
-        float best[8];
-        int arg[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
-#pragma unroll
-        for (int widx = 0; widx < 9; ++widx) {
-          const int t = (oa + widx / 3) * 4 + (ob + widx % 3);
-          float f[8];
-          unpack8(v[t], f);
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (ok[t] && f[k] > best[k]) { best[k] = f[k]; arg[k] = widx; }
-        }
-        if (gate) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (!(best[k] > 0.f)) arg[k] = 255;
-        }
-        const long long o = (((long long)n * g.P + p) * g.Q + q) * g.C + c0;
-        *reinterpret_cast<uint4*>(y + o) = pack8(best);
-        if (qs.q) *reinterpret_cast<uint2*>(qs.q + o) = q_pack8(qs, qsc, best, qmax);
-        if (mask) {
-          uint2 m;
-          m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
-          m.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
-          *reinterpret_cast<uint2*>(mask + o) = m;
-        }
-      }
-  }
-  if (qs.q) q_flush(qs, qmax);
-}
-
 // NH x NW = max number of windows covering one input pixel (ceil(k / stride) per axis).
 template <int NH, int NW, bool MAX>
 __global__ void pool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
@@ -486,49 +420,6 @@ __global__ void pool_bwd_k3s2(const bf16_t* __restrict__ dy, const uint8_t* __re
   }
 }
 
-// 2x2 / stride-2 max pooling (VGG-16's five pools): each input pixel lies in at most one
-// window, so one thread owns a window's 2 x 2 input block for 8 channels — one dy load and one
-// mask load feed four pixel stores (the per-pixel gather above re-reads both for each of the
-// four).  Blocks without a window (floor-mode edges) store zeros; same arithmetic as
-// pool_bwd_k<1, 1, true> (0 + dy where the argmax matches), so the results are bitwise equal.
-__global__ void __launch_bounds__(256) pool_bwd_k2s2(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
-                              bf16_t* __restrict__ dx, PoolGeom g, FDiv fBW, FDiv fBH, int BW, int BH, QSide qs) {
-  const int cv = g.C / 8;
-  float qmax = 0.f;
-  const float qsc = qs.q ? qs.slot[0] : 0.f;
-  const long long total = (long long)g.N * BH * BW * cv;
-  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const uint32_t blk = udiv((uint32_t)i, g.fcv), bh_ = udiv(blk, fBW), n = udiv(bh_, fBH);
-    const int c0 = (int)((uint32_t)i - blk * cv) * 8;
-    const int bw = (int)(blk - bh_ * BW), bh = (int)(bh_ - n * BH);
-    const bool win = bh < g.P && bw < g.Q;
-    const long long o = (((long long)n * g.P + min(bh, g.P - 1)) * g.Q + min(bw, g.Q - 1)) * g.C + c0;
-    const uint4 dv = *reinterpret_cast<const uint4*>(dy + o);
-    const uint2 mv = *reinterpret_cast<const uint2*>(mask + o);
-    float f[8];
-    unpack8(dv, f);
-    const uint32_t mw[2] = {mv.x, mv.y};
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int h = 2 * bh + a - g.ph, w = 2 * bw + b - g.pw;
-        if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
-        float acc[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          acc[k] = 0.f;
-          if (win && (int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == a * 2 + b) acc[k] += f[k];
-        }
-        const long long od = (((long long)n * g.H + h) * g.W + w) * g.C + c0;
-        *reinterpret_cast<uint4*>(dx + od) = pack8(acc);
-        if (qs.q) *reinterpret_cast<uint2*>(qs.q + od) = q_pack8(qs, qsc, acc, qmax);
-      }
-  }
-  if (qs.q) q_flush(qs, qmax);
-}
-
 static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long long P, long long Q, long long kh,
                        long long kw, long long sh, long long sw, long long ph, long long pw) {
   PoolGeom g;
@@ -541,187 +432,9 @@ static PoolGeom mkgeom(long long N, long long H, long long W, long long C, long 
   return g;
 }
 
-// 3x3 / stride-1 max pooling through an LDS row band (GoogLeNet's Inception pool branches).
-// The per-output gathers (maxpool_fwd_k<3, 3>, pool_bwd_k<3, 3, true>) issue 9 global loads per
-// 16-byte output; each input row is fetched from L2 by the three rows of windows that use it, and
-// both ran at ~2.9 TB/s effective in isolation at GoogLeNet b128 (profiles/r5_pool_band.txt).  Tried
-// here (opt-in, slower — see band_shape):
-// one workgroup owns (image, run of R output rows, group of cg channel chunks): it stages the R + 2
-// input rows (all columns, its channel chunks) in LDS with one coalesced load each, then every
-// output reads its 9 window taps from LDS.  The windows are scanned (forward) and summed
-// (backward) in the order of the gathers, so the results are bitwise equal.
-struct BandGeom {
-  int R, cg, ngrp, nb;
-  FDiv fWcg, fQcg, fcg;
-};
-
-__global__ void __launch_bounds__(256) maxpool3s1_band(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                       uint8_t* __restrict__ mask, PoolGeom g, int gate, BandGeom b) {
-  extern __shared__ uint4 band[];  // (R + 2) x W x cg input chunks
-  const int bid = xcd_block(blockIdx.x, gridDim.x);
-  const int wg = bid / b.ngrp, ch0 = (bid - wg * b.ngrp) * b.cg;
-  const int n = wg / b.nb, p0 = (wg - n * b.nb) * b.R;
-  const int rows = min(b.R, g.P - p0);
-  const int h0 = p0 - g.ph;  // input row of band row 0
-  const int wcg = g.W * b.cg;
-  const int items1 = (rows + 2) * wcg;
-  for (int it = threadIdx.x; it < items1; it += blockDim.x) {
-    const uint32_t r = udiv((uint32_t)it, b.fWcg);
-    const int rem = it - (int)r * wcg;
-    const uint32_t w = udiv((uint32_t)rem, b.fcg);
-    const int lc = rem - (int)w * b.cg;
-    const int h = h0 + (int)r;
-    if ((unsigned)h < (unsigned)g.H)
-      band[it] = *reinterpret_cast<const uint4*>(x + (((long long)n * g.H + h) * g.W + w) * g.C + (ch0 + lc) * 8);
-  }
-  __syncthreads();
-  const int qcg = g.Q * b.cg;
-  const int items2 = rows * qcg;
-  for (int it = threadIdx.x; it < items2; it += blockDim.x) {
-    const uint32_t r = udiv((uint32_t)it, b.fQcg);
-    const int rem = it - (int)r * qcg;
-    const uint32_t q = udiv((uint32_t)rem, b.fcg);
-    const int lc = rem - (int)q * b.cg;
-    const int ws = (int)q - g.pw;
-    float best[8];
-    int arg[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const int h = h0 + (int)r + a;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int w = ws + c;
-        if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
-        float f[8];
-        unpack8(band[((int)r + a) * wcg + w * b.cg + lc], f);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (f[k] > best[k]) { best[k] = f[k]; arg[k] = a * 3 + c; }
-      }
-    }
-    if (gate) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (!(best[k] > 0.f)) arg[k] = 255;
-    }
-    const long long o = (((long long)n * g.P + p0 + (int)r) * g.Q + q) * g.C + (ch0 + lc) * 8;
-    *reinterpret_cast<uint4*>(y + o) = pack8(best);
-    if (mask) {
-      uint2 m;
-      m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
-      m.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
-      *reinterpret_cast<uint2*>(mask + o) = m;
-    }
-  }
-}
-
-// backward: the workgroup owns R input rows; the windows covering them are pooled rows
-// hp0 - 2 .. hp0 + R - 1 (hp0 = first row + ph), staged with their argmax masks
-__global__ void __launch_bounds__(256) pool3s1_band_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
-                                                        bf16_t* __restrict__ dx, PoolGeom g, BandGeom b) {
-  extern __shared__ uint4 band[];  // (R + 2) x Q x cg gradient chunks, then as many uint2 masks
-  const int bid = xcd_block(blockIdx.x, gridDim.x);
-  const int wg = bid / b.ngrp, ch0 = (bid - wg * b.ngrp) * b.cg;
-  const int n = wg / b.nb, h0 = (wg - n * b.nb) * b.R;
-  const int rows = min(b.R, g.H - h0);
-  const int pr0 = h0 + g.ph - 2;  // pooled row of band row 0
-  const int qcg = g.Q * b.cg;
-  const int items1 = (rows + 2) * qcg;
-  uint2* mband = reinterpret_cast<uint2*>(band + items1);
-  for (int it = threadIdx.x; it < items1; it += blockDim.x) {
-    const uint32_t r = udiv((uint32_t)it, b.fQcg);
-    const int rem = it - (int)r * qcg;
-    const uint32_t q = udiv((uint32_t)rem, b.fcg);
-    const int lc = rem - (int)q * b.cg;
-    const int p = pr0 + (int)r;
-    if ((unsigned)p < (unsigned)g.P) {
-      const long long o = (((long long)n * g.P + p) * g.Q + q) * g.C + (ch0 + lc) * 8;
-      band[it] = *reinterpret_cast<const uint4*>(dy + o);
-      mband[it] = *reinterpret_cast<const uint2*>(mask + o);
-    }
-  }
-  __syncthreads();
-  const int wcg = g.W * b.cg;
-  const int items2 = rows * wcg;
-  for (int it = threadIdx.x; it < items2; it += blockDim.x) {
-    const uint32_t r = udiv((uint32_t)it, b.fWcg);
-    const int rem = it - (int)r * wcg;
-    const uint32_t w = udiv((uint32_t)rem, b.fcg);
-    const int lc = rem - (int)w * b.cg;
-    const int h = h0 + (int)r;
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // windows p = h + ph - 2 .. h + ph (band rows r .. r + 2), q = w + pw - 2 .. w + pw, ascending
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int p = pr0 + (int)r + t;
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int q = (int)w + g.pw - 2 + u;
-        if ((unsigned)p >= (unsigned)g.P || (unsigned)q >= (unsigned)g.Q) continue;
-        const int widx = (2 - t) * 3 + (2 - u);  // this pixel's offset inside window (p, q)
-        const int li = ((int)r + t) * qcg + q * b.cg + lc;
-        float f[8];
-        unpack8(band[li], f);
-        const uint2 mv = mband[li];
-        const uint32_t mw[2] = {mv.x, mv.y};
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if ((int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == widx) acc[k] += f[k];
-      }
-    }
-    *reinterpret_cast<uint4*>(dx + (((long long)n * g.H + h) * g.W + w) * g.C + (ch0 + lc) * 8) = pack8(acc);
-  }
-}
-
-// Band shape: cg = the largest divisor of the C / 8 chunks that is <= 8 (128-byte runs), then the
-// most rows whose (R + 2)-row tile fits SN_POOL_BAND_LDS bytes (default 40 KB).  Opt-in
-// (SN_POOL_BAND=1): 10-20 % SLOWER than the gathers at every GoogLeNet shape (3a forward 38.3 vs
-// 33.5 us, backward 41.1 vs 33.8; GoogLeNet 22.09-22.16 vs 22.25-22.30 k img/s,
-// profiles/r5_pool_band.txt) — the gathers' re-reads hit L2 and the band's load / barrier /
-// compute phases serialise within a workgroup.
-static bool band_shape(long long rows_total, long long width, long long C, int item_bytes, BandGeom* b) {
-  const char* e = std::getenv("SN_POOL_BAND");
-  if (!e || std::atoi(e) == 0) return false;
-  const char* lb = std::getenv("SN_POOL_BAND_LDS");
-  const long long budget = lb ? std::atoll(lb) : 40 * 1024;
-  const int cv = (int)(C / 8);
-  int cg = 1;
-  for (int c = 8; c >= 1; --c)
-    if (cv % c == 0) { cg = c; break; }
-  const long long per_row = width * cg * item_bytes;
-  long long R = budget / per_row - 2;
-  if (R < 2) return false;
-  if (R > rows_total) R = rows_total;
-  // balance the bands: the fewest bands of this height, then the shortest height giving as many
-  const long long nbands = (rows_total + R - 1) / R;
-  R = (rows_total + nbands - 1) / nbands;
-  b->R = (int)R;
-  b->cg = cg;
-  b->ngrp = cv / cg;
-  b->nb = (int)nbands;
-  b->fcg = make_fdiv((uint32_t)cg);
-  return true;
-}
-
-// SN_POOL_K2S2=1: 2x2 / stride-2 max-pool backward with one thread per window block.  Opt-in:
-// 6 % faster on VGG's two largest pools at b256 but slower on the small ones, VGG-16 b2048 fp8
-// unchanged (11.31 vs 11.32 k img/s, profiles/r4_pool_block_ab.txt)
-static bool k2s2_ok() {
-  const char* e = std::getenv("SN_POOL_K2S2");
-  return e && std::atoi(e) != 0;
-}
-
-// SN_POOL_K3S1=1: 3x3 / stride-1 max pooling (forward and backward) with one thread per 2 x 2
-// block.  Opt-in: fewer loads, but lower occupancy than the per-output gathers whose re-reads hit
-// L1 / L2 — 5-25 % slower at GoogLeNet's Inception shapes, GoogLeNet 20.8-21.0 vs 21.0-21.1 k
-// img/s (profiles/r4_pool_block_ab.txt)
-static bool k3s1_ok() {
-  const char* e = std::getenv("SN_POOL_K3S1");
-  return e && std::atoi(e) != 0;
-}
-
+// (Round 6 removed the measured-and-rejected opt-in variants: LDS row-band 3x3 / stride-1 pooling,
+// block-per-thread 2x2 / stride-2 backward and 3x3 / stride-1 forward / backward —
+// docs/PERF_NOTES.md rounds 4-5.)
 extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long N, long long H, long long W,
                            long long C, long long P, long long Q, long long kh, long long kw, long long sh,
                            long long sw, long long ph, long long pw, long long method, long long gate,
@@ -735,21 +448,8 @@ extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long 
   const bool vec = (C % 8) == 0;
   long long total = N * P * Q * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
-  BandGeom bg{};
-  if (method == 0 && vec && !q && kh == 3 && kw == 3 && sh == 1 && sw == 1 && P == H + 2 * ph - 2 &&
-      Q == W + 2 * pw - 2 && band_shape(P, W, C, 16, &bg)) {
-    bg.fWcg = make_fdiv((uint32_t)(W * bg.cg));
-    bg.fQcg = make_fdiv((uint32_t)(Q * bg.cg));
-    const size_t lds = (size_t)(bg.R + 2) * W * bg.cg * 16;
-    hipLaunchKernelGGL(maxpool3s1_band, dim3((unsigned)(N * bg.nb * bg.ngrp)), dim3(256), lds, st, x, y, mask, g,
-                       (int)gate, bg);
-  } else if (method == 0 && vec && kh == kw && (kh == 2 || kh == 3)) {
-    if (kh == 3 && sh == 1 && sw == 1 && k3s1_ok()) {
-      const int BP = (int)((P + 1) / 2), BQ = (int)((Q + 1) / 2);
-      const long long nt = N * BP * BQ * (C / 8);
-      hipLaunchKernelGGL(maxpool_fwd_k3s1, dim3(sn_blocks(nt, 256, 16384)), dim3(256), 0, st, x, y, mask, g,
-                         (int)gate, qs, make_fdiv((uint32_t)BQ), make_fdiv((uint32_t)BP), BQ, BP);
-    } else if (kh == 3)
+  if (method == 0 && vec && kh == kw && (kh == 2 || kh == 3)) {
+    if (kh == 3)
       hipLaunchKernelGGL((maxpool_fwd_k<3, 3>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate, qs);
     else hipLaunchKernelGGL((maxpool_fwd_k<2, 2>), grid, dim3(256), 0, st, x, y, mask, g, (int)gate, qs);
   } else if (method == 0) {
@@ -764,63 +464,6 @@ extern "C" int sn_pool_fwd(const bf16_t* x, bf16_t* y, uint8_t* mask, long long 
     else hipLaunchKernelGGL(avepool_fwd<false>, ag, dim3(bs), 0, st, x, y, g);
   }
   return SN_CHECK_LAUNCH();
-}
-
-// 3x3 / stride-1 max pooling (GoogLeNet's Inception pool branches): the per-pixel gather
-// loads 9 windows (dy + mask) per input pixel; one thread per 2 x 2 input block loads the 4 x 4
-// windows that cover it — 4 per pixel.  Each pixel sums its windows in ascending (p, q) order
-// starting from 0, as pool_bwd_k<3, 3, true> does, so the results are bitwise equal.
-__global__ void __launch_bounds__(256) pool_bwd_k3s1(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
-                              bf16_t* __restrict__ dx, PoolGeom g, FDiv fBW, FDiv fBH, int BW, int BH, QSide qs) {
-  const int cv = g.C / 8;
-  float qmax = 0.f;
-  const float qsc = qs.q ? qs.slot[0] : 0.f;
-  const long long total = (long long)g.N * BH * BW * cv;
-  for (long long i = xcd_block(blockIdx.x, gridDim.x) * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const uint32_t blk = udiv((uint32_t)i, g.fcv), bh_ = udiv(blk, fBW), n = udiv(bh_, fBH);
-    const int c0 = (int)((uint32_t)i - blk * cv) * 8;
-    const int bw = (int)(blk - bh_ * BW), bh = (int)(bh_ - n * BH);
-    // windows p0 .. p0 + 3 (q0 .. q0 + 3) cover input rows 2 bh, 2 bh + 1 (columns 2 bw, 2 bw + 1)
-    const int p0 = 2 * bh + g.ph - 2, q0 = 2 * bw + g.pw - 2;
-    uint4 dv[16];
-    uint2 mv[16];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int pc = min(max(p0 + t, 0), g.P - 1), qc = min(max(q0 + u, 0), g.Q - 1);
-        const long long o = (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0;
-        dv[t * 4 + u] = *reinterpret_cast<const uint4*>(dy + o);
-        mv[t * 4 + u] = *reinterpret_cast<const uint2*>(mask + o);
-      }
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int h = 2 * bh + a, w = 2 * bw + b;
-        if (h >= g.H || w >= g.W) continue;
-        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-#pragma unroll
-          for (int u = 0; u < 3; ++u) {
-            const int p = p0 + a + t, q = q0 + b + u, wi = (a + t) * 4 + (b + u);
-            if (p < 0 || p >= g.P || q < 0 || q >= g.Q) continue;
-            const int widx = (2 - t) * 3 + (2 - u);  // this pixel's offset inside window (p, q)
-            float f[8];
-            unpack8(dv[wi], f);
-            const uint32_t mw[2] = {mv[wi].x, mv[wi].y};
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if ((int)((mw[k >> 2] >> ((k & 3) * 8)) & 0xff) == widx) acc[k] += f[k];
-          }
-        const long long od = (((long long)n * g.H + h) * g.W + w) * g.C + c0;
-        *reinterpret_cast<uint4*>(dx + od) = pack8(acc);
-        if (qs.q) *reinterpret_cast<uint2*>(qs.q + od) = q_pack8(qs, qsc, acc, qmax);
-      }
-  }
-  if (qs.q) q_flush(qs, qmax);
 }
 
 extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, long long N, long long H, long long W,
@@ -847,26 +490,6 @@ extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, lo
     else
       hipLaunchKernelGGL((pool_bwd_k3s2<false>), g2, dim3(256), 0, st, dy, mask, dx, g, make_fdiv((uint32_t)BW),
                          make_fdiv((uint32_t)BH), BW, BH);
-  } else if (vec && method == 0 && kh == 2 && kw == 2 && sh == 2 && sw == 2 && k2s2_ok()) {
-    if (q && !(qslot && qpart)) return 9;
-    // one thread per 2x2 input block over the padded extent [0, H + ph) x [0, W + pw)
-    const int BH = (int)((H + ph + 1) / 2), BW = (int)((W + pw + 1) / 2);
-    const long long nt = N * BH * BW * (C / 8);
-    hipLaunchKernelGGL(pool_bwd_k2s2, dim3(sn_blocks(nt, 256, 16384)), dim3(256), 0, st, dy, mask, dx, g,
-                       make_fdiv((uint32_t)BW), make_fdiv((uint32_t)BH), BW, BH, qs);
-  } else if (BandGeom bg{}; vec && method == 0 && !q && kh == 3 && kw == 3 && sh == 1 && sw == 1 &&
-             P == H + 2 * ph - 2 && Q == W + 2 * pw - 2 && band_shape(H, Q, C, 24, &bg)) {
-    bg.fWcg = make_fdiv((uint32_t)(W * bg.cg));
-    bg.fQcg = make_fdiv((uint32_t)(Q * bg.cg));
-    const size_t lds = (size_t)(bg.R + 2) * Q * bg.cg * 24;
-    hipLaunchKernelGGL(pool3s1_band_bwd, dim3((unsigned)(N * bg.nb * bg.ngrp)), dim3(256), lds, st, dy, mask, dx, g,
-                       bg);
-  } else if (vec && method == 0 && kh == 3 && kw == 3 && sh == 1 && sw == 1 && ph <= 2 && pw <= 2 && k3s1_ok()) {
-    if (q && !(qslot && qpart)) return 9;
-    const int BH = (int)((H + 1) / 2), BW = (int)((W + 1) / 2);
-    const long long nt = N * BH * BW * (C / 8);
-    hipLaunchKernelGGL(pool_bwd_k3s1, dim3(sn_blocks(nt, 256, 16384)), dim3(256), 0, st, dy, mask, dx, g,
-                       make_fdiv((uint32_t)BW), make_fdiv((uint32_t)BH), BW, BH, qs);
   } else if (vec && nh == nw && nh >= 1 && nh <= 3) {
     if (q && !(qslot && qpart)) return 9;
 #define SN_POOL_BWD_K(NN)                                                                                  \

@@ -270,28 +270,25 @@ static bool plrn_ok(long long N, long long H, long long W, long long C, long lon
 static int plrn_fwd_pix(long long C) {
   // (pixel, chunk) items per workgroup: 256 (one per thread) beat 512 / 1024 / 2048 at both
   // CaffeNet shapes (pool1/norm1 51.5 -> 47.8 us, pool2/norm2 31.1 -> 28.3 us,
-  // profiles/r4_plrn_tiles.txt); SN_PLRN_FWD_ITEMS overrides
-  const char* e = std::getenv("SN_PLRN_FWD_ITEMS");
-  const long long items = e ? std::atoll(e) : 256;
+  // profiles/r4_plrn_tiles.txt)
+  const long long items = 256;
   return (int)(items / (C / 8) > 0 ? items / (C / 8) : 1);
 }
 // backward tile: for each channel group cg (a divisor of the C / 8 chunks, at least 4 chunks =
 // 64 B of a pixel, or the whole pixel) the most block rows (<= 7, least halo recomputation)
-// whose (rows + 1) x Q x cg tile fits the LDS budget (SN_PLRN_LDS bytes, default 32 KB); of
+// whose (rows + 1) x Q x cg tile fits the LDS budget (32 KB); of
 // those, the shape whose grid is closest to 2560 workgroups (10 per CU: enough to fill every
 // CU with short blocks, few enough that the halo rows stay a small share).  Measured on CaffeNet
 // (profiles/r4_plrn_tiles.txt): pool1/norm1 74.4 -> 63.3 us (cg 12 -> 4), pool2/norm2 45.4 ->
-// 42.4 us (cg 16 -> 8).  SN_PLRN_CG forces the group size.
+// 42.4 us (cg 16 -> 8).
 static bool plrn_bwd_tile(long long N, long long Q, long long C, long long BH, int item_bytes, int* rows, int* cg) {
   const int cv = (int)(C / 8);
-  const char* e = std::getenv("SN_PLRN_LDS");
-  const long long budget = e ? std::atoll(e) : 32 * 1024;
-  const char* fc = std::getenv("SN_PLRN_CG");
+  const long long budget = 32 * 1024;
   double best = 1e30;
   bool found = false;
   for (int c = cv; c >= 1; --c) {
     if (cv % c) continue;
-    if (fc ? c != std::atoi(fc) : (c != cv && c < 4)) continue;
+    if (c != cv && c < 4) continue;
     int r = 7;
     while (r >= 1 && (long long)(r + 1) * Q * c * item_bytes > budget) --r;
     if (r < 1) continue;
@@ -332,8 +329,7 @@ extern "C" int sn_pool_lrn_fwd(const bf16_t* x, bf16_t* pooled, uint8_t* mask, b
 extern "C" int sn_pool_lrn_supported(long long N, long long H, long long W, long long C, long long P, long long Q,
                                      long long ph, long long pw, long long size) {
   if (!plrn_ok(N, H, W, C, P, Q, ph, pw, size)) return 0;
-  const char* me = std::getenv("SN_PLRN_MASK_LDS");
-  const int item_bytes = (me ? std::atoi(me) != 0 : 1) ? 24 : 16;
+  const int item_bytes = 24;  // argmax mask staged in LDS (sn_lrn_pool_bwd)
   const long long BH = (H + ph + 1) / 2, BW = (W + pw + 1) / 2;
   int rows = 0, cg = 0;
   if (!plrn_bwd_tile(N, Q, C, BH, item_bytes, &rows, &cg)) return 0;
@@ -346,10 +342,9 @@ extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_
   if (!plrn_ok(N, H, W, C, P, Q, ph, pw, size)) return 4;
   PLGeom g = plgeom(N, H, W, C, P, Q, ph, pw, size, alpha, beta, k);
   g.BH = (int)((H + ph + 1) / 2);
-  // argmax mask staged in LDS by phase 1 (SN_PLRN_MASK_LDS=0: phase 2 reads it from global
-  // memory): pool1/norm1 63.5 -> 62.2 us, pool2/norm2 42.5 -> 41.3 us (profiles/r4_plrn_tiles.txt)
-  const char* me = std::getenv("SN_PLRN_MASK_LDS");
-  const int mlds = me ? std::atoi(me) != 0 : 1;
+  // argmax mask staged in LDS by phase 1 (instead of phase 2 reading it from global memory):
+  // pool1/norm1 63.5 -> 62.2 us, pool2/norm2 42.5 -> 41.3 us (profiles/r4_plrn_tiles.txt)
+  const int mlds = 1;
   const int item_bytes = mlds ? 24 : 16;
   if (!plrn_bwd_tile(N, Q, C, g.BH, item_bytes, &g.rows, &g.cg)) return 4;
   g.ngrp = (int)(C / 8) / g.cg;

@@ -20,7 +20,7 @@ from dataclasses import dataclass, field
 
 import torch
 
-from .. import proto
+from .. import ops, proto
 from .blob import Blob
 from .filler import fill
 from .layer import Layer, Param, create_layer
@@ -447,12 +447,13 @@ class Net:
 
     # -- execution ---------------------------------------------------------------------
     def forward_from_to(self, start: int, end: int):
-        for li in range(start, end + 1):
-            layer = self.layers[li]
-            layer.forward(self.bottom_vecs[li], self.top_vecs[li])
-            if self.debug_info:
-                self._debug_forward(li)
-        return self.loss_value()
+        with ops.precision(self.dtype):  # fp32 nets on the GPU: the fp32 device mode (ops.f32dev)
+            for li in range(start, end + 1):
+                layer = self.layers[li]
+                layer.forward(self.bottom_vecs[li], self.top_vecs[li])
+                if self.debug_info:
+                    self._debug_forward(li)
+            return self.loss_value()
 
     def loss_value(self):
         """Weighted sum of the loss tops as a device scalar (no host sync)."""
@@ -490,14 +491,15 @@ class Net:
         self.prefill_loss_diffs()
         for hook in self.pre_backward_hooks:  # e.g. batched dgrad weight flips
             hook()
-        for li in range(start, end - 1, -1):
-            if self.layer_need_backward[li]:
-                self.layers[li].backward(self.top_vecs[li], self.bottom_need_backward[li],
-                                         self.bottom_vecs[li])
-                if self.debug_info:
-                    self._debug_backward(li)
-            for hook in self.backward_hooks:  # e.g. overlapped per-layer solver update
-                hook(li)
+        with ops.precision(self.dtype):
+            for li in range(start, end - 1, -1):
+                if self.layer_need_backward[li]:
+                    self.layers[li].backward(self.top_vecs[li], self.bottom_need_backward[li],
+                                             self.bottom_vecs[li])
+                    if self.debug_info:
+                        self._debug_backward(li)
+                for hook in self.backward_hooks:  # e.g. overlapped per-layer solver update
+                    hook(li)
 
     def backward(self) -> None:
         self.backward_from_to(len(self.layers) - 1, 0)

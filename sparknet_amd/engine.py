@@ -23,6 +23,7 @@ import torch
 
 from . import ops
 from .core.solver import Solver
+from .utils import features
 from .utils.trace import trace_range
 
 from .ops.spec import ConvSpec
@@ -32,7 +33,10 @@ log = logging.getLogger("sparknet_amd.engine")
 
 def fuse_relu(net) -> int:
     """Fold in-place ReLU (slope 0) into the producing Convolution / InnerProduct
-    epilogue.  Returns the number of fused pairs.  The ReLU layer keeps its backward."""
+    epilogue.  Returns the number of fused pairs.  The ReLU layer keeps its backward.
+    fp32 nets on the GPU (the fp32 device mode, ops.f32dev) run the plain layer graph."""
+    if net.device.type == "cuda" and net.dtype == torch.float32:
+        return 0
     n = 0
     for li in range(1, len(net.layers)):
         relu = net.layers[li]
@@ -52,7 +56,6 @@ def fuse_relu(net) -> int:
     fuse_dropout(net)
     fuse_concat(net)
     fuse_pool_lrn(net)
-    fuse_siblings(net)
     batch_weight_flips(net)
     return n
 
@@ -66,7 +69,7 @@ def fuse_pool_lrn(net) -> int:
     LDS and gathered straight into the pooling input gradient.  Requires the pooled blob to
     be read by the LRN alone (not a net output, no in-place LRN).  Returns the count."""
     from .ops import hip
-    if net.device.type != "cuda" or net.debug_info or os.environ.get("SN_FUSE_POOL_LRN", "1") == "0":
+    if net.device.type != "cuda" or net.debug_info or not features.enabled("fuse_pool_lrn"):
         return 0
     outputs = set(getattr(net, "output_blob_ids", ()))
     n = 0
@@ -136,7 +139,7 @@ def fuse_concat(net) -> int:
     part is a ReLU output, so the concat output is its own gate) and the Concat backward
     hands each part a channel-slice view of the output gradient, which the producing
     convolution's wgrad / dgrad GEMMs read in place.  GPU only; returns the count."""
-    if net.device.type != "cuda" or os.environ.get("SN_ZERO_COPY_CONCAT", "1") == "0":
+    if net.device.type != "cuda" or not features.enabled("zero_copy_concat"):
         return 0
     from .layers.common import ConcatSlots
     from .ops import hip
@@ -183,170 +186,6 @@ def fuse_concat(net) -> int:
     return n
 
 
-class SiblingGroup:
-    """1x1 convolutions that read the same blob (through one Split) run as ONE GEMM
-    (engine.fuse_siblings): GoogLeNet's Inception 3x3_reduce / 5x5_reduce pairs.  Caffe
-    runs every sibling as its own im2col + GEMM and sums their data gradients in the Split
-    backward (split_layer.cu, net.cpp InsertSplits).  Here the leader (first sibling in
-    layer order) runs the merged forward into one NHWC buffer whose channel slices are the
-    siblings' tops; the siblings' consumers write their data gradients straight into the
-    matching slices of one merged gradient buffer (ops.hip.conv_backward dx_out); the
-    leader's backward then runs ONE weight-gradient GEMM (M = the summed widths, bias
-    through the ones column) and ONE data-gradient GEMM (reduction over the summed widths),
-    and the Split drops the followers' tops from its sum.  Parameters stay per layer
-    (checkpoints and solver untouched): the merged weights / bias are gathered from the
-    bf16 compute copies each forward, the merged gradients scattered back."""
-
-    def __init__(self, layers, tops, split_layer, split_tops):
-        self.layers = layers
-        self.tops = tops
-        self.spans, off = [], 0
-        for l in layers:
-            self.spans.append((off, l.K))
-            off += l.K
-        self.total = off
-        self.split_layer, self.split_tops = split_layer, split_tops
-        self.out = self.dout = None
-        self.w = self.b = None
-
-    def forward(self, part, bottoms, tops):
-        if part != 0:
-            assert self.out is not None, "sibling group: the leader's forward did not run first"
-            return
-        from .ops import hip
-        lead = self.layers[0]
-        x = bottoms[0].data
-        s = lead.spec(bottoms[0])
-        sm = ConvSpec(s.N, s.H, s.W, s.C, self.total, 1, 1)
-        if self.w is None or self.w.device != x.device:
-            self.w = torch.empty((self.total, 1, 1, s.C), dtype=torch.bfloat16, device=x.device)
-            self.b = torch.zeros((self.total,), dtype=torch.float32, device=x.device)
-            self.dw = torch.empty((self.total, 1, 1, s.C), dtype=torch.float32, device=x.device)
-            self.db = torch.empty((self.total,), dtype=torch.float32, device=x.device)
-        segs = []  # the merged bf16 weights and fp32 bias, gathered in one launch
-        for l, (off, k) in zip(self.layers, self.spans):
-            segs.append((l.weight.compute, self.w[off:off + k], False))
-            if l.bias is not None:
-                segs.append((l.bias.data, self.b[off:off + k], False))
-        hip.copy_segments(segs)
-        self.out = hip.conv_forward(x, self.w, self.b, sm, relu=True)
-        self.dout = torch.empty_like(self.out)  # the siblings' consumers write their dx slices here
-        for t, (off, k) in zip(self.tops, self.spans):
-            t.data = self.out[..., off:off + k]
-
-    def diff_slice(self, part):
-        off, k = self.spans[part]
-        return self.dout[..., off:off + k]
-
-    def backward(self, part, tops, propagate_down, bottoms):
-        if part != 0:
-            return
-        from .ops import hip
-        lead = self.layers[0]
-        for t, (off, k) in zip(self.tops, self.spans):  # a consumer that did not write in place
-            d = t.diff
-            if d.data_ptr() != self.dout.data_ptr() + 2 * off:
-                self.dout[..., off:off + k].copy_(d)
-        s = lead.spec(bottoms[0])
-        sm = ConvSpec(s.N, s.H, s.W, s.C, self.total, 1, 1)
-        need_w = [l.param_grads_needed(0) for l in self.layers]
-        need_b = [l.bias is not None and l.param_grads_needed(1) for l in self.layers]
-        dw = self.dw if any(need_w) else None
-        db = self.db if any(need_b) else None
-        gate = bottoms[0].data if lead.relu_gate else None
-        dx = hip.conv_backward(self.dout, bottoms[0].data, self.w, sm, bool(propagate_down[0]), dw, db, gate,
-                               None, dw_acc=False, db_acc=False)
-        segs = []  # the merged gradients scattered into the layers' gradient slices in one launch
-        for l, (off, k), nw, nb in zip(self.layers, self.spans, need_w, need_b):
-            if nw:
-                segs.append((dw[off:off + k], l.weight.diff, not l.grad_overwrite(0)))
-            if nb:
-                segs.append((db[off:off + k], l.bias.diff, not l.grad_overwrite(1)))
-        hip.copy_segments(segs)
-        if propagate_down[0]:
-            bottoms[0].diff = dx
-        self.out = self.dout = None
-
-
-def fuse_siblings(net) -> int:
-    """Merge the 1x1 / stride-1 Convolutions that read the same Split (Inception reduce
-    layers) into one GEMM per direction (see :class:`SiblingGroup`).  Eligible siblings:
-    ungrouped 1x1 / stride 1 / pad 0 bf16 convs with the fused ReLU epilogue, one bottom, not
-    writing a zero-copy concat slot, whose top is read only by its fused in-place ReLU and
-    one stride-1 implicit-GEMM Convolution (which then reads its input as a channel slice
-    of the merged output and writes its data gradient into the merged gradient).  GPU only,
-    opt-in (``SN_FUSE_SIBLINGS=1``): on GoogLeNet b128 it cuts the summed kernel time per step
-    by 12 % (11.56 -> 10.14 ms) but not the 4-stream critical path (wall 5.78 vs 5.82 ms; bench
-    20.8 k vs 19.3-20.1 k img/s, docs/PERF_NOTES.md); returns the number of groups."""
-    if net.device.type != "cuda" or os.environ.get("SN_FUSE_SIBLINGS", "0") != "1":
-        return 0
-    from .ops import hip
-    outputs = set(getattr(net, "output_blob_ids", ()))
-    n = 0
-    for ls, split in enumerate(net.layers):
-        if split.type_name != "Split" or not net.layer_need_backward[ls] or split.skip_tops:
-            continue
-        cands = []
-        for ti, tb in enumerate(net.top_ids[ls]):
-            readers = [lj for lj in range(len(net.layers)) if tb in net.bottom_ids[lj]]
-            if len(readers) != 1:
-                continue
-            li = readers[0]
-            conv = net.layers[li]
-            if (conv.type_name != "Convolution" or len(net.bottom_ids[li]) != 1 or len(net.top_ids[li]) != 1
-                    or not conv.fuse_relu or conv.concat_slot is not None or conv.fp8_slots is not None
-                    or conv.fp8_dgrad_slots is not None or conv.folded_input is not None
-                    or getattr(conv, "sibling", None) is not None or getattr(conv, "slab_grad", None) is not None
-                    or not net.layer_need_backward[li]):
-                continue
-            s = conv.spec(net.bottom_vecs[li][0])
-            if (s.R, s.S, s.sh, s.sw, s.ph, s.pw) != (1, 1, 1, 1, 0, 0) or not hip._slice_ok(s) \
-                    or hip._image_chunk(s) < s.N:
-                continue
-            top = net.top_ids[li][0]
-            if top in outputs:
-                continue
-            users = [lj for lj in range(li + 1, len(net.layers)) if top in net.bottom_ids[lj]]
-            relus = [lj for lj in users if net.layers[lj].type_name == "ReLU" and getattr(net.layers[lj], "fused", False)
-                     and net.bottom_ids[lj] == [top] and net.top_ids[lj] == [top]]
-            others = [lj for lj in users if lj not in relus]
-            if len(others) != 1:
-                continue
-            cons = net.layers[others[0]]
-            if (cons.type_name != "Convolution" or len(net.bottom_ids[others[0]]) != 1
-                    or getattr(cons, "dx_slot", None) is not None or cons.fp8_slots is not None
-                    or cons.fp8_dgrad_slots is not None):
-                continue
-            cs = cons.spec(net.bottom_vecs[others[0]][0])
-            if not hip._slice_ok(cs) or hip._image_chunk(cs) < cs.N or (cs.sh, cs.sw) != (1, 1):
-                continue
-            cands.append((ti, li, conv, others[0], cons))
-        if len(cands) < 2:
-            continue
-        relu_gate = {c[2].relu_gate for c in cands}
-        if len(relu_gate) != 1:
-            continue
-        cands.sort(key=lambda c: c[1])
-        group = SiblingGroup([c[2] for c in cands], [net.top_vecs[c[1]][0] for c in cands], split,
-                             [c[0] for c in cands])
-        gid = ("sib", ls)
-        for part, (ti, li, conv, lc, cons) in enumerate(cands):
-            conv.sibling = (group, part)
-            cons.dx_slot = (group, part)
-            ex = conv.__dict__.setdefault("sched_extra", {})
-            if part == 0:
-                ex["fwd_w"] = {gid}
-                # the leader's backward reads every sibling's top gradient and writes every
-                # sibling's parameter gradients
-                ex["bwd_r"] = {("d", net.top_ids[c[1]][0]) for c in cands}
-                ex["bwd_w"] = {("p", p.offset) for c in cands for p in c[2].params}
-            else:
-                ex["fwd_r"] = {gid}
-        split.skip_tops = frozenset(c[0] for c in cands[1:])
-        n += 1
-    return n
-
-
 def fuse_dropout(net) -> int:
     """Apply an in-place TRAIN-phase Dropout inside the producing InnerProduct's epilogue
     (after its fused bias + ReLU: CaffeNet fc6 -> relu6 -> drop6, fc7 -> relu7 -> drop7),
@@ -355,7 +194,7 @@ def fuse_dropout(net) -> int:
     dy / (1-p) where the dropout output is > 0, else 0 — exactly Caffe's ReLU-after-in-place-
     dropout gate (relu_layer.cu reads the overwritten bottom) times dropout_layer.cu's
     mask * scale.  Both standalone dropout passes disappear.  GPU only; returns the count."""
-    if net.device.type != "cuda" or os.environ.get("SN_FUSE_DROPOUT", "1") == "0":
+    if net.device.type != "cuda" or not features.enabled("fuse_dropout"):
         return 0
     n = 0
     for li in range(1, len(net.layers)):
@@ -402,8 +241,8 @@ def batch_weight_flips(net) -> int:
     for li, layer in enumerate(net.layers):
         if layer.type_name != "Convolution" or not net.layer_need_backward[li]:
             continue
-        if not any(net.bottom_need_backward[li]) or layer.sibling is not None:
-            continue  # merged siblings: the group's data gradient reads the merged weights
+        if not any(net.bottom_need_backward[li]):
+            continue
         specs = [layer.spec(b) for b in net.bottom_vecs[li]]
         if not all(hip.dgrad_uses_flip(s) for s in specs):
             continue
@@ -604,12 +443,12 @@ def fuse_splitk_updates(solver) -> int:
     of the reduce kernel + solver update; the flat gradient of fused params is not
     written.  Returns the number of layers.
 
-    Opt-in (SN_FUSE_SPLITK=1): measured on one MI355X, same box, alternating runs, it is
+    Opt-in (SN_FEATURES=fuse_splitk=1): measured on one MI355X, same box, alternating runs, it is
     2 % slower on CaffeNet and 5 % slower on GoogLeNet than the wide split-K reduce kernel
     it replaces (docs/PERF_NOTES.md, "split-K slabs consumed by the solver")."""
     net = solver.net
     if (net.device.type != "cuda" or not solver.overlap_eligible() or net.debug_info
-            or os.environ.get("SN_FUSE_SPLITK", "0") != "1"):
+            or not features.enabled("fuse_splitk")):
         return 0
     from .ops import hip
     users: dict = {}
@@ -640,7 +479,7 @@ def fuse_input_fold(net, feeder) -> bool:
     the space-to-depth path (AlexNet/CaffeNet conv1), make the feeder write the folded
     tensor directly (one fused augment + fold kernel) and the convolution read it.  The
     NHWC data blob is then no longer written during training steps.  GPU only."""
-    if feeder is None or feeder.device.type != "cuda":
+    if feeder is None or feeder.device.type != "cuda" or net.dtype == torch.float32:
         return False
     from .ops import hip
     try:
@@ -692,7 +531,7 @@ def enable_fp8(net, min_macs_per_input: float = 1000.0, dgrad: bool = False, dgr
     with fewer than ``min_macs_per_input`` forward MACs per input element (where the
     quantisation pass over a large activation costs more than the faster product saves),
     except 64 -> 64 3x3 convs (VGG's conv1_2), which run the e4m3 direct kernel
-    (ops.hip.direct_fp8_ok; SN_CONV_DIRECT_FP8=0 returns them to bf16).
+    (ops.hip.direct_fp8_ok; SN_FEATURES=conv_direct_fp8=0 returns them to bf16).
 
     ``dgrad``: also run the data gradients of stride-1 Convolutions in e4m3 (the output
     gradient and the flip-transposed weights quantised per tensor; weight gradients stay
@@ -754,7 +593,7 @@ def fuse_fp8_quant(net) -> int:
     come out of pooling layers keep their quantisation pass).  The slots use delayed
     scaling, so the side stores start once the first fp8_update_scales has initialised them
     (eager warm-up steps); the bytes equal the separate pass's.  Returns the pairs fused."""
-    if getattr(net.ctx, "fp8", None) is None or os.environ.get("SN_FP8_FUSED_QUANT", "1") == "0":
+    if getattr(net.ctx, "fp8", None) is None or not features.enabled("fuse_fp8_quant"):
         return 0
     from .ops import hip
     outputs = set(getattr(net, "output_blob_ids", ()))
@@ -815,7 +654,7 @@ def fp8_step(net) -> None:
         net.ctx.fp8.update()
 
 
-_DEPFREE_LRU = os.environ.get("SN_BRANCH_DEPFREE", "1") == "1"
+_DEPFREE_LRU = features.enabled("branch_depfree")
 
 
 class BranchStreams:
@@ -848,7 +687,7 @@ class BranchStreams:
         self.side = None  # created on first run (the plan itself is device-independent)
         L = len(net.layers)
         # layer.sched_extra: hazards a fusion pass adds that the blob lists do not show
-        # ({"fwd_r", "fwd_w", "bwd_r", "bwd_w"} token sets; engine.fuse_siblings)
+        # ({"fwd_r", "fwd_w", "bwd_r", "bwd_w"} token sets)
         ex = [getattr(net.layers[li], "sched_extra", None) or {} for li in range(L)]
         fwd = [(li, {("v", b) for b in net.bottom_ids[li]} | set(ex[li].get("fwd_r", ())),
                 {("v", b) for b in net.top_ids[li]} | set(ex[li].get("fwd_w", ()))) for li in range(L)]
@@ -888,7 +727,7 @@ class BranchStreams:
                 # top diff is the constant loss weight) takes the least recently used stream
                 # too, instead of queueing on the main stream behind the towers (GoogLeNet
                 # 22.36-22.42 -> 22.46-22.56 k img/s, profiles/r5_branch_depfree.txt;
-                # SN_BRANCH_DEPFREE=0: the main stream)
+                # SN_FEATURES=branch_depfree=0: the main stream)
                 sid = min(range(self.n), key=lambda s: tail[s])
             if self.star and sid != 0 and any(stream_of[d] not in (0, sid) for d in deps):
                 sid = 0  # star topology: side streams only ever wait on the main stream
@@ -1041,12 +880,14 @@ def release_activations(net) -> int:
     return n
 
 
+GRAPH_RELEASE = None  # None: decide by memory use; True / False force it (tests)
+
+
 def _release_before_capture(dev) -> bool:
     """release_activations before a capture when the warm-up holds over 45 % of the device
-    (SN_GRAPH_RELEASE=1 / 0 forces it on / off)."""
-    env = os.environ.get("SN_GRAPH_RELEASE", "")
-    if env in ("0", "1"):
-        return env == "1"
+    (engine.GRAPH_RELEASE = True / False forces it on / off)."""
+    if GRAPH_RELEASE is not None:
+        return bool(GRAPH_RELEASE)
     if dev.type != "cuda":
         return False
     total = torch.cuda.get_device_properties(dev).total_memory
@@ -1057,9 +898,10 @@ class GraphStep:
     """One captured solver iteration (iter_size = 1)."""
 
     def __init__(self, solver: Solver, warmup: int = 2, pre=None, overlap: bool = True, fuse_fc: bool = True,
-                 streams: int = 2):
+                 streams: int = 2, comm=None):
         self.solver = solver
         self.pre = pre  # callable run (eagerly) before each replay, e.g. feeder.stage
+        self.comm = comm  # N > 1 ranks: adopt rank 0's GEMM choices before capture (gemm.sync_tuned)
         self.graph = None
         self.loss = None
         self.warmup = warmup
@@ -1076,11 +918,8 @@ class GraphStep:
         self.n_streams = streams if not solver.net.debug_info else 1
         self.branches = None
         self._use_branches = False
-        # weight gradients (+ fused FC updates) on a side stream during backward
-        # (ops.hip.WgradStream); like the branch streams, not in the autotuning iteration
-        self.wgrad_stream = None
-        self.use_wgrad_stream = (os.environ.get("SN_WGRAD_STREAM", "0") == "1" and solver.device.type == "cuda"
-                                 and not solver.net.debug_info)
+        # (weight gradients on a side stream measured slower three times — L2 thrash between
+        # concurrent GEMMs, docs/PERF_NOTES.md rounds 3 and 5 — and were removed in round 6)
 
     def _body(self):
         s = self.solver
@@ -1095,20 +934,8 @@ class GraphStep:
             self.overlap.begin()
         if self._use_branches and self.branches is None:
             self.branches = branch_streams(net, self.n_streams) or False
-        side_wgrad = self.use_wgrad_stream and self._use_branches
-        if side_wgrad:
-            from .ops import hip
-            if self.wgrad_stream is None:
-                # SN_WGRAD_PRIO: HIP stream priority of the side stream (0 = normal; the
-                # capture stream's is SN_MAIN_PRIO): the data-gradient chain is the critical path
-                self.wgrad_stream = torch.cuda.Stream(s.device, priority=int(os.environ.get("SN_WGRAD_PRIO", "0")))
-            hip.WgradStream.begin(self.wgrad_stream)
-        try:
-            loss = (self.branches.forward_backward() if self._use_branches and self.branches
-                    else net.forward_backward())
-        finally:
-            if side_wgrad:
-                hip.WgradStream.join()
+        loss = (self.branches.forward_backward() if self._use_branches and self.branches
+                else net.forward_backward())
         net.finish_param_diffs()
         fp8_step(net)
         for cb in s.callbacks:
@@ -1123,7 +950,7 @@ class GraphStep:
     def capture(self) -> None:
         s = self.solver
         dev = s.device
-        side = torch.cuda.Stream(dev, priority=int(os.environ.get("SN_MAIN_PRIO", "0")))
+        side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for w in range(self.warmup):
@@ -1135,6 +962,9 @@ class GraphStep:
                 s.iter += 1
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
+        if self.comm is not None:
+            from .ops import gemm as _gemm
+            _gemm.sync_tuned(self.comm)  # every rank captures the same kernel for each product
         if _release_before_capture(dev):
             release_activations(s.net)
         self.graph = torch.cuda.CUDAGraph()
@@ -1199,7 +1029,8 @@ class LocalSGDTrainer:
         self.feeder = feeder
         self.round = 0
         self.use_graph = use_graph and solver.device.type == "cuda"
-        self.step_fn = (GraphStep(solver, pre=self._pre, overlap=overlap_update, fuse_fc=fuse_fc, streams=streams)
+        self.step_fn = (GraphStep(solver, pre=self._pre, overlap=overlap_update, fuse_fc=fuse_fc, streams=streams,
+                                  comm=comm)
                         if self.use_graph else None)
         self.log_every = log_every
         self.times = {"compute": 0.0, "allreduce": 0.0}

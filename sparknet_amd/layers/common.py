@@ -72,15 +72,9 @@ class SplitLayer(Layer):
         for t in tops:
             t.data = bottoms[0].data  # ShareData: no copy
 
-    # top indices whose gradient reaches the bottom through another top (engine.fuse_siblings:
-    # sibling convolutions merged into one GEMM whose data gradient covers them all)
-    skip_tops: frozenset = frozenset()
-
     def backward(self, tops, propagate_down, bottoms):
         if not propagate_down[0]:
             return
-        if self.skip_tops:
-            tops = [t for i, t in enumerate(tops) if i not in self.skip_tops]
         if len(tops) == 1:
             bottoms[0].diff = tops[0].diff
             return

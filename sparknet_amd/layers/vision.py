@@ -236,8 +236,6 @@ class ConvolutionLayer(Layer):
     folded_input = None  # S2D-folded bottom 0 written by a fused augment (engine.fuse_input_fold)
     concat_slot = None  # (ConcatSlots, part): top 0 is written into a zero-copy Concat buffer (engine.fuse_concat)
     flipped_weights = None  # dgrad weights flipped at the start of backward (engine.batch_weight_flips)
-    sibling = None  # (SiblingGroup, part): merged with the 1x1 siblings of its Split (engine.fuse_siblings)
-    dx_slot = None  # (SiblingGroup, part): the data gradient goes into the merged sibling gradient
 
     def layer_setup(self, bottoms, tops):
         cp = self.lp.convolution_param
@@ -278,8 +276,6 @@ class ConvolutionLayer(Layer):
             t.reshape((s.N, s.K, s.P, s.Q), self.dtype)
 
     def forward(self, bottoms, tops):
-        if self.sibling is not None:
-            return self.sibling[0].forward(self.sibling[1], bottoms, tops)
         w = self.weight.compute
         bias = self.bias.data if self.bias is not None else None
         self._ws = [{} for _ in bottoms]  # forward -> backward scratch (e.g. folded input)
@@ -372,16 +368,12 @@ class ConvolutionLayer(Layer):
     supports_grad_overwrite = True
 
     def backward(self, tops, propagate_down, bottoms):
-        if self.sibling is not None:
-            return self.sibling[0].backward(self.sibling[1], tops, propagate_down, bottoms)
         w = self.weight.compute
         dw = self.weight.diff if self.param_grads_needed(0) else None
         db = self.bias.diff if (self.bias is not None and self.param_grads_needed(1)) else None
         for i, (t, b) in enumerate(zip(tops, bottoms)):
             s = self.spec(b)
             gate = b.data if self.relu_gate else None
-            dx_out = self.dx_slot[0].diff_slice(self.dx_slot[1]) if (
-                self.dx_slot is not None and i == 0 and propagate_down[i]) else None
             ws = self._ws[i] if i < len(getattr(self, "_ws", ())) else None
             if self.flipped_weights is not None:  # flipped for the whole net (engine.batch_weight_flips)
                 ws = {} if ws is None else ws
@@ -413,8 +405,7 @@ class ConvolutionLayer(Layer):
                     sink.begin()
                     sink.end()  # this pass's gradient went to the flat buffer
                 dx = ops.conv_backward(t.diff, b.data, w, s, bool(propagate_down[i]), dw, db, gate, ws,
-                                       dw_acc=dw_acc, db_acc=db_acc,
-                                       **({"dx_out": dx_out} if dx_out is not None else {}))
+                                       dw_acc=dw_acc, db_acc=db_acc)
             if ws is not None and "fp8_dx_side_out" in ws:
                 self.fp8_dx_out[0]._fp8_dy_side = ws.pop("fp8_dx_side_out")
             if propagate_down[i]:

@@ -9,12 +9,16 @@ Every op has two implementations with identical semantics:
 """
 from __future__ import annotations
 
+import contextlib
+import threading
+
 import torch
 
 from . import ref
 from .spec import POOL_AVE, POOL_MAX, POOL_STOCHASTIC, ConvNdSpec, ConvSpec, PoolSpec  # noqa: F401
 
 _hip = None
+_state = threading.local()
 
 
 def _hipmod():
@@ -25,8 +29,35 @@ def _hipmod():
     return _hip
 
 
+def f32_active() -> bool:
+    """Inside ``precision(torch.float32)``: GPU tensors take the fp32 device path."""
+    return getattr(_state, "f32", False)
+
+
+@contextlib.contextmanager
+def precision(dtype):
+    """Net forward / backward of a ``dtype`` net: fp32 nets on the GPU route every op to
+    :mod:`.f32dev` (fp32 MFMA products + the reference formulas), bf16 nets to :mod:`.hip`."""
+    prev = f32_active()
+    _state.f32 = dtype == torch.float32
+    try:
+        yield
+    finally:
+        _state.f32 = prev
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    """The bf16 HIP engine serves this tensor (a GPU tensor outside the fp32 device mode)."""
+    return t.is_cuda and not f32_active()
+
+
 def _impl(t: torch.Tensor):
-    return _hipmod() if t.is_cuda else ref
+    if not t.is_cuda:
+        return ref
+    if f32_active():
+        from . import f32dev
+        return f32dev
+    return _hipmod()
 
 
 def _dispatch(name):
@@ -55,28 +86,34 @@ accuracy = _dispatch("accuracy")
 def pool_backward(dy, x, s, aux=None, y=None, gate=False):
     """gate=True: x is a slope-0 in-place ReLU output whose backward is fused here (MAX
     pooling on the GPU encodes it in the forward's argmax mask)."""
-    if dy.is_cuda:
+    if _gpu(dy):
         return _hipmod().pool_backward(dy, x, s, aux, y, gate)
     return ref.pool_backward(dy, x, s, gate)
 
 
 def pool_forward_aux(x, s, gate=False):
     """Forward returning (y, aux) where aux is the GPU argmax mask (None on CPU)."""
-    if x.is_cuda:
+    if _gpu(x):
         return _hipmod().pool_forward_mask(x, s, gate)
     return ref.pool_forward(x, s), None
 
 
 def dropout_forward(x, ratio, rng_state, stream):
-    if x.is_cuda:
+    if _gpu(x):
         return _hipmod().dropout_forward(x, ratio, rng_state, stream)
+    if x.is_cuda:
+        from . import f32dev
+        return f32dev.dropout_forward(x, ratio, rng_state, stream)
     seed, counter = (int(v) for v in rng_state.tolist())
     return ref.dropout_forward(x, ratio, seed, counter, stream)
 
 
 def dropout_backward(dy, ratio, rng_state, stream, gate=None):
-    if dy.is_cuda:
+    if _gpu(dy):
         return _hipmod().dropout_backward(dy, ratio, rng_state, stream, gate)
+    if dy.is_cuda:
+        from . import f32dev
+        return f32dev.dropout_backward(dy, ratio, rng_state, stream, gate)
     seed, counter = (int(v) for v in rng_state.tolist())
     return ref.dropout_backward(dy, ratio, seed, counter, stream, gate)
 

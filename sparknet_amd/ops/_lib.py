@@ -48,11 +48,8 @@ class SnGemmArgs(C.Structure):
                 ("sgd_lr_mult", C.c_float), ("sgd_decay_mult", C.c_float), ("sgd_flags", C.c_int),
                 ("drop_rng", C.c_void_p), ("drop_stream", C.c_int), ("drop_thr", C.c_uint),
                 ("drop_scale", C.c_float), ("gate_scale", C.c_float), ("lds_store", C.c_int),
-                ("addr_legacy", C.c_int),
                 ("q_out", C.c_void_p), ("q_ld", C.c_longlong), ("q_gstride", C.c_longlong), ("q_slot", C.c_void_p),
-                ("q_e5m2", C.c_int), ("q_part", C.c_void_p),
-                ("fix_ws", C.c_void_p), ("fix_ld", C.c_longlong), ("fix_sstride", C.c_longlong),
-                ("fix_cnt", C.c_void_p)]
+                ("q_e5m2", C.c_int), ("q_part", C.c_void_p)]
 
 
 def lib_path(name: str = "libsn_kernels.so") -> Path:

@@ -1,0 +1,129 @@
+"""fp32 device mode: the reference's numerics on the MI355X.
+
+Caffe computes every layer in fp32 (``/root/reference/libccaffe/ccaffe.h:3`` ``#define DTYPE
+float``; its convolutions are im2col + SGEMM, ``caffe/src/caffe/layers/base_conv_layer.cpp:
+312-376``, ``caffe/src/caffe/util/math_functions.cu:14-28``).  A net built with
+``dtype=torch.float32`` on a ROCm device runs its products on ``csrc/kernels/fp32.hip``:
+exact-f32 matrix cores (``v_mfma_f32_16x16x4_f32``, a k-ordered fmaf chain per output) fed
+by an explicit NHWC im2col — the reference's own algorithm, on MFMA instead of SGEMM.  The
+remaining (bandwidth-bound) layers run the fp32 formulas of :mod:`.ref` on device tensors.
+The production bf16 engine is untouched: ``ops.precision(torch.float32)`` (entered by
+``Net`` for fp32 nets on the GPU) routes the dispatch here.
+
+Layouts: activations NHWC fp32, weights [K][R][S][Cg] (the engine's internal layout).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib, ref
+from .spec import ConvSpec
+
+F32 = torch.float32
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, bias=None, relu=False, accumulate=False):
+    """out[M][N] (+)= a[M][K] @ b[N][K]^T (+ bias, ReLU) — rows K-contiguous, fp32."""
+    M, K = a.shape
+    N = b.shape[0]
+    assert a.dtype == b.dtype == out.dtype == F32 and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1
+    assert b.shape[1] == K and out.shape[0] == M and out.shape[1] == N
+    _lib.call("gemm_f32", a, a.stride(0), b, b.stride(0), out, out.stride(0), M, N, K,
+              bias if bias is not None else None, int(accumulate), int(relu))
+    return out
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _im2col(x, s: ConvSpec, g: int) -> torch.Tensor:
+    col = torch.empty((s.N * s.P * s.Q, s.R * s.S * s.Cg), dtype=F32, device=x.device)
+    _lib.call("im2col_f32", x, col, s.N, s.H, s.W, s.C, s.P, s.Q, s.R, s.S, s.sh, s.sw, s.ph, s.pw, s.dh, s.dw,
+              s.Cg, g * s.Cg)
+    return col
+
+
+def conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None):
+    x = _c(x.to(F32))
+    y = torch.empty((s.N, s.P, s.Q, s.K), dtype=F32, device=x.device)
+    y2 = y.view(-1, s.K)
+    w2 = _c(w.to(F32)).view(s.K, -1)
+    for g in range(s.groups):
+        col = _im2col(x, s, g)
+        gemm_nt(col, w2[g * s.Kg:(g + 1) * s.Kg], y2[:, g * s.Kg:(g + 1) * s.Kg],
+                bias=b[g * s.Kg:(g + 1) * s.Kg].float().contiguous() if b is not None else None, relu=relu)
+    return y
+
+
+def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
+                  dw_acc=True, db_acc=True, dx_out=None):
+    """Caffe's order (base_conv_layer.cpp:338-376): per group, dW += dY^T col (col = im2col(x)),
+    dcol = dY W, dx = col2im(dcol); db = the column sum of dY."""
+    dy = _c(dy.to(F32))
+    x = _c(x.to(F32))
+    dy2 = dy.view(-1, s.K)
+    w2 = _c(w.to(F32)).view(s.K, -1)
+    if db is not None:
+        ref._acc(db, dy2.sum(0), db_acc)
+    dx = torch.empty((s.N, s.H, s.W, s.C), dtype=F32, device=x.device) if need_dx else None
+    for g in range(s.groups):
+        dyg = dy2[:, g * s.Kg:(g + 1) * s.Kg]
+        if dw is not None:
+            col = _im2col(x, s, g)
+            dwg = dw.view(s.K, -1)[g * s.Kg:(g + 1) * s.Kg]
+            # reduction over pixels: both operands pixel-contiguous ([Kg][M], [kred][M])
+            gemm_nt(_c(dyg.t()), _c(col.t()), dwg, accumulate=dw_acc)
+        if need_dx:
+            dcol = torch.empty((s.N * s.P * s.Q, s.R * s.S * s.Cg), dtype=F32, device=x.device)
+            gemm_nt(_c(dyg), _c(w2[g * s.Kg:(g + 1) * s.Kg].t()), dcol)
+            _lib.call("col2im_f32", dcol, dx, s.N, s.H, s.W, s.C, s.P, s.Q, s.R, s.S, s.sh, s.sw, s.ph, s.pw,
+                      s.dh, s.dw, s.Cg, g * s.Cg, 0)
+    if dx is not None:
+        dx = ref._gated(dx, gate.to(F32) if gate is not None else None)
+        if dx_out is not None:
+            dx_out.copy_(dx)
+            return dx_out
+    return dx
+
+
+def linear_forward(x2, w, b, relu=False):
+    x2 = _c(x2.to(F32))
+    y = torch.empty((x2.shape[0], w.shape[0]), dtype=F32, device=x2.device)
+    return gemm_nt(x2, _c(w.to(F32)), y, bias=b.float().contiguous() if b is not None else None, relu=relu)
+
+
+def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=True, db_acc=True):
+    """inner_product_layer.cu:22-54: dW (+)= dY^T X, db (+)= colsum(dY), dX = dY W."""
+    dy2 = _c(dy2.to(F32))
+    x2 = _c(x2.to(F32))
+    if dw is not None:
+        gemm_nt(_c(dy2.t()), _c(x2.t()), dw, accumulate=dw_acc)
+    if db is not None:
+        ref._acc(db, dy2.sum(0), db_acc)
+    if not need_dx:
+        return None
+    dx = torch.empty_like(x2)
+    gemm_nt(dy2, _c(w.to(F32).t()), dx)
+    return ref._gated(dx, gate.reshape(x2.shape).to(F32) if gate is not None else None)
+
+
+def dropout_forward(x, ratio, rng_state, stream):
+    """dropout_layer.cu: the device Philox keep mask of the bf16 engine (same bits)."""
+    x = _c(x.to(F32))
+    y = torch.empty_like(x)
+    _lib.call("dropout_f32", x, y, x.numel(), rng_state, int(stream), float(ratio), None)
+    return y
+
+
+def dropout_backward(dy, ratio, rng_state, stream, gate=None):
+    dy = _c(dy.to(F32))
+    dx = torch.empty_like(dy)
+    _lib.call("dropout_f32", dy, dx, dy.numel(), rng_state, int(stream), float(ratio),
+              _c(gate.to(F32)) if gate is not None else None)
+    return dx
+
+
+def __getattr__(name):
+    # every other op: the fp32 formulas of the reference module, on device tensors
+    return getattr(ref, name)

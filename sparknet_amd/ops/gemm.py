@@ -23,6 +23,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
+from ..utils import features
 
 OP_DENSE, OP_IM2COL, OP_FLIPW = 0, 1, 2
 EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_SGD, EPI_BF16_DROP = 0, 1, 2, 3, 4
@@ -112,30 +113,17 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 
 
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
-         6: (256, 256), 7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (128, 64),
+         6: (256, 256), 7: (256, 128), 10: (128, 64),
          11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192), 15: (128, 192), 16: (192, 128),
-         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64), 21: (64, 256), 22: (64, 128),
-         # v_mfma_f32_32x32x16_bf16 twins of tiles 0, 10, 16, 13, 1, 11 (csrc/kernels/gemm_mf32.hip)
-         23: (128, 128), 24: (128, 64), 25: (192, 128), 26: (256, 128), 27: (256, 64), 28: (256, 256),
-         # persistent ring-pipelined tiles (csrc/kernels/gemm_pk.h): one 512-thread block per CU
-         30: (256, 128), 31: (256, 64), 32: (256, 96), 33: (128, 128), 34: (256, 192), 36: (128, 256),
-         37: (192, 384), 38: (256, 256), 39: (256, 128),
-         # gemm256_kernel with the 8-phase schedule (csrc/kernels/gemm_t256p8.hip)
-         40: (256, 256), 41: (256, 128)}
-PK_TILES = frozenset((30, 31, 32, 33, 34, 36, 37, 38))
+         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64), 21: (64, 256), 22: (64, 128)}
+# (round 6 removed the measured-and-rejected families: the v_mfma 32x32x16 twins 23-28, the
+# persistent ring tiles 30-39, the 4- and 8-phase gemm256 schedules 8 / 9 / 40 / 41 —
+# docs/PERF_NOTES.md rounds 4-5)
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
-_SLOTS = {6: 256, 7: 256, 8: 256, 9: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512, 21: 512,
-          22: 768, 24: 768, 26: 256, 28: 256,
-          30: 256, 31: 256, 32: 256, 33: 256, 34: 256, 36: 256, 37: 256, 38: 256, 39: 256, 40: 256, 41: 256}
-_KTILE_US = {6: 2.0, 7: 1.1, 8: 2.0, 9: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55, 26: 1.1, 28: 2.0,
-             30: 0.75, 31: 0.45, 32: 0.6, 33: 0.45, 34: 1.1, 36: 0.75, 37: 1.3, 38: 1.2, 40: 1.6, 41: 0.9}
-# autotune candidates 11-14 (SN_GEMM_TILE8W=0 drops them)
-_TILE8W = os.environ.get("SN_GEMM_TILE8W", "1") != "0"
+_SLOTS = {6: 256, 7: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512, 21: 512, 22: 768}
+_KTILE_US = {6: 2.0, 7: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55}
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
-_RASTER_N = int(os.environ.get("SN_GEMM_RASTER_N", "-1"))  # -1: heuristic
-_TILE256 = os.environ.get("SN_GEMM_TILE256", "1") != "0"  # autotune candidates 6 / 7 (gemm256_kernel)
-_TILE64 = os.environ.get("SN_GEMM_TILE64", "1") != "0"  # autotune candidate 10 (128x64, 3 blocks / CU)
 
 
 def choose_tile(M: int, N: int, b_kcontig: bool = False) -> int:
@@ -259,66 +247,15 @@ def gemm(M: int, N: int, K: int, A, B, out: torch.Tensor, ldc: int, *, epi: int,
 
 _NO_XTRA = (0, 0, 0.0, 1.0)
 # bf16 epilogues of the 4-wave tiles store through LDS as whole 16-B row chunks
-# (SnGemmArgs.lds_store); SN_GEMM_LDS_EPI=0 keeps the per-fragment stores (A/B)
-_LDS_EPI = os.environ.get("SN_GEMM_LDS_EPI", "1") != "0"
-_LDS_EPI_TILES = frozenset(int(t) for t in os.environ.get("SN_GEMM_LDS_EPI_TILES", "0,1,4,5,10,12,13,14,15,16,17,18,19,20").split(","))
-# SnGemmArgs.addr_legacy: 1 = the general per-lane DMA address decode only (A/B probes of
-# the scalar-offset fast paths; SN_GEMM_LEGACY_ADDR=1); 2 = the lane-parallel row table of MC
-# im2col operands instead of the per-instruction pixel walk (SN_GEMM_LEGACY_ADDR=2: an A/B
-# only, 8-10 % slower on the CaffeNet weight gradients, profiles/r5_wgrad_rowtab_ab.txt)
-_ADDR_LEGACY = int(os.environ.get("SN_GEMM_LEGACY_ADDR", "0"))
-
-
+# (SnGemmArgs.lds_store)
+_LDS_EPI = True
+_LDS_EPI_TILES = frozenset((0, 1, 4, 5, 10, 12, 13, 14, 15, 16, 17, 18, 19, 20))
 def _drop_fields(xtra):
     """(drop_rng, drop_stream, drop_thr, drop_scale, gate_scale) of SnGemmArgs."""
     rng, dstream, ratio, gscale = xtra
     if not rng:
         return (0, 0, 0, 1.0, gscale)
     return (rng, dstream, int(4294967295 * ratio) & 0xffffffff, 1.0 / (1.0 - ratio), gscale)
-
-
-# In-launch deterministic split-K combine (SN_GEMM_FIXUP=1): the gemm_kernel tile family
-# (not the gemm256 / persistent tiles) reduces its own slabs in the last-arriving block of each
-# output tile.  Counters: one zeroed pool per device, handed out round-robin (each launch's
-# counters return to zero when it completes; the pool is far larger than the counters of all
-# launches one step keeps in flight, so concurrent branch-stream launches never share one).
-# SN_GEMM_FIXUP: 0 = always the reduce launch (default), 1 = the combine where _fixup_pays,
-# 2 = always.  Measured SLOWER on every CaffeNet split-K product it can replace (fc6 forward
-# 35 -> 60 us, conv5 weight gradient 65 -> 82 us; bench.py -4 % CaffeNet, -1 % GoogLeNet:
-# profiles/r5_splitk_combine_ab.txt): one block reading (splits - 1) 32-64 KB fp32 tiles is
-# latency-bound at ~18 GB/s, where the reduce launch reads every slab chip-wide.
-_FIXUP = int(os.environ.get("SN_GEMM_FIXUP", "0"))
-FIX_READ_BW = 18e9     # bytes/s one last-arriving block reads the other slices' slabs at (measured)
-REDUCE_RATE = 2.5e12   # bytes/s of the splitk_reduce launches (CaffeNet step trace, r5)
-REDUCE_LAUNCH = 2e-6   # s: the extra kernel boundary of a reduce launch
-
-
-def _fixup_pays(M, N, groups, splits, bm, bn) -> bool:
-    """The combine serialises (splits-1) fp32 tiles of reading on each tile's last block; the
-    reduce launch reads every slab chip-wide plus one kernel boundary.  At the measured rates
-    only small tiles split a few ways combine (e.g. 128x64 in 2 slices)."""
-    t_fix = (splits - 1) * bm * bn * 4 / FIX_READ_BW
-    t_red = splits * M * (-(-N // 4) * 4) * groups * 4 / REDUCE_RATE + REDUCE_LAUNCH
-    return t_fix < t_red
-# (the tiles whose waves hold <= 16 accumulator fragments: the kernel compiles the combine
-# only there, larger register tiles would spill)
-_FIX_TILES = frozenset((0, 1, 2, 3, 4, 5, 10, 12, 13, 18, 19, 20, 21, 22, 23, 24, 27))
-_FIX_POOL: dict = {}
-_FIX_POOL_INTS = 1 << 20
-
-
-def _fix_counters(n: int, device) -> int:
-    pool = _FIX_POOL.get(device)
-    if pool is None:
-        assert not torch.cuda.is_current_stream_capturing(), "split-K counter pool created during capture"
-        pool = [torch.zeros(_FIX_POOL_INTS, dtype=torch.int32, device=device), 0]
-        _FIX_POOL[device] = pool
-    assert n <= _FIX_POOL_INTS, n
-    if pool[1] + n > _FIX_POOL_INTS:
-        pool[1] = 0
-    off = pool[1]
-    pool[1] += -(-n // 32) * 32  # 128-B aligned slices
-    return pool[0].data_ptr() + 4 * off
 
 
 def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc, ones, sg,
@@ -332,7 +269,7 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     f8 = (deq[2] if len(deq) > 2 else 1) if fp8 else 0
     bm, bn = TILES[tile]
     tm_, tn_ = -(-M // bm), -(-N // bn)
-    raster = int(_RASTER_N if _RASTER_N >= 0 else (1 < tn_ <= 8 and tm_ >= 8 * tn_))
+    raster = int(1 < tn_ <= 8 and tm_ >= 8 * tn_)
     gp = gate.data_ptr() if gate is not None else 0
     bg = bias_grad.data_ptr() if bias_grad is not None else 0
     if splits == 1:
@@ -343,7 +280,6 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
                                sa, sb, out.data_ptr(), ldc, c_gstride, 0,
                                bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, f8, *dq, raster,
                                ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), lds)
-        args.addr_legacy = _ADDR_LEGACY
         side = _SIDE
         if side is not None and side.covers(out):
             q = _side_fields(side, out, ldc, c_gstride, N, tile, e, lds)
@@ -359,32 +295,11 @@ def _launch(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bi
     sink = _DEFER_SINK
     deferred = (sink is not None and epi == EPI_F32 and not fp8 and (bias_grad is None or not bias_acc)
                 and sink.accepts(out, bias_grad))
-    if (_FIXUP and not deferred and not fp8 and tile in _FIX_TILES and epi != EPI_SGD
-            and (_FIXUP == 2 or _fixup_pays(M, N, groups, splits, bm, bn))):
-        # in-launch combine: the last K-slice block of each tile sums the slabs (split order)
-        # and runs the real epilogue — no splitk_reduce launch (gemm_kernel fix_cnt)
-        assert groups * splits * M * ldw * 4 < (1 << 31), "split-K combine: slab offsets are 31-bit"
-        ws = torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device)
-        e = EPI_BF16_DROP if (epi == EPI_BF16 and xtra[0]) else epi
-        lds = int(_LDS_EPI and epi == EPI_BF16 and tile in _LDS_EPI_TILES and ldc % 8 == 0 and c_gstride % 8 == 0
-                  and out.data_ptr() % 16 == 0)
-        args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, e,
-                               sa, sb, out.data_ptr(), ldc, c_gstride, 0,
-                               bias.data_ptr() if bias is not None else 0, int(relu), tile, gp, f8, *dq, raster,
-                               ones, bg, int(bias_acc), *sg, *_drop_fields(xtra), lds)
-        args.addr_legacy = _ADDR_LEGACY
-        args.fix_ws, args.fix_ld, args.fix_sstride = ws.data_ptr(), ldw, M * ldw
-        args.fix_cnt = _fix_counters(groups * tm_ * tn_, out.device)
-        _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
-        if _lib.DEBUG_SYNC:
-            _lib.debug_sync("gemm")
-        return
     ws = (sink.slab(groups * splits * M * ldw, out.device).view(groups, splits, M, ldw) if deferred
           else torch.empty((groups, splits, M, ldw), dtype=torch.float32, device=out.device))
     args = _lib.SnGemmArgs(M, N, K, groups, splits, kchunk, a_mc, a_mode, b_mc, b_mode, EPI_F32,
                            sa, sb, ws.data_ptr(), ldw, splits * M * ldw, M * ldw, 0, 0, tile, 0, f8, *dq, raster,
                            ones, 0, 0, *sg, *_drop_fields(_NO_XTRA))
-    args.addr_legacy = _ADDR_LEGACY
     _lib.check(_lib.kernels().sn_gemm(C.byref(args), C.c_void_p(_lib.stream_ptr())), "gemm")
     if deferred:
         # the solver update sums these slabs itself (engine.fuse_splitk_updates)
@@ -443,9 +358,9 @@ def new_side_part(device) -> torch.Tensor:
 
 
 _SIDE = None
-# the per-fragment epilogue stores side outputs too (SN_FP8_SIDE_FRAG=0: LDS-staged launches only;
+# the per-fragment epilogue stores side outputs too (SN_FEATURES=fp8_side_frag=0: LDS-staged launches only;
 # VGG-16 b2048 8.98k / 8.97k with vs 8.96k / 8.94k img/s without, profiles/r3_fp8_dgrad.txt)
-_SIDE_FRAG = os.environ.get("SN_FP8_SIDE_FRAG", "1") == "1"
+_SIDE_FRAG = features.enabled("fp8_side_frag")
 SIDE_STATS = {"used": 0, "missed": 0}  # consumer lookups of a side output (tests, probes)
 
 
@@ -476,7 +391,7 @@ def _side_fields(side, out, ldc, c_gstride, N, tile, epi, lds):
     launch cannot store the side output (the side is then marked incomplete)."""
     off = (out.data_ptr() - side.base.data_ptr()) // 2
     qp = side.q.data_ptr() + off
-    if ((not lds and not _SIDE_FRAG) or epi not in (EPI_BF16, EPI_BF16_DROP) or tile in (6, 7, 8, 9, 39, 40, 41) or tile in PK_TILES
+    if ((not lds and not _SIDE_FRAG) or epi not in (EPI_BF16, EPI_BF16_DROP) or tile in (6, 7)
             or N % 8 or ldc % 8
             or c_gstride % 8 or qp % 8):
         side.ok = False
@@ -515,16 +430,21 @@ class defer_reduce:
 # The cost model picks a tile and split-K factor from the shape alone; the first eager
 # call of every distinct GEMM (shape, operand kinds and geometry, epilogue) instead times
 # the candidate tiles x split factors on scratch outputs and caches the fastest.  Graph
-# captures replay the cached choice.  SN_GEMM_AUTOTUNE=0 keeps the model's choice (fully
-# reproducible tile selection across processes).
-_AUTOTUNE = os.environ.get("SN_GEMM_AUTOTUNE", "1") != "0"
+# captures replay the cached choice.
+# OFF by default (SN_GEMM_AUTOTUNE=1 turns it on, e.g. to build the database): first-call
+# timing is noisy, so two processes on one box could pick different tiles for one product
+# and train on different summation orders (profiles/r5_fp8_fidelity_lr.txt), and N ranks
+# tuning independently would each replay their own kernels (the slowest sets the job's
+# rate).  The production path is the committed database plus the cost model for anything
+# it lacks (recorded in _MISSES; tests/test_tune_db_gpu.py keeps the zoo models covered),
+# and a tuned run with N > 1 ranks adopts rank 0's choices before capture (sync_tuned).
+_AUTOTUNE = os.environ.get("SN_GEMM_AUTOTUNE", "0") == "1"
 _TUNED: dict = {}
+_MISSES: set = set()  # database misses served by the cost model (keys)
 _TUNE_LOG = os.environ.get("SN_GEMM_TUNE_LOG", "0") == "1"
-_TUNE_PASSES = int(os.environ.get("SN_GEMM_TUNE_PASSES", "3"))
+_TUNE_PASSES = 3
 # The 64-row tiles (21, 22) are autotune candidates for products with M <= 64, or whose M they
-# pad less than 128-row tiles do (SN_GEMM_THIN=0
-# drops them).  SN_GEMM_THIN_RETUNE=1 also re-times such products' database choice against
-# them on first use (off by default: database entries stay authoritative and reproducible).
+# pad less than 128-row tiles do.
 # Round 4 made the tiles opt-in after cifar10_quick stopped learning when its conv1 weight
 # gradient (M 32, N 201 with the bias column, K 102400) picked tile 22 at 229-way split-K.
 # Root cause (round 5, docs/PERF_NOTES.md "thin tiles"): not the tile.  Tiles 0, 10, 21 and 22
@@ -532,9 +452,7 @@ _TUNE_PASSES = int(os.environ.get("SN_GEMM_TUNE_PASSES", "3"))
 # test_thin_tiles_bitwise_equal_at_same_split); the same failure reproduces with tile 0 or 10
 # at 229 splits, and the fp32 CPU engine spikes too: at the reference solver's lr 0.001 that
 # synthetic-pattern training is unstable under ANY summation order (tests/test_training_gpu.py).
-_THIN = os.environ.get("SN_GEMM_THIN", "1") == "1"
-_THIN_RETUNE = _THIN and os.environ.get("SN_GEMM_THIN_RETUNE", "0") == "1"
-_THIN_DONE: set = set()
+_THIN = True
 # Tuning database: choices measured offline on an MI355X (scripts/build_tune_db.sh, many
 # more timing passes than a first-call tune) are loaded at import so the production
 # models run a fixed, reproducible tile / split-K per GEMM; first-call timing only fills
@@ -589,21 +507,21 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
     tiles = [0, 1, 2]
     if N >= 256:
         tiles.append(3)
-    if epi != EPI_SGD and _TILE256 and M >= 256:
+    if epi != EPI_SGD and M >= 256:
         tiles.append(7)
         if N > 128:
             tiles.append(6)
-    if epi != EPI_SGD and _TILE8W and M >= 256 and N > 64:
+    if epi != EPI_SGD and M >= 256 and N > 64:
         tiles += [12, 13]
         if N > 128:
             tiles.append(11)
         if N > 128 and (b_kc_dense or N % 192 == 0):
             tiles.append(14)
-    if epi != EPI_SGD and _TILE8W and N > 64:
+    if epi != EPI_SGD and N > 64:
         tiles.append(16)
         if b_kc_dense and N > 128:
             tiles.append(15)
-    if epi != EPI_SGD and _TILE8W and M >= 192:
+    if epi != EPI_SGD and M >= 192:
         tiles.append(18)
         if b_kc_dense and N % 96 == 0:
             tiles.append(17)
@@ -616,8 +534,7 @@ def _candidates(M, N, K, groups, b_kc_dense, epi):
         # GoogLeNet's 192-, 160-, 320-channel convs)
         tiles += [21, 22]
     if epi != EPI_SGD:
-        if _TILE64:
-            tiles.append(10)
+        tiles.append(10)
         if b_kc_dense and N % 96 == 0:
             tiles.append(4)
         if N % 48 == 0 and N <= 96 and M >= 256:
@@ -655,26 +572,11 @@ def _candidates_fp8(M, N, K, groups, epi, xtra, mc=False):
     return list(dict.fromkeys(out))
 
 
-# Experiment knob: cap the split-K factor of every product (0 = no cap).  With several
-# branch streams in flight (Inception) other streams may fill the CUs a split would.
-_MAX_SPLITS = int(os.environ.get("SN_GEMM_MAX_SPLITS", "0"))
-# the same cap for bf16-output products only (forward / dgrad), weight gradients untouched
-_MAX_SPLITS_BF16 = int(os.environ.get("SN_GEMM_MAX_SPLITS_BF16", "0"))
-
-
 def _tuned_config(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
                   ones, sg, xtra=_NO_XTRA, deq=None):
-    cfg = _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
-                            ones, sg, xtra, deq)
-    t, s, kc = cfg
-    cap = _MAX_SPLITS
-    if _MAX_SPLITS_BF16 > 0 and epi in (EPI_BF16, EPI_BF16_DROP):
-        cap = _MAX_SPLITS_BF16 if cap <= 0 else min(cap, _MAX_SPLITS_BF16)
-    if cap <= 0 or s <= cap:
-        return cfg
-    bk = 128 if deq is not None else BK
-    kc = -(-(-(-K // cap)) // bk) * bk
-    return (t, max(1, -(-K // kc)), kc)
+    # (split-K caps were measured neutral or slower, docs/PERF_NOTES.md round 2; removed)
+    return _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad,
+                             bias_acc, ones, sg, xtra, deq)
 
 
 def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu, gate, bias_grad, bias_acc,
@@ -685,8 +587,9 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     key = (M, N, K, groups, a_mc, a_mode, b_mc, b_mode, epi, gate is not None, bias_grad is not None, bool(xtra[0]),
            _geom_key(sa), _geom_key(sb)) + ((("fp8",) if len(deq) < 3 or deq[2] == 1 else ("fp8", deq[2])) if fp8 else ()) + (out.dtype,)
     hit = _TUNED.get(key)
-    if hit is not None and not (_THIN_RETUNE and M <= 64 and hit[0] not in (21, 22) and key not in _THIN_DONE
-                                and not fp8 and epi != EPI_SGD):
+    if hit is None and not _AUTOTUNE and epi != EPI_SGD:
+        _MISSES.add(key)
+    if hit is not None:
         return hit
     tile = 0 if fp8 else choose_tile(M, N, b_kc_dense)
     if epi == EPI_SGD and tile not in (0, 1, 2, 3):
@@ -697,7 +600,7 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
         splits = -(-K // kchunk)
     else:
         splits, kchunk = choose_splits(M, N, K, groups, tile)
-    default = (tile, splits, kchunk) if hit is None else hit  # a thin re-tune must beat the database entry
+    default = (tile, splits, kchunk)
     extent = (groups - 1) * c_gstride + (M - 1) * ldc + (N - (1 if ones >= 0 else 0))
     if (not _AUTOTUNE or epi == EPI_SGD or not out.is_cuda or torch.cuda.is_current_stream_capturing()
             or (out.is_contiguous() and extent > out.numel())):
@@ -708,8 +611,6 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     runs = []
     cands = (_candidates_fp8(M, N, K, groups, epi, xtra, bool(a_mc or b_mc)) if fp8
              else _candidates(M, N, K, groups, b_kc_dense, epi))
-    if hit is not None and hit not in cands:
-        cands = [hit] + cands
     for cand in cands:
         t, s, kc = cand
 
@@ -749,13 +650,39 @@ def _tuned_config_raw(M, N, K, groups, ops, epi, out, ldc, c_gstride, bias, relu
     best = min(times, key=times.get) if times else default
     if default in times and times[best] > 0.97 * times[default]:
         best = default
-    _THIN_DONE.add(key)
     if _TUNE_LOG:
         print(f"[gemm-tune] M={M} N={N} K={K} g={groups} modes={ops[1:3]}/{ops[4:]} epi={epi} "
               f"default={default} best={best} " +
               " ".join(f"{c[0]}/{c[1]}:{v * 1000 / reps:.1f}" for c, v in sorted(times.items())), flush=True)
     _TUNED[key] = best
     return best
+
+
+def set_autotune(on: bool) -> None:
+    """Enable / disable first-call timing of products the database does not cover."""
+    global _AUTOTUNE
+    _AUTOTUNE = bool(on)
+
+
+def tune_misses() -> list:
+    """Products (database keys) this process ran on the cost model's choice because the
+    tuning database has no entry for them (autotune off)."""
+    return sorted(_MISSES, key=repr)
+
+
+def sync_tuned(comm) -> int:
+    """Adopt rank 0's tile / split-K choices on every rank (a tuned run at N > 1: each rank's
+    first-call timings differ, so without this the ranks would capture different kernels for
+    one product).  Call after the eager warm-up iterations and before graph capture.
+    Returns the number of entries rank 0 sent."""
+    if comm is None or not getattr(comm, "active", False) or comm.world_size <= 1:
+        return 0
+    import torch.distributed as dist
+    payload = [{_key_to_str(k): list(v) for k, v in _TUNED.items()} if comm.rank == 0 else None]
+    dist.broadcast_object_list(payload, src=0)
+    for ks, v in payload[0].items():
+        _TUNED[_key_from_str(ks)] = tuple(v)
+    return len(payload[0])
 
 
 # --- dense helpers ---------------------------------------------------------------------

@@ -15,6 +15,7 @@ import os
 import torch
 
 from . import _lib
+from ..utils import features
 from .gemm import (EPI_BF16, EPI_F32, EPI_F32_ACC, ConvGeom, Dense, FlipW, Im2col, colsum, gemm,
                    linear_dgrad, linear_fwd, linear_wgrad)
 from .spec import POOL_MAX, ConvNdSpec, ConvSpec, PoolSpec
@@ -41,48 +42,6 @@ def chan_stride(t: torch.Tensor) -> int:
     if ld < Cc or t.stride(1) != W * ld or (N > 1 and t.stride(0) != H * W * ld):
         return 0
     return ld
-
-
-class WgradStream:
-    """Weight gradients on a side stream.  A weight gradient (and, for fused InnerProduct
-    layers, the solver update in its epilogue) feeds nothing later in backward, so while
-    it is enabled conv / InnerProduct backward issue it on ``stream`` — forked from the
-    main stream at that point — and the data gradient (the critical path) continues on
-    the main stream concurrently: tail waves of one GEMM fill with the other, and the
-    bandwidth-bound fused FC update overlaps compute-bound conv backward.  ``join()``
-    (before the param-diff finish / solver update) makes the main stream wait for it.
-    Star topology only (the side stream waits on the main stream alone): layers already
-    running on a BranchStreams side stream keep their wgrad inline.  Tensors the side
-    work reads (activations, top diffs) stay referenced by their blobs until the join."""
-    stream = None
-    main = None
-    used = False
-
-    @classmethod
-    def begin(cls, stream) -> None:
-        cls.stream, cls.main, cls.used = stream, torch.cuda.current_stream(stream.device), False
-
-    @classmethod
-    def join(cls) -> None:
-        if cls.stream is not None and cls.used:
-            cls.main.wait_stream(cls.stream)
-        cls.stream = cls.main = None
-        cls.used = False
-
-
-_WGRAD_KINDS = os.environ.get("SN_WGRAD_KINDS", "conv,fc,fcsgd").split(",")
-
-
-@contextlib.contextmanager
-def wgrad_side(kind: str = "conv"):
-    ss = WgradStream.stream
-    if ss is None or kind not in _WGRAD_KINDS or torch.cuda.current_stream(ss.device) != WgradStream.main:
-        yield
-        return
-    ss.wait_stream(WgradStream.main)
-    WgradStream.used = True
-    with torch.cuda.stream(ss):
-        yield
 
 
 def as_bf16(t: torch.Tensor | None) -> torch.Tensor | None:
@@ -275,8 +234,8 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
 # instead of the implicit GEMM for two thin shapes: 64 -> 64 channels with pad 1 (VGG-16's
 # conv1_2 forward and data gradient) and 48 -> 96 with pad 0 (CaffeNet / AlexNet conv1 after
 # the space-to-depth fold)
-_DIRECT_C64 = os.environ.get("SN_CONV_DIRECT_C64", "1") != "0"
-_DIRECT_K96 = os.environ.get("SN_CONV_DIRECT_K96", "1") != "0"
+_DIRECT_C64 = features.enabled("conv_direct_c64")
+_DIRECT_K96 = features.enabled("conv_direct_k96")
 
 
 def direct_c64_ok(s: ConvSpec) -> bool:
@@ -296,14 +255,14 @@ def direct_conv_ok(s: ConvSpec) -> bool:
 # outputs — GoogLeNet's conv2/3x3, 64 -> 192 — as 96-output direct launches writing channel
 # slices of the output: 2 x 64.6 us vs 155 us for the implicit GEMM at b128 (the GEMM re-reads
 # its 9x im2col A operand and the whole weight panel per 128-row tile; scripts/direct96_probe.py).
-# SN_CONV_DIRECT96=0 keeps the GEMM.
-_DIRECT96 = os.environ.get("SN_CONV_DIRECT96", "1") != "0"
+# (SN_FEATURES=conv_direct96=0 keeps the GEMM.)
+_DIRECT96 = features.enabled("conv_direct96")
 
 
 # 1x1 convolutions with <= 64 inputs and 64 outputs (GoogLeNet's conv2/3x3_reduce) on the
-# tap-packed direct kernel's <1, 64> instance (SN_CONV_PACKED11=1; measured in
+# tap-packed direct kernel's <1, 64> instance (SN_FEATURES=conv_packed11=1; measured in
 # profiles/r5_packed11.txt)
-_PACKED11 = os.environ.get("SN_CONV_PACKED11", "0") == "1"
+_PACKED11 = features.enabled("conv_packed11")
 
 
 def packed11_conv_ok(s: ConvSpec) -> bool:
@@ -320,8 +279,8 @@ def direct96_split_ok(s: ConvSpec) -> bool:
 
 # CaffeNet / AlexNet conv1 after the fold (48 -> 96, 3x3, pad 0) on the tap-packed direct kernel
 # (csrc/kernels/conv_packed.hip: 14 instead of 18 K steps, 192-pixel row-major tiles instead of
-# 16 x 16 ones); SN_CONV_PACKED=0 returns it to the 64-channel direct kernel
-_PACKED = os.environ.get("SN_CONV_PACKED", "1") != "0"
+# 16 x 16 ones); SN_FEATURES=conv_packed=0 returns it to the 64-channel direct kernel
+_PACKED = features.enabled("conv_packed")
 
 
 def packed_conv_ok(s: ConvSpec) -> bool:
@@ -335,8 +294,8 @@ def packed_conv_ok(s: ConvSpec) -> bool:
 # GoogLeNet conv1 after the 2x2 fold (115 x 115 x 16 -> 112 x 112 x 64, 4x4 taps, pad 0) on the
 # same tap-packed direct kernel's <4, 64> instance: the input rows of a 192-pixel tile staged
 # once in LDS instead of the implicit GEMM's per-tap re-reads of its 256x64 tiles;
-# SN_CONV_PACKED44=0 returns it to the GEMM
-_PACKED44 = os.environ.get("SN_CONV_PACKED44", "1") != "0"
+# SN_FEATURES=conv_packed44=0 returns it to the GEMM
+_PACKED44 = features.enabled("conv_packed44")
 
 
 def packed44_conv_ok(s: ConvSpec) -> bool:
@@ -351,9 +310,9 @@ def packed44_conv_ok(s: ConvSpec) -> bool:
 # engine.enable_fp8 (forward, and the data gradient with an e4m3 output gradient; the layer's
 # weight gradient then runs fp8 too): forward 1.37x the bf16 direct kernel at VGG conv1_2's
 # shape (profiles/r4_direct8_probe.txt), VGG-16 b2048 fp8 step 186 -> 181 ms with the thin tiles
-# and 192 -> 182 ms without (profiles/r4_vgg16_fp8_variants.jsonl).  SN_CONV_DIRECT_FP8=0 keeps
+# and 192 -> 182 ms without (profiles/r4_vgg16_fp8_variants.jsonl).  SN_FEATURES=conv_direct_fp8=0 keeps
 # these layers bf16.
-_DIRECT_FP8 = os.environ.get("SN_CONV_DIRECT_FP8", "1") != "0"
+_DIRECT_FP8 = features.enabled("conv_direct_fp8")
 
 
 def direct_fp8_ok(s: ConvSpec) -> bool:
@@ -417,8 +376,8 @@ def _pad_cols(t2: torch.Tensor, n: int) -> torch.Tensor:
 def conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=None, ws=None,
                   dw_acc=True, db_acc=True, dx_out=None):
     """``dx_out``: write the data gradient there — contiguous, or a channel slice of a wider
-    NHWC buffer (engine.fuse_siblings: the merged sibling gradient), which the stride-1
-    implicit dgrad writes in place (ldc = the slice's pixel stride)."""
+    NHWC buffer, which the stride-1 implicit dgrad writes in place (ldc = the slice's pixel
+    stride)."""
     if dx_out is not None and need_dx:
         if chan_stride(dx_out) == s.C or (_implicit_ok(s) and s.sh == s.sw == 1 and s.dh == s.dw == 1
                                           and s.Kg % 8 == 0 and chan_stride(dx_out) and _image_chunk(s) >= s.N
@@ -495,13 +454,11 @@ def _conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=
         dyq = ws.get("fp8_dyq")
         if dyq is None:
             dyq = ws["fp8_dyq"] = _fp8_dyq(dy, ws, s)
-        with wgrad_side():
-            _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc)
+        _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc)
         dw = None
         if db is not None:
             db, fused_db = None, False
-    with wgrad_side():
-        _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, ldd, ldx)
+    _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, ldd, ldx)
     if not need_dx:
         return None
     return _conv_dgrad(dy, x, w, s, M, gate, ws, ldd, ldx, dx_out)
@@ -557,7 +514,7 @@ def _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, 
 # (profiles/r5_fp8_bias_ab.txt): the separate pass reads every dy once more (6.3 ms / step,
 # 11.27-11.31k vs 11.51-11.55k img/s) and tests/test_fp8_fidelity_gpu.py passes both ways
 # (max deviation 0.071 exact vs 0.093 quantised, bound 0.234).
-FP8_WGRAD_BIAS = os.environ.get("SN_FP8_WGRAD_BIAS", "1") == "1"
+FP8_WGRAD_BIAS = features.enabled("fp8_wgrad_bias")
 
 
 def fp8_wgrad_ok(s: ConvSpec) -> bool:
@@ -590,7 +547,7 @@ def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc):
     e4m3 copy kept from the forward (MC), both read transposed from LDS by
     ds_read_b64_tr_b8; fp32 accumulation, split-K slabs, dequantised epilogue.  The bias
     gradient, by default, rides on the product as an e4m3 ones column, i.e. it is the column
-    sum of the QUANTISED dy, whose small entries are rounded or flushed; SN_FP8_WGRAD_BIAS=0
+    sum of the QUANTISED dy, whose small entries are rounded or flushed; SN_FEATURES=fp8_wgrad_bias=0
     computes the exact column sum of the bf16 dy in a separate pass instead (FP8_WGRAD_BIAS;
     reference: base_conv_layer.cpp:338-376, conv_layer.cu:35-53)."""
     sc, ix, xq, idy = f8w
@@ -716,13 +673,12 @@ def linear_forward(x2, w, b, relu=False, dropout=None):
 
 def linear_backward(dy2, x2, w, need_dx, dw=None, db=None, gate=None, dw_acc=True, db_acc=True, gate_scale=1.0):
     dy2 = _c(dy2)
-    with wgrad_side("fc"):
-        if dw is not None:
-            # the bias gradient comes out of the weight-gradient GEMM when it can (ones column)
-            if not linear_wgrad(dy2, _c(x2), dw, accumulate=dw_acc, db=db, db_acc=db_acc) and db is not None:
-                colsum(dy2, db, accumulate=db_acc)
-        elif db is not None:
+    if dw is not None:
+        # the bias gradient comes out of the weight-gradient GEMM when it can (ones column)
+        if not linear_wgrad(dy2, _c(x2), dw, accumulate=dw_acc, db=db, db_acc=db_acc) and db is not None:
             colsum(dy2, db, accumulate=db_acc)
+    elif db is not None:
+        colsum(dy2, db, accumulate=db_acc)
     if not need_dx:
         return None
     return linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None,
@@ -739,9 +695,8 @@ def linear_backward_sgd(dy2, x2, w, need_dx, sgd, db=None, gate=None, db_acc=Tru
         dx = linear_dgrad(dy2, _c(w), gate=gate.reshape(x2.shape) if gate is not None else None,
                           gate_scale=gate_scale)
     from .gemm import linear_wgrad_sgd
-    with wgrad_side("fcsgd"):  # forked after the dgrad: the update overwrites w
-        if not linear_wgrad_sgd(dy2, x2, sgd, db, db_acc) and db is not None:
-            colsum(dy2, db, accumulate=db_acc)
+    if not linear_wgrad_sgd(dy2, x2, sgd, db, db_acc) and db is not None:
+        colsum(dy2, db, accumulate=db_acc)
     return dx
 
 
@@ -1161,21 +1116,6 @@ def solver_update(kind, data, diff, history, compute, tables, hyper, l1, clip, g
          tables.get("src"))
 
 
-def copy_segments(segs) -> None:
-    """One launch for up to 8 (src, dst, accumulate) tensor copies (csrc/kernels/segcopy.hip):
-    contiguous bf16 / fp32 tensors of equal element counts, converting between the two and
-    optionally adding into dst."""
-    rows = []
-    for src, dst, acc in segs:
-        assert src.is_contiguous() and dst.is_contiguous() and src.numel() == dst.numel()
-        rows.append((src.data_ptr(), dst.data_ptr(), src.numel(), int(src.dtype == torch.float32),
-                     int(dst.dtype == torch.float32), int(acc)))
-    for i in range(0, len(rows), 8):
-        chunk = [v for r in rows[i:i + 8] for v in r]
-        arr = (C.c_longlong * len(chunk))(*chunk)
-        call("copy_segments", arr, len(chunk) // 6)
-
-
 def scale_shadow(flat, shadow, scale: float):
     call("scale_shadow", flat, shadow, flat.numel(), float(scale))
 
@@ -1213,8 +1153,10 @@ def augment(src_u8, dst, crop, mean=None, mean_mode=0, scale=1.0, rng_state=None
             offs_out=None, labels=None, label_out=None):
     N, Cc, Hs, Ws = src_u8.shape
     assert labels is None or labels.numel() == N
-    call("augment", _c(src_u8), dst, N, Cc, Hs, Ws, crop, crop, mean, int(mean_mode), float(scale), rng_state,
-         int(train), int(mirror), offs_out, *_labels(labels, label_out))
+    # an fp32 data blob (the fp32 device mode) gets the fp32 twin of the kernel
+    call("augment_f32" if dst.dtype == torch.float32 else "augment", _c(src_u8), dst, N, Cc, Hs, Ws, crop, crop,
+         mean, int(mean_mode), float(scale), rng_state, int(train), int(mirror), offs_out,
+         *_labels(labels, label_out))
     return dst
 
 

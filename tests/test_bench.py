@@ -100,3 +100,55 @@ def test_comm_inactive_at_world_one_without_force():
     from sparknet_amd.parallel.comm import Comm
     c = Comm()
     assert c.world_size == 1 and not c.active
+
+
+def test_gemm_autotune_off_by_default_and_rank_sync_cpu():
+    """Kernel selection is fixed by the committed database + cost model unless asked for
+    (VERDICT r5 #6): a fresh process imports gemm with first-call tuning OFF, bench.py does
+    not turn it on without --autotune, and sync_tuned adopts rank 0's choices over gloo."""
+    code = r'''
+import os, sys
+os.environ.pop("SN_GEMM_AUTOTUNE", None)
+sys.path.insert(0, ".")
+from sparknet_amd.ops import gemm as G
+assert G._AUTOTUNE is False
+import bench
+sys.argv = ["bench.py"]
+assert bench.parse().autotune is False
+'''
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=_clean_env(), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+def _sync_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from sparknet_amd.ops import gemm as G
+    from sparknet_amd.parallel import Comm
+    import torch
+    comm = Comm(backend="gloo")
+    key = (1, 2, 3, 1, 0, 0, 0, 0, 0, False, False, False, (8,), (8,), torch.bfloat16)
+    G._TUNED[key] = (rank, 1, 64)  # every rank "tuned" a different tile
+    n = G.sync_tuned(comm)
+    q.put((rank, G._TUNED[key], n))
+    dist.destroy_process_group()
+
+
+def test_sync_tuned_adopts_rank0_choices_gloo():
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sync_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert [r[1] for r in res] == [(0, 1, 64), (0, 1, 64)], res
+    assert all(r[2] >= 1 for r in res)

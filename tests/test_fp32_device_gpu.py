@@ -1,0 +1,96 @@
+"""The fp32 device mode: a net built with dtype=torch.float32 on the GPU runs
+the reference's numerics — Caffe's fp32 im2col + GEMM (/root/reference/libccaffe/ccaffe.h:3,
+caffe/src/caffe/layers/base_conv_layer.cpp:312-376) on exact-f32 matrix cores
+(csrc/kernels/fp32.hip, ops/f32dev.py).
+
+* the fp32 MFMA GEMM against a float64 product (ragged M / N / K, unaligned rows, bias / ReLU /
+  accumulate epilogues);
+* convolution forward / data / weight / bias gradients against the fp32 CPU engine (groups,
+  strides, padding, dilation);
+* CaffeNet: one SGD iteration from identical weights and batches — every parameter's update
+  within 1e-3 (relative to the layer's largest update) of the fp32 CPU engine, where the bf16
+  engine's floor is ~15 % on conv1 (tests/test_bench_fidelity_gpu.py).
+Reference check pattern: caffe/src/caffe/test/test_gradient_based_solver.cpp:225-320."""
+import pytest
+import torch
+
+from sparknet_amd import models
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (300, 200, 77), (5, 1000, 4096), (1000, 7, 363), (257, 129, 1)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "acc"])
+def test_gemm_f32_matches_fp64(gpu, M, N, K, epi):
+    from sparknet_amd.ops import f32dev
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    a = torch.randn(M, K + 3, generator=g)[:, :K]  # unaligned row stride
+    b = torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    c0 = torch.randn(M, N, generator=g)
+    ref = a.double() @ b.double().t()
+    out = c0.clone().to(gpu) if epi == "acc" else torch.empty(M, N, device=gpu)
+    f32dev.gemm_nt(a.to(gpu), b.to(gpu), out, bias=bias.to(gpu) if epi == "bias_relu" else None,
+                   relu=epi == "bias_relu", accumulate=epi == "acc")
+    if epi == "acc":
+        ref = ref + c0.double()
+    elif epi == "bias_relu":
+        ref = torch.relu(ref + bias.double())
+    err = (out.double().cpu() - ref).abs().max().item()
+    scale = (a.double().abs() @ b.double().abs().t()).max().item()
+    assert err <= 4e-7 * scale + 1e-6, (err, scale)
+
+
+@pytest.mark.parametrize("case", [(2, 13, 13, 16, 24, 3, 3, 1, 1, 1, 1), (2, 27, 27, 8, 16, 5, 5, 1, 2, 2, 1),
+                                  (3, 23, 23, 3, 8, 11, 11, 4, 0, 1, 1), (2, 9, 9, 8, 8, 3, 3, 2, 2, 1, 2)])
+def test_conv_f32_matches_cpu_engine(gpu, case):
+    from sparknet_amd.ops import f32dev, ref
+    from sparknet_amd.ops.spec import ConvSpec
+    N, H, W, C, K, R, S, st, pd, g, dil = case
+    s = ConvSpec(N, H, W, C, K, R, S, st, st, pd, pd, dil, dil, g)
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(N, H, W, C, generator=gen)
+    w = torch.randn(K, R, S, C // g, generator=gen) * 0.2
+    b = torch.randn(K, generator=gen)
+    dy = torch.randn(N, s.P, s.Q, K, generator=gen)
+    y = f32dev.conv_forward(x.to(gpu), w.to(gpu), b.to(gpu), s)
+    yr = ref.conv_forward(x, w, b, s)
+    assert torch.allclose(y.cpu(), yr, rtol=1e-5, atol=1e-4)
+    dw, db = torch.zeros(K, R, S, C // g, device=gpu), torch.zeros(K, device=gpu)
+    dwr, dbr = torch.zeros_like(w), torch.zeros(K)
+    dx = f32dev.conv_backward(dy.to(gpu), x.to(gpu), w.to(gpu), s, True, dw, db)
+    dxr = ref.conv_backward(dy, x, w, s, True, dwr, dbr)
+    for a_, b_ in ((dx, dxr), (dw, dwr), (db, dbr)):
+        assert torch.allclose(a_.cpu(), b_, rtol=1e-5, atol=2e-4 * max(1.0, b_.abs().max().item())), \
+            (a_.cpu() - b_).abs().max()
+
+
+def _fp32_gpu_updates(fid, dev, w0, x, y):
+    """bench.py --dtype fp32's step: fp32 net on the GPU, the device feeder (fp32 augment),
+    eager, no fusions."""
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.data.prefetch import DeviceFeeder, TensorSource
+    from sparknet_amd.engine import LocalSGDTrainer, fuse_input_fold, fuse_relu
+    solver = Solver(fid._solver_param(), device=dev, seed=1701, build_test_nets=False, dtype=torch.float32)
+    net = solver.net
+    net.flat_data.copy_(w0.to(dev))
+    net.sync_compute()
+    assert fuse_relu(net) == 0
+    feeder = DeviceFeeder(TensorSource(x, y, fid.B, pin=True), net.blob_by_name("data"), net.blob_by_name("label"),
+                          crop=227, mean=fid.MEAN, mirror=True, train=True, rng_state=net.ctx.rng_state, device=dev)
+    assert not fuse_input_fold(net, feeder)
+    tr = LocalSGDTrainer(solver, None, tau=1000, feeder=feeder, use_graph=False)
+    tr.local_step()
+    torch.cuda.synchronize()
+    return fid._updates(solver, w0)
+
+
+def test_caffenet_fp32_one_step_matches_cpu_engine(gpu):
+    import test_bench_fidelity_gpu as fid
+    x, y = fid._data(n=2 * fid.B)
+    w0 = fid._initial_weights()
+    uc = fid._one_step_updates(torch.device("cpu"), w0, x, y)
+    ug = _fp32_gpu_updates(fid, gpu, w0, x, y)
+    errs = fid._errs(ug, uc)
+    bad = {k: v for k, v in errs.items() if v[0] > 1e-3 or v[1] > 1e-3}
+    assert not bad, bad

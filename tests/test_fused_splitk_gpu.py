@@ -28,7 +28,7 @@ def _solver(dev, batch=32):
 
 def _run(dev, fuse, monkeypatch, steps=4):
     from sparknet_amd.engine import GraphStep
-    monkeypatch.setenv("SN_FUSE_SPLITK", "1" if fuse else "0")  # opt-in path
+    monkeypatch.setenv("SN_FEATURES", "fuse_splitk=1" if fuse else "fuse_splitk=0")  # opt-in path
     solver = _solver(dev)
     g = torch.Generator().manual_seed(3)
     batches = iter([(torch.randn(32, 3, 227, 227, generator=g) * 40, torch.randint(0, 10, (32, 1), generator=g).float())

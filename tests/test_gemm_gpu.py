@@ -236,9 +236,8 @@ def test_fp8_conv_dgrad(gpu, case, fmt, tile, monkeypatch):
 # 4-wave tiles (19, 20: dense only): every operand
 # layout, ragged edges, short and long K (the phased DMA pipeline issues zero-page DMAs past
 # the last K-step), split-K, the bias-gradient column and the implicit-GEMM convolutions
-# 23-28: the v_mfma_f32_32x32x16_bf16 twins of tiles 0, 10, 16, 13, 1, 11 (gemm_mf32.hip)
-BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 40, 41, 23, 24, 25, 26, 27, 28]
-MC_B = {6, 7, 11, 12, 13, 40, 41, 23, 24, 26, 27, 28}  # tiles with MC (k-strided) A and B operand instances
+BIG_TILES = [6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20]
+MC_B = {6, 7, 11, 12, 13}  # tiles with MC (k-strided) A and B operand instances
 
 
 @pytest.mark.parametrize("tile", BIG_TILES)
@@ -251,7 +250,7 @@ def test_gemm256_layouts(gpu, tile, M, N, K, monkeypatch):
     _close(G.linear_fwd(x, w, b, relu=True), torch.relu(x.float() @ w.float().t() + b))
     dy = _bf(M, N, device=gpu)
     w2 = _bf(N, K, device=gpu)
-    if tile in MC_B or tile in (16, 18, 19, 20, 25):  # NN: MC B operand (192-row tiles: MC A excluded)
+    if tile in MC_B or tile in (16, 18, 19, 20):  # NN: MC B operand (192-row tiles: MC A excluded)
         _close(G.linear_dgrad(dy, w2), dy.float() @ w2.float())
     if tile not in MC_B:
         return
@@ -367,33 +366,42 @@ def test_tile64_layouts(gpu, M, N, K, monkeypatch):
     _close(y, ref.conv_forward(x.float().cpu(), w.float().cpu(), None, s).to(gpu))
 
 
-@pytest.mark.parametrize("tile", [0, 1, 5, 11, 12])
-@pytest.mark.parametrize("case", [(2, 13, 13, 64, 384, 3, 3, 1, 1, 1), (2, 27, 27, 96, 256, 5, 5, 1, 2, 2),
-                                  (2, 7, 7, 192, 96, 3, 3, 1, 1, 2), (3, 9, 9, 32, 40, 3, 3, 2, 1, 1)])
-def test_fast_dma_addressing_bitwise(gpu, tile, case, monkeypatch):
-    """The scalar-offset DMA address paths (uniform-tap / tap-straddle implicit im2col,
-    soffset-advanced dense operands) stage exactly the bytes of the general per-lane
-    decode (SnGemmArgs.addr_legacy = 1): outputs of fwd / dgrad / wgrad are bitwise equal."""
-    from sparknet_amd.ops import gemm as G, hip
+# MC im2col stager (weight gradients): per-lane pixel state advanced BKE pixels per K-step
+# with one q and one p carry (gemm_impl.h GStager).  Geometries that exercise every carry
+# pattern: several images per K-step (P*Q < 64), a 1x1 output, stride 2 + padding, dilation,
+# 5x5 taps over 48-channel groups, a pixel count that is not a multiple of 64, and split-K
+# slices starting mid-image (the state is decoded per slice at its first row).
+@pytest.mark.parametrize("tile", [0, 10, 1, 13, 6])
+@pytest.mark.parametrize("splits", [1, 3, 7])
+@pytest.mark.parametrize("case", [(5, 13, 13, 64, 96, 3, 3, 1, 1, 1, 1), (9, 3, 3, 32, 64, 3, 3, 1, 1, 1, 1),
+                                  (70, 1, 1, 16, 32, 1, 1, 1, 0, 1, 1), (3, 17, 15, 24, 40, 3, 3, 2, 1, 1, 1),
+                                  (2, 12, 12, 32, 48, 3, 3, 1, 2, 1, 2), (2, 27, 27, 96, 64, 5, 5, 1, 2, 2, 1),
+                                  (4, 7, 9, 8, 16, 2, 3, 1, 0, 1, 1)])
+def test_mc_im2col_wgrad_geometries(gpu, tile, splits, case, monkeypatch):
+    from sparknet_amd.ops import gemm as G, hip, ref
     from sparknet_amd.ops.spec import ConvSpec
-    monkeypatch.setattr(G, "_FORCE_TILE", tile)
-    if tile in (19, 20):
-        pytest.skip("3-stage 4-wave tiles: dense operands only")
-    N, H, W, Cc, K, R, S, st, pd, g = case
-    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, 1, 1, g)
+    N, H, W, Cc, K, R, S, st, pd, g, dil = case
+    s = ConvSpec(N, H, W, Cc, K, R, S, st, st, pd, pd, dil, dil, g)
     x = _bf(N, H, W, Cc, device=gpu)
-    w = (torch.randn(K, R, S, Cc // g, device=gpu) * 0.1).to(torch.bfloat16)
     dy = _bf(N, s.P, s.Q, K, device=gpu)
-    outs = []
-    for legacy in (0, 1):
-        monkeypatch.setattr(G, "_ADDR_LEGACY", legacy)
-        y = hip.conv_forward(x, w, None, s)
-        dw = torch.zeros(K, R, S, Cc // g, device=gpu)
-        dx = hip.conv_backward(dy, x, w, s, True, dw, None) if tile in (0, 1, 11, 12) else None
-        outs.append((y, dx, dw))
-    for a, b in zip(outs[0], outs[1]):
-        if a is not None:
-            assert torch.equal(a, b)
+    M, kred = N * s.P * s.Q, R * S * (Cc // g)
+    dw = torch.zeros(K, kred, device=gpu)
+    db = torch.zeros(K, device=gpu)
+    geom = hip._geom(s)
+    monkeypatch.setattr(G, "_FORCE_TILE", tile)
+    A = G.Dense(dy.view(M, K), K, kcontig=False, gstride=K // g)
+    B = G.Im2col(x, geom, kcontig=False, gstride=Cc // g)
+    try:
+        G.gemm(K // g, kred, M, A, B, dw, kred, epi=G.EPI_F32, groups=g, c_gstride=(K // g) * kred,
+               splits=splits, bias_grad=db if kred % 8 == 0 else None, bias_acc=False)
+    except RuntimeError as e:
+        pytest.skip(f"tile {tile}: no instance ({e})")
+    w = torch.zeros(K, R, S, Cc // g)
+    dw_r, db_r = torch.zeros(K, R, S, Cc // g), torch.zeros(K)
+    ref.conv_backward(dy.float().cpu(), x.float().cpu(), w, s, False, dw_r, db_r)
+    _close(dw, dw_r.view(K, kred).to(gpu), 1e-2)
+    if kred % 8 == 0:
+        _close(db, db_r.to(gpu), 1e-3)
 
 
 def _db_tiles():

@@ -193,7 +193,7 @@ def test_fp8_fused_quant_is_bitwise_equal(gpu, monkeypatch):
     net_p = models.vgg16(train_batch=4, test_batch=4, crop=32, classes=10)
     res = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("SN_FP8_FUSED_QUANT", fused)
+        monkeypatch.setenv("SN_FEATURES", f"fuse_fp8_quant={fused}")
         sp = models.zoo.vgg16_solver(net_p)
         sp.base_lr = 0.002
         solver = Solver(sp, device=torch.device("cuda:0"), seed=5, build_test_nets=False)
@@ -227,7 +227,7 @@ def test_fp8_fused_quant_is_bitwise_equal(gpu, monkeypatch):
 @pytest.mark.parametrize("fp8", [False, True])
 def test_release_activations_before_capture_is_bitwise_equal(gpu, monkeypatch, fp8):
     """engine.release_activations (run before a capture when the warm-up holds most of the
-    device, forced here with SN_GRAPH_RELEASE=1): the captured iteration re-creates every
+    device, forced here with engine.GRAPH_RELEASE): the captured iteration re-creates every
     activation, gradient, workspace and fp8 side output it dropped, so training is bitwise equal
     to a capture that kept the warm-up's buffers."""
     from sparknet_amd.core.solver import Solver
@@ -235,7 +235,8 @@ def test_release_activations_before_capture_is_bitwise_equal(gpu, monkeypatch, f
     net_p = models.vgg16(train_batch=4, test_batch=4, crop=32, classes=10)
     res = {}
     for rel in ("1", "0"):
-        monkeypatch.setenv("SN_GRAPH_RELEASE", rel)
+        from sparknet_amd import engine as _engine
+        monkeypatch.setattr(_engine, "GRAPH_RELEASE", rel == "1")
         sp = models.zoo.vgg16_solver(net_p)
         sp.base_lr = 0.002
         solver = Solver(sp, device=torch.device("cuda:0"), seed=5, build_test_nets=False)
@@ -349,7 +350,7 @@ def test_fused_dropout_matches_standalone(gpu, monkeypatch):
     l0, g0, net0 = _run(n, gpu, True)  # fused (default)
     fused = [l.name for l in net0.layers if getattr(l, "fused_dropout", None) is not None]
     assert fused == ["fc6", "fc7"], fused
-    monkeypatch.setenv("SN_FUSE_DROPOUT", "0")
+    monkeypatch.setenv("SN_FEATURES", "fuse_dropout=0")
     l1, g1, net1 = _run(n, gpu, True, weights=net0.flat_data.detach().float().cpu())
     assert not any(getattr(l, "fused_dropout", None) for l in net1.layers)
     assert torch.equal(net0.blob_by_name("fc6").data, net1.blob_by_name("fc6").data)
@@ -378,7 +379,7 @@ def test_googlenet_zero_copy_concat_bitwise(gpu, monkeypatch):
             l.pooling_param.global_pooling = True
     res = {}
     for mode in ("copy", "zero"):
-        monkeypatch.setenv("SN_ZERO_COPY_CONCAT", "1" if mode == "zero" else "0")
+        monkeypatch.setenv("SN_FEATURES", "zero_copy_concat=1" if mode == "zero" else "zero_copy_concat=0")
         net = Net(n, phase=proto.TRAIN, seed=3, device=gpu)
         fuse_relu(net)
         cats = [l for l in net.layers if l.type_name == "Concat"]

@@ -12,6 +12,8 @@
   5-17) under EVERY summation order — the fp32 CPU engine too (scripts/
   cifar_quick_cpu_traj.py) — so whether step 300 lands inside a spike was a coin flip on
   the split count (round-4 'thin tile' report; profiles/r5_cifar_stability.txt).
+  Learning parity at the reference rate (base_lr 0.001) is therefore UNPINNED by this
+  test; what it pins is learning at half that rate under both summation orders.
 * A 20-step loss trajectory of a small CaffeNet (dropout 0) on the bf16 GPU engine stays
   within 5 % (relative) of the fp32 CPU engine from identical initial weights, and both
   decrease.
