@@ -943,7 +943,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 
 
   auto compute = [&](const char* la) __attribute__((always_inline)) {
     const char* lb = la + A_BYTES;
-    if constexpr (FP8 && MFR * NFR > 16) {    } else if constexpr (FP8 && MFR * NFR > 16) {
+    if constexpr (FP8 && MFR * NFR > 16) {
       // large fp8 tiles (gemm_fp8big.hip): B fragments held, A fragments streamed per row
       // group, so at most NFR + 1 fragments (8 VGPRs each) live beside the accumulators
       i32x8 fb8[NFR];
