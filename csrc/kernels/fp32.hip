@@ -29,6 +29,8 @@ struct F32Args {
   const float* bias;
   long long lda, ldb, ldc;
   int M, N, K, accumulate, relu;
+  int kchunk;              // split-K: block row y of the grid reduces k in [y*kchunk, (y+1)*kchunk)
+  long long c_split;       // ... into its own fp32 slab C + y * c_split (plain store; host sums)
 };
 
 __global__ void __launch_bounds__(F_NT, 2) gemm_f32_kernel(F32Args a) {
@@ -38,6 +40,8 @@ __global__ void __launch_bounds__(F_NT, 2) gemm_f32_kernel(F32Args a) {
   const int tiles_m = (a.M + F_BM - 1) / F_BM;
   const int bid = xcd_block(blockIdx.x, gridDim.x);
   const int m0 = (bid % tiles_m) * F_BM, n0 = (bid / tiles_m) * F_BN;
+  const int kbeg = blockIdx.y * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  float* const Cs = a.C + blockIdx.y * a.c_split;
   const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
 
   // staging: each thread moves 4 rows x 4 k (one float4 per row) of A and of B per stage
@@ -49,15 +53,15 @@ __global__ void __launch_bounds__(F_NT, 2) gemm_f32_kernel(F32Args a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + lr + 32 * j, n = n0 + lr + 32 * j, k = k0 + lk;
-      if (vec && k + 3 < a.K) {
+      if (vec && k + 3 < kend) {
         ra[j] = m < a.M ? *reinterpret_cast<const float4*>(a.A + (long long)m * a.lda + k) : make_float4(0, 0, 0, 0);
         rb[j] = n < a.N ? *reinterpret_cast<const float4*>(a.B + (long long)n * a.ldb + k) : make_float4(0, 0, 0, 0);
       } else {
         float va[4], vb[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          va[t] = (m < a.M && k + t < a.K) ? a.A[(long long)m * a.lda + k + t] : 0.f;
-          vb[t] = (n < a.N && k + t < a.K) ? a.B[(long long)n * a.ldb + k + t] : 0.f;
+          va[t] = (m < a.M && k + t < kend) ? a.A[(long long)m * a.lda + k + t] : 0.f;
+          vb[t] = (n < a.N && k + t < kend) ? a.B[(long long)n * a.ldb + k + t] : 0.f;
         }
         ra[j] = make_float4(va[0], va[1], va[2], va[3]);
         rb[j] = make_float4(vb[0], vb[1], vb[2], vb[3]);
@@ -82,16 +86,16 @@ __global__ void __launch_bounds__(F_NT, 2) gemm_f32_kernel(F32Args a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (a.K + F_BK - 1) / F_BK;
+  const int nk = kend > kbeg ? (kend - kbeg + F_BK - 1) / F_BK : 0;
   const int fr = lane & 15, fk = lane >> 4;  // fragment row / k of this lane
   if (nk > 0) {
-    load(0);
+    load(kbeg);
     store(0);
   }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int b = kt & 1;
-    if (kt + 1 < nk) load((kt + 1) * F_BK);  // in flight under this stage's MFMAs
+    if (kt + 1 < nk) load(kbeg + (kt + 1) * F_BK);  // in flight under this stage's MFMAs
     const float* la = sA[b];
     const float* lb = sB[b];
 #pragma unroll
@@ -123,7 +127,7 @@ __global__ void __launch_bounds__(F_NT, 2) gemm_f32_kernel(F32Args a) {
         const int n = n0 + wn + 16 * j + (lane & 15);
         if (n >= a.N) continue;
         float v = acc[i][j][r];
-        float* c = a.C + (long long)m * a.ldc + n;
+        float* c = Cs + (long long)m * a.ldc + n;
         if (a.accumulate) v += *c;
         if (a.bias) v += a.bias[n];
         if (a.relu) v = fmaxf(v, 0.f);
@@ -223,14 +227,19 @@ extern "C" int sn_dropout_f32(const float* x, float* y, long long n, const long 
   return SN_CHECK_LAUNCH();
 }
 
+// splits > 1: C is [splits][M][ldc] fp32 slabs written plainly (no bias / ReLU / accumulate);
+// the host sums them in split order (deterministic).
 extern "C" int sn_gemm_f32(const float* A, long long lda, const float* B, long long ldb, float* C, long long ldc,
                            long long M, long long N, long long K, const float* bias, long long accumulate,
-                           long long relu, hipStream_t st) {
+                           long long relu, long long splits, long long kchunk, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
   if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return 3;
-  F32Args a{A, B, C, bias, lda, ldb, ldc, (int)M, (int)N, (int)K, (int)accumulate, (int)relu};
+  if (splits < 1 || (splits > 1 && (bias || accumulate || relu || kchunk % F_BK))) return 3;
+  if (splits == 1) kchunk = K;
+  F32Args a{A, B, C, bias, lda, ldb, ldc, (int)M, (int)N, (int)K, (int)accumulate, (int)relu, (int)kchunk,
+            M * ldc};
   const long long tiles = ((M + F_BM - 1) / F_BM) * ((N + F_BN - 1) / F_BN);
-  hipLaunchKernelGGL(gemm_f32_kernel, dim3((unsigned)tiles), dim3(F_NT), 0, st, a);
+  hipLaunchKernelGGL(gemm_f32_kernel, dim3((unsigned)tiles, (unsigned)splits), dim3(F_NT), 0, st, a);
   return SN_CHECK_LAUNCH();
 }
 

@@ -41,15 +41,31 @@ SN_DEV void reduce_store(const ReduceOut& o, int g, int r, int c, float4 a) {
   if (o.mode == 0) {
     const long long base = g * o.out_gstride + (long long)r * o.ldo + c;
     bf16_t* p = reinterpret_cast<bf16_t*>(o.out) + base;
+    float v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (c + k < o.cols) {
-        float v = acc[k] + (o.bias ? o.bias[(long long)g * o.cols + c + k] : 0.f);
-        if (o.relu) v = fmaxf(v, 0.f);
-        if (o.gate) v = bf2f(o.gate[base + k]) > 0.f ? v * o.gate_scale : 0.f;
-        if (o.drop_rng) v = dropout_keep(o.drop_rng, o.drop_stream, o.drop_thr, base + k) ? v * o.drop_scale : 0.f;
-        p[k] = f2bf(v);
+      v[k] = acc[k] + ((o.bias && c + k < o.cols) ? o.bias[(long long)g * o.cols + c + k] : 0.f);
+      if (o.relu) v[k] = fmaxf(v[k], 0.f);
+      if (o.gate && c + k < o.cols) v[k] = bf2f(o.gate[base + k]) > 0.f ? v[k] * o.gate_scale : 0.f;
+    }
+    if (o.drop_rng) {
+      if ((base & 3) == 0) {  // the 4 columns are one Philox draw (as the GEMM epilogue)
+        const uint4 u = dropout_bits4(o.drop_rng, o.drop_stream, (unsigned long long)base >> 2);
+        const uint32_t b[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = b[k] > o.drop_thr ? v[k] * o.drop_scale : 0.f;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[k] = dropout_keep(o.drop_rng, o.drop_stream, o.drop_thr, base + k) ? v[k] * o.drop_scale : 0.f;
       }
+    }
+    if (c + 3 < o.cols && (base & 3) == 0) {  // one 8-byte store for the 4 bf16 outputs
+      *reinterpret_cast<uint2*>(p) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < o.cols) p[k] = f2bf(v[k]);
     }
   } else {
     float* p = reinterpret_cast<float*>(o.out) + g * o.out_gstride + (long long)r * o.ldo + c;

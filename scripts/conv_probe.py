@@ -20,6 +20,8 @@ CASES = {  # N, H, W, C, K, R, S, stride, pad
     "gn_3b_3x3": (128, 28, 28, 128, 192, 3, 3, 1, 1),
     "cn_conv3": (256, 13, 13, 256, 384, 3, 3, 1, 1),
     "cn_conv4g": (256, 13, 13, 192, 192, 3, 3, 1, 1),
+    "cn_conv2g": (256, 27, 27, 48, 128, 5, 5, 1, 2),  # CaffeNet conv2, one of its two groups
+    "cn_conv5g": (256, 13, 13, 192, 128, 3, 3, 1, 1),
 }
 
 

@@ -22,14 +22,37 @@ from .spec import ConvSpec
 F32 = torch.float32
 
 
+_BK = 32  # the kernel's k per stage: split-K chunks are multiples of it
+
+
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, bias=None, relu=False, accumulate=False):
-    """out[M][N] (+)= a[M][K] @ b[N][K]^T (+ bias, ReLU) — rows K-contiguous, fp32."""
+    """out[M][N] (+)= a[M][K] @ b[N][K]^T (+ bias, ReLU) — rows K-contiguous, fp32.  Products
+    with few 128x128 output tiles and a long reduction (the weight gradients: K = pixels)
+    split K over up to ~512 blocks into fp32 slabs summed in split order."""
     M, K = a.shape
     N = b.shape[0]
     assert a.dtype == b.dtype == out.dtype == F32 and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1
     assert b.shape[1] == K and out.shape[0] == M and out.shape[1] == N
-    _lib.call("gemm_f32", a, a.stride(0), b, b.stride(0), out, out.stride(0), M, N, K,
-              bias if bias is not None else None, int(accumulate), int(relu))
+    tiles = -(-M // 128) * -(-N // 128)
+    splits = max(1, min(512 // tiles, K // 2048)) if tiles < 256 else 1
+    if splits > 1:
+        kchunk = -(-(-(-K // splits)) // _BK) * _BK
+        splits = -(-K // kchunk)
+    if splits == 1:
+        _lib.call("gemm_f32", a, a.stride(0), b, b.stride(0), out, out.stride(0), M, N, K,
+                  bias if bias is not None else None, int(accumulate), int(relu), 1, K)
+        return out
+    ws = torch.empty((splits, M, N), dtype=F32, device=out.device)
+    _lib.call("gemm_f32", a, a.stride(0), b, b.stride(0), ws, N, M, N, K, None, 0, 0, splits, kchunk)
+    r = ws.sum(0)
+    if bias is not None:
+        r += bias
+    if relu:
+        r.clamp_(min=0)
+    if accumulate:
+        out += r
+    else:
+        out.copy_(r)
     return out
 
 

@@ -7,9 +7,13 @@ caffe/src/caffe/layers/base_conv_layer.cpp:312-376) on exact-f32 matrix cores
   accumulate epilogues);
 * convolution forward / data / weight / bias gradients against the fp32 CPU engine (groups,
   strides, padding, dilation);
-* CaffeNet: one SGD iteration from identical weights and batches — every parameter's update
-  within 1e-3 (relative to the layer's largest update) of the fp32 CPU engine, where the bf16
-  engine's floor is ~15 % on conv1 (tests/test_bench_fidelity_gpu.py).
+* CaffeNet b256: one SGD iteration from identical weights and batches — every weight update
+  within 1e-3 of the fp32 CPU engine's in relative L2 norm (2e-3 in the largest element),
+  every bias update within 3e-3 (L2) / 2e-2 (largest element), where the bf16 engine's floor
+  is ~11 % (L2) / ~15 % (max) on conv1 (tests/test_bench_fidelity_gpu.py).  The bias bounds
+  are fp32 summation-order noise: a bias gradient sums 43,264-774,400 pixel terms that nearly
+  cancel at this initialisation (conv2's: 186,624 terms, max-element deviation ~1e-2 between
+  two fp32 reduction orders; measured on one MI355X, profiles/r6_fp32_device.txt).
 Reference check pattern: caffe/src/caffe/test/test_gradient_based_solver.cpp:225-320."""
 import pytest
 import torch
@@ -19,7 +23,8 @@ from sparknet_amd import models
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (300, 200, 77), (5, 1000, 4096), (1000, 7, 363), (257, 129, 1)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (300, 200, 77), (5, 1000, 4096), (1000, 7, 363), (257, 129, 1),
+                                   (64, 200, 100003), (96, 363, 20000)])  # the last two: split-K slabs
 @pytest.mark.parametrize("epi", ["plain", "bias_relu", "acc"])
 def test_gemm_f32_matches_fp64(gpu, M, N, K, epi):
     from sparknet_amd.ops import f32dev
@@ -92,5 +97,10 @@ def test_caffenet_fp32_one_step_matches_cpu_engine(gpu):
     uc = fid._one_step_updates(torch.device("cpu"), w0, x, y)
     ug = _fp32_gpu_updates(fid, gpu, w0, x, y)
     errs = fid._errs(ug, uc)
-    bad = {k: v for k, v in errs.items() if v[0] > 1e-3 or v[1] > 1e-3}
+    bad = {}
+    for k, (emax, el2) in errs.items():
+        bias = k.endswith("/1")
+        if el2 > (3e-3 if bias else 1e-3) or emax > (2e-2 if bias else 2e-3):
+            bad[k] = (emax, el2)
+    print("fp32 device vs fp32 CPU engine (max, L2):", {k: (round(a, 6), round(b, 6)) for k, (a, b) in errs.items()})
     assert not bad, bad
