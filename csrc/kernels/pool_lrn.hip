@@ -31,7 +31,7 @@ struct PLGeom {
   int cg, ngrp;     // backward: channel chunks per workgroup, channel groups
   int size;
   float alpha, beta, k;
-  FDiv fcv, fQ, fP, fcg, fQcg, fBWcg, fWcv;
+  FDiv fcv, fQ, fP, fcg, fQcg, fBWcg;
 };
 
 SN_DEV float plrn_pow(float s, float beta) { return sn_powneg(s, beta); }
@@ -258,60 +258,6 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
   }
 }
 
-// Whole-pixel form: a workgroup owns every channel of its rows (cg = C / 8) and phase 2 gives
-// each lane one 8-channel chunk of one input pixel, chunks fastest, so a wave's store writes
-// 1 KB of contiguous dx (the block form above writes 64-byte runs of 2x2 blocks).  Same
-// windows, same accumulation order: bitwise equal to lrn_pool_bwd.
-template <int SIZE>
-__global__ void __launch_bounds__(256) lrn_pool_bwd_px(const bf16_t* __restrict__ xp, const bf16_t* __restrict__ dyn,
-                                                       const uint8_t* __restrict__ mask, bf16_t* __restrict__ dx,
-                                                       PLGeom g) {
-  extern __shared__ uint4 tile[];  // (rows + 1) x Q x cv chunks, then their argmax masks
-  const int cv = g.C >> 3;
-  const int wg = xcd_block(blockIdx.x, gridDim.x);
-  const int n = wg / g.nb;
-  const int bh0 = (wg - n * g.nb) * g.rows;
-  const int qcv = g.Q * cv;
-  const int items1 = (g.rows + 1) * qcv;
-  plrn_bwd_phase1<SIZE, true>(xp, dyn, mask, g, tile, n, bh0, 0, cv, items1);
-  __syncthreads();
-  const uint2* mt = reinterpret_cast<const uint2*>(tile + items1);
-  const int wcv = g.W * cv;
-  const int items2 = 2 * min(g.rows, g.BH - bh0) * wcv;
-  for (int it = threadIdx.x; it < items2; it += blockDim.x) {
-    const uint32_t r2 = udiv((uint32_t)it, g.fWcv);
-    const int rem = it - (int)r2 * wcv;
-    const uint32_t wu = udiv((uint32_t)rem, g.fcv);
-    const int lc = rem - (int)wu * cv;
-    const int ia = (int)r2 & 1, rb = (int)r2 >> 1;
-    const int bh = bh0 + rb;
-    const int h = 2 * bh + ia - g.ph;
-    if ((unsigned)h >= (unsigned)g.H) continue;
-    const int w = (int)wu, wp = w + g.pw, bw = wp >> 1, ib = wp & 1;
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int wa = 0; wa < 2; ++wa) {
-      const int p = bh - 1 + wa;
-      if ((wa == 0 && ia == 1) || p < 0 || p >= g.P) continue;
-#pragma unroll
-      for (int wb = 0; wb < 2; ++wb) {
-        const int q = bw - 1 + wb;
-        if ((wb == 0 && ib == 1) || q < 0 || q >= g.Q) continue;
-        const int idx = (rb + wa) * qcv + q * cv + lc;
-        float f[8];
-        unpack8(tile[idx], f);
-        const uint2 mv = mt[idx];
-        const uint32_t mw[2] = {mv.x, mv.y};
-        const int widx = (ia + 2 * (1 - wa)) * 3 + (ib + 2 * (1 - wb));
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
-          if ((int)((mw[kk >> 2] >> ((kk & 3) * 8)) & 0xff) == widx) acc[kk] += f[kk];
-      }
-    }
-    *reinterpret_cast<uint4*>(dx + (((long long)n * g.H + h) * g.W + w) * g.C + lc * 8) = pack8(acc);
-  }
-}
-
 static PLGeom plgeom(long long N, long long H, long long W, long long C, long long P, long long Q, long long ph,
                      long long pw, long long size, float alpha, float beta, float k) {
   PLGeom g{};
@@ -400,19 +346,6 @@ extern "C" int sn_pool_lrn_supported(long long N, long long H, long long W, long
   return BH <= P + 1 && BW <= Q + 1 ? 1 : 0;
 }
 
-// Backward form (A/B probe, sn_plrn_bwd_variant): 0 the block form (lrn_pool_bwd), 1 / 2 the
-// whole-pixel form (lrn_pool_bwd_px) with a 32 / 64 KB LDS tile.
-static int g_plrn_variant = 0;
-extern "C" void sn_plrn_bwd_variant(int v) { g_plrn_variant = v; }
-
-// whole-pixel tile: the most block rows (<= 7) whose (rows + 1) x Q x C/8 chunks (gradient + mask)
-// fit `budget`
-static int plrn_px_rows(long long Q, long long C, long long budget) {
-  int r = 7;
-  while (r >= 1 && (long long)(r + 1) * Q * (C / 8) * 24 > budget) --r;
-  return r;
-}
-
 extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_t* mask, bf16_t* dx, long long N,
                                long long H, long long W, long long C, long long P, long long Q, long long ph,
                                long long pw, long long size, float alpha, float beta, float k, hipStream_t st) {
@@ -422,26 +355,6 @@ extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_
   g.BW = (int)((W + pw + 1) / 2);
   // every pooled row the blocks read exists in the tile: blocks bh read rows bh-1, bh
   if (g.BH > P + 1 || g.BW > Q + 1) return 4;
-  const long long px_budget = g_plrn_variant == 2 ? 64 * 1024 : 32 * 1024;
-  const int px_rows = g_plrn_variant ? plrn_px_rows(Q, C, px_budget) : 0;
-  if (px_rows >= 1) {
-    g.rows = px_rows;
-    g.cg = (int)(C / 8);
-    g.ngrp = 1;
-    g.nb = (g.BH + g.rows - 1) / g.rows;
-    g.fcg = make_fdiv((uint32_t)g.cg);
-    g.fQcg = make_fdiv((uint32_t)(Q * g.cg));
-    g.fWcv = make_fdiv((uint32_t)(W * g.cg));
-    dim3 grid((unsigned)(N * g.nb));
-    const size_t lds = (size_t)(g.rows + 1) * Q * g.cg * 24;
-    switch (size) {
-      case 3: hipLaunchKernelGGL(lrn_pool_bwd_px<3>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
-      case 5: hipLaunchKernelGGL(lrn_pool_bwd_px<5>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
-      case 7: hipLaunchKernelGGL(lrn_pool_bwd_px<7>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
-      default: hipLaunchKernelGGL(lrn_pool_bwd_px<9>, grid, dim3(256), lds, st, xp, dyn, mask, dx, g); break;
-    }
-    return SN_CHECK_LAUNCH();
-  }
   // argmax mask staged in LDS by phase 1 (instead of phase 2 reading it from global memory):
   // pool1/norm1 63.5 -> 62.2 us, pool2/norm2 42.5 -> 41.3 us (profiles/r4_plrn_tiles.txt)
   const int mlds = 1;

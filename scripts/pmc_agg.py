@@ -11,9 +11,12 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "gemm" not in k and "splitk" not in k:
+        if "gemm" not in k and "splitk" not in k and "Cijk" not in k:
             continue
         k = k.replace("(anonymous namespace)::", "").split("(SnGemmArgs")[0].split("(")[0][-70:]
+        if "--by-grid" in sys.argv:
+            k += (f"  grid={r.get('Grid_Size', '?')} wg={r.get('Workgroup_Size', '?')} lds={r.get('LDS_Block_Size', '?')}"
+                  f" vgpr={r.get('VGPR_Count', '?')} agpr={r.get('Accum_VGPR_Count', '?')}")
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in vals.items():
     print(k)

@@ -111,26 +111,3 @@ def test_pool_lrn_eligibility_matches_kernels(gpu, case):
         with pytest.raises(RuntimeError):
             hip.lrn_pool_backward(dy, p_ref, m_ref, s, size, alpha, beta, k)
 
-
-@pytest.mark.parametrize("form", [1, 2])
-@pytest.mark.parametrize("case", CASES)
-def test_lrn_pool_backward_pixel_form_bitwise(gpu, case, form):
-    """The whole-pixel backward form (lrn_pool_bwd_px: all channels per workgroup, one chunk
-    of one input pixel per lane) is bitwise equal to the unfused launches."""
-    import ctypes
-    from sparknet_amd.ops import _lib, hip
-    N, H, W, C, pad, size = case
-    s = PoolSpec(N, H, W, C, 3, 3, 2, 2, pad, pad)
-    alpha, beta, k = 1e-4 * 50, 0.75, 1.0
-    x = _inputs(N, H, W, C, 5).to(gpu).clamp_min(0)
-    p_ref, m_ref = hip.pool_forward_mask(x, s, True)
-    dy = _inputs(N, s.P, s.Q, C, 6).to(gpu)
-    dx_ref = hip.pool_backward(hip.lrn_backward(dy, p_ref, size, alpha, beta, k), x, s, m_ref, gate=True)
-    setv = _lib.kernels().sn_plrn_bwd_variant
-    setv.argtypes = [ctypes.c_int]
-    setv(form)
-    try:
-        dx = hip.lrn_pool_backward(dy, p_ref, m_ref, s, size, alpha, beta, k)
-    finally:
-        setv(0)
-    assert torch.equal(dx, dx_ref)
