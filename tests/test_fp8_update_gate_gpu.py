@@ -18,7 +18,7 @@ the layers that run both), the same initial weights and Philox dropout draws on 
 * teeth: with the conv5_x e4m3 weight gradients made to drop 7/8 of their reduction the
   gate fails on them.
 
-What the floor says (profiles/r6_fp8_gate.txt): e4m3 storage moves VGG-16's one-step updates
+What the floor says (profiles/r6_fp8_gates.txt): e4m3 storage moves VGG-16's one-step updates
 by 20-45 % (relative L2; bf16 storage alone 3-17 %), and CDNA4-style per-32-element E8M0 block
 scales (fp8emu block=32) do NOT lower it (0.2-0.6): the deviation is the 3-bit mantissa's, not
 the dynamic range's, so block scales were not built into the GEMM.  The GPU lands on the floor
