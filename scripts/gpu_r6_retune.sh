@@ -11,6 +11,10 @@ mkdir -p gpurun_out
 DB=sparknet_amd/ops/gemm_tuned.json
 [ -f gpurun_out/gemm_tuned_r6.json ] && cp gpurun_out/gemm_tuned_r6.json $DB
 [ "$STRIP" = "1" ] && { python scripts/tune_db_strip.py $DB wgrad >> gpurun_out/r6r_tune.log || exit 1; }
+# heartbeat: the first VGG-16 b2048 tuning steps print nothing for minutes
+( while sleep 50; do echo "[hb] $(date +%T)"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 IFS='|' read -ra CFGS <<< "$MODELS"
 for cfg in "${CFGS[@]}"; do
   [ -z "$cfg" ] && continue
