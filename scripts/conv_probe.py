@@ -22,6 +22,8 @@ CASES = {  # N, H, W, C, K, R, S, stride, pad
     "cn_conv4g": (256, 13, 13, 192, 192, 3, 3, 1, 1),
     "cn_conv2g": (256, 27, 27, 48, 128, 5, 5, 1, 2),  # CaffeNet conv2, one of its two groups
     "cn_conv5g": (256, 13, 13, 192, 128, 3, 3, 1, 1),
+    "vgg_conv3_2": (128, 56, 56, 256, 256, 3, 3, 1, 1),  # VGG-16 at 1/16 of its b2048 batch
+    "vgg_conv4_2": (256, 28, 28, 512, 512, 3, 3, 1, 1),
 }
 
 

@@ -10,7 +10,7 @@ TILES=0 WGRAD_TILES=0,10 bash scripts/pmc_tiles.sh > gpurun_out/r6m_pmc.txt 2>&1
 tail -40 gpurun_out/r6m_pmc.txt
 bash scripts/pmc_blas.sh > gpurun_out/r6m_pmc_blas.txt 2>&1 || { echo "pmc blas failed"; tail -20 gpurun_out/r6m_pmc_blas.txt; exit 1; }
 tail -60 gpurun_out/r6m_pmc_blas.txt
-timeout -k 10 300 python -u scripts/conv_probe.py --case cn_conv2g,cn_conv5g,cn_conv3 --tiles -1,0,13,16,17 > gpurun_out/r6m_conv.txt 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/conv_probe.py --case cn_conv2g,cn_conv5g,cn_conv3 --tiles=-1,0,13,16,17 > gpurun_out/r6m_conv.txt 2>&1 || exit 1
 grep -v amdgpu gpurun_out/r6m_conv.txt
 run() {  # name, bench args...
   local n=$1; shift
