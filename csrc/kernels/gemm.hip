@@ -158,8 +158,7 @@ extern "C" int sn_gemm(const SnGemmArgs* args, hipStream_t stream) {
     case 11:
     case 12:
     case 13:
-    case 14:
-    case 23: return a.epi == EPI_SGD ? 4 : sn_gemm_big8(a, stream);  // gemm_big8.hip
+    case 14: return a.epi == EPI_SGD ? 4 : sn_gemm_big8(a, stream);  // gemm_big8.hip
     case 21:
     case 22: return sn_gemm_tiles_c(a, stream);  // gemm_tiles_c.hip (64-row tiles)
     case 15:

@@ -9,9 +9,6 @@ int sn_gemm_big8(const SnGemmArgs& a, hipStream_t stream) {
     case 12: return launch_big<256, 128, 8, 2>(a, stream);  // waves 2x4 of 128x32
     case 13: return launch_big<256, 128, 4, 4>(a, stream);  // waves 4x2 of 64x64
     case 14: return launch_big<256, 192, 8, 3>(a, stream);  // waves 2x4 of 128x48
-    // 4 waves of 128x128 (one wave per SIMD, 256 accumulator registers each): a quarter of the
-    // 64x64 wave tile's LDS fragment reads per MFMA
-    case 23: return launch_big<256, 256, 8, 8, 4>(a, stream);
     default: return 4;
   }
 }

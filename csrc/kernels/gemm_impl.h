@@ -875,8 +875,7 @@ SN_DEV void epi_store(const SnGemmArgs& args, int grp, int split, int m, int n, 
 // docs/PERF_NOTES.md round 5, and were removed in round 6)
 template <int AMC, int AMODE, int BMC, int BMODE, int EPI, int BM, int BN, int NW, int NS, int FP8 = 0,
           int NFR = 4, int MFR = 4>
-__global__ void __launch_bounds__(NW * 64, (NW == 4 && MFR * NFR <= 16) ? (BM * BN <= 128 * 64 ? 3 : 2) : 1)
-    gemm_kernel(SnGemmArgs args) {
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? (BM * BN <= 128 * 64 ? 3 : 2) : 1) gemm_kernel(SnGemmArgs args) {
   // LDS rows are 128 B in both precisions: BK = 64 bf16 or 128 fp8 reduction elements
   constexpr int ES = FP8 ? 1 : 2, BKE = FP8 ? 128 : BK;
   // MFMA operand formats: src A of the instruction is our B fragment (cbsz), src B our A
@@ -976,28 +975,7 @@ __global__ void __launch_bounds__(NW * 64, (NW == 4 && MFR * NFR <= 16) ? (BM * 
       __builtin_amdgcn_s_setprio(0);
       return;
     }
-    if constexpr (MFR * NFR >= 64) {
-      // 128x128 wave tiles (one wave per SIMD): the accumulators take 256 registers, so only
-      // the k-substep's NFR B fragments stay live and the A fragments stream one ahead
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8_t fb[NFR];
-#pragma unroll
-        for (int i = 0; i < NFR; ++i) fb[i] = read_frag<BMC, BNL>(lb, wn0 + 16 * i, s, lane);
-        bf16x8_t fa = read_frag<AMC, BM>(la, wm0, s, lane);
-#pragma unroll
-        for (int j = 0; j < MFR; ++j) {
-          bf16x8_t fn = fa;
-          if (j + 1 < MFR) fn = read_frag<AMC, BM>(la, wm0 + 16 * (j + 1), s, lane);
-          __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int i = 0; i < NFR; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa, acc[i][j], 0, 0, 0);
-          __builtin_amdgcn_s_setprio(0);
-          fa = fn;
-        }
-      }
-      return;
-    } else if constexpr (MFR * NFR > 16 || (EPI == EPI_SGD && BM == 128 && BN == 128 && NW == 4 && NS == 2)) {
+    if constexpr (MFR * NFR > 16 || (EPI == EPI_SGD && BM == 128 && BN == 128 && NW == 4 && NS == 2)) {
       // 128-row wave tiles: fragments of one 32-deep k-substep at a time (the accumulators
       // already take 4 * MFR * NFR VGPRs); EPI_SGD: the prefetched master / history rows do
 #pragma unroll

@@ -115,15 +115,14 @@ def _operand(op, fp8: bool = False) -> tuple[_lib.SnOperand, int, int]:
 TILES = {0: (128, 128), 1: (256, 64), 2: (256, 128), 3: (128, 256), 4: (128, 96), 5: (256, 48),
          6: (256, 256), 7: (256, 128), 10: (128, 64),
          11: (256, 256), 12: (256, 128), 13: (256, 128), 14: (256, 192), 15: (128, 192), 16: (192, 128),
-         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64), 21: (64, 256), 22: (64, 128),
-         23: (256, 256)}
+         17: (192, 96), 18: (192, 64), 19: (128, 128), 20: (128, 64), 21: (64, 256), 22: (64, 128)}
 # (round 6 removed the measured-and-rejected families: the v_mfma 32x32x16 twins 23-28, the
 # persistent ring tiles 30-39, the 4- and 8-phase gemm256 schedules 8 / 9 / 40 / 41 —
 # docs/PERF_NOTES.md rounds 4-5)
 # gemm256_kernel tiles (6, 7) and the 8-wave 2-stage gemm_kernel tiles (11-14) run one
 # 512-thread block per CU
-_SLOTS = {6: 256, 7: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512, 21: 512, 22: 768, 23: 256}
-_KTILE_US = {6: 2.0, 7: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55, 23: 1.6}
+_SLOTS = {6: 256, 7: 256, 10: 768, 11: 256, 12: 256, 13: 256, 14: 256, 19: 256, 20: 512, 21: 512, 22: 768}
+_KTILE_US = {6: 2.0, 7: 1.1, 11: 2.0, 12: 1.1, 13: 1.1, 14: 1.55}
 _FORCE_TILE = int(os.environ.get("SN_GEMM_TILE", "-1"))  # tuning / A-B experiments only
 
 
