@@ -675,9 +675,10 @@ def sync_tuned(comm) -> int:
     first-call timings differ, so without this the ranks would capture different kernels for
     one product).  Call after the eager warm-up iterations and before graph capture.
     Returns the number of entries rank 0 sent."""
-    if comm is None or not getattr(comm, "active", False) or comm.world_size <= 1:
-        return 0
     import torch.distributed as dist
+    if (comm is None or not getattr(comm, "active", False) or comm.world_size <= 1
+            or not (dist.is_available() and dist.is_initialized())):
+        return 0  # (a stand-in communicator without a process group: nothing to agree with)
     payload = [{_key_to_str(k): list(v) for k, v in _TUNED.items()} if comm.rank == 0 else None]
     dist.broadcast_object_list(payload, src=0)
     for ks, v in payload[0].items():
