@@ -33,6 +33,10 @@ struct F32Args {
   long long c_split;       // ... into its own fp32 slab C + y * c_split (plain store; host sums)
 };
 
+// AT / BT: the operand is stored [K][M] / [K][N] (k-strided rows, e.g. the activations and
+// output gradients of a weight gradient, or the weights of a data gradient) and is staged
+// transposed into the same [row][k] LDS image, so no operand is ever copied to K-contiguous form.
+template <bool AT, bool BT>
 __global__ void __launch_bounds__(F_NT, 2) gemm_f32_kernel(F32Args a) {
   __shared__ float sA[2][F_BM * F_LD];
   __shared__ float sB[2][F_BN * F_LD];
@@ -44,40 +48,64 @@ __global__ void __launch_bounds__(F_NT, 2) gemm_f32_kernel(F32Args a) {
   float* const Cs = a.C + blockIdx.y * a.c_split;
   const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
 
-  // staging: each thread moves 4 rows x 4 k (one float4 per row) of A and of B per stage
-  const int lr = tid >> 3, lk = (tid & 7) * 4;  // rows lr + 32 j, k chunk lk
+  // staging: a K-contiguous operand moves 4 rows x 4 k per thread and stage (one float4 along k
+  // per row); a transposed one 4 k-rows x 4 rows (one float4 along the rows per k-row), written
+  // to LDS transposed
+  const int lr = tid >> 3, lk = (tid & 7) * 4;  // K-contiguous: rows lr + 32 j, k chunk lk
+  const int tr = (tid & 31) * 4, tk = tid >> 5;  // transposed: rows tr..tr+3, k rows tk + 8 j
   const bool vec = (a.lda % 4) == 0 && (a.ldb % 4) == 0 && (reinterpret_cast<uintptr_t>(a.A) % 16) == 0 &&
                    (reinterpret_cast<uintptr_t>(a.B) % 16) == 0;
   float4 ra[4], rb[4];
-  auto load = [&](int k0) __attribute__((always_inline)) {
+  auto load_op = [&](const float* X, long long ld, int r0, int rows, bool trans, int k0, float4* rx)
+                     __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int m = m0 + lr + 32 * j, n = n0 + lr + 32 * j, k = k0 + lk;
-      if (vec && k + 3 < kend) {
-        ra[j] = m < a.M ? *reinterpret_cast<const float4*>(a.A + (long long)m * a.lda + k) : make_float4(0, 0, 0, 0);
-        rb[j] = n < a.N ? *reinterpret_cast<const float4*>(a.B + (long long)n * a.ldb + k) : make_float4(0, 0, 0, 0);
-      } else {
-        float va[4], vb[4];
+      if (!trans) {
+        const int r = r0 + lr + 32 * j, k = k0 + lk;
+        if (vec && k + 3 < kend) {
+          rx[j] = r < rows ? *reinterpret_cast<const float4*>(X + (long long)r * ld + k) : make_float4(0, 0, 0, 0);
+        } else {
+          float v[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          va[t] = (m < a.M && k + t < kend) ? a.A[(long long)m * a.lda + k + t] : 0.f;
-          vb[t] = (n < a.N && k + t < kend) ? a.B[(long long)n * a.ldb + k + t] : 0.f;
+          for (int t = 0; t < 4; ++t) v[t] = (r < rows && k + t < kend) ? X[(long long)r * ld + k + t] : 0.f;
+          rx[j] = make_float4(v[0], v[1], v[2], v[3]);
         }
-        ra[j] = make_float4(va[0], va[1], va[2], va[3]);
-        rb[j] = make_float4(vb[0], vb[1], vb[2], vb[3]);
+      } else {
+        const int r = r0 + tr, k = k0 + tk + 8 * j;
+        if (k < kend && vec && r + 3 < rows) {
+          rx[j] = *reinterpret_cast<const float4*>(X + (long long)k * ld + r);
+        } else {
+          float v[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = (k < kend && r + t < rows) ? X[(long long)k * ld + r + t] : 0.f;
+          rx[j] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  };
+  auto load = [&](int k0) __attribute__((always_inline)) {
+    load_op(a.A, a.lda, m0, a.M, AT, k0, ra);
+    load_op(a.B, a.ldb, n0, a.N, BT, k0, rb);
+  };
+  auto store_op = [&](float* sx, bool trans, const float4* rx) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!trans) {
+        float* p = &sx[(lr + 32 * j) * F_LD + lk];
+        *reinterpret_cast<float2*>(p) = make_float2(rx[j].x, rx[j].y);
+        *reinterpret_cast<float2*>(p + 2) = make_float2(rx[j].z, rx[j].w);
+      } else {
+        const int k = tk + 8 * j;
+        sx[(tr + 0) * F_LD + k] = rx[j].x;
+        sx[(tr + 1) * F_LD + k] = rx[j].y;
+        sx[(tr + 2) * F_LD + k] = rx[j].z;
+        sx[(tr + 3) * F_LD + k] = rx[j].w;
       }
     }
   };
   auto store = [&](int b) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float* pa = &sA[b][(lr + 32 * j) * F_LD + lk];
-      float* pb = &sB[b][(lr + 32 * j) * F_LD + lk];
-      *reinterpret_cast<float2*>(pa) = make_float2(ra[j].x, ra[j].y);
-      *reinterpret_cast<float2*>(pa + 2) = make_float2(ra[j].z, ra[j].w);
-      *reinterpret_cast<float2*>(pb) = make_float2(rb[j].x, rb[j].y);
-      *reinterpret_cast<float2*>(pb + 2) = make_float2(rb[j].z, rb[j].w);
-    }
+    store_op(sA[b], AT, ra);
+    store_op(sB[b], BT, rb);
   };
 
   f32x4 acc[4][4];
@@ -140,33 +168,50 @@ struct F32Conv {
   int N, H, W, C, P, Q, R, S, sh, sw, ph, pw, dh, dw, Cg, coff;
 };
 
-// col[(n,p,q)][(r,s,c)] = x[n][p*sh-ph+r*dh][q*sw-pw+s*dw][coff+c] (0 outside the image)
+// col[(n,p,q)][(r,s,c)] = x[n][p*sh-ph+r*dh][q*sw-pw+s*dw][coff+c] (0 outside the image).
+// A col row is the taps' channel runs back to back, so consecutive lanes take consecutive
+// VW-channel chunks of it (float4 when the channel offsets allow): every wave-instruction
+// stores one contiguous 1 KB (256 B scalar) piece of col and reads contiguous runs of x.
+// IT = uint32_t decodes the index in 32 bits when the item count allows.
+template <int VW, typename IT>
 __global__ void im2col_f32_k(const float* __restrict__ x, float* __restrict__ col, F32Conv g) {
-  const int kred = g.R * g.S * g.Cg;
-  const long long total = (long long)g.N * g.P * g.Q * kred;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int k = (int)(i % kred);
-    const long long m = i / kred;
-    const int q = (int)(m % g.Q), p = (int)((m / g.Q) % g.P), n = (int)(m / ((long long)g.Q * g.P));
-    const int c = k % g.Cg, tap = k / g.Cg, s = tap % g.S, r = tap / g.S;
+  const int cq = g.Cg / VW, taps = g.R * g.S;
+  const IT items = (IT)g.N * g.P * g.Q * taps * cq;
+  for (IT i = blockIdx.x * (IT)blockDim.x + threadIdx.x; i < items; i += (IT)gridDim.x * blockDim.x) {
+    const IT t = i / cq;
+    const int c = (int)(i - t * cq) * VW;
+    const IT m = t / taps;
+    const int tap = (int)(t - m * taps);
+    const int pq = (int)(m % (IT)(g.P * g.Q)), n = (int)(m / (IT)(g.P * g.Q));
+    const int p = pq / g.Q, q = pq - p * g.Q, r = tap / g.S, s = tap - r * g.S;
     const int h = p * g.sh - g.ph + r * g.dh, w = q * g.sw - g.pw + s * g.dw;
-    col[i] = ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
-                 ? x[(((long long)n * g.H + h) * g.W + w) * g.C + g.coff + c]
-                 : 0.f;
+    const bool in = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+    const float* src = x + (((long long)n * g.H + (in ? h : 0)) * g.W + (in ? w : 0)) * g.C + g.coff + c;
+    float* dst = col + (long long)i * VW;
+    if constexpr (VW == 4)
+      *reinterpret_cast<float4*>(dst) = in ? *reinterpret_cast<const float4*>(src) : make_float4(0, 0, 0, 0);
+    else
+      *dst = in ? *src : 0.f;
   }
 }
 
-// dx[n][h][w][coff+c] (=|+=) sum over the (p, q, r, s) that read (h, w) of dcol[(n,p,q)][(r,s,c)]
+// dx[n][h][w][coff+c] (=|+=) sum over the (p, q, r, s) that read (h, w) of dcol[(n,p,q)][(r,s,c)]:
+// one thread per (input pixel, 4-channel chunk) gathers its taps in (r, s) order
+template <bool V4>
 __global__ void col2im_f32_k(const float* __restrict__ dcol, float* __restrict__ dx, F32Conv g, int accumulate) {
   const int kred = g.R * g.S * g.Cg;
-  const long long total = (long long)g.N * g.H * g.W * g.Cg;
+  constexpr int CW = V4 ? 4 : 1;
+  const int chunks = g.Cg / CW;
+  const long long total = (long long)g.N * g.H * g.W * chunks;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % g.Cg);
-    const long long pix = i / g.Cg;
-    const int w = (int)(pix % g.W), h = (int)((pix / g.W) % g.H), n = (int)(pix / ((long long)g.W * g.H));
-    float acc = 0.f;
+    const long long pix = i / chunks;
+    const int c = (int)(i - pix * chunks) * CW;
+    const int hw = (int)(pix % ((long long)g.H * g.W)), n = (int)(pix / ((long long)g.H * g.W));
+    const int h = hw / g.W, w = hw - h * g.W;
+    float acc[CW];
+#pragma unroll
+    for (int t = 0; t < CW; ++t) acc[t] = 0.f;
     for (int r = 0; r < g.R; ++r) {
       const int hh = h + g.ph - r * g.dh;
       if (hh < 0 || hh % g.sh) continue;
@@ -177,11 +222,21 @@ __global__ void col2im_f32_k(const float* __restrict__ dcol, float* __restrict__
         if (ww < 0 || ww % g.sw) continue;
         const int q = ww / g.sw;
         if (q >= g.Q) continue;
-        acc += dcol[(((long long)n * g.P + p) * g.Q + q) * kred + (r * g.S + s) * g.Cg + c];
+        const float* src = dcol + (((long long)n * g.P + p) * g.Q + q) * kred + (r * g.S + s) * g.Cg + c;
+        if constexpr (V4) {
+          const float4 v = *reinterpret_cast<const float4*>(src);
+          acc[0] += v.x;
+          acc[1] += v.y;
+          acc[2] += v.z;
+          acc[3] += v.w;
+        } else {
+          acc[0] += src[0];
+        }
       }
     }
     float* o = dx + pix * g.C + g.coff + c;
-    *o = accumulate ? *o + acc : acc;
+#pragma unroll
+    for (int t = 0; t < CW; ++t) o[t] = accumulate ? o[t] + acc[t] : acc[t];
   }
 }
 
@@ -216,6 +271,98 @@ __global__ void dropout_f32_k(const float* __restrict__ x, float* __restrict__ y
   }
 }
 
+// ---- pooling on NHWC fp32 (pooling_layer.cu semantics) ----
+struct F32Pool {
+  int N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw;
+};
+
+// MAX: the first maximum of the window clipped to the image, in row-major scan order (strict >,
+// from -FLT_MAX), and its flat index h * W + w (MaxPoolForward); AVE: the window sum over its
+// image part divided by the size of the window clipped to the padded image (AvePoolForward)
+template <bool MAX>
+__global__ void pool_f32_fwd(const float* __restrict__ x, float* __restrict__ y, int* __restrict__ mask, F32Pool g) {
+  const long long total = (long long)g.N * g.P * g.Q * g.C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    const long long pix = i / g.C;
+    const int q = (int)(pix % g.Q), p = (int)((pix / g.Q) % g.P), n = (int)(pix / ((long long)g.Q * g.P));
+    int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
+    int he = min(hs + g.kh, MAX ? g.H : g.H + g.ph), we = min(ws + g.kw, MAX ? g.W : g.W + g.pw);
+    const int pool_size = (he - hs) * (we - ws);
+    hs = max(hs, 0);
+    ws = max(ws, 0);
+    he = min(he, g.H);
+    we = min(we, g.W);
+    const float* xn = x + (long long)n * g.H * g.W * g.C + c;
+    if (MAX) {
+      float best = -3.402823466e+38f;
+      int arg = -1;
+      for (int h = hs; h < he; ++h)
+        for (int w = ws; w < we; ++w) {
+          const float v = xn[((long long)h * g.W + w) * g.C];
+          if (v > best) {
+            best = v;
+            arg = h * g.W + w;
+          }
+        }
+      y[i] = best;
+      mask[i] = arg;
+    } else {
+      float acc = 0.f;
+      for (int h = hs; h < he; ++h)
+        for (int w = ws; w < we; ++w) acc += xn[((long long)h * g.W + w) * g.C];
+      y[i] = acc / (float)pool_size;
+    }
+  }
+}
+
+// the gather adjoint: each input element sums, in window order, the output gradients of the
+// windows that selected it (MAX) or that cover it, divided by their sizes (AVE)
+template <bool MAX>
+__global__ void pool_f32_bwd(const float* __restrict__ dy, const int* __restrict__ mask, float* __restrict__ dx,
+                             F32Pool g) {
+  const long long total = (long long)g.N * g.H * g.W * g.C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    const long long pix = i / g.C;
+    const int w = (int)(pix % g.W), h = (int)((pix / g.W) % g.H), n = (int)(pix / ((long long)g.W * g.H));
+    const int hp = h + g.ph, wp = w + g.pw;
+    const int p0 = hp < g.kh ? 0 : (hp - g.kh) / g.sh + 1, p1 = min(hp / g.sh + 1, g.P);
+    const int q0 = wp < g.kw ? 0 : (wp - g.kw) / g.sw + 1, q1 = min(wp / g.sw + 1, g.Q);
+    const long long base = (long long)n * g.P * g.Q;
+    float acc = 0.f;
+    for (int p = p0; p < p1; ++p)
+      for (int q = q0; q < q1; ++q) {
+        const long long o = (base + (long long)p * g.Q + q) * g.C + c;
+        if (MAX) {
+          if (mask[o] == h * g.W + w) acc += dy[o];
+        } else {
+          const int hs = p * g.sh - g.ph, ws = q * g.sw - g.pw;
+          const int he = min(hs + g.kh, g.H + g.ph), we = min(ws + g.kw, g.W + g.pw);
+          acc += dy[o] / (float)((he - hs) * (we - ws));
+        }
+      }
+    dx[i] = acc;
+  }
+}
+
+// ReLU with negative slope (relu_layer.cu): y = x > 0 ? x : x * slope; dx = dy * (x > 0 ? 1 : slope),
+// the reference formulas' own operations, one pass each
+__global__ void relu_f32_fwd(const float* __restrict__ x, float* __restrict__ y, long long n, float slope) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    y[i] = v > 0.f ? v : v * slope;
+  }
+}
+
+__global__ void relu_f32_bwd(const float* __restrict__ dy, const float* __restrict__ x, float* __restrict__ dx,
+                             long long n, float slope) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dx[i] = dy[i] * (x[i] > 0.f ? 1.f : slope);
+}
+
 }  // namespace
 
 extern "C" int sn_dropout_f32(const float* x, float* y, long long n, const long long* rng, long long stream,
@@ -229,9 +376,10 @@ extern "C" int sn_dropout_f32(const float* x, float* y, long long n, const long 
 
 // splits > 1: C is [splits][M][ldc] fp32 slabs written plainly (no bias / ReLU / accumulate);
 // the host sums them in split order (deterministic).
+// trans: bit 0 = A stored [K][M], bit 1 = B stored [K][N] (lda / ldb are then the k-row strides)
 extern "C" int sn_gemm_f32(const float* A, long long lda, const float* B, long long ldb, float* C, long long ldc,
                            long long M, long long N, long long K, const float* bias, long long accumulate,
-                           long long relu, long long splits, long long kchunk, hipStream_t st) {
+                           long long relu, long long splits, long long kchunk, long long trans, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
   if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return 3;
   if (splits < 1 || (splits > 1 && (bias || accumulate || relu || kchunk % F_BK))) return 3;
@@ -239,7 +387,13 @@ extern "C" int sn_gemm_f32(const float* A, long long lda, const float* B, long l
   F32Args a{A, B, C, bias, lda, ldb, ldc, (int)M, (int)N, (int)K, (int)accumulate, (int)relu, (int)kchunk,
             M * ldc};
   const long long tiles = ((M + F_BM - 1) / F_BM) * ((N + F_BN - 1) / F_BN);
-  hipLaunchKernelGGL(gemm_f32_kernel, dim3((unsigned)tiles, (unsigned)splits), dim3(F_NT), 0, st, a);
+  const dim3 grid((unsigned)tiles, (unsigned)splits);
+  switch (trans & 3) {
+    case 0: hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(F_NT), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(F_NT), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(F_NT), 0, st, a); break;
+    default: hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(F_NT), 0, st, a); break;
+  }
   return SN_CHECK_LAUNCH();
 }
 
@@ -248,8 +402,15 @@ extern "C" int sn_im2col_f32(const float* x, float* col, long long N, long long 
                              long long ph, long long pw, long long dh, long long dw, long long Cg, long long coff,
                              hipStream_t st) {
   const F32Conv g = mkf32conv(N, H, W, C, P, Q, R, S, sh, sw, ph, pw, dh, dw, Cg, coff);
-  const long long total = N * P * Q * R * S * Cg;
-  hipLaunchKernelGGL(im2col_f32_k, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, x, col, g);
+  const bool v4 = Cg % 4 == 0 && coff % 4 == 0 && C % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(col) % 16 == 0;
+  const long long items = N * P * Q * R * S * (v4 ? Cg / 4 : Cg);
+  const dim3 grid(sn_blocks(items, 256, 16384));
+  const bool i32 = items < (1ll << 31) - 256ll * 16384;
+  if (v4 && i32) hipLaunchKernelGGL((im2col_f32_k<4, uint32_t>), grid, dim3(256), 0, st, x, col, g);
+  else if (v4) hipLaunchKernelGGL((im2col_f32_k<4, long long>), grid, dim3(256), 0, st, x, col, g);
+  else if (i32) hipLaunchKernelGGL((im2col_f32_k<1, uint32_t>), grid, dim3(256), 0, st, x, col, g);
+  else hipLaunchKernelGGL((im2col_f32_k<1, long long>), grid, dim3(256), 0, st, x, col, g);
   return SN_CHECK_LAUNCH();
 }
 
@@ -258,8 +419,44 @@ extern "C" int sn_col2im_f32(const float* dcol, float* dx, long long N, long lon
                              long long ph, long long pw, long long dh, long long dw, long long Cg, long long coff,
                              long long accumulate, hipStream_t st) {
   const F32Conv g = mkf32conv(N, H, W, C, P, Q, R, S, sh, sw, ph, pw, dh, dw, Cg, coff);
-  const long long total = N * H * W * Cg;
-  hipLaunchKernelGGL(col2im_f32_k, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, dcol, dx, g,
-                     (int)accumulate);
+  const bool v4 = Cg % 4 == 0 && coff % 4 == 0 && C % 4 == 0 && reinterpret_cast<uintptr_t>(dx) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dcol) % 16 == 0;
+  const long long total = N * H * W * (v4 ? Cg / 4 : Cg);
+  if (v4)
+    hipLaunchKernelGGL(col2im_f32_k<true>, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, dcol, dx, g,
+                       (int)accumulate);
+  else
+    hipLaunchKernelGGL(col2im_f32_k<false>, dim3(sn_blocks(total, 256, 16384)), dim3(256), 0, st, dcol, dx, g,
+                       (int)accumulate);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_pool_f32(const float* x, float* y, int* mask, long long N, long long H, long long W, long long C,
+                           long long P, long long Q, long long kh, long long kw, long long sh, long long sw,
+                           long long ph, long long pw, long long max_pool, hipStream_t st) {
+  const F32Pool g{(int)N, (int)H, (int)W, (int)C, (int)P, (int)Q, (int)kh, (int)kw, (int)sh, (int)sw, (int)ph, (int)pw};
+  const dim3 grid(sn_blocks(N * P * Q * C, 256, 16384));
+  if (max_pool) hipLaunchKernelGGL(pool_f32_fwd<true>, grid, dim3(256), 0, st, x, y, mask, g);
+  else hipLaunchKernelGGL(pool_f32_fwd<false>, grid, dim3(256), 0, st, x, y, mask, g);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_pool_f32_bwd(const float* dy, const int* mask, float* dx, long long N, long long H, long long W,
+                               long long C, long long P, long long Q, long long kh, long long kw, long long sh,
+                               long long sw, long long ph, long long pw, long long max_pool, hipStream_t st) {
+  const F32Pool g{(int)N, (int)H, (int)W, (int)C, (int)P, (int)Q, (int)kh, (int)kw, (int)sh, (int)sw, (int)ph, (int)pw};
+  const dim3 grid(sn_blocks(N * H * W * C, 256, 16384));
+  if (max_pool) hipLaunchKernelGGL(pool_f32_bwd<true>, grid, dim3(256), 0, st, dy, mask, dx, g);
+  else hipLaunchKernelGGL(pool_f32_bwd<false>, grid, dim3(256), 0, st, dy, mask, dx, g);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_relu_f32(const float* x, float* y, long long n, float slope, hipStream_t st) {
+  hipLaunchKernelGGL(relu_f32_fwd, dim3(sn_blocks(n, 256, 16384)), dim3(256), 0, st, x, y, n, slope);
+  return SN_CHECK_LAUNCH();
+}
+
+extern "C" int sn_relu_f32_bwd(const float* dy, const float* x, float* dx, long long n, float slope, hipStream_t st) {
+  hipLaunchKernelGGL(relu_f32_bwd, dim3(sn_blocks(n, 256, 16384)), dim3(256), 0, st, dy, x, dx, n, slope);
   return SN_CHECK_LAUNCH();
 }

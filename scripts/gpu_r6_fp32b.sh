@@ -1,0 +1,8 @@
+# round 6: fp32 device mode after in-place k-major operands and run-wise im2col / col2im
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_fp32_device_gpu.py > gpurun_out/fp32b_tests.log 2>&1 || { tail -30 gpurun_out/fp32b_tests.log; exit 1; }
+tail -2 gpurun_out/fp32b_tests.log
+timeout -k 10 300 python bench.py --dtype fp32 --steps 10 --warmup 2 > gpurun_out/fp32b_bench.json 2> gpurun_out/fp32b_bench.err || { tail gpurun_out/fp32b_bench.err; exit 1; }
+cut -c1-200 gpurun_out/fp32b_bench.json
+bash scripts/gpu_r6_fp32prof.sh

@@ -88,6 +88,9 @@ def pool_backward(dy, x, s, aux=None, y=None, gate=False):
     pooling on the GPU encodes it in the forward's argmax mask)."""
     if _gpu(dy):
         return _hipmod().pool_backward(dy, x, s, aux, y, gate)
+    if dy.is_cuda:  # fp32 device mode
+        from . import f32dev
+        return f32dev.pool_backward(dy, x, s, aux, y, gate)
     return ref.pool_backward(dy, x, s, gate)
 
 
@@ -95,6 +98,9 @@ def pool_forward_aux(x, s, gate=False):
     """Forward returning (y, aux) where aux is the GPU argmax mask (None on CPU)."""
     if _gpu(x):
         return _hipmod().pool_forward_mask(x, s, gate)
+    if x.is_cuda:  # fp32 device mode
+        from . import f32dev
+        return f32dev.pool_forward_aux(x, s, gate)
     return ref.pool_forward(x, s), None
 
 

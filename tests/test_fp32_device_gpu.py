@@ -46,6 +46,28 @@ def test_gemm_f32_matches_fp64(gpu, M, N, K, epi):
     assert err <= 4e-7 * scale + 1e-6, (err, scale)
 
 
+@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (300, 200, 77), (6, 1003, 5001), (96, 363, 20000), (130, 9, 3)])
+@pytest.mark.parametrize("a_t,b_t", [(True, False), (False, True), (True, True)])
+def test_gemm_f32_kmajor_operands(gpu, M, N, K, a_t, b_t):
+    """Operands stored k-major ([K][M] / [K][N]) are read in place, with row strides wider than
+    the rows (a channel slice of a wider tensor), through the plain and the split-K paths."""
+    from sparknet_amd.ops import f32dev
+    g = torch.Generator(device="cpu").manual_seed(M + 3 * N + K)
+    a_full = torch.randn(K, M + 5, generator=g) if a_t else torch.randn(M, K + 5, generator=g)
+    b_full = torch.randn(K, N + 4, generator=g) if b_t else torch.randn(N, K + 4, generator=g)
+    ag, bg = a_full.to(gpu), b_full.to(gpu)
+    a = ag[:, 1:M + 1] if a_t else ag[:, 1:K + 1]
+    b = bg[:, 4:N + 4] if b_t else bg[:, 4:K + 4]
+    am = (a.t() if a_t else a).double().cpu()
+    bm = (b.t() if b_t else b).double().cpu()
+    out = torch.empty(M, N, device=gpu)
+    f32dev.gemm(a, b, out, M, N, K, a_t=a_t, b_t=b_t)
+    ref = am @ bm.t()
+    err = (out.double().cpu() - ref).abs().max().item()
+    scale = (am.abs() @ bm.abs().t()).max().item()
+    assert err <= 4e-7 * scale + 1e-6, (err, scale)
+
+
 @pytest.mark.parametrize("case", [(2, 13, 13, 16, 24, 3, 3, 1, 1, 1, 1), (2, 27, 27, 8, 16, 5, 5, 1, 2, 2, 1),
                                   (3, 23, 23, 3, 8, 11, 11, 4, 0, 1, 1), (2, 9, 9, 8, 8, 3, 3, 2, 2, 1, 2)])
 def test_conv_f32_matches_cpu_engine(gpu, case):
@@ -104,3 +126,37 @@ def test_caffenet_fp32_one_step_matches_cpu_engine(gpu):
             bad[k] = (emax, el2)
     print("fp32 device vs fp32 CPU engine (max, L2):", {k: (round(a, 6), round(b, 6)) for k, (a, b) in errs.items()})
     assert not bad, bad
+
+
+@pytest.mark.parametrize("case", [(2, 55, 55, 16, 3, 3, 2, 2, 0, 0), (2, 13, 15, 8, 3, 3, 2, 2, 1, 1),
+                                  (3, 14, 14, 12, 3, 3, 1, 1, 1, 1), (2, 7, 7, 8, 7, 7, 1, 1, 0, 0),
+                                  (2, 9, 9, 4, 2, 2, 2, 2, 0, 0)])
+@pytest.mark.parametrize("method", ["max", "ave"])
+def test_pool_f32_matches_reference(gpu, case, method):
+    """fp32 pooling kernels (pooling_layer.cu semantics: clipped windows, ceil-mode outputs,
+    AVE divisor over the padded window) against the fp32 reference formulas, both passes."""
+    from sparknet_amd.ops import f32dev, ref
+    from sparknet_amd.ops.spec import POOL_AVE, POOL_MAX, PoolSpec
+    N, H, W, C, kh, kw, sh, sw, ph, pw = case
+    s = PoolSpec(N, H, W, C, kh, kw, sh, sw, ph, pw, POOL_MAX if method == "max" else POOL_AVE)
+    g = torch.Generator().manual_seed(H * 31 + C)
+    x = torch.randn(N, H, W, C, generator=g)
+    y, mask = f32dev.pool_forward_aux(x.to(gpu), s)
+    yr = ref.pool_forward(x, s)
+    assert torch.allclose(y.cpu(), yr, rtol=1e-6, atol=1e-6)
+    dy = torch.randn(N, s.P, s.Q, C, generator=g)
+    dx = f32dev.pool_backward(dy.to(gpu), x.to(gpu), s, mask)
+    dxr = ref.pool_backward(dy, x, s)
+    assert torch.allclose(dx.cpu(), dxr, rtol=1e-5, atol=1e-5)
+
+
+
+@pytest.mark.parametrize("slope", [0.0, 0.1])
+def test_relu_f32_bitwise_reference(gpu, slope):
+    from sparknet_amd.ops import f32dev, ref
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, 7, 9, 16, generator=g)
+    x[0, 0, 0, :4] = 0.0
+    dy = torch.randn(3, 7, 9, 16, generator=g)
+    assert torch.equal(f32dev.relu_forward(x.to(gpu), slope).cpu(), ref.relu_forward(x, slope))
+    assert torch.equal(f32dev.relu_backward(dy.to(gpu), x.to(gpu), slope).cpu(), ref.relu_backward(dy, x, slope))
