@@ -36,7 +36,7 @@ def timed(fn, reps=20, passes=5):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tiles", default="0,1,2,3,4,5,10,12,13,16,17,18,19,20,23,24,26,27")
+    ap.add_argument("--tiles", default="0,1,2,3,4,5,10,12,13,16,17,18,19,20,21,22")
     ap.add_argument("--splits", default="1,2,3,4,6,8,12,16")
     args = ap.parse_args()
     from sparknet_amd.ops import gemm as G

@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 CASES = {  # N, H, W, C(per group), K(per group), R, S, stride, pad
+    "conv1f": (256, 57, 57, 48, 96, 3, 3, 1, 0),  # CaffeNet conv1 after the 4x4 space-to-depth fold
     "conv2": (256, 27, 27, 48, 128, 5, 5, 1, 2),
     "conv3": (256, 13, 13, 256, 384, 3, 3, 1, 1),
     "conv4": (256, 13, 13, 192, 192, 3, 3, 1, 1),
