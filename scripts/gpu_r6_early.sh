@@ -1,4 +1,4 @@
-# round 6: fragment reads issued before the next stage's LDS-DMA (EARLY_FRAGS) — numerics, probes, benches
+# round 6: gemm_kernel A/B (numerics, conv probe, benches)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gemm_gpu.py tests/test_bench_fidelity_gpu.py > gpurun_out/early_tests.log 2>&1 || { tail -30 gpurun_out/early_tests.log; exit 1; }
