@@ -5,4 +5,4 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/r6d_plrn_tests.log
 timeout -k 10 200 python -u scripts/plrn_probe.py > gpurun_out/r6d_plrn_probe.txt 2>&1 || { cat gpurun_out/r6d_plrn_probe.txt; exit 1; }
 grep -v amdgpu.ids gpurun_out/r6d_plrn_probe.txt
-bash scripts/gpu_r6_fp8.sh
+bash scripts/archive/gpu_r6_fp8.sh

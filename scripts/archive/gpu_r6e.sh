@@ -5,4 +5,4 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/fp32chk_tests.log
 timeout -k 10 300 python bench.py --dtype fp32 --steps 10 --warmup 2 > gpurun_out/fp32chk_bench.json 2> gpurun_out/fp32chk_bench.err || { tail gpurun_out/fp32chk_bench.err; exit 1; }
 cut -c1-200 gpurun_out/fp32chk_bench.json
-bash scripts/gpu_r6d.sh
+bash scripts/archive/gpu_r6d.sh
