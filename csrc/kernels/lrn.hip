@@ -26,6 +26,12 @@ struct LrnP {
 
 SN_DEV float powneg(float s, float beta) { return sn_powneg(s, beta); }
 
+// The across-channel kernels (here and in pool_lrn.hip) spell out every multiply-add that
+// -ffp-contract=fast could otherwise fuse or not depending on how a loop is unrolled: the
+// square sums and the scale are explicit fmas, and the products the backward sums are
+// rounded on their own (an fma with a zero addend, which the adds cannot absorb).  A rolled
+// square sum had compiled to v_fma_f32 and the unrolled one in the fused LRN -> pool
+// backward to v_pk_mul_f32 + v_add_f32: the fused and unfused paths differed by one ulp.
 // Load the 24 channels [c0-8, c0+16) of a pixel as fp32 (zeros outside [0, C)).  The
 // three 16-B loads are unconditional (clamped chunk index) and masked afterwards, so
 // they are all in flight together.
@@ -66,9 +72,9 @@ __global__ void lrn_across_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict_
 #pragma unroll
       for (int d = 0; d < SIZE; ++d) {
         float e = v[8 + t - PRE + d];
-        s += e * e;
+        s = __builtin_fmaf(e, e, s);
       }
-      float sc = p.k + a * s;
+      float sc = __builtin_fmaf(a, s, p.k);
       o[t] = v[8 + t] * powneg(sc, p.beta);
     }
     *reinterpret_cast<uint4*>(y + (long long)pix * p.C + c0) = pack8(o);
@@ -99,11 +105,11 @@ __global__ void lrn_across_bwd(const bf16_t* __restrict__ x, const bf16_t* __res
 #pragma unroll
       for (int d = 0; d < SIZE; ++d) {
         float e = xv[j - PRE + d];
-        s += e * e;
+        s = __builtin_fmaf(e, e, s);
       }
-      float sc = p.k + a * s;
+      float sc = __builtin_fmaf(a, s, p.k);
       // channels outside [0, C) have x = dy = 0 (load24), so r is 0 there without a branch
-      r[j] = gv[j] * xv[j] * powneg(sc, p.beta + 1.f);
+      r[j] = __builtin_fmaf(gv[j] * xv[j], powneg(sc, p.beta + 1.f), 0.f);
       if (j >= 8 && j < 16) gv[j] = gv[j] * powneg(sc, p.beta);  // reuse: dy * scale^-beta
     }
     float o[8];
@@ -113,7 +119,7 @@ __global__ void lrn_across_bwd(const bf16_t* __restrict__ x, const bf16_t* __res
       // windows that contain channel c = c0+t start at c' - pre <= c <= c' + post
 #pragma unroll
       for (int d = -PRE; d <= POST; ++d) acc += r[8 + t - d];
-      o[t] = gv[8 + t] - cache_ratio * xv[8 + t] * acc;
+      o[t] = __builtin_fmaf(-(cache_ratio * xv[8 + t]), acc, gv[8 + t]);
       if (p.gate && !(xv[8 + t] > 0.f)) o[t] = 0.f;
     }
     *reinterpret_cast<uint4*>(dx + base + c0) = pack8(o);
@@ -131,9 +137,9 @@ __global__ void lrn_across_fwd_scalar(const bf16_t* __restrict__ x, bf16_t* __re
       float s = 0.f;
       for (int d = 0; d < p.size; ++d) {
         int cc = c - p.pre + d;
-        if (cc >= 0 && cc < p.C) { float e = bf2f(row[cc]); s += e * e; }
+        if (cc >= 0 && cc < p.C) { float e = bf2f(row[cc]); s = __builtin_fmaf(e, e, s); }
       }
-      y[i * p.C + c] = f2bf(bf2f(row[c]) * powneg(p.k + a * s, p.beta));
+      y[i * p.C + c] = f2bf(bf2f(row[c]) * powneg(__builtin_fmaf(a, s, p.k), p.beta));
     }
   }
 }
@@ -155,13 +161,13 @@ __global__ void lrn_across_bwd_scalar(const bf16_t* __restrict__ x, const bf16_t
         float s = 0.f;
         for (int d = 0; d < p.size; ++d) {
           int cc = cp - p.pre + d;
-          if (cc >= 0 && cc < p.C) { float e = bf2f(xr[cc]); s += e * e; }
+          if (cc >= 0 && cc < p.C) { float e = bf2f(xr[cc]); s = __builtin_fmaf(e, e, s); }
         }
-        float sc = p.k + a * s;
-        acc += bf2f(gr[cp]) * bf2f(xr[cp]) * powneg(sc, p.beta + 1.f);
+        float sc = __builtin_fmaf(a, s, p.k);
+        acc += __builtin_fmaf(bf2f(gr[cp]) * bf2f(xr[cp]), powneg(sc, p.beta + 1.f), 0.f);
         if (cp == c) own = bf2f(gr[c]) * powneg(sc, p.beta);
       }
-      const float v = own - cache_ratio * bf2f(xr[c]) * acc;
+      const float v = __builtin_fmaf(-(cache_ratio * bf2f(xr[c])), acc, own);
       dx[i * p.C + c] = f2bf(p.gate && !(bf2f(xr[c]) > 0.f) ? 0.f : v);
     }
   }

@@ -31,7 +31,7 @@ struct PLGeom {
   int cg, ngrp;     // backward: channel chunks per workgroup, channel groups
   int size;
   float alpha, beta, k;
-  FDiv fcv, fQ, fP, fcg, fQcg, fBWcg;
+  FDiv fcv, fQ, fP, fcg, fQcg, fBWcg, fBW, fBH;
 };
 
 SN_DEV float plrn_pow(float s, float beta) { return sn_powneg(s, beta); }
@@ -111,9 +111,9 @@ __global__ void __launch_bounds__(256) pool_lrn_fwd(const bf16_t* __restrict__ x
 #pragma unroll
       for (int d = 0; d < SIZE; ++d) {
         float e = v[8 + t - PRE + d];
-        s += e * e;
+        s = __builtin_fmaf(e, e, s);
       }
-      float sc = g.k + a * s;
+      float sc = __builtin_fmaf(a, s, g.k);
       o[t] = v[8 + t] * plrn_pow(sc, g.beta);
     }
     *reinterpret_cast<uint4*>(y + (pix0 + lp) * g.C + ch * 8) = pack8(o);
@@ -169,11 +169,11 @@ SN_DEV void plrn_bwd_phase1(const bf16_t* __restrict__ xp, const bf16_t* __restr
 #pragma unroll
       for (int d = 0; d < SIZE; ++d) {
         float e = xv[j - PRE + d];
-        s += e * e;
+        s = __builtin_fmaf(e, e, s);
       }
-      float sc = g.k + a * s;
+      float sc = __builtin_fmaf(a, s, g.k);
       // channels outside [0, C) have x = dy = 0 (plrn_load24): rr is 0 there without a branch
-      rr[j] = gv[j] * xv[j] * plrn_pow(sc, g.beta + 1.f);
+      rr[j] = __builtin_fmaf(gv[j] * xv[j], plrn_pow(sc, g.beta + 1.f), 0.f);
       if (j >= 8 && j < 16) gv[j] = gv[j] * plrn_pow(sc, g.beta);
     }
     float o[8];
@@ -182,7 +182,7 @@ SN_DEV void plrn_bwd_phase1(const bf16_t* __restrict__ xp, const bf16_t* __restr
       float acc = 0.f;
 #pragma unroll
       for (int d = -PRE; d <= POST; ++d) acc += rr[8 + t - d];
-      o[t] = gv[8 + t] - cache_ratio * xv[8 + t] * acc;
+      o[t] = __builtin_fmaf(-(cache_ratio * xv[8 + t]), acc, gv[8 + t]);
     }
     tile[it] = pack8(o);
   }
@@ -255,6 +255,120 @@ __global__ void __launch_bounds__(256) lrn_pool_bwd(const bf16_t* __restrict__ x
         }
         *reinterpret_cast<uint4*>(dx + (((long long)n * g.H + h) * g.W + w) * g.C + c0) = pack8(acc);
       }
+  }
+}
+
+// The other order — a cross-channel LRN whose output feeds a 3x3 / stride-2 max pooling
+// (AlexNet's norm1 -> pool1 and norm2 -> pool2, GoogLeNet's conv2/norm2 -> pool2) — fused in
+// BACKWARD only.  A workgroup owns a run of g.pix 2x2 input blocks (linear over image, block
+// row, block column) with ALL their channels:
+//   phase 1: one item per (block, 8-channel chunk) gathers the pooling gradient of the block's
+//            4 pixels from the 4 windows covering it (pool_bwd_k3s2's order), rounded to bf16
+//            as that kernel stores it, into LDS;
+//   phase 2: one item per (pixel, chunk) runs the LRN backward (lrn_across_bwd's arithmetic,
+//            with the fused ReLU gate), its neighbour channels read from the LDS tile.
+// The LRN-output gradient (the full-resolution tensor the unfused pair writes and re-reads)
+// never reaches HBM; the result is bitwise equal to the two launches.  (The forward stays two
+// launches: the LRN of a 3x3 window's 9 pixels would be recomputed by up to 4 windows.)
+template <int SIZE>
+__global__ void __launch_bounds__(256) pool_lrn_bwd_rev(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                        const bf16_t* __restrict__ x, bf16_t* __restrict__ dx,
+                                                        PLGeom g) {
+  extern __shared__ uint4 tile[];  // g.pix blocks x 4 pixels x cv chunks of the pooling gradient
+  constexpr int PRE = (SIZE - 1) / 2, POST = SIZE - PRE - 1;
+  const int cv = g.C >> 3;
+  const long long nblk = (long long)g.N * g.BH * g.BW;
+  const long long blk0 = (long long)xcd_block(blockIdx.x, gridDim.x) * g.pix;
+  const int nb = (int)min((long long)g.pix, nblk - blk0);
+  // phase 1: pooling backward of the run's blocks into LDS
+  const int items1 = nb * cv;
+  for (int it = threadIdx.x; it < items1; it += blockDim.x) {
+    const uint32_t lb = udiv((uint32_t)it, g.fcv);
+    const int ch = it - (int)lb * cv, c0 = ch * 8;
+    const uint32_t blk = (uint32_t)(blk0 + lb), bh_ = udiv(blk, g.fBW), n = udiv(bh_, g.fBH);
+    const int bw = (int)(blk - bh_ * g.BW), bh = (int)(bh_ - n * g.BH);
+    uint4 dv[4];
+    uint2 mv[4];
+    bool ok[4];
+#pragma unroll
+    for (int wa = 0; wa < 2; ++wa)
+#pragma unroll
+      for (int wb = 0; wb < 2; ++wb) {
+        const int p = bh - 1 + wa, q = bw - 1 + wb, t = wa * 2 + wb;
+        ok[t] = p >= 0 && p < g.P && q >= 0 && q < g.Q;
+        const int pc = min(max(p, 0), g.P - 1), qc = min(max(q, 0), g.Q - 1);
+        const long long o = (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0;
+        dv[t] = *reinterpret_cast<const uint4*>(dy + o);
+        mv[t] = *reinterpret_cast<const uint2*>(mask + o);
+      }
+    float f[4][8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) unpack8(dv[t], f[t]);
+#pragma unroll
+    for (int ia = 0; ia < 2; ++ia)
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) {
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int wa = t >> 1, wb = t & 1;
+          if ((wa == 0 && ia == 1) || (wb == 0 && ib == 1)) continue;
+          const int widx = (ia + 2 * (1 - wa)) * 3 + (ib + 2 * (1 - wb));
+          const uint32_t mw[2] = {mv[t].x, mv[t].y};
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+            if (ok[t] && (int)((mw[kk >> 2] >> ((kk & 3) * 8)) & 0xff) == widx) acc[kk] += f[t][kk];
+        }
+        tile[((int)lb * 4 + ia * 2 + ib) * cv + ch] = pack8(acc);
+      }
+  }
+  __syncthreads();
+  // phase 2: LRN backward of the run's pixels
+  const float a = g.alpha / g.size;
+  const float cache_ratio = 2.f * g.alpha * g.beta / g.size;
+  const int items2 = 4 * nb * cv;
+  for (int it = threadIdx.x; it < items2; it += blockDim.x) {
+    const uint32_t lp = udiv((uint32_t)it, g.fcv);
+    const int ch = it - (int)lp * cv, c0 = ch * 8;
+    const uint32_t lb = lp >> 2, sub = lp & 3;
+    const uint32_t blk = (uint32_t)(blk0 + lb), bh_ = udiv(blk, g.fBW), n = udiv(bh_, g.fBH);
+    const int bw = (int)(blk - bh_ * g.BW), bh = (int)(bh_ - n * g.BH);
+    const int h = 2 * bh + (int)(sub >> 1) - g.ph, w = 2 * bw + (int)(sub & 1) - g.pw;
+    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
+    const long long base = (((long long)n * g.H + h) * g.W + w) * g.C;
+    float xv[24], gv[24];
+    plrn_load24(x + base, c0, g.C, xv);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int c = ch - 1 + j;
+      const bool cok = c >= 0 && c < cv;
+      unpack8(tile[(int)lp * cv + min(max(c, 0), cv - 1)], gv + 8 * j);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) gv[8 * j + t] = cok ? gv[8 * j + t] : 0.f;
+    }
+    float rr[24];
+#pragma unroll
+    for (int j = 8 - POST; j < 16 + PRE; ++j) {
+      float s2 = 0.f;
+#pragma unroll
+      for (int d = 0; d < SIZE; ++d) {
+        float ev = xv[j - PRE + d];
+        s2 = __builtin_fmaf(ev, ev, s2);
+      }
+      float sc = __builtin_fmaf(a, s2, g.k);
+      rr[j] = __builtin_fmaf(gv[j] * xv[j], plrn_pow(sc, g.beta + 1.f), 0.f);
+      if (j >= 8 && j < 16) gv[j] = gv[j] * plrn_pow(sc, g.beta);
+    }
+    float o[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float acc = 0.f;
+#pragma unroll
+      for (int d = -PRE; d <= POST; ++d) acc += rr[8 + t - d];
+      o[t] = __builtin_fmaf(-(cache_ratio * xv[8 + t]), acc, gv[8 + t]);
+      if (g.gate && !(xv[8 + t] > 0.f)) o[t] = 0.f;
+    }
+    *reinterpret_cast<uint4*>(dx + base + c0) = pack8(o);
   }
 }
 
@@ -379,5 +493,39 @@ extern "C" int sn_lrn_pool_bwd(const bf16_t* xp, const bf16_t* dyn, const uint8_
     default: SN_PLRN_BWD(9); break;
   }
 #undef SN_PLRN_BWD
+  return SN_CHECK_LAUNCH();
+}
+
+// LRN -> 3x3 / stride-2 max pooling, backward (pool_lrn_bwd_rev): dx at the LRN input from
+// the pooled gradient dy and the argmax mask (pool_forward_mask's format), with the gate of
+// the in-place ReLU that produced x when `gate` is set
+extern "C" int sn_pool_lrn_bwd_rev(const bf16_t* dy, const uint8_t* mask, const bf16_t* x, bf16_t* dx, long long N,
+                                   long long H, long long W, long long C, long long P, long long Q, long long ph,
+                                   long long pw, long long size, float alpha, float beta, float k, long long gate,
+                                   hipStream_t st) {
+  if (!plrn_ok(N, H, W, C, P, Q, ph, pw, size)) return 4;
+  PLGeom g = plgeom(N, H, W, C, P, Q, ph, pw, size, alpha, beta, k);
+  g.gate = (int)gate;
+  g.BH = (int)((H + ph + 1) / 2);
+  g.BW = (int)((W + pw + 1) / 2);
+  if (g.BH > P + 1 || g.BW > Q + 1) return 4;
+  g.fBW = make_fdiv((uint32_t)g.BW);
+  g.fBH = make_fdiv((uint32_t)g.BH);
+  // blocks per workgroup: about 256 phase-1 items (one per thread) and 1024 phase-2 items.
+  // Isolated at AlexNet b256 / GoogLeNet b128 (scripts/plrn_rev_probe.py, profiles/r6_lrn_pool_rev.txt):
+  // 128 / 256 / 512 / 1024 items -> norm1 152.5 / 141.4 / 139.0 / 181.2 us, norm2 84.4 / 77.0 /
+  // 83.5 / 106.9, GoogLeNet conv2/norm2 139.8 / 119.2 / 129.5 / 177.8 (unfused 150.1 / 89.3 / 141.1)
+  g.pix = (int)max(1LL, 256 / (C / 8));
+  const long long nblk = N * g.BH * g.BW;
+  if (nblk >= (1ll << 31) || 4 * nblk * (C / 8) >= (1ll << 32)) return 4;
+  const dim3 grid((unsigned)((nblk + g.pix - 1) / g.pix));
+  const size_t lds = (size_t)g.pix * 4 * (C / 8) * sizeof(uint4);
+  if (lds > 64 * 1024) return 4;
+  switch (size) {
+    case 3: hipLaunchKernelGGL(pool_lrn_bwd_rev<3>, grid, dim3(256), lds, st, dy, mask, x, dx, g); break;
+    case 5: hipLaunchKernelGGL(pool_lrn_bwd_rev<5>, grid, dim3(256), lds, st, dy, mask, x, dx, g); break;
+    case 7: hipLaunchKernelGGL(pool_lrn_bwd_rev<7>, grid, dim3(256), lds, st, dy, mask, x, dx, g); break;
+    default: hipLaunchKernelGGL(pool_lrn_bwd_rev<9>, grid, dim3(256), lds, st, dy, mask, x, dx, g); break;
+  }
   return SN_CHECK_LAUNCH();
 }

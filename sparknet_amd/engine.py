@@ -56,6 +56,7 @@ def fuse_relu(net) -> int:
     fuse_dropout(net)
     fuse_concat(net)
     fuse_pool_lrn(net)
+    fuse_lrn_pool_backward(net)
     batch_weight_flips(net)
     return n
 
@@ -92,6 +93,51 @@ def fuse_pool_lrn(net) -> int:
         lrn.pool_fused = True
         lrn.top = net.top_vecs[lj][0]
         pool.fused_lrn = lrn
+        n += 1
+    return n
+
+
+def fuse_lrn_pool_backward(net) -> int:
+    """The other order: a cross-channel LRN whose output only a 3x3 / stride-2 max pooling
+    reads (AlexNet's norm1 -> pool1 and norm2 -> pool2, GoogLeNet's conv2/norm2 -> pool2).
+    Backward only: the pooling layer's backward computes the LRN INPUT gradient in one launch
+    (csrc/kernels/pool_lrn.hip: pool_lrn_bwd_rev, bitwise equal to the two kernels) and the
+    LRN layer's backward is skipped.  Caffe runs the two backwards as separate passes
+    (pooling_layer.cu:217-260, lrn_layer.cu:121-177).  The forward stays two launches.
+    Returns the count."""
+    from .ops import hip
+    if net.device.type != "cuda" or net.debug_info or not features.enabled("fuse_lrn_pool_bwd"):
+        return 0
+    outputs = set(getattr(net, "output_blob_ids", ()))
+    n = 0
+    for lj, lrn in enumerate(net.layers):
+        if lrn.type_name != "LRN" or lrn.pool_fused or lrn.within or len(net.top_ids[lj]) != 1:
+            continue
+        blob = net.top_ids[lj][0]
+        if blob in outputs or blob == net.bottom_ids[lj][0]:
+            continue
+        readers = [li for li in range(lj + 1, len(net.layers)) if blob in net.bottom_ids[li]]
+        if len(readers) != 1:
+            continue
+        li = readers[0]
+        pool = net.layers[li]
+        if (pool.type_name != "Pooling" or len(net.top_ids[li]) != 1 or pool.global_pooling
+                or pool.fused_lrn is not None or pool.relu_gate or net.top_ids[li][0] == blob):
+            continue
+        if not (net.layer_need_backward[li] and net.layer_need_backward[lj] and net.bottom_need_backward[li][0]
+                and net.bottom_need_backward[lj][0]):
+            continue
+        s = pool.spec(net.bottom_vecs[li][0])
+        if not hip.pool_lrn_rev_eligible(s, lrn.size, lrn.within):
+            continue
+        pool.bwd_lrn = lrn
+        lrn.bottom = net.bottom_vecs[lj][0]
+        # BranchStreams: the pooling backward now reads the LRN input and writes its gradient
+        bid = net.bottom_ids[lj][0]
+        ex = dict(getattr(pool, "sched_extra", None) or {})
+        ex["bwd_r"] = set(ex.get("bwd_r", ())) | {("v", bid)}
+        ex["bwd_w"] = set(ex.get("bwd_w", ())) | {("d", bid)}
+        pool.sched_extra = ex
         n += 1
     return n
 

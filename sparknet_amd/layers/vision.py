@@ -512,6 +512,7 @@ class PoolingLayer(Layer):
 
     relu_gate = False  # backward of the slope-0 in-place ReLU producing the bottom is fused here
     fused_lrn = None   # the LRN reading this layer's output, run inside its kernels (engine.fuse_pool_lrn)
+    bwd_lrn = None     # the LRN producing this layer's input: backward run here (engine.fuse_lrn_pool_backward)
     # engine.fuse_fp8_quant: (consumer conv, its x slot) / (producer conv, its dy slot) — the
     # pooling kernels also store the consumer's e4m3 input / the producer's fp8 output gradient
     fp8_out = None
@@ -605,6 +606,13 @@ class PoolingLayer(Layer):
             bottoms[0].diff = hip.lrn_pool_backward(f.top.diff, tops[0].data, self.aux, s, f.size, f.alpha, f.beta,
                                                     f.k)
             return
+        f = self.bwd_lrn
+        if f is not None and self.aux is not None and self.fp8_dx_out is None and bottoms[0].data.is_cuda:
+            from ..ops import hip
+            f.bottom.diff = hip.pool_lrn_backward_rev(tops[0].diff, self.aux, f.bottom.data, s, f.size, f.alpha,
+                                                      f.beta, f.k, f.relu_gate)
+            f.bwd_done = True
+            return
         side = (self._fp8_side(self.fp8_dx_out, (s.N, s.H, s.W, s.C), "bwd", bottoms[0].data.device)
                 if bottoms[0].data.is_cuda else None)
         if side is not None:
@@ -648,8 +656,13 @@ class LRNLayer(Layer):
     relu_gate = False  # engine.fuse_relu_backward: the in-place ReLU producing the bottom
     pool_fused = False  # forward and backward run inside the preceding max pooling's kernels
     top = None          # this layer's top Blob (set with pool_fused)
+    bottom = None       # this layer's bottom Blob (engine.fuse_lrn_pool_backward)
+    bwd_done = False    # this step's backward already run by the max pooling after it
 
     def backward(self, tops, propagate_down, bottoms):
+        if self.bwd_done:
+            self.bwd_done = False
+            return
         if not propagate_down[0] or (self.pool_fused and bottoms[0].data.is_cuda):
             return
         x = bottoms[0].data

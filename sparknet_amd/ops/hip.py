@@ -903,6 +903,33 @@ def lrn_pool_backward(dy, pooled, mask, s: PoolSpec, size: int, alpha: float, be
     return dx
 
 
+def pool_lrn_rev_eligible(s: PoolSpec, size: int, within: bool) -> bool:
+    """A cross-channel LRN feeding a 3x3 / stride-2 max pooling whose backwards
+    sn_pool_lrn_bwd_rev runs as one launch (csrc/kernels/pool_lrn.hip: plrn_ok and the
+    2x2-block row coverage, mirrored here)."""
+    if s.method != POOL_MAX or within or (s.kh, s.kw, s.sh, s.sw) != (3, 3, 2, 2) or s.C % 8 or size not in (3, 5, 7, 9):
+        return False
+    if s.ph >= 3 or s.pw >= 3 or s.N * s.H * s.W * s.C >= 1 << 32 or s.C > 8192:
+        return False
+    if 2 * (s.P - 1) - s.ph >= s.H or 2 * (s.Q - 1) - s.pw >= s.W:
+        return False
+    return (s.H + s.ph + 1) // 2 <= s.P + 1 and (s.W + s.pw + 1) // 2 <= s.Q + 1
+
+
+def pool_lrn_backward_rev(dy, mask, x, s: PoolSpec, size: int, alpha: float, beta: float, k: float,
+                          gate: bool = False):
+    """Gradient at an LRN's input from the gradient at the output of the max pooling that
+    reads the LRN's output (pool_bwd_k3s2 then lrn_across_bwd in one launch; the LRN-output
+    gradient lives only in registers).  x: the LRN input; gate: the in-place ReLU that
+    produced x."""
+    x = _c(x)
+    assert tuple(x.shape) == (s.N, s.H, s.W, s.C) and tuple(mask.shape) == (s.N, s.P, s.Q, s.C)
+    dx = torch.empty_like(x)
+    call("pool_lrn_bwd_rev", _c(dy), _c(mask), x, dx, s.N, s.H, s.W, s.C, s.P, s.Q, s.ph, s.pw, int(size),
+         float(alpha), float(beta), float(k), int(gate))
+    return dx
+
+
 def lrn_forward(x, size, alpha, beta, k, within=False):
     x = _c(x)
     N, H, W, Cc = x.shape

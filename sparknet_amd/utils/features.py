@@ -16,6 +16,7 @@ import os
 DEFAULTS = {
     # engine fusion passes (engine.py)
     "fuse_pool_lrn": True,      # max pool + cross-channel LRN in one kernel each way
+    "fuse_lrn_pool_bwd": True,  # LRN -> max pool: the two backwards in one kernel
     "zero_copy_concat": True,   # producers write straight into the Concat top
     "fuse_dropout": True,       # Dropout forward in the InnerProduct epilogue
     "fuse_fp8_quant": True,     # fp8 quantisation in the producing GEMM's epilogue

@@ -6,7 +6,10 @@
   CaffeNet's pool1/norm1 and pool2/norm2 shapes, GoogLeNet's pool1/norm1 and a padded
   odd-sized case, with and without the folded ReLU gate; and they track the fp32 CPU
   reference (ops.ref);
-* net level: CaffeNet fuses both pairs, and a fused GPU step equals an unfused one.
+* net level: CaffeNet fuses both pairs, and a fused GPU step equals an unfused one;
+* the other order (LRN -> max pool, AlexNet / GoogLeNet; engine.fuse_lrn_pool_backward):
+  the one-launch backward (pool_lrn_bwd_rev) is BITWISE equal to pool_bwd_k3s2 followed by
+  lrn_across_bwd, and AlexNet / GoogLeNet steps with it equal steps without it.
 Reference: caffe/src/caffe/layers/pooling_layer.cu:11-47,217-260, lrn_layer.cu:9-177."""
 import pytest
 import torch
@@ -111,3 +114,63 @@ def test_pool_lrn_eligibility_matches_kernels(gpu, case):
         with pytest.raises(RuntimeError):
             hip.lrn_pool_backward(dy, p_ref, m_ref, s, size, alpha, beta, k)
 
+
+
+REV_CASES = [  # N, H, W, C, pad, LRN size: LRN input shape = pooling input shape
+    (4, 55, 55, 96, 0, 5),    # AlexNet norm1 -> pool1
+    (4, 27, 27, 256, 0, 5),   # AlexNet norm2 -> pool2
+    (2, 56, 56, 192, 0, 5),   # GoogLeNet conv2/norm2 -> pool2/3x3_s2
+    (3, 14, 15, 40, 1, 3),    # padded, odd sizes
+    (2, 13, 13, 8, 0, 9),     # one channel chunk: every neighbour chunk is outside [0, C)
+    (2, 9, 12, 24, 2, 7),
+]
+
+
+@pytest.mark.parametrize("gate", [False, True])
+@pytest.mark.parametrize("case", REV_CASES)
+def test_lrn_pool_backward_rev_bitwise(gpu, case, gate):
+    from sparknet_amd.ops import hip
+    N, H, W, C, pad, size = case
+    s = PoolSpec(N, H, W, C, 3, 3, 2, 2, pad, pad)
+    assert hip.pool_lrn_rev_eligible(s, size, False)
+    alpha, beta, k = 1e-4 * 50, 0.75, 1.0
+    x = _inputs(N, H, W, C, 5).to(gpu)
+    if gate:
+        x = x.clamp_min(0)
+    y = hip.lrn_forward(x, size, alpha, beta, k)
+    _, mask = hip.pool_forward_mask(y, s, False)
+    dy = _inputs(N, s.P, s.Q, C, 6).to(gpu)
+    dl = hip.pool_backward(dy, y, s, mask)
+    dx_ref = hip.lrn_backward(dl, x, size, alpha, beta, k, gate=gate)
+    dx = hip.pool_lrn_backward_rev(dy, mask, x, s, size, alpha, beta, k, gate)
+    assert torch.equal(dx, dx_ref)
+
+
+@pytest.mark.parametrize("model", ["alexnet", "googlenet"])
+def test_step_lrn_pool_bwd_fused_equals_unfused(gpu, model, monkeypatch):
+    from sparknet_amd import engine, models
+    from sparknet_amd.core.solver import Solver
+    B, crop = (8, 227) if model == "alexnet" else (4, 224)
+    want = 2 if model == "alexnet" else 1
+    results = []
+    for fuse in (True, False):
+        monkeypatch.setenv("SN_FEATURES", "" if fuse else "fuse_lrn_pool_bwd=0")
+        sp = models.zoo.solver_for(model, train_batch=B, test_batch=B, crop=crop, classes=10)
+        solver = Solver(sp, device=torch.device(gpu), seed=5, build_test_nets=False)
+        net = solver.net
+        engine.fuse_relu(net)
+        n = sum(l.bwd_lrn is not None for l in net.layers if l.type_name == "Pooling")
+        assert n == (want if fuse else 0)
+        g = torch.Generator().manual_seed(9)
+        x = torch.randn(B, 3, crop, crop, generator=g) * 50
+        lab = torch.randint(0, 10, (B, 1), generator=g).float()
+        losses = []
+        for _ in range(3):
+            net.blob_by_name("data").set_nchw(x)
+            net.blob_by_name("label").set_nchw(lab)
+            losses.append(float(solver.iteration()))
+            solver.iter += 1
+        torch.cuda.synchronize()
+        results.append((losses, net.flat_data.detach().clone()))
+    assert results[0][0] == results[1][0]
+    assert torch.equal(results[0][1], results[1][1])
