@@ -1,5 +1,8 @@
-// libsn_core: the C ABI of csrc/core/sn_core.h implemented over an embedded CPython
-// interpreter that drives the sparknet_amd engine (sparknet_amd/capi.py).  The compute
+// libsn_core: the C ABI of csrc/core/sn_core.h.  Construction (net / solver from protobuf),
+// the DB verbs and HDF5 weights go through an embedded CPython interpreter that drives the
+// sparknet_amd engine (sparknet_amd/capi.py); once a verb's native plan exists, the solver
+// step loop (captured hipGraphs), test / forward / backward, flat and per-blob weight and
+// activation access and .caffemodel save / load run in C++ without entering it.  The compute
 // path underneath is the same as for Python callers: HIP kernels from libsn_kernels.so on
 // the GPU, RCCL for collectives.  If the interpreter is not running (a C / JVM host
 // program) it is started on first use and the package root is derived from this
@@ -378,6 +381,15 @@ struct NativeWeights {
   cast_fn_t cast = nullptr;
   std::map<std::pair<int, int>, ParamDesc> params;  // (layer, index)
   std::vector<float> stage;                         // host staging for layout conversion
+  // layer names / types / parameter counts (the native .caffemodel IO); `complete` when
+  // every parameter of every layer has a descriptor above
+  struct Layer {
+    std::string name, type;
+    int nparams = 0;
+  };
+  std::vector<Layer> layers;
+  std::string net_name;
+  bool complete = false;
 };
 
 // Per-state native plans.  A plan that could not be built (CPU state, data layers fed
@@ -816,6 +828,24 @@ NativeWeights* native_weights(void* s) {
       w->params[{(int)v[0], (int)v[1]}] = p;
     }
   }
+  if (PyObject* ls = PyDict_GetItemString(d, "layers")) {  // borrowed
+    const Py_ssize_t nl = PySequence_Size(ls);
+    for (Py_ssize_t i = 0; i < nl && !PyErr_Occurred(); ++i) {
+      PyObject* row = PySequence_GetItem(ls, i);
+      const char* nm = nullptr;
+      const char* ty = nullptr;
+      int np = 0;
+      if (row && PyArg_ParseTuple(row, "ssi", &nm, &ty, &np)) w->layers.push_back({nm, ty, np});
+      Py_XDECREF(row);
+    }
+    w->complete = !PyErr_Occurred();
+    for (size_t li = 0; w->complete && li < w->layers.size(); ++li)
+      for (int pi = 0; pi < w->layers[li].nparams; ++pi)
+        if (!w->params.count({(int)li, pi})) w->complete = false;
+  }
+  if (PyObject* nn = PyDict_GetItemString(d, "net_name")) {  // borrowed
+    if (const char* c = PyUnicode_AsUTF8(nn)) w->net_name = c;
+  }
   Py_DECREF(d);
   if (PyErr_Occurred()) {
     fetch_error("weights_plan");
@@ -920,6 +950,253 @@ int param_set(NativeWeights* w, const ParamDesc& p, int diff, const float* in, l
   }
   HIPOK(hipStreamSynchronize(w->stream));  // `in` may be reused as soon as this returns
   return 0;
+}
+
+// ---- native .caffemodel IO (Net::ToProto / Net::CopyTrainedLayersFrom, caffe/src/caffe/net.cpp:
+// 816-858, 953-961; blob.cpp:463-530) over the protobuf wire format: NetParameter { name = 1;
+// layer = 100 (LayerParameter { name = 1; type = 2; blobs = 7 }); legacy layers = 2
+// (V1LayerParameter { name = 4; blobs = 6 }) }, BlobProto { num..width = 1..4 (legacy 4-D);
+// data = 5 (packed float); double_data = 8; shape = 7 (BlobShape { dim = 1, packed int64 }) }.
+
+void pb_varint(std::string& o, unsigned long long v) {
+  while (v >= 0x80) {
+    o.push_back((char)(v | 0x80));
+    v >>= 7;
+  }
+  o.push_back((char)v);
+}
+
+void pb_bytes(std::string& o, int field, const std::string& b) {
+  pb_varint(o, ((unsigned long long)field << 3) | 2);
+  pb_varint(o, b.size());
+  o += b;
+}
+
+// BlobProto of one parameter (Caffe layout, fp32 data)
+int pb_blob(NativeWeights* w, const ParamDesc& p, std::string& out) {
+  std::vector<float> v((size_t)p.count);
+  if (param_get(w, p, 0, v.data(), p.count)) return 1;
+  std::string shape, dims;
+  for (int a = 0; a < p.ndim; ++a) pb_varint(dims, (unsigned long long)(long long)p.cs[a]);
+  pb_bytes(shape, 1, dims);
+  out.clear();
+  pb_bytes(out, 7, shape);
+  std::string data(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(float));  // little endian
+  pb_bytes(out, 5, data);
+  return 0;
+}
+
+int save_caffemodel_native(NativeWeights* w, const char* path) {
+  std::string net, layer, blob;
+  if (!w->net_name.empty()) pb_bytes(net, 1, w->net_name);
+  for (size_t li = 0; li < w->layers.size(); ++li) {
+    layer.clear();
+    pb_bytes(layer, 1, w->layers[li].name);
+    pb_bytes(layer, 2, w->layers[li].type);
+    for (int pi = 0; pi < w->layers[li].nparams; ++pi) {
+      if (pb_blob(w, w->params.at({(int)li, pi}), blob)) return 1;
+      pb_bytes(layer, 7, blob);
+    }
+    pb_bytes(net, 100, layer);
+  }
+  FILE* f = std::fopen(path, "wb");
+  if (!f) {
+    g_err = std::string("cannot open ") + path + " for writing";
+    return 1;
+  }
+  const bool ok = std::fwrite(net.data(), 1, net.size(), f) == net.size();
+  if (std::fclose(f) != 0 || !ok) {
+    g_err = std::string("short write to ") + path;
+    return 1;
+  }
+  return 0;
+}
+
+// A bounds-checked reader over one message.
+struct PbReader {
+  const unsigned char* p;
+  const unsigned char* end;
+  bool bad = false;
+  bool more() const { return !bad && p < end; }
+  unsigned long long varint() {
+    unsigned long long v = 0;
+    for (int sh = 0; sh < 64; sh += 7) {
+      if (p >= end) break;
+      const unsigned char b = *p++;
+      v |= (unsigned long long)(b & 0x7f) << sh;
+      if (!(b & 0x80)) return v;
+    }
+    bad = true;
+    return 0;
+  }
+  // next field: number and wire type; a length-delimited payload in [*lp, *lp + *ln)
+  bool field(int* num, int* wt, const unsigned char** lp, size_t* ln) {
+    const unsigned long long key = varint();
+    *num = (int)(key >> 3);
+    *wt = (int)(key & 7);
+    switch (*wt) {
+      case 0: *ln = (size_t)varint(); return !bad;  // the value, for varints
+      case 1: *lp = p; *ln = 8; break;
+      case 2: *ln = (size_t)varint(); *lp = p; break;
+      case 5: *lp = p; *ln = 4; break;
+      default: bad = true; return false;
+    }
+    if (bad || (size_t)(end - p) < *ln) {
+      bad = true;
+      return false;
+    }
+    p += *ln;
+    return true;
+  }
+};
+
+struct PbBlob {
+  std::vector<long long> shape;
+  bool legacy = false;
+  long long leg[4] = {0, 0, 0, 0};  // num, channels, height, width (proto2 default 0)
+  std::vector<float> data;
+};
+
+bool parse_blob(const unsigned char* b, size_t n, PbBlob* out) {
+  PbReader r{b, b + n};
+  std::vector<double> dd;
+  while (r.more()) {
+    int num, wt;
+    const unsigned char* lp = nullptr;
+    size_t ln = 0;
+    if (!r.field(&num, &wt, &lp, &ln)) return false;
+    if (num >= 1 && num <= 4 && wt == 0) {
+      out->legacy = true;
+      out->leg[num - 1] = (long long)(int)ln;
+    } else if (num == 5 && wt == 2) {  // packed floats
+      const size_t k = out->data.size();
+      out->data.resize(k + ln / 4);
+      std::memcpy(out->data.data() + k, lp, (ln / 4) * 4);
+    } else if (num == 5 && wt == 5) {
+      float f;
+      std::memcpy(&f, lp, 4);
+      out->data.push_back(f);
+    } else if (num == 8 && (wt == 2 || wt == 1)) {
+      const size_t k = dd.size();
+      dd.resize(k + ln / 8);
+      std::memcpy(dd.data() + k, lp, (ln / 8) * 8);
+    } else if (num == 7 && wt == 2) {  // BlobShape
+      PbReader sr{lp, lp + ln};
+      while (sr.more()) {
+        int sn, swt;
+        const unsigned char* slp = nullptr;
+        size_t sln = 0;
+        if (!sr.field(&sn, &swt, &slp, &sln)) return false;
+        if (sn != 1) continue;
+        if (swt == 0) {
+          out->shape.push_back((long long)sln);
+        } else if (swt == 2) {
+          PbReader dr{slp, slp + sln};
+          while (dr.more()) out->shape.push_back((long long)dr.varint());
+          if (dr.bad) return false;
+        }
+      }
+    }
+  }
+  if (out->data.empty() && !dd.empty()) out->data.assign(dd.begin(), dd.end());
+  return !r.bad;
+}
+
+// Blob::ShapeEquals (blob.cpp:463-478): legacy 4-D dims compare against the target padded to 4 axes
+bool blob_shape_equals(const PbBlob& b, const ParamDesc& p) {
+  if (b.legacy) {
+    if (p.ndim > 4) return false;
+    long long t[4] = {1, 1, 1, 1};
+    for (int a = 0; a < p.ndim; ++a) t[4 - p.ndim + a] = p.cs[a];
+    return t[0] == b.leg[0] && t[1] == b.leg[1] && t[2] == b.leg[2] && t[3] == b.leg[3];
+  }
+  if ((int)b.shape.size() != p.ndim) return false;
+  for (int a = 0; a < p.ndim; ++a)
+    if (b.shape[a] != p.cs[a]) return false;
+  return true;
+}
+
+std::string shape_str(const PbBlob& b) {
+  std::string s = "(";
+  if (b.legacy) {
+    for (int a = 0; a < 4; ++a) s += std::to_string(b.leg[a]) + (a < 3 ? ", " : "");
+  } else {
+    for (size_t a = 0; a < b.shape.size(); ++a) s += std::to_string(b.shape[a]) + (a + 1 < b.shape.size() ? ", " : "");
+  }
+  return s + ")";
+}
+
+// 1: error (g_err set), 2: a form this reader leaves to the Python path (V0 layers)
+int load_caffemodel_native(NativeWeights* w, const char* path) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) {
+    g_err = std::string("cannot open ") + path;
+    return 1;
+  }
+  std::vector<unsigned char> buf;
+  unsigned char chunk[1 << 16];
+  size_t k;
+  while ((k = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + k);
+  std::fclose(f);
+  std::map<std::string, int> index;
+  for (size_t li = 0; li < w->layers.size(); ++li) index.emplace(w->layers[li].name, (int)li);  // first wins
+  PbReader r{buf.data(), buf.data() + buf.size()};
+  while (r.more()) {
+    int num, wt;
+    const unsigned char* lp = nullptr;
+    size_t ln = 0;
+    if (!r.field(&num, &wt, &lp, &ln)) break;
+    if (wt != 2 || (num != 100 && num != 2)) continue;
+    const bool v1 = num == 2;
+    PbReader lr{lp, lp + ln};
+    std::string name;
+    std::vector<std::pair<const unsigned char*, size_t>> blobs;
+    while (lr.more()) {
+      int fn, fwt;
+      const unsigned char* flp = nullptr;
+      size_t fln = 0;
+      if (!lr.field(&fn, &fwt, &flp, &fln)) break;
+      if (fwt != 2) continue;
+      if (v1 && fn == 1) return 2;  // a V0 layer inside: upgrade on the Python path
+      if (fn == (v1 ? 4 : 1)) name.assign(reinterpret_cast<const char*>(flp), fln);
+      if (fn == (v1 ? 6 : 7)) blobs.emplace_back(flp, fln);
+    }
+    if (lr.bad) break;
+    auto it = index.find(name);
+    if (it == index.end()) continue;  // "Ignoring source layer"
+    const int li = it->second;
+    if ((int)blobs.size() != w->layers[li].nparams) {
+      g_err = "Incompatible number of blobs for layer '" + name + "'";
+      return 1;
+    }
+    for (int pi = 0; pi < (int)blobs.size(); ++pi) {
+      PbBlob b;
+      if (!parse_blob(blobs[pi].first, blobs[pi].second, &b)) {
+        r.bad = true;
+        break;
+      }
+      const ParamDesc& p = w->params.at({li, pi});
+      std::string ts = "(";
+      for (int a = 0; a < p.ndim; ++a) ts += std::to_string(p.cs[a]) + (a + 1 < p.ndim ? ", " : "");
+      ts += ")";
+      if (!blob_shape_equals(b, p) || (long long)b.data.size() != p.count) {
+        g_err = "Cannot copy param of layer '" + name + "'; shape mismatch. Source " + shape_str(b) +
+                " (" + std::to_string(b.data.size()) + " values), target " + ts;
+        return 1;
+      }
+      if (param_set(w, p, 0, b.data.data(), p.count)) return 1;
+    }
+  }
+  if (r.bad) {
+    g_err = std::string("malformed NetParameter in ") + path;
+    return 1;
+  }
+  return 0;
+}
+
+bool native_model_path(const char* path) {
+  const size_t n = std::strlen(path);
+  return !(n >= 3 && std::strcmp(path + n - 3, ".h5") == 0);
 }
 
 }  // namespace
@@ -1210,12 +1487,21 @@ void* sn_weights_device_ptr(void* s) {
   return p;
 }
 
+// .caffemodel files are written and read natively once the weights plan exists and covers
+// every parameter (HDF5 files, V0 nets and parameters outside the flat buffers: the Python path)
 int sn_save_weights_to_file(void* s, const char* path) {
+  NativeWeights* w = native_weights(s);
+  if (w && w->complete && native_model_path(path)) return save_caffemodel_native(w, path);
   Gil g;
   return status(call(s, "save_weights", "(s)", path));
 }
 
 int sn_load_weights_from_file(void* s, const char* path) {
+  NativeWeights* w = native_weights(s);
+  if (w && w->complete && native_model_path(path)) {
+    const int rc = load_caffemodel_native(w, path);
+    if (rc != 2) return rc;
+  }
   Gil g;
   return status(call(s, "load_weights", "(s)", path));
 }

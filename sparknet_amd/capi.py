@@ -365,7 +365,9 @@ class CoreState:
         return {"data": int(data.data_ptr()), "count": int(net.num_param_elems), "cuda": int(data.is_cuda),
                 "compute": int(comp.data_ptr()) if shadow else 0, "compute_count": int(comp.numel()) if shadow else 0,
                 "stream": int(torch.cuda.current_stream(self.device).cuda_stream) if data.is_cuda else 0,
-                "diff": int(net.flat_diff.data_ptr()), "params": self._param_table()}
+                "diff": int(net.flat_diff.data_ptr()), "params": self._param_table(),
+                "net_name": str(net.name or ""),
+                "layers": [(str(l.name), str(l.type_name), len(l.params)) for l in net.layers]}
 
     def _param_table(self) -> list:
         """Per-parameter rows for the native sn_blob_* verbs on layer parameters:

@@ -399,3 +399,100 @@ def test_native_forward_plan_updates_batchnorm_stats_once(core_lib):
         assert float(b[2][0]) == pytest.approx(float(a[2][0]), rel=1e-6), (a[2], b[2])
         for x, y in zip(a[:2], b[:2]):
             np.testing.assert_allclose(y, x, rtol=2e-2, atol=1e-3 * (np.abs(x).max() + 1e-6))
+
+
+def test_native_caffemodel_io_matches_python(core_lib, tmp_path, monkeypatch):
+    """sn_save_weights_to_file / sn_load_weights_from_file read and write .caffemodel files in
+    C++ (protobuf wire format, Net::ToProto / CopyTrainedLayersFrom semantics, net.cpp:816-858)
+    once the weights plan exists: no interpreter entry; the native file holds the same blobs as
+    the Python writer's, each reader loads the other's file, legacy 4-D blob dims load, and
+    shape / blob-count mismatches fail with Caffe's messages."""
+    from sparknet_amd import proto
+    lib = C.CDLL(core_lib)
+    lib.sn_create_state.restype = C.c_void_p
+    lib.sn_last_error.restype = C.c_char_p
+    lib.sn_num_params.restype = C.c_longlong
+    lib.sn_python_entries.restype = C.c_longlong
+    st = C.c_void_p(lib.sn_create_state())
+    buf, n = C.c_char_p(), C.c_int()
+    assert lib.sn_parse_solver_prototxt(SOLVER.encode(), C.byref(buf), C.byref(n)) == 0
+    assert lib.sn_set_device(st, -1) == 0
+    assert lib.sn_load_solver_from_protobuf(st, buf, n) == 0, lib.sn_last_error()
+
+    def fill(p, batch, nd, shape, user):
+        cnt = int(np.prod([shape[i] for i in range(nd)]))
+        arr = np.ctypeslib.as_array(p, shape=(cnt,))
+        arr[:] = np.sin(0.07 * np.arange(cnt)).astype(np.float32) if nd == 4 else (np.arange(cnt) % 3)
+
+    cb = CB(fill)
+    assert lib.sn_set_train_data_callback(st, 0, cb, None) == 0
+    assert lib.sn_set_train_data_callback(st, 1, cb, None) == 0
+    assert lib.sn_solver_step(st, 2) == 0, lib.sn_last_error()
+    nparam = lib.sn_num_params(st)
+    w0 = (C.c_float * nparam)()
+    assert lib.sn_get_weights(st, w0, C.c_longlong(nparam)) == 0  # builds the weights plan
+    zeros = (C.c_float * nparam)()
+
+    def weights():
+        out = (C.c_float * nparam)()
+        assert lib.sn_get_weights(st, out, C.c_longlong(nparam)) == 0
+        return np.frombuffer(out, dtype=np.float32).copy()
+
+    ref = np.frombuffer(w0, dtype=np.float32).copy()
+    nat, py = str(tmp_path / "native.caffemodel"), str(tmp_path / "python.caffemodel")
+    monkeypatch.setenv("SN_NATIVE_STEP", "1")
+    e0 = lib.sn_python_entries()
+    assert lib.sn_save_weights_to_file(st, nat.encode()) == 0, lib.sn_last_error()
+    assert lib.sn_python_entries() == e0
+    monkeypatch.setenv("SN_NATIVE_STEP", "0")
+    assert lib.sn_save_weights_to_file(st, py.encode()) == 0, lib.sn_last_error()
+    a, b = proto.read_net(nat), proto.read_net(py)
+    blobs_b = {l.name: l.blobs for l in b.layer}
+    assert [l.name for l in a.layer] == [l.name for l in b.layer]
+    assert [l.type for l in a.layer] == [l.type for l in b.layer]
+    checked = 0
+    for la in a.layer:
+        assert len(la.blobs) == len(blobs_b[la.name])
+        for x, y in zip(la.blobs, blobs_b[la.name]):
+            assert list(x.shape.dim) == list(y.shape.dim)
+            np.testing.assert_array_equal(np.asarray(x.data, np.float32), np.asarray(y.data, np.float32))
+            checked += 1
+    assert checked >= 4
+    # each reader loads the other's file
+    for reader_native, path in ((True, py), (False, nat), (True, nat)):
+        assert lib.sn_set_weights(st, zeros, C.c_longlong(nparam)) == 0
+        monkeypatch.setenv("SN_NATIVE_STEP", "1" if reader_native else "0")
+        e0 = lib.sn_python_entries()
+        assert lib.sn_load_weights_from_file(st, path.encode()) == 0, lib.sn_last_error()
+        if reader_native:
+            assert lib.sn_python_entries() == e0
+        np.testing.assert_array_equal(weights(), ref)
+    monkeypatch.setenv("SN_NATIVE_STEP", "1")
+    # legacy (num, channels, height, width) dims: the 4-D weights load; a 2-D blob pads to (1, 1, r, c)
+    leg = proto.read_net(py)
+    for layer in leg.layer:
+        for bp in layer.blobs:
+            dims = [1] * (4 - len(bp.shape.dim)) + list(bp.shape.dim)
+            bp.ClearField("shape")
+            bp.num, bp.channels, bp.height, bp.width = dims
+    proto.write_binary(str(tmp_path / "legacy.caffemodel"), leg)
+    assert lib.sn_set_weights(st, zeros, C.c_longlong(nparam)) == 0
+    assert lib.sn_load_weights_from_file(st, str(tmp_path / "legacy.caffemodel").encode()) == 0, lib.sn_last_error()
+    np.testing.assert_array_equal(weights(), ref)
+    # mismatches: Caffe's messages
+    bad = proto.read_net(py)
+    lyr = next(l for l in bad.layer if len(l.blobs))
+    lyr.blobs[0].shape.dim[0] += 1
+    proto.write_binary(str(tmp_path / "bad_shape.caffemodel"), bad)
+    assert lib.sn_load_weights_from_file(st, str(tmp_path / "bad_shape.caffemodel").encode()) != 0
+    assert b"shape mismatch" in lib.sn_last_error() and lyr.name.encode() in lib.sn_last_error()
+    bad = proto.read_net(py)
+    lyr = next(l for l in bad.layer if len(l.blobs))
+    del lyr.blobs[-1]
+    proto.write_binary(str(tmp_path / "bad_count.caffemodel"), bad)
+    assert lib.sn_load_weights_from_file(st, str(tmp_path / "bad_count.caffemodel").encode()) != 0
+    assert b"Incompatible number of blobs" in lib.sn_last_error()
+    (tmp_path / "trunc.caffemodel").write_bytes(open(py, "rb").read()[:-7])
+    assert lib.sn_load_weights_from_file(st, str(tmp_path / "trunc.caffemodel").encode()) != 0
+    lib.sn_free(buf)
+    lib.sn_destroy_state(st)
