@@ -13,11 +13,16 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <unistd.h>
+
+#include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
+#include <filesystem>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -1194,6 +1199,185 @@ int load_caffemodel_native(NativeWeights* w, const char* path) {
   return 0;
 }
 
+// ---- native record databases (ccaffe.cpp:51-81 create_db / write_to_db / commit_db_txn /
+// close_db; caffe/src/caffe/util/db_lmdb.cpp): Datum records into an LMDB environment (the
+// bulk-loaded B+tree of sparknet_amd/data/lmdb.py write_lmdb, page for page) or the sndb
+// record file; LevelDB stays on the Python path (sparknet_amd/data/leveldb.py).
+struct NativeDB {
+  std::string path;
+  bool lmdb = false;
+  FILE* f = nullptr;  // sndb
+  std::map<std::string, std::string> all;  // lmdb: committed records, key order (memcmp order)
+  std::vector<std::pair<std::string, std::string>> txn;
+  long long count = 0;
+};
+
+std::mutex g_db_mu;
+std::unordered_map<void*, std::unique_ptr<NativeDB>> g_dbs;
+
+NativeDB* find_db(void* s) {
+  std::lock_guard<std::mutex> lk(g_db_mu);
+  auto it = g_dbs.find(s);
+  return it == g_dbs.end() ? nullptr : it->second.get();
+}
+
+// Datum { channels = 1; height = 2; width = 3; data = 4; label = 5; encoded = 7 }, every field
+// present, in field order (what Python's SerializeToString writes for capi.write_to_db)
+std::string datum_bytes(const char* image, int label, int c, int h, int w) {
+  std::string o;
+  pb_varint(o, 1 << 3), pb_varint(o, (unsigned long long)(long long)c);
+  pb_varint(o, 2 << 3), pb_varint(o, (unsigned long long)(long long)h);
+  pb_varint(o, 3 << 3), pb_varint(o, (unsigned long long)(long long)w);
+  pb_bytes(o, 4, std::string(image, (size_t)c * h * w));
+  pb_varint(o, 5 << 3), pb_varint(o, (unsigned long long)(long long)label);
+  pb_varint(o, 7 << 3), pb_varint(o, 0);
+  return o;
+}
+
+constexpr int kPage = 4096, kPageHdr = 16, kMaxKey = 511;
+constexpr uint16_t MDB_P_BRANCH = 0x01, MDB_P_LEAF = 0x02, MDB_P_OVERFLOW = 0x04, MDB_P_META = 0x08, MDB_F_BIGDATA = 0x01;
+constexpr unsigned long long MDB_P_INVALID = ~0ull;
+
+template <typename T>
+void put_le(std::string& o, T v) {
+  o.append(reinterpret_cast<const char*>(&v), sizeof v);
+}
+
+std::string lmdb_node(const std::string& key, uint16_t lo, uint16_t hi, uint16_t flags, const std::string& payload) {
+  std::string b;
+  put_le<uint16_t>(b, lo), put_le<uint16_t>(b, hi), put_le<uint16_t>(b, flags), put_le<uint16_t>(b, (uint16_t)key.size());
+  b += key;
+  b += payload;
+  if (b.size() & 1) b.push_back('\0');
+  return b;
+}
+
+struct LmdbPages {
+  FILE* f;
+  unsigned long long next = 2, branch = 0, leaf = 0, overflow = 0;
+  bool ok = true;
+  void put(unsigned long long pg, const std::string& data) {
+    ok = ok && fseeko(f, (off_t)(pg * kPage), SEEK_SET) == 0 && std::fwrite(data.data(), 1, data.size(), f) == data.size();
+  }
+  unsigned long long over(const std::string& v) {
+    const unsigned long long n = (kPageHdr + v.size() + kPage - 1) / kPage, pg = next;
+    next += n;
+    std::string b;
+    put_le<unsigned long long>(b, pg), put_le<uint16_t>(b, 0), put_le<uint16_t>(b, MDB_P_OVERFLOW), put_le<uint32_t>(b, (uint32_t)n);
+    b += v;
+    b.resize((size_t)(n * kPage), '\0');
+    put(pg, b);
+    overflow += n;
+    return pg;
+  }
+  unsigned long long page(const std::vector<std::string>& nodes, uint16_t flags) {
+    const unsigned long long pg = next++;
+    std::string b((size_t)kPage, '\0');
+    size_t upper = kPage;
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      upper -= nodes[i].size();
+      std::memcpy(&b[upper], nodes[i].data(), nodes[i].size());
+      const uint16_t u = (uint16_t)upper;
+      std::memcpy(&b[kPageHdr + 2 * i], &u, 2);
+    }
+    std::string h;
+    put_le<unsigned long long>(h, pg), put_le<uint16_t>(h, 0), put_le<uint16_t>(h, flags);
+    put_le<uint16_t>(h, (uint16_t)(kPageHdr + 2 * nodes.size())), put_le<uint16_t>(h, (uint16_t)upper);
+    std::memcpy(&b[0], h.data(), h.size());
+    put(pg, b);
+    ++(flags & MDB_P_BRANCH ? branch : leaf);
+    return pg;
+  }
+};
+
+// MDB_db: pad, flags, depth, branch / leaf / overflow page counts, entries, root
+void db_meta(std::string& b, uint32_t pad, uint16_t depth, unsigned long long branch, unsigned long long leaf,
+             unsigned long long overflow, unsigned long long entries, unsigned long long root) {
+  put_le<uint32_t>(b, pad), put_le<uint16_t>(b, 0), put_le<uint16_t>(b, depth);
+  put_le<unsigned long long>(b, branch), put_le<unsigned long long>(b, leaf), put_le<unsigned long long>(b, overflow);
+  put_le<unsigned long long>(b, entries), put_le<unsigned long long>(b, root);
+}
+
+int write_lmdb_native(const std::string& dir, const std::map<std::string, std::string>& data) {
+  std::error_code ec;
+  std::filesystem::create_directories(dir, ec);
+  const std::string fname = dir + "/data.mdb";
+  FILE* f = std::fopen((fname + ".tmp").c_str(), "w+b");
+  if (!f) {
+    g_err = "cannot create " + fname;
+    return 1;
+  }
+  const size_t nodemax = (size_t)((((kPage - kPageHdr) / 2) & ~1) - 2);
+  LmdbPages w{f};
+  std::vector<std::pair<std::string, unsigned long long>> level;  // (first key, page) of each page
+  std::vector<std::string> cur;
+  size_t used = kPageHdr;
+  std::string first;
+  for (const auto& kv : data) {
+    const std::string& k = kv.first;
+    const std::string& v = kv.second;
+    const uint16_t lo = (uint16_t)(v.size() & 0xFFFF), hi = (uint16_t)(v.size() >> 16);
+    std::string nd;
+    if (8 + k.size() + v.size() > nodemax) {
+      std::string pgb;
+      put_le<unsigned long long>(pgb, w.over(v));
+      nd = lmdb_node(k, lo, hi, MDB_F_BIGDATA, pgb);
+    } else {
+      nd = lmdb_node(k, lo, hi, 0, v);
+    }
+    if (!cur.empty() && used + 2 + nd.size() > (size_t)kPage) {
+      level.emplace_back(first, w.page(cur, MDB_P_LEAF));
+      cur.clear(), used = kPageHdr;
+    }
+    if (cur.empty()) first = k;
+    cur.push_back(std::move(nd));
+    used += 2 + cur.back().size();
+  }
+  if (!cur.empty()) level.emplace_back(first, w.page(cur, MDB_P_LEAF));
+  uint16_t depth = level.empty() ? 0 : 1;
+  while (level.size() > 1) {
+    std::vector<std::pair<std::string, unsigned long long>> nxt;
+    cur.clear(), used = kPageHdr;
+    for (const auto& kp : level) {
+      const unsigned long long pg = kp.second;
+      const uint16_t lo = (uint16_t)(pg & 0xFFFF), hi = (uint16_t)((pg >> 16) & 0xFFFF), fl = (uint16_t)((pg >> 32) & 0xFFFF);
+      std::string nd = lmdb_node(cur.empty() ? std::string() : kp.first, lo, hi, fl, std::string());
+      if (!cur.empty() && used + 2 + nd.size() > (size_t)kPage) {
+        nxt.emplace_back(first, w.page(cur, MDB_P_BRANCH));
+        cur.clear(), used = kPageHdr;
+        nd = lmdb_node(std::string(), lo, hi, fl, std::string());  // leftmost key of a branch page is implicit
+      }
+      if (cur.empty()) first = kp.first;
+      cur.push_back(std::move(nd));
+      used += 2 + cur.back().size();
+    }
+    nxt.emplace_back(first, w.page(cur, MDB_P_BRANCH));
+    level.swap(nxt);
+    ++depth;
+  }
+  const unsigned long long root = level.empty() ? MDB_P_INVALID : level[0].second, last_pg = w.next - 1;
+  const unsigned long long mapsize = std::max<unsigned long long>(w.next * kPage, 1ull << 20);
+  for (unsigned long long pg = 0; pg < 2; ++pg) {
+    std::string m;
+    put_le<unsigned long long>(m, pg), put_le<uint16_t>(m, 0), put_le<uint16_t>(m, MDB_P_META);
+    put_le<uint16_t>(m, 0), put_le<uint16_t>(m, 0);
+    put_le<uint32_t>(m, 0xBEEFC0DEu), put_le<uint32_t>(m, 1), put_le<unsigned long long>(m, 0);
+    put_le<unsigned long long>(m, mapsize);
+    db_meta(m, (uint32_t)kPage, 0, 0, 0, 0, 0, MDB_P_INVALID);  // free DB (md_pad holds the page size)
+    db_meta(m, 0, depth, w.branch, w.leaf, w.overflow, data.size(), root);
+    put_le<unsigned long long>(m, last_pg), put_le<unsigned long long>(m, 1);
+    m.resize(kPage, '\0');
+    w.put(pg, m);
+  }
+  bool ok = w.ok && std::fflush(f) == 0 && ftruncate(fileno(f), (off_t)(w.next * kPage)) == 0;
+  ok = std::fclose(f) == 0 && ok;
+  if (!ok || std::rename((fname + ".tmp").c_str(), fname.c_str()) != 0) {
+    g_err = "write error on " + fname;
+    return 1;
+  }
+  return 0;
+}
+
 bool native_model_path(const char* path) {
   const size_t n = std::strlen(path);
   return !(n >= 3 && std::strcmp(path + n - 3, ".h5") == 0);
@@ -1223,6 +1407,11 @@ void* sn_create_state(void) {
 
 void sn_destroy_state(void* state) {
   if (!state) return;
+  if (NativeDB* db = find_db(state)) {  // an unclosed native DB: its sndb file handle
+    if (db->f) std::fclose(db->f);
+    std::lock_guard<std::mutex> lk(g_db_mu);
+    g_dbs.erase(state);
+  }
   drop_native(state);  // before the Python state (which owns the captured graphs)
   Gil g;
   Py_DECREF(static_cast<PyObject*>(state));
@@ -1596,29 +1785,108 @@ int sn_set_mode_gpu(void* s) { return sn_set_device(s, 0); }
 
 // -- databases ----------------------------------------------------------------------------------
 int sn_create_db(void* s, const char* db_name, const char* db_type) {
+  std::string t(db_type ? db_type : "");
+  for (auto& ch : t) ch = (char)std::tolower((unsigned char)ch);
+  {
+    std::lock_guard<std::mutex> lk(g_db_mu);
+    g_dbs.erase(s);
+  }
+  if (native_enabled() && (t == "lmdb" || t == "sndb")) {
+    std::error_code ec;
+    if (std::filesystem::is_directory(db_name, ec)) std::filesystem::remove_all(db_name, ec);
+    auto db = std::make_unique<NativeDB>();
+    db->path = db_name;
+    db->lmdb = t == "lmdb";
+    if (!db->lmdb) {
+      db->f = std::fopen(db_name, "wb");
+      if (!db->f || std::fwrite("SNDB1\n", 1, 6, db->f) != 6) {
+        if (db->f) std::fclose(db->f);
+        g_err = std::string("cannot create ") + db_name;
+        return 1;
+      }
+    }
+    std::lock_guard<std::mutex> lk(g_db_mu);
+    g_dbs[s] = std::move(db);
+    return 0;
+  }
   Gil g;
   return status(call(s, "create_db", "(ss)", db_name, db_type));
 }
 
 int sn_write_to_db(void* s, const char* image, int label, int channels, int height, int width, const char* key) {
+  if (NativeDB* db = find_db(s)) {
+    const std::string rec = datum_bytes(image, label, channels, height, width);
+    if (!db->lmdb) {
+      const uint32_t n = (uint32_t)rec.size();
+      if (std::fwrite(&n, 4, 1, db->f) != 1 || std::fwrite(rec.data(), 1, rec.size(), db->f) != rec.size()) {
+        g_err = "sn_write_to_db: write error on " + db->path;
+        return 1;
+      }
+    } else {
+      char auto_key[32];
+      std::snprintf(auto_key, sizeof auto_key, "%08lld", db->count);
+      std::string k = key && *key ? std::string(key) : std::string(auto_key);
+      if (k.empty() || k.size() > (size_t)kMaxKey) {
+        g_err = "LMDB keys must be 1..511 bytes";
+        return 1;
+      }
+      db->txn.emplace_back(std::move(k), rec);
+    }
+    ++db->count;
+    return 0;
+  }
   Gil g;
   Py_ssize_t n = (Py_ssize_t)channels * height * width;
   return status(call(s, "write_to_db", "(y#iiiis)", image, n, label, channels, height, width, key ? key : ""));
 }
 
 int sn_commit_db_txn(void* s) {
+  if (NativeDB* db = find_db(s)) {
+    if (!db->lmdb) return std::fflush(db->f) == 0 ? 0 : 1;
+    for (auto& kv : db->txn) db->all[kv.first] = std::move(kv.second);  // a later put of a key wins
+    db->txn.clear();
+    return 0;
+  }
   Gil g;
   return status(call(s, "commit_db_txn", nullptr));
 }
 
 int sn_close_db(void* s) {
+  if (NativeDB* db = find_db(s)) {
+    int rc = sn_commit_db_txn(s);
+    if (!db->lmdb) {
+      rc = std::fclose(db->f) == 0 ? rc : 1;
+    } else if (rc == 0) {
+      rc = write_lmdb_native(db->path, db->all);
+    }
+    std::lock_guard<std::mutex> lk(g_db_mu);
+    g_dbs.erase(s);
+    return rc;
+  }
   Gil g;
   return status(call(s, "close_db", nullptr));
 }
 
+// BlobProto { num = 1, channels, height, width, data (packed) } (ccaffe.cpp:83-97), written natively
 int sn_save_mean_image(const float* mean, int channels, int height, int width, const char* filename) {
-  return module_call("save_mean_image", "(Kiiis)", (unsigned long long)(uintptr_t)mean, channels, height, width,
-                     filename);
+  std::string o;
+  pb_varint(o, 1 << 3), pb_varint(o, 1);
+  pb_varint(o, 2 << 3), pb_varint(o, (unsigned long long)(long long)channels);
+  pb_varint(o, 3 << 3), pb_varint(o, (unsigned long long)(long long)height);
+  pb_varint(o, 4 << 3), pb_varint(o, (unsigned long long)(long long)width);
+  const size_t n = (size_t)channels * height * width;
+  pb_bytes(o, 5, std::string(reinterpret_cast<const char*>(mean), n * sizeof(float)));
+  FILE* f = std::fopen(filename, "wb");
+  if (!f) {
+    g_err = std::string("cannot open ") + filename + " for writing";
+    return 1;
+  }
+  const bool ok = std::fwrite(o.data(), 1, o.size(), f) == o.size();
+  if (std::fclose(f) != 0 || !ok) {
+    g_err = std::string("short write to ") + filename;
+    return 1;
+  }
+  return 0;
 }
 
 // -- blobs --------------------------------------------------------------------------------------

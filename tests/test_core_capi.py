@@ -496,3 +496,47 @@ def test_native_caffemodel_io_matches_python(core_lib, tmp_path, monkeypatch):
     assert lib.sn_load_weights_from_file(st, str(tmp_path / "trunc.caffemodel").encode()) != 0
     lib.sn_free(buf)
     lib.sn_destroy_state(st)
+
+
+@pytest.mark.parametrize("backend", ["lmdb", "sndb"])
+def test_native_db_verbs_byte_equal_python(core_lib, tmp_path, monkeypatch, backend):
+    """sn_create_db / sn_write_to_db / sn_commit_db_txn / sn_close_db write LMDB environments
+    and sndb record files in C++ (no interpreter entry) that are byte-identical to the Python
+    writers' (SN_NATIVE_STEP=0): explicit, automatic and duplicate keys, values past an LMDB
+    page (overflow pages) and enough records for a two-level B+tree; sn_save_mean_image too."""
+    from sparknet_amd.data.db import DatumReader
+    lib = C.CDLL(core_lib)
+    lib.sn_create_state.restype = C.c_void_p
+    lib.sn_last_error.restype = C.c_char_p
+    lib.sn_python_entries.restype = C.c_longlong
+    st = C.c_void_p(lib.sn_create_state())
+    rng = np.random.default_rng(7)
+    recs = []
+    for i in range(400):
+        c, h, w = (3, 40, 40) if i % 97 == 5 else (3, 4, 4)  # 4800-byte images span overflow pages
+        key = b"" if i % 5 == 0 else (b"k%05d" % (i % 350))       # auto keys, and duplicates of k00000..
+        recs.append((rng.integers(0, 256, c * h * w, dtype=np.uint8).tobytes(), int(i % 10 - 2), c, h, w, key))
+    out = {}
+    for native in (True, False):
+        monkeypatch.setenv("SN_NATIVE_STEP", "1" if native else "0")
+        path = str(tmp_path / f"{backend}_{int(native)}")
+        e0 = lib.sn_python_entries()
+        assert lib.sn_create_db(st, path.encode(), backend.encode()) == 0, lib.sn_last_error()
+        for i, (img, label, c, h, w, key) in enumerate(recs):
+            assert lib.sn_write_to_db(st, img, label, c, h, w, key) == 0, lib.sn_last_error()
+            if i % 150 == 149:
+                assert lib.sn_commit_db_txn(st) == 0
+        assert lib.sn_close_db(st) == 0, lib.sn_last_error()
+        mean = np.linspace(-1, 1, 12, dtype=np.float32)
+        mpath = path + ".mean.binaryproto"
+        assert lib.sn_save_mean_image(mean.ctypes.data_as(C.POINTER(C.c_float)), 3, 2, 2, mpath.encode()) == 0
+        if native:
+            assert lib.sn_python_entries() == e0
+        f = os.path.join(path, "data.mdb") if backend == "lmdb" else path
+        out[native] = (open(f, "rb").read(), open(mpath, "rb").read())
+        rd = DatumReader(path)
+        assert len(rd) == (len({k for *_, k in recs if k} | {b"%08d" % i for i, r in enumerate(recs) if not r[5]})
+                           if backend == "lmdb" else len(recs))
+    assert out[True][0] == out[False][0]
+    assert out[True][1] != b"" and out[True][1] == out[False][1]
+    lib.sn_destroy_state(st)
