@@ -344,7 +344,7 @@ __global__ void pool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restr
           for (int k = 0; k < 8; ++k) acc[k] += f[k] * scale;
         }
       }
-    *reinterpret_cast<uint4*>(dx + (long long)pix * g.C + c0) = pack8(acc);
+    if (dx) *reinterpret_cast<uint4*>(dx + (long long)pix * g.C + c0) = pack8(acc);
     if (qs.q) *reinterpret_cast<uint2*>(qs.q + (long long)pix * g.C + c0) = q_pack8(qs, qsc, acc, qmax);
   }
   if (qs.q) q_flush(qs, qmax);
@@ -477,8 +477,10 @@ extern "C" int sn_pool_bwd(const bf16_t* dy, const uint8_t* mask, bf16_t* dx, lo
   long long total = N * H * W * (vec ? C / 8 : C);
   dim3 grid(sn_blocks(total, 256, 16384));
   const long long nh = (kh + sh - 1) / sh, nw = (kw + sw - 1) / sw;
-  // fp8 side output: the pool_bwd_k paths only
+  // fp8 side output: the pool_bwd_k paths only.  dx null: the side output alone (the consuming
+  // conv reads nothing but the fp8 bytes, engine.fuse_fp8_quant fp8_dx_only)
   if (q && (!vec || (kh == 3 && kw == 3 && sh == 2 && sw == 2) || nh != nw || nh < 1 || nh > 3)) return 9;
+  if (!dx && !q) return 9;
   if (vec && kh == 3 && kw == 3 && sh == 2 && sw == 2) {
     // 2x2 input pixels per thread over the padded extent [0, H + ph) x [0, W + pw)
     const int BH = (int)((H + ph + 1) / 2), BW = (int)((W + pw + 1) / 2);

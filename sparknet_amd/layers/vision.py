@@ -314,6 +314,7 @@ class ConvolutionLayer(Layer):
     # also stores the producer's fp8 output gradient
     fp8_out = None
     fp8_dx_out = None
+    fp8_dx_only = False  # store the fp8 input gradient alone (engine.fuse_fp8_quant)
     _fp8_x_side = None
     _fp8_dy_side = None
 
@@ -618,7 +619,7 @@ class PoolingLayer(Layer):
         if side is not None:
             from ..ops import hip
             bottoms[0].diff = hip.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data,
-                                                self.relu_gate, side=side)
+                                                self.relu_gate, side=side, side_only=self.fp8_dx_only)
             self.fp8_dx_out[0]._fp8_dy_side = side
             return
         bottoms[0].diff = ops.pool_backward(tops[0].diff, bottoms[0].data, s, self.aux, tops[0].data,

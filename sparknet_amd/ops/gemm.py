@@ -331,6 +331,7 @@ class Fp8Side:
         self.slot = slot
         self.e5m2 = bool(e5m2)
         self.ok = True
+        self.only = False  # the bf16 base was not written: the fp8 bytes are the only copy
         self.launches = 0
         # block |max| partials (zero between uses: the fold kernel clears them); pass a persistent
         # buffer so a captured graph does not re-zero a fresh one every replay

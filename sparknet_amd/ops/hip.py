@@ -454,10 +454,12 @@ def _conv_backward(dy, x, w, s: ConvSpec, need_dx: bool, dw=None, db=None, gate=
         dyq = ws.get("fp8_dyq")
         if dyq is None:
             dyq = ws["fp8_dyq"] = _fp8_dyq(dy, ws, s)
-        _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc)
+        _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc, _dy_fp8_only(ws))
         dw = None
         if db is not None:
             db, fused_db = None, False
+    if (dw is not None or db is not None) and _dy_fp8_only(ws):
+        _no_bf16_dy("a bf16 weight / bias gradient")
     _conv_wgrad(dy2, x, s, M, kred, plan, fused_db, dw, db, ws, dw_acc, db_acc, ldd, ldx)
     if not need_dx:
         return None
@@ -523,6 +525,34 @@ def fp8_wgrad_ok(s: ConvSpec) -> bool:
     return _implicit_ok(s) and s.Kg % 16 == 0 and s.Cg % 16 == 0 and s.C % 16 == 0 and s.K % 16 == 0
 
 
+def conv_dy_fp8_only_ok(layer, s: ConvSpec) -> bool:
+    """Would this conv's backward read its output gradient only as fp8 bytes — e4m3 data
+    gradient (the flip path), e4m3 weight gradient with the bias on its ones column, no
+    space-to-depth plan?  Then the max pooling above may store that gradient as fp8 alone
+    (engine.fuse_fp8_quant fp8_dx_only); conv_backward raises if a bf16 read happens anyway."""
+    if layer.fp8_dgrad_slots is None or not fp8_dgrad_ok(s) or _s2d_plan(s) is not None:
+        return False
+    if not (s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0):
+        return False
+    need_w = layer.param_grads_needed(0)
+    need_b = layer.bias is not None and layer.param_grads_needed(1)
+    if need_w and not (layer.fp8_wgrad and fp8_wgrad_ok(s)):
+        return False
+    return not need_b or (need_w and (s.R * s.S * s.Cg) % 16 == 0 and FP8_WGRAD_BIAS)
+
+
+def _dy_fp8_only(ws) -> bool:
+    """The output gradient exists only as the fp8 side output of the layer above (a max
+    pooling's backward with side_only): its bf16 tensor was never written."""
+    f8 = ws.get("fp8_dgrad") if ws else None
+    return bool(f8 is not None and len(f8) > 3 and f8[3] is not None and getattr(f8[3], "only", False))
+
+
+def _no_bf16_dy(what: str):
+    raise RuntimeError(f"conv backward: {what} would read the bf16 output gradient, which the max pooling "
+                       "above stored only as fp8 (engine.fuse_fp8_quant fp8_dx_only; SN_FEATURES=fp8_dx_only=0)")
+
+
 def _fp8_dyq(dy, ws, s):
     """fp8 bytes of the output gradient for this layer's fp8 data / weight gradients: the
     side output of the layer above's dgrad epilogue when it covers dy, else one pass."""
@@ -538,10 +568,12 @@ def _fp8_dyq(dy, ws, s):
     e5 = sc.is_e5m2(idy)
     from .gemm import side_bytes
     dyq = side_bytes(side, dy, e5)
+    if dyq is None and _dy_fp8_only(ws):
+        _no_bf16_dy("quantising dy")
     return dyq if dyq is not None else quant_fp8(_c(dy), sc.slot(idy), e5m2=e5)
 
 
-def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc):
+def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc, dy_fp8_only=False):
     """Weight gradient as an fp8 product with the reduction over pixels: A = the output
     gradient (e4m3 / e5m2, MC: [pixels][K]), B = the implicit im2col of the layer input's
     e4m3 copy kept from the forward (MC), both read transposed from LDS by
@@ -554,6 +586,8 @@ def _conv_wgrad_fp8(dy2, dyq, s, M, kred, f8w, dw, db, dw_acc, db_acc):
     # the ones column of B is an e4m3 1.0 dequantised by dy's factor only
     fused_db = db is not None and kred % 16 == 0 and FP8_WGRAD_BIAS
     if db is not None and not fused_db:
+        if dy_fp8_only:
+            _no_bf16_dy("the exact bias gradient")
         colsum(dy2, db, accumulate=db_acc)
     A = Dense(dyq.view(M, s.K), s.K, kcontig=False, gstride=s.Kg)
     B = Im2col(xq, _geom(s), kcontig=False, gstride=s.Cg)
@@ -568,6 +602,9 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
     ldo = chan_stride(dx)  # C, or the pitch of a channel-slice destination (conv_backward dx_out)
     if gate is not None and chan_stride(gate) != ldo:  # the gate (= x) must share dx's layout
         gate = _c(gate)
+    if _dy_fp8_only(ws) and not (s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s)
+                                 and s.Kg % 8 == 0):
+        _no_bf16_dy("a bf16 data gradient")
     if s.sh == 1 and s.sw == 1 and s.dh == 1 and s.dw == 1 and _implicit_ok(s) and s.Kg % 8 == 0:
         # dgrad == forward conv of dy with flipped / transposed weights, pad' = R-1-pad.
         # A flip pass + KC (ds_read_b128) B operand measures faster than reading the
@@ -579,6 +616,8 @@ def _conv_dgrad(dy, x, w, s, M, gate, ws, ldd=0, ldx=0, dx_out=None):
         f8 = ws.get("fp8_dgrad") if ws is not None else None
         if f8 is not None and fp8_dgrad_ok(s) and ldd == s.K:
             return _conv_dgrad_fp8(dy, w, s, g2, kr2, pre, gate, dx, f8, ws.get("fp8_dyq"))
+        if _dy_fp8_only(ws):
+            _no_bf16_dy("a bf16 data gradient")
         if (direct_c64_ok(s) and ldd == s.K and ldx == s.C and dy.is_contiguous() and dx.is_contiguous()
                 and not DGRAD_INPLACE_WEIGHTS and not _side_covers(dx)):
             if pre is None:
@@ -648,6 +687,8 @@ def _conv_dgrad_fp8(dy, w, s, g2, kr2, wt, gate, dx, f8, ws_dyq=None):
         from .gemm import side_bytes
         dyq = side_bytes(side, dy, e5)
     if dyq is None:
+        if len(f8) > 3 and getattr(f8[3], "only", False):
+            _no_bf16_dy("quantising dy for the data gradient")
         dyq = quant_fp8(dy, sc.slot(idy), e5m2=e5)
     wtq = quant_fp8(wt, sc.slot(iwt))
     if direct_fp8_ok(s) and not e5 and dx.is_contiguous() and not _side_covers(dx):
@@ -844,8 +885,14 @@ def pool_forward(x, s: PoolSpec):
     return pool_forward_mask(x, s)[0]
 
 
-def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False, side=None):
-    """side: an ops.gemm.Fp8Side over dx (pool_side_ok backward; not with a non-MAX gate)."""
+def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False, side=None, side_only=False):
+    """side: an ops.gemm.Fp8Side over dx (pool_side_ok backward; not with a non-MAX gate).
+    side_only: store the fp8 bytes alone — the returned bf16 dx is NOT written (its only
+    reader takes the fp8 copy, engine.fuse_fp8_quant's fp8_dx_only; side.only marks it so
+    conv_backward refuses any path that would read the bf16 values)."""
+    if side_only:
+        assert side is not None and s.method == POOL_MAX
+        side.only = True
     if side is not None:
         assert pool_side_ok(s, True) and not (gate and s.method != POOL_MAX)
         assert tuple(side.base.shape) == (s.N, s.H, s.W, s.C)
@@ -858,7 +905,7 @@ def pool_backward(dy, x, s: PoolSpec, mask=None, y=None, gate=False, side=None):
     nb = _pool_images(s)
     for n0 in range(0, s.N, nb):
         n1 = min(s.N, n0 + nb)
-        call("pool_bwd", dy[n0:n1], mask[n0:n1] if mask is not None else None, dx[n0:n1],
+        call("pool_bwd", dy[n0:n1], mask[n0:n1] if mask is not None else None, None if side_only else dx[n0:n1],
              *_pool_args(dataclasses.replace(s, N=n1 - n0)), *_side_args(side, dx, n0, n1))
     if side is not None:
         side.launches += 1

@@ -33,6 +33,7 @@ DEFAULTS = {
     # fp8 details
     "fp8_wgrad_bias": True,     # fp8 weight-gradient bias through the e4m3 ones column
     "fp8_side_frag": True,      # per-fragment epilogues also store the fp8 side output
+    "fp8_dx_only": True,        # a max pooling stores its input gradient as fp8 alone when the conv reads only that
 }
 
 _cache: tuple[str, dict] = ("", {})

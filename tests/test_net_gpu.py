@@ -414,3 +414,40 @@ def test_fp8_layer_selection_threshold(gpu, direct, monkeypatch):
     assert enable_fp8(solver.net) == (14 if direct else 13)
     chosen = {layer.name for layer in solver.net.layers if getattr(layer, "fp8_slots", None) is not None}
     assert ("conv1_2" in chosen) == direct and "fc8" not in chosen and "conv2_1" in chosen and "fc6" in chosen
+
+
+def test_fp8_pool_dx_only_is_bitwise_equal(gpu, monkeypatch):
+    """engine.fuse_fp8_quant fp8_dx_only: where the conv below a max pooling reads its output
+    gradient only as fp8 (e4m3 data and weight gradients, bias on the ones column), the
+    pooling backward stores just the fp8 bytes, not the bf16 gradient — graph-captured
+    training is bitwise equal to storing both, and no bf16 read of the skipped tensor happens
+    (conv_backward raises on one)."""
+    from sparknet_amd.core.solver import Solver
+    from sparknet_amd.engine import GraphStep, enable_fp8, fuse_relu
+    net_p = models.vgg16(train_batch=4, test_batch=4, crop=32, classes=10)
+    res = {}
+    for only in ("1", "0"):
+        monkeypatch.setenv("SN_FEATURES", f"fp8_dx_only={only}")
+        sp = models.zoo.vgg16_solver(net_p)
+        sp.base_lr = 0.002
+        solver = Solver(sp, device=torch.device("cuda:0"), seed=5, build_test_nets=False)
+        fuse_relu(solver.net)
+        enable_fp8(solver.net, 0.0, dgrad=True, wgrad=True)
+        pools = [ly for ly in solver.net.layers if ly.type_name == "Pooling"]
+        n_only = sum(bool(ly.fp8_dx_only) for ly in pools)
+        if only == "1":
+            assert n_only >= 3, [(ly.name, ly.fp8_dx_out is not None, ly.fp8_dx_only) for ly in pools]
+        else:
+            assert n_only == 0
+        g = torch.Generator().manual_seed(2)
+        x = torch.randn(4, 3, 32, 32, generator=g) * 0.5
+        y = torch.tensor([[1.0], [3.0], [5.0], [7.0]])
+
+        def pre():
+            solver.net.blob_by_name("data").set_nchw(x)
+            solver.net.blob_by_name("label").set_nchw(y)
+        st = GraphStep(solver, warmup=2, pre=pre, overlap=False)
+        losses = [float(st.step()) for _ in range(6)]
+        res[only] = (losses, solver.net.flat_data.clone())
+    assert res["1"][0] == res["0"][0], (res["1"][0], res["0"][0])
+    assert torch.equal(res["1"][1], res["0"][1])
