@@ -47,6 +47,12 @@ def _patterns(n, classes=10, seed=0):
 
 @pytest.mark.parametrize("order", ["tuned", "thin229"])
 def test_cifar10_quick_learns_synthetic_patterns(gpu, order, monkeypatch):
+    """cifar10_quick learns the synthetic patterns through the captured-graph local-SGD path,
+    with the tuned kernels and with conv1's weight gradient forced onto the 64-row tile at 229
+    splits.  It trains at base_lr 0.0005, HALF the reference solver's 0.001: on this synthetic
+    set the reference rate is chaotic under every summation order, the fp32 CPU engine's
+    included (profiles/r5_cifar_stability.txt), so parity at the reference rate is unpinned
+    here; tests/test_bench_fidelity_gpu.py pins the per-parameter update instead."""
     from sparknet_amd.core.solver import Solver
     from sparknet_amd.data.prefetch import DeviceFeeder, TensorSource
     from sparknet_amd.engine import LocalSGDTrainer, fuse_relu
