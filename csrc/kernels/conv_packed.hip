@@ -42,11 +42,17 @@ struct GeoP {
 //                       up to 56 16-B chunks = 9 taps x 48 channels; 7 rows x 57 px x 96 B)
 //   <4, 64,  8, 22528>: GoogLeNet conv1 after the 2x2 fold (115 x 115 x 16 -> 112 x 112 x 64;
 //                       32 chunks = 16 taps x 16 channels; 6 rows x 115 px x 32 B)
+//   <3, 64,  3, 16384>: VGG-16 conv1_1 after its fold (226 x 226 x 8 -> 224 x 224 x 64;
+//                       9 chunks = 9 taps x 8 channels; 4 rows x 226 px x 16 B)
 // 8 waves: wave (mi, ni) owns 48 pixels x KOUT / 2 channels (3 x KOUT / 32 MFMA fragments).
+// q (optional, engine.fuse_fp8_quant): the output also stored as e4m3 with the scale of the
+// (initialised) delayed-scaling slot qslot — the bytes quant_fp8 would produce from the bf16
+// output — and the block's |max| into one of 256 partials 128 B apart (sn_fp8_fold_amax).
 template <int TAPS, int KOUT, int KS, int PCAP>
 __global__ void __launch_bounds__(NT, 1)
 conv_packed_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, const float* __restrict__ bias,
-                   bf16_t* __restrict__ y, GeoP g, int relu) {
+                   bf16_t* __restrict__ y, GeoP g, int relu, uint8_t* __restrict__ q, const float* __restrict__ qslot,
+                   float* __restrict__ qpart) {
   constexpr int NF = KOUT / 16, NFW = NF / 2;     // N fragments: all, per wave
   constexpr int W_BYTES = KS * NF * 1024;         // fragment-ordered weights
   constexpr int PER_T = (PCAP / 16 + NT - 1) / NT;
@@ -101,6 +107,8 @@ long long tile = blockIdx.x;
   for (int i = 0; i < NFW; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k) bv[i][k] = bias ? bias[ni * (KOUT / 2) + i * 16 + (lane >> 4) * 4 + k] : 0.f;
+  const float qsc = q ? qslot[0] : 0.f;
+  float qmax = 0.f;
   int cur = 0;
   for (; tile < g.tiles; tile += gridDim.x) {
     const long long next = tile + gridDim.x;
@@ -182,16 +190,43 @@ long long tile = blockIdx.x;
           for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
         }
         *reinterpret_cast<uint2*>(yo + ch) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if (q) {
+          float f[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float b = bf2f(f2bf(v[k]));  // the stored bf16 value
+            qmax = fmaxf(qmax, fabsf(b));
+            f[k] = fminf(fmaxf(b * qsc, -448.f), 448.f);
+          }
+          int wq = 0;
+          wq = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], wq, false);
+          wq = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], wq, true);
+          *reinterpret_cast<uint32_t*>(q + ((long long)n_img * PQ + m) * KOUT + ch) = (uint32_t)wq;
+        }
       }
     }
     __syncthreads();  // next patch in LDS, and every wave is done reading this one
     cur ^= 1;
   }
+  if (q) {  // block |max| -> partial (every thread reaches this: the tile loop has no early exit)
+    __shared__ float red[NT / 64];
+    qmax = wave_max(qmax);
+    if (lane == 0) red[wave] = qmax;
+    __syncthreads();
+    if (tid == 0) {
+      float m = 0.f;
+#pragma unroll
+      for (int i = 0; i < NT / 64; ++i) m = fmaxf(m, red[i]);
+      if (m > 0.f) atomicMax(reinterpret_cast<unsigned int*>(qpart + (blockIdx.x & 255) * 32), __float_as_uint(m));
+    }
+  }
 }
 
 template <int TAPS, int KOUT, int KS, int PCAP>
 int launch_packed(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N, long long H,
-                  long long W, long long C, long long K, long long relu, hipStream_t st) {
+                  long long W, long long C, long long K, long long relu, hipStream_t st, uint8_t* q = nullptr,
+                  const float* qslot = nullptr, float* qpart = nullptr) {
+  if (q && !(qslot && qpart)) return 9;
   if (N <= 0 || H <= 0 || W <= 0) return 0;
   if (K != KOUT || C <= 0 || C % 8 || (long long)TAPS * TAPS * (C / 8) > 4LL * KS || H < TAPS || W < TAPS ||
       W > 4096)
@@ -209,7 +244,7 @@ int launch_packed(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y
   const int cus = sn_cu_count();
   const long long grid = g.tiles < cus ? g.tiles : cus;  // persistent: one block per CU
   hipLaunchKernelGGL((conv_packed_kernel<TAPS, KOUT, KS, PCAP>), dim3((unsigned)grid), dim3(NT), 0, st, x, w, bias, y,
-                     g, (int)relu);
+                     g, (int)relu, q, qslot, qpart);
   return SN_CHECK_LAUNCH();
 }
 
@@ -230,6 +265,17 @@ extern "C" int sn_conv_packed3x3(const bf16_t* x, const bf16_t* w, const float* 
 extern "C" int sn_conv_packed1x1(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N,
                                  long long H, long long W, long long C, long long K, long long relu, hipStream_t st) {
   return launch_packed<1, 64, 2, 36864>(x, w, bias, y, N, H, W, C, K, relu, st);
+}
+
+// <3, 64, 3, 16384>: y[N][H-2][W-2][64] = conv3x3(x[N][H][W][8], w[64][3][3][8]), stride 1, pad 0 —
+// VGG-16 conv1_1 (224 x 224 x 3, 3x3 pad 1) after its fold (the pad baked in, channels padded to
+// 8: 226 x 226 x 8): 9 taps x one 16-B chunk = 3 K steps (the implicit GEMM ran its 72-deep
+// reduction as two 64-deep steps of 128-row tiles, one output write per 16 KB tile, 84 TF/s)
+// q / qslot / qpart: the e4m3 side output of conv1_2's input under --dtype fp8 (null: none)
+extern "C" int sn_conv_packed3x3k64(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N,
+                                    long long H, long long W, long long C, long long K, long long relu,
+                                    uint8_t* q, const float* qslot, float* qpart, hipStream_t st) {
+  return launch_packed<3, 64, 3, 16384>(x, w, bias, y, N, H, W, C, K, relu, st, q, qslot, qpart);
 }
 
 extern "C" int sn_conv_packed4x4(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* y, long long N,

@@ -190,6 +190,18 @@ def _conv_forward(x, w, b, s: ConvSpec, relu=False, ws=None, folded=None, out=No
         y, ldy = out, chan_stride(out)
     else:
         y, ldy = torch.empty((s.N, s.P, s.Q, s.K), dtype=BF16, device=x.device), s.K
+    if ldx == s.C and ldy == s.K and x.is_contiguous() and packed3x3k64_ok(s):
+        # the packed kernel also stores a fused fp8 side output (engine.fuse_fp8_quant: conv1_2's
+        # e4m3 input under --dtype fp8), in the e4m3 format only
+        from . import gemm as G
+        side = G._SIDE if _side_covers(y) else None
+        if side is None or not side.e5m2:
+            q = (None, None, None)
+            if side is not None:
+                q = (side.q.data_ptr() + (y.data_ptr() - side.base.data_ptr()) // 2, side.slot, side.part)
+                side.launches += 1
+            call("conv_packed3x3k64", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu), *q)
+            return y
     direct_io = ldx == s.C and ldy == s.K and x.is_contiguous() and not _side_covers(y)
     if direct_io and packed_conv_ok(s):
         call("conv_packed3x3", x, _c(w), b, y, s.N, s.H, s.W, s.C, s.K, int(relu))
@@ -304,6 +316,20 @@ def packed44_conv_ok(s: ConvSpec) -> bool:
         return False
     rows = min(s.H, (191 + s.Q - 1) // s.Q + 4)  # input rows one 192-pixel tile touches
     return rows * s.W * s.C * 2 <= 22528 and s.P * s.Q * 64 < 2 ** 31
+
+
+# VGG-16 conv1_1 after its fold (226 x 226 x 8 -> 224 x 224 x 64, 3x3, pad 0) on the tap-packed
+# kernel's <3, 64> instance: 3 K steps of 32 instead of the implicit GEMM's two 64-deep steps per
+# 128-row tile; SN_FEATURES=conv_packed_k64=0 returns it to the GEMM
+_PACKED_K64 = features.enabled("conv_packed_k64")
+
+
+def packed3x3k64_ok(s: ConvSpec) -> bool:
+    if not (_PACKED_K64 and s.K == 64 and s.C == 8 and s.groups == 1 and s.R == 3 and s.S == 3
+            and s.sh == 1 and s.sw == 1 and s.ph == 0 and s.pw == 0 and s.dh == 1 and s.dw == 1 and s.Q > 0):
+        return False
+    rows = min(s.H, (191 + s.Q - 1) // s.Q + 3)  # input rows one 192-pixel tile touches
+    return rows * s.W * s.C * 2 <= 16384 and s.P * s.Q * 64 < 2 ** 31
 
 
 # the e4m3 direct kernel (csrc/kernels/conv3x3_fp8.hip) for the same 64 -> 64 products under

@@ -29,6 +29,7 @@ DEFAULTS = {
     "conv_packed": True,        # tap-packed direct conv (CaffeNet conv1)
     "conv_packed44": True,      # tap-packed <4, 4> instance
     "conv_packed11": False,     # tap-packed 1x1 64 -> 64 (neutral end to end, opt-in)
+    "conv_packed_k64": True,    # tap-packed <3, 64> instance (VGG-16 conv1_1 after its fold)
     "conv_direct_fp8": True,    # e4m3 direct conv for fp8 layers
     # fp8 details
     "fp8_wgrad_bias": True,     # fp8 weight-gradient bias through the e4m3 ones column

@@ -442,6 +442,46 @@ def test_conv_packed11(gpu, N, H, W, C, relu, bias, monkeypatch):
     close(y, hip.conv_forward(x, w, b, s, relu=relu), 1e-2)
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 226, 226), (1, 20, 35), (3, 9, 200), (2, 3, 3), (300, 12, 12)])
+@pytest.mark.parametrize("relu,bias", [(True, True), (False, False)])
+def test_conv_packed3x3k64(gpu, N, H, W, relu, bias, monkeypatch):
+    """The tap-packed direct kernel's <3 taps, 64 outputs> instance (VGG-16 conv1_1 after its
+    fold is (N, 226, 226, 8)): ragged last tiles, a one-pixel image, wide rows, more tiles than
+    CUs, against the fp32 reference and the implicit-GEMM path."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    monkeypatch.setattr(hip, "_PACKED_K64", True)
+    s = ConvSpec(N, H, W, 8, 64, 3, 3, 1, 1, 0, 0, 1, 1, 1)
+    assert hip.packed3x3k64_ok(s)
+    x = rnd(N, H, W, 8)
+    w = rnd(64, 3, 3, 8, scale=0.1)
+    b = torch.randn(64, device="cuda") if bias else None
+    y = hip.conv_forward(x, w, b, s, relu=relu)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b)
+    if relu:
+        ref = torch.relu(ref)
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+    monkeypatch.setattr(hip, "_PACKED_K64", False)
+    close(y, hip.conv_forward(x, w, b, s, relu=relu), 1e-2)
+
+
+def test_conv_packed3x3k64_vgg_conv1_1(gpu, monkeypatch):
+    """VGG-16 conv1_1 (224 x 224 x 3, 3x3, pad 1) through conv_forward: the fold (pad baked in,
+    channels padded to 8) feeds the packed <3, 64> kernel; against the fp32 reference."""
+    from sparknet_amd.ops import hip
+    import torch.nn.functional as F
+    monkeypatch.setattr(hip, "_PACKED_K64", True)
+    s = ConvSpec(2, 224, 224, 3, 64, 3, 3, 1, 1, 1, 1, 1, 1, 1)
+    plan = hip.s2d_plan(s)
+    assert plan is not None and hip.packed3x3k64_ok(plan[4])
+    x = rnd(2, 224, 224, 3)
+    w = rnd(64, 3, 3, 3, scale=0.1)
+    b = torch.randn(64, device="cuda")
+    y = hip.conv_forward(x, w, b, s, relu=True)
+    ref = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1))
+    close(y, ref.permute(0, 2, 3, 1), 1e-2)
+
+
 def test_conv_packed44_googlenet_conv1(gpu, monkeypatch):
     """GoogLeNet conv1 (224 x 224 x 3, 7 x 7 / 2, pad 3) through conv_forward: the 2x2
     space-to-depth fold feeds the packed 4x4 kernel; against the fp32 reference."""
