@@ -167,7 +167,9 @@ def main():
         _lib.kernels()
         from sparknet_amd.ops import gemm as G
         G.set_autotune(args.autotune)
-    comm = (Comm(backend="gloo" if args.share_gpu else None, device=dev if dev.type == "cuda" else None,
+    # --cpu runs gloo even on a GPU host (nccl has no CPU tensors)
+    comm = (Comm(backend="gloo" if (args.share_gpu or dev.type != "cuda") else None,
+                 device=dev if dev.type == "cuda" else None,
                  watchdog=True, timeout_s=600.0) if world > 1 or force_comm else None)
     bad = diag.check_placement(comm, args.gpus, args.share_gpu or dev.type != "cuda",
                                torch.cuda.current_device() if dev.type == "cuda" else local_rank, local_rank)

@@ -77,7 +77,9 @@ def setup(args):
         from ..ops import _lib
         _lib.kernels()
     from ..parallel import Comm
-    comm = (Comm(backend="gloo" if share_gpu() else None, device=dev if dev.type == "cuda" else None,
+    # a CPU job (--cpu) runs gloo even where RCCL is available: nccl has no CPU tensors
+    comm = (Comm(backend="gloo" if (share_gpu() or dev.type != "cuda") else None,
+                 device=dev if dev.type == "cuda" else None,
                  timeout_s=getattr(args, "pg_timeout", 300.0), watchdog=True) if world > 1 else None)
     return rank, world, dev, comm
 

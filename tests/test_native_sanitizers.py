@@ -26,5 +26,10 @@ def test_loader_under_sanitizer(tmp_path, san):
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="halt_on_error=1:detect_leaks=1",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    if "ThreadSanitizer: unexpected memory mapping" in r.stderr:
+        # TSan's shadow layout does not accept this host's address-space layout (high-entropy
+        # mmap randomisation, or another runtime preloaded into the process): an environment
+        # limit, not a finding
+        pytest.skip("ThreadSanitizer cannot map its shadow memory on this host")
     assert r.returncode == 0 and "bad=0" in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])
     assert "WARNING: ThreadSanitizer" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr
