@@ -673,7 +673,7 @@ def fuse_fp8_quant(net) -> int:
                 # the conv reads that gradient only as fp8 (e4m3 data and weight gradients, bias
                 # on the ones column): the pooling stores the fp8 bytes alone, not the bf16
                 # tensor too — VGG-16 b2048 writes 25 GB less per step
-                pool.fp8_dx_only = (features.enabled("fp8_dx_only")
+                pool.fp8_dx_only = (features.enabled("fp8_dx_only") and not net.debug_info  # debug_info prints diffs
                                     and hip.conv_dy_fp8_only_ok(prod, prod.spec(net.bottom_vecs[prods[-1]][0])))
                 n += 1
     for pi, prod in enumerate(net.layers):
